@@ -1,0 +1,160 @@
+/*
+ * rcdc.h -- C ABI of librcdc, the MI355X-native content-defined chunker that
+ * replaces rustic_core's Rabin CDC hot path.
+ *
+ * Drop-in point (reference = rustic_core 0.12.0, /root/reference):
+ *   crates/core/src/chunker.rs:21-58  ChunkIter::from_config(&ConfigFile, R, size_hint)
+ *                                     + Iterator<Item = RusticResult<Vec<u8>>>
+ *   crates/core/src/chunker/rabin.rs:82-191  RabinChunkIter::{new, next}
+ * called from crates/core/src/archiver/file_archiver.rs:144-160
+ * (FileArchiver::backup_reader), one iterator per file on pariter workers
+ * (crates/core/src/archiver.rs:195).
+ *
+ * Contract: every function returns cut offsets (END offset of each chunk,
+ * i.e. the prefix sums of the chunk lengths the reference iterator yields)
+ * that are bit-identical to what rabin.rs ChunkIter::next produces on the
+ * same bytes with the same (poly, min, avg, max).  A Rust `ChunkIter::Gpu`
+ * variant slices its buffer at these offsets.
+ *
+ * Plain C types only (pointers + sizes); no HIP or torch types appear in a
+ * signature.  Device pointers are passed as `const void *` / `uint64_t`.
+ * All entry points are thread-safe for distinct contexts/streams/plans; one
+ * context may be shared by threads (internal lock around its HIP stream).
+ */
+#ifndef RCDC_H
+#define RCDC_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RCDC_ABI_VERSION 1u
+
+/* Status codes map onto rustic_core ErrorKind (crates/core/src/error.rs:108-124). */
+typedef enum {
+    RCDC_OK = 0,
+    RCDC_ERR_UNSUPPORTED = 1,   /* ErrorKind::Unsupported  (rabin.rs:22-40)           */
+    RCDC_ERR_INVALID_INPUT = 2, /* ErrorKind::InvalidInput (configfile.rs:166-171)     */
+    RCDC_ERR_INTERNAL = 3,      /* ErrorKind::Internal     (HIP runtime failures)      */
+    RCDC_ERR_INPUT_OUTPUT = 4,  /* ErrorKind::InputOutput  (rabin.rs:131-138,174-180)  */
+    RCDC_ERR_CAPACITY = 5       /* caller's cut buffer too small; counts still valid   */
+} rcdc_status;
+
+typedef struct rcdc_ctx rcdc_ctx;       /* one device + chunker parameters      */
+typedef struct rcdc_stream rcdc_stream; /* one file fed in pieces               */
+typedef struct rcdc_plan rcdc_plan;     /* a fixed batch layout in device memory */
+
+typedef struct {
+    const uint8_t *data; /* host pointer (rcdc_chunk_batch)                */
+    uint64_t len;
+} rcdc_buf;
+
+/* ---- parameters -------------------------------------------------------- */
+
+/* check_rabin_params -- replaces crates/core/src/chunker/rabin.rs:17-42.
+ * avg must be a power of two, min <= avg <= max.  Additionally rejected with
+ * RCDC_ERR_UNSUPPORTED: min < 64 (the reference slices vec[len-64..],
+ * rabin.rs:150) and max > 2^40.                                            */
+rcdc_status rcdc_check_params(uint64_t avg, uint64_t min, uint64_t max);
+
+/* ConfigFile::poly -- replaces crates/core/src/repofile/configfile.rs:165-175
+ * (u64::from_str_radix(hex, 16)); RCDC_ERR_INVALID_INPUT on a bad string.   */
+rcdc_status rcdc_parse_poly(const char *hex, uint64_t *poly);
+
+/* ---- context ------------------------------------------------------------ */
+
+/* Replaces Rabin64::new_with_polynom(6, &poly) + RabinChunkIter::new
+ * (crates/core/src/chunker.rs:29-38, rabin.rs:82-104).  Builds the Rabin64
+ * out/mod tables once per context (the reference rebuilds them per file) and
+ * uploads them to `device`.  deg(poly) must be in [9, 56].                  */
+rcdc_status rcdc_ctx_create(uint64_t poly, uint64_t min, uint64_t avg_pow2,
+                            uint64_t max, int device, rcdc_ctx **out);
+void rcdc_ctx_destroy(rcdc_ctx *ctx);
+
+/* Message of the last failing call on this thread ("" if none). */
+const char *rcdc_last_error(void);
+
+/* Upper bound on the number of chunks of an n-byte stream. */
+uint64_t rcdc_max_cuts(const rcdc_ctx *ctx, uint64_t n);
+
+/* ---- independent host streams (per-file parallel path, archiver.rs:195) - */
+
+/* Chunk n independent host buffers.  Their bytes are copied H2D through
+ * pinned staging buffers on the context's stream, scanned on the device and
+ * only the cut offsets are copied back.  Cuts of stream i are written
+ * consecutively to cuts[] in stream order; cut_counts[i] receives the count.
+ * If the total exceeds cuts_cap, RCDC_ERR_CAPACITY is returned with every
+ * cut_counts[i] valid and cuts[] untouched.                                 */
+rcdc_status rcdc_chunk_batch(rcdc_ctx *ctx, const rcdc_buf *bufs, uint32_t n,
+                             uint64_t *cuts, uint64_t cuts_cap,
+                             uint64_t *cut_counts);
+
+/* ---- one file fed in pieces (the Read-driven iterator) ------------------ */
+
+/* Replaces the read loop of rabin.rs:110-191: the caller feeds the file in
+ * arbitrary pieces (any split gives the same cuts, like the reference's
+ * read()-independence).  After each feed, *n_cuts cut offsets (absolute,
+ * from the start of the file) that are now final are written to cuts[].
+ * is_final = 1 marks EOF (the reference's Ok(0)); then the last cut is the
+ * file length.  Bytes are retained internally only until they can no longer
+ * influence a cut (at most max + 128 bytes).                               */
+rcdc_status rcdc_stream_open(rcdc_ctx *ctx, rcdc_stream **out);
+rcdc_status rcdc_stream_feed(rcdc_stream *st, const uint8_t *data,
+                             uint64_t len, int is_final, uint64_t *cuts,
+                             uint64_t cap, uint64_t *n_cuts);
+void rcdc_stream_close(rcdc_stream *st);
+
+/* ---- device-resident batches (the measured hot path) ------------------- */
+
+/* A plan fixes a batch layout: n streams at byte offsets offs[i] (any
+ * alignment) with lengths lens[i] inside a device arena of arena_len bytes.
+ * It owns the device work lists, per-segment summaries and the cut output.
+ * Requires the arena base pointer passed to rcdc_plan_run to be 256-B
+ * aligned (hipMalloc / torch allocations are).                             */
+rcdc_status rcdc_plan_create(rcdc_ctx *ctx, const uint64_t *offs,
+                             const uint64_t *lens, uint32_t n,
+                             uint64_t arena_len, rcdc_plan **out);
+void rcdc_plan_destroy(rcdc_plan *plan);
+
+/* Enqueue scan + resolve on `hip_stream` (a hipStream_t, or 0 for the
+ * context's own stream) over the device arena `d_arena`.  Asynchronous. */
+rcdc_status rcdc_plan_run(rcdc_plan *plan, const void *d_arena,
+                          void *hip_stream);
+
+/* Synchronise with the last run and copy the results to the host: same
+ * layout and capacity rule as rcdc_chunk_batch.                           */
+rcdc_status rcdc_plan_results(rcdc_plan *plan, uint64_t *cuts,
+                              uint64_t cuts_cap, uint64_t *cut_counts);
+
+/* Device-side view of the results (valid after the run completes):
+ * stream i's cuts are d_cuts[cut_base[i] .. cut_base[i] + d_counts[i]).   */
+rcdc_status rcdc_plan_device_results(rcdc_plan *plan, uint64_t *d_cuts,
+                                     uint64_t *d_counts,
+                                     const uint64_t **cut_base);
+
+/* Scan-kernel geometry chosen by the plan (for profiling / roofline). */
+typedef struct {
+    uint64_t scanned_bytes;   /* bytes the scan kernel must hash         */
+    uint64_t segments;        /* per-lane segments                       */
+    uint32_t segment_bytes;   /* S                                        */
+    uint32_t work_items;      /* 64-segment wave work items               */
+    uint32_t scan_blocks;     /* workgroups of the scan launch            */
+    uint32_t reserved;
+} rcdc_plan_info;
+rcdc_status rcdc_plan_get_info(const rcdc_plan *plan, rcdc_plan_info *info);
+
+/* ---- FixedSize chunker (crates/core/src/chunker/fixed_size.rs:41-70) ---- */
+/* Cuts every `size` bytes, last chunk short; returns the count.           */
+uint64_t rcdc_fixed_cuts(uint64_t n, uint64_t size, uint64_t *cuts,
+                         uint64_t cap);
+
+/* ABI version of the loaded library (== RCDC_ABI_VERSION). */
+uint32_t rcdc_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RCDC_H */

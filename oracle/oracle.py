@@ -1,0 +1,178 @@
+"""ctypes front-end of the CPU ORACLE (``oracle/libcdc_ref.so``).
+
+TEST INFRASTRUCTURE ONLY: imported by ``tests/``, ``__graft_entry__.smoke()``
+and the ``cpu_baseline`` leg of ``bench.py`` -- as the checker, never as the
+thing measured or shipped.  The product (``rustic_core_amd``) never imports
+this module.
+
+The C code restates ``crates/core/src/chunker/rabin.rs:107-191`` and the
+rustic_cdc 0.3.1 Rabin64 arithmetic (see ``oracle/cdc_ref.h`` for the
+file:line map and the parity pin).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_SO = os.path.join(_HERE, "libcdc_ref.so")
+
+DEFAULT_POLY = 0x003DA3358B4DC173  # rabin.rs:336 test polynomial
+KiB = 1024
+MiB = 1024 * KiB
+DEFAULT_MIN = 512 * KiB  # configfile.rs:39
+DEFAULT_AVG = 1 * MiB    # configfile.rs:37
+DEFAULT_MAX = 8 * MiB    # configfile.rs:41
+
+
+def build() -> str:
+    """Compile the oracle with its Makefile (gcc)."""
+    subprocess.run(["make", "-s", "-C", _HERE], check=True)
+    return _SO
+
+
+class _Tables(ctypes.Structure):
+    _fields_ = [
+        ("out_table", ctypes.c_uint64 * 256),
+        ("mod_table", ctypes.c_uint64 * 256),
+        ("degree", ctypes.c_int),
+        ("shift", ctypes.c_int),
+    ]
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        src = os.path.join(_HERE, "cdc_ref.c")
+        if not os.path.exists(_SO) or (
+            os.path.exists(src) and os.path.getmtime(src) > os.path.getmtime(_SO)
+        ):
+            build()
+        L = ctypes.CDLL(_SO)
+        u64, sz, p = ctypes.c_uint64, ctypes.c_size_t, ctypes.c_void_p
+        L.cdc_ref_tables_init.argtypes = [ctypes.POINTER(_Tables), u64]
+        L.cdc_ref_tables_init.restype = ctypes.c_int
+        L.cdc_ref_check_params.argtypes = [u64, u64, u64]
+        L.cdc_ref_check_params.restype = ctypes.c_int
+        L.cdc_ref_chunk.argtypes = [ctypes.POINTER(_Tables), p, sz, u64, u64, u64,
+                                    ctypes.c_int, p, sz]
+        L.cdc_ref_chunk.restype = sz
+        L.cdc_ref_chunk_owned.argtypes = [ctypes.POINTER(_Tables), p, sz, u64, u64,
+                                          u64, p, sz]
+        L.cdc_ref_chunk_owned.restype = sz
+        L.cdc_ref_chunk_many_owned.argtypes = [ctypes.POINTER(_Tables), p, p, p, sz,
+                                               u64, u64, u64, ctypes.c_int, p]
+        L.cdc_ref_chunk_many_owned.restype = u64
+        L.cdc_ref_fixed.argtypes = [sz, u64, p, sz]
+        L.cdc_ref_fixed.restype = sz
+        L.cdc_ref_candidates.argtypes = [ctypes.POINTER(_Tables), p, sz, u64, sz, sz, p]
+        L.cdc_ref_candidates.restype = None
+        L.cdc_ref_stdrng_fill.argtypes = [u64, p, sz]
+        L.cdc_ref_stdrng_fill.restype = None
+        L.cdc_ref_stdrng_fill_at.argtypes = [u64, u64, p, sz]
+        L.cdc_ref_stdrng_fill_at.restype = None
+        _lib = L
+    return _lib
+
+
+_tables_cache: dict = {}
+
+
+def tables(poly: int = DEFAULT_POLY) -> _Tables:
+    t = _tables_cache.get(poly)
+    if t is None:
+        t = _Tables()
+        if lib().cdc_ref_tables_init(ctypes.byref(t), poly) != 0:
+            raise ValueError(f"unsupported polynomial {poly:#x}")
+        _tables_cache[poly] = t
+    return t
+
+
+def _ptr(a: np.ndarray) -> int:
+    return a.ctypes.data
+
+
+def _as_u8(data) -> np.ndarray:
+    if isinstance(data, np.ndarray):
+        return np.ascontiguousarray(data, dtype=np.uint8).reshape(-1)
+    return np.frombuffer(bytes(data), dtype=np.uint8)
+
+
+def chunk_cuts(data, poly=DEFAULT_POLY, min_size=DEFAULT_MIN, avg=DEFAULT_AVG,
+               max_size=DEFAULT_MAX, prefill64: bool = False) -> np.ndarray:
+    """End offsets of every chunk (ChunkIter::next semantics, rabin.rs:107-191)."""
+    a = _as_u8(data)
+    n = a.size
+    cap = n // max(min_size, 1) + 2
+    cuts = np.zeros(cap, dtype=np.uint64)
+    k = lib().cdc_ref_chunk(ctypes.byref(tables(poly)), _ptr(a), n, min_size, avg,
+                            max_size, int(prefill64), _ptr(cuts), cap)
+    assert k <= cap
+    return cuts[:k].copy()
+
+
+def chunk_cuts_owned(data, poly=DEFAULT_POLY, min_size=DEFAULT_MIN, avg=DEFAULT_AVG,
+                     max_size=DEFAULT_MAX) -> np.ndarray:
+    """Same cuts, reference-equivalent work (owned chunk buffers, 4 KiB reads)."""
+    a = _as_u8(data)
+    n = a.size
+    cap = n // max(min_size, 1) + 2
+    cuts = np.zeros(cap, dtype=np.uint64)
+    k = lib().cdc_ref_chunk_owned(ctypes.byref(tables(poly)), _ptr(a), n, min_size,
+                                  avg, max_size, _ptr(cuts), cap)
+    return cuts[:k].copy()
+
+
+def chunk_many_owned(arena: np.ndarray, offs, lens, poly=DEFAULT_POLY,
+                     min_size=DEFAULT_MIN, avg=DEFAULT_AVG, max_size=DEFAULT_MAX,
+                     nthreads: int = 1) -> np.ndarray:
+    """Chunk many files in parallel (per-file threads, archiver.rs:195). Returns counts."""
+    offs = np.ascontiguousarray(offs, dtype=np.uint64)
+    lens = np.ascontiguousarray(lens, dtype=np.uint64)
+    counts = np.zeros(offs.size, dtype=np.uint64)
+    lib().cdc_ref_chunk_many_owned(ctypes.byref(tables(poly)), _ptr(arena), _ptr(offs),
+                                   _ptr(lens), offs.size, min_size, avg, max_size,
+                                   nthreads, _ptr(counts))
+    return counts
+
+
+def fixed_cuts(n: int, size: int) -> np.ndarray:
+    cap = n // size + 2
+    cuts = np.zeros(cap, dtype=np.uint64)
+    k = lib().cdc_ref_fixed(n, size, _ptr(cuts), cap)
+    return cuts[:k].copy()
+
+
+def candidates(data, first: int, count: int, poly=DEFAULT_POLY,
+               mask: int = DEFAULT_AVG - 1) -> np.ndarray:
+    """flags[i] = fp(data[p-64:p]) & mask == 0 for p = first + i."""
+    a = _as_u8(data)
+    assert first >= 64 and first + count - 1 <= a.size
+    flags = np.zeros(count, dtype=np.uint8)
+    lib().cdc_ref_candidates(ctypes.byref(tables(poly)), _ptr(a), a.size, mask, first,
+                             count, _ptr(flags))
+    return flags
+
+
+def check_params(avg: int, min_size: int, max_size: int) -> bool:
+    return lib().cdc_ref_check_params(avg, min_size, max_size) == 0
+
+
+def stdrng_bytes(seed: int, n: int, skip: int = 0) -> np.ndarray:
+    """rand 0.10 ``StdRng::seed_from_u64(seed).fill_bytes`` (optionally from byte ``skip``)."""
+    assert skip % 64 == 0
+    buf = np.empty(n, dtype=np.uint8)
+    lib().cdc_ref_stdrng_fill_at(seed, skip, _ptr(buf), n)
+    return buf
+
+
+def table_arrays(poly: int = DEFAULT_POLY):
+    t = tables(poly)
+    return (np.array(t.out_table[:], dtype=np.uint64),
+            np.array(t.mod_table[:], dtype=np.uint64), t.degree, t.shift)

@@ -1,0 +1,128 @@
+"""ctypes binding of ``librcdc.so`` (the C ABI declared in ``include/rcdc.h``).
+
+The library is built in-tree by ``__graft_entry__.build()`` /
+``rustic_core_amd/csrc/Makefile``.  There is no fallback: if the shared
+library is missing or a symbol is absent, loading raises ``RcdcLibraryError``
+-- the chunker never silently runs on the CPU.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "librcdc.so")
+CSRC = os.path.join(_HERE, "csrc")
+
+# Every entry point of include/rcdc.h (checked by tests/test_abi.py).
+EXPORTS = (
+    "rcdc_abi_version", "rcdc_last_error", "rcdc_check_params", "rcdc_parse_poly",
+    "rcdc_ctx_create", "rcdc_ctx_destroy", "rcdc_max_cuts", "rcdc_chunk_batch",
+    "rcdc_stream_open", "rcdc_stream_feed", "rcdc_stream_close", "rcdc_plan_create",
+    "rcdc_plan_destroy", "rcdc_plan_run", "rcdc_plan_results", "rcdc_plan_device_results",
+    "rcdc_plan_get_info", "rcdc_fixed_cuts",
+)
+ABI_VERSION = 1
+
+
+class RcdcLibraryError(RuntimeError):
+    """librcdc.so could not be loaded (not built, wrong ABI)."""
+
+
+class Buf(ctypes.Structure):
+    _fields_ = [("data", ctypes.c_void_p), ("len", ctypes.c_uint64)]
+
+
+class PlanInfo(ctypes.Structure):
+    _fields_ = [
+        ("scanned_bytes", ctypes.c_uint64),
+        ("segments", ctypes.c_uint64),
+        ("segment_bytes", ctypes.c_uint32),
+        ("work_items", ctypes.c_uint32),
+        ("scan_blocks", ctypes.c_uint32),
+        ("reserved", ctypes.c_uint32),
+    ]
+
+
+def build(verbose: bool = False) -> str:
+    """Compile librcdc.so for gfx950 with hipcc (cross-compiles without a GPU)."""
+    out = subprocess.run(["make", "-s", "-C", CSRC], capture_output=not verbose, text=True)
+    if out.returncode != 0:
+        raise RcdcLibraryError(f"building librcdc.so failed:\n{out.stdout}\n{out.stderr}")
+    return LIB_PATH
+
+
+_lib = None
+
+
+def lib() -> ctypes.CDLL:
+    global _lib
+    if _lib is not None:
+        return _lib
+    # One HIP runtime per process: torch ships its own libamdhip64 (soname
+    # libamdhip64.so.7, but NEEDED as "libamdhip64.so").  Loading torch first
+    # makes librcdc bind to that already-loaded runtime; loading librcdc
+    # first would pull /opt/rocm's copy and torch would then load a second
+    # one ("no ROCm-capable device" from whichever initialises last).
+    try:
+        import torch  # noqa: F401
+    except ImportError:  # pragma: no cover - torch-free embedding
+        pass
+    if not os.path.exists(LIB_PATH):
+        raise RcdcLibraryError(
+            f"{LIB_PATH} not found: build it with __graft_entry__.build() "
+            "(hipcc --offload-arch=gfx950); there is no CPU fallback")
+    try:
+        L = ctypes.CDLL(LIB_PATH)
+    except OSError as e:  # pragma: no cover - environment specific
+        raise RcdcLibraryError(f"cannot load {LIB_PATH}: {e}") from e
+    for name in EXPORTS:
+        if not hasattr(L, name):
+            raise RcdcLibraryError(f"{LIB_PATH} lacks symbol {name}")
+    u64, u32, vp, st = ctypes.c_uint64, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_int
+    P = ctypes.POINTER
+    L.rcdc_abi_version.restype = u32
+    L.rcdc_abi_version.argtypes = []
+    if L.rcdc_abi_version() != ABI_VERSION:
+        raise RcdcLibraryError("librcdc.so ABI version mismatch")
+    L.rcdc_last_error.restype = ctypes.c_char_p
+    L.rcdc_last_error.argtypes = []
+    L.rcdc_check_params.restype = st
+    L.rcdc_check_params.argtypes = [u64, u64, u64]
+    L.rcdc_parse_poly.restype = st
+    L.rcdc_parse_poly.argtypes = [ctypes.c_char_p, P(u64)]
+    L.rcdc_ctx_create.restype = st
+    L.rcdc_ctx_create.argtypes = [u64, u64, u64, u64, ctypes.c_int, P(vp)]
+    L.rcdc_ctx_destroy.restype = None
+    L.rcdc_ctx_destroy.argtypes = [vp]
+    L.rcdc_max_cuts.restype = u64
+    L.rcdc_max_cuts.argtypes = [vp, u64]
+    L.rcdc_chunk_batch.restype = st
+    L.rcdc_chunk_batch.argtypes = [vp, P(Buf), u32, vp, u64, vp]
+    L.rcdc_stream_open.restype = st
+    L.rcdc_stream_open.argtypes = [vp, P(vp)]
+    L.rcdc_stream_feed.restype = st
+    L.rcdc_stream_feed.argtypes = [vp, vp, u64, ctypes.c_int, vp, u64, P(u64)]
+    L.rcdc_stream_close.restype = None
+    L.rcdc_stream_close.argtypes = [vp]
+    L.rcdc_plan_create.restype = st
+    L.rcdc_plan_create.argtypes = [vp, vp, vp, u32, u64, P(vp)]
+    L.rcdc_plan_destroy.restype = None
+    L.rcdc_plan_destroy.argtypes = [vp]
+    L.rcdc_plan_run.restype = st
+    L.rcdc_plan_run.argtypes = [vp, vp, vp]
+    L.rcdc_plan_results.restype = st
+    L.rcdc_plan_results.argtypes = [vp, vp, u64, vp]
+    L.rcdc_plan_device_results.restype = st
+    L.rcdc_plan_device_results.argtypes = [vp, P(u64), P(u64), P(P(u64))]
+    L.rcdc_plan_get_info.restype = st
+    L.rcdc_plan_get_info.argtypes = [vp, P(PlanInfo)]
+    L.rcdc_fixed_cuts.restype = u64
+    L.rcdc_fixed_cuts.argtypes = [u64, u64, vp, u64]
+    _lib = L
+    return L
+
+
+def last_error() -> str:
+    return lib().rcdc_last_error().decode(errors="replace")

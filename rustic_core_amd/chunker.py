@@ -1,0 +1,334 @@
+"""Host-side mirror of rustic_core's chunker surface, backed by librcdc.
+
+Reference (rustic_core 0.12.0):
+  crates/core/src/chunker.rs:16-59          ChunkIter::{Rabin, FixedSize}, from_config
+  crates/core/src/chunker/rabin.rs:17-42    check_rabin_params
+  crates/core/src/chunker/rabin.rs:82-191   RabinChunkIter::{new, next}
+  crates/core/src/chunker/fixed_size.rs     FixedSizeChunkIter
+  crates/core/src/repofile/configfile.rs    ConfigFile chunker fields / getters
+
+``ChunkIter.from_config(config, reader, size_hint)`` returns an iterator that
+yields every chunk of ``reader`` as ``bytes``, exactly the chunks the Rust
+iterator yields.  For Rabin the cut points come from the MI355X kernels
+(rcdc_stream_feed); the bytes themselves never leave the host buffer.
+There is no CPU fallback for the Rabin path: without librcdc.so or a GPU the
+constructor raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import enum
+import io
+import os
+import threading
+from dataclasses import dataclass
+from typing import Iterator, Optional
+
+import numpy as np
+
+from . import _lib
+from .errors import ErrorKind, RusticError, status_error
+
+KB = 1024
+MB = 1024 * KB
+# configfile.rs:36-41
+DEFAULT_CHUNK_SIZE = 1 * MB
+DEFAULT_CHUNK_MIN_SIZE = 512 * KB
+DEFAULT_CHUNK_MAX_SIZE = 8 * MB
+# Bytes requested from the reader per read(): large reads, the cut points do
+# not depend on how the stream is split (the reference reads 4 KiB, rabin.rs:12).
+READ_SIZE = 16 * MB
+
+
+class Chunker(enum.Enum):
+    """configfile.rs `Chunker` (default Rabin)."""
+    Rabin = "rabin"
+    FixedSize = "fixed_size"
+
+
+@dataclass
+class ConfigFile:
+    """The chunker-related fields of rustic's repository ``ConfigFile``."""
+    version: int = 2
+    chunker_polynomial: str = ""
+    chunker: Optional[Chunker] = None
+    chunk_size_: Optional[int] = None
+    chunk_min_size_: Optional[int] = None
+    chunk_max_size_: Optional[int] = None
+
+    @classmethod
+    def new(cls, version: int, poly: int) -> "ConfigFile":
+        # configfile.rs:151-158: format!("{poly:x}")
+        return cls(version=version, chunker_polynomial=f"{poly:x}")
+
+    def poly(self) -> int:
+        """configfile.rs:165-175 (`u64::from_str_radix(.., 16)`)."""
+        out = ctypes.c_uint64(0)
+        st = _lib.lib().rcdc_parse_poly(self.chunker_polynomial.encode(), ctypes.byref(out))
+        if st:
+            raise status_error(st, _lib.last_error())
+        return out.value
+
+    def get_chunker(self) -> Chunker:
+        return self.chunker or Chunker.Rabin
+
+    def chunk_size(self) -> int:
+        return DEFAULT_CHUNK_SIZE if self.chunk_size_ is None else self.chunk_size_
+
+    def chunk_min_size(self) -> int:
+        return DEFAULT_CHUNK_MIN_SIZE if self.chunk_min_size_ is None else self.chunk_min_size_
+
+    def chunk_max_size(self) -> int:
+        return DEFAULT_CHUNK_MAX_SIZE if self.chunk_max_size_ is None else self.chunk_max_size_
+
+    def has_same_chunker(self, other: "ConfigFile") -> bool:
+        """configfile.rs:274-285."""
+        if self.get_chunker() != other.get_chunker():
+            return False
+        if self.get_chunker() == Chunker.Rabin:
+            return (self.chunker_polynomial == other.chunker_polynomial
+                    and self.chunk_size() == other.chunk_size()
+                    and self.chunk_min_size() == other.chunk_min_size()
+                    and self.chunk_max_size() == other.chunk_max_size())
+        return self.chunk_size() == other.chunk_size()
+
+
+def check_rabin_params(chunk_size: int, chunk_min_size: int, chunk_max_size: int) -> None:
+    """rabin.rs:17-42 -- raises ``RusticError(ErrorKind.Unsupported)``."""
+    st = _lib.lib().rcdc_check_params(chunk_size, chunk_min_size, chunk_max_size)
+    if st:
+        raise status_error(st, _lib.last_error())
+
+
+# ---------------------------------------------------------------------------
+# device contexts (one per (poly, params, device); the reference rebuilds the
+# Rabin64 tables per file at chunker.rs:30, we build them once)
+# ---------------------------------------------------------------------------
+_ctx_lock = threading.Lock()
+_ctx_cache: dict = {}
+
+
+def default_device() -> int:
+    return int(os.environ.get("RCDC_DEVICE", os.environ.get("LOCAL_RANK", "0")))
+
+
+class Context:
+    """Owns an ``rcdc_ctx`` (tables on one device + chunker parameters)."""
+
+    def __init__(self, poly: int, min_size: int, avg: int, max_size: int,
+                 device: Optional[int] = None):
+        L = _lib.lib()
+        self.poly, self.min_size, self.avg, self.max_size = poly, min_size, avg, max_size
+        self.device = default_device() if device is None else device
+        h = ctypes.c_void_p()
+        st = L.rcdc_ctx_create(poly, min_size, avg, max_size, self.device, ctypes.byref(h))
+        if st:
+            raise status_error(st, _lib.last_error())
+        self._h = h
+
+    @classmethod
+    def get(cls, poly: int, min_size: int, avg: int, max_size: int,
+            device: Optional[int] = None) -> "Context":
+        dev = default_device() if device is None else device
+        key = (poly, min_size, avg, max_size, dev)
+        with _ctx_lock:
+            c = _ctx_cache.get(key)
+            if c is None:
+                c = cls(poly, min_size, avg, max_size, dev)
+                _ctx_cache[key] = c
+            return c
+
+    @property
+    def handle(self) -> ctypes.c_void_p:
+        return self._h
+
+    def max_cuts(self, n: int) -> int:
+        return int(_lib.lib().rcdc_max_cuts(self._h, n))
+
+    def chunk_batch(self, buffers) -> list:
+        """Chunk independent host buffers; returns one ``np.uint64`` cut array each."""
+        bufs = [np.ascontiguousarray(np.frombuffer(b, dtype=np.uint8)) if not isinstance(
+            b, np.ndarray) else np.ascontiguousarray(b, dtype=np.uint8).reshape(-1)
+            for b in buffers]
+        n = len(bufs)
+        arr = (_lib.Buf * max(n, 1))()
+        cap = 0
+        for i, b in enumerate(bufs):
+            arr[i].data = b.ctypes.data if b.size else None
+            arr[i].len = b.size
+            cap += self.max_cuts(b.size)
+        cuts = np.zeros(max(cap, 1), dtype=np.uint64)
+        counts = np.zeros(max(n, 1), dtype=np.uint64)
+        st = _lib.lib().rcdc_chunk_batch(self._h, arr, n, cuts.ctypes.data, cap,
+                                         counts.ctypes.data)
+        if st:
+            raise status_error(st, _lib.last_error())
+        out, o = [], 0
+        for i in range(n):
+            k = int(counts[i])
+            out.append(cuts[o:o + k].copy())
+            o += k
+        return out
+
+    def __del__(self):  # pragma: no cover - interpreter shutdown order
+        try:
+            if getattr(self, "_h", None):
+                _lib.lib().rcdc_ctx_destroy(self._h)
+                self._h = None
+        except Exception:
+            pass
+
+
+class _Stream:
+    """rcdc_stream: one file fed in pieces; returns final cut offsets."""
+
+    def __init__(self, ctx: Context):
+        self._ctx = ctx
+        h = ctypes.c_void_p()
+        st = _lib.lib().rcdc_stream_open(ctx.handle, ctypes.byref(h))
+        if st:
+            raise status_error(st, _lib.last_error())
+        self._h = h
+
+    def feed(self, data: bytes, is_final: bool) -> np.ndarray:
+        L = _lib.lib()
+        a = np.frombuffer(data, dtype=np.uint8) if len(data) else np.zeros(0, np.uint8)
+        # bound: cuts come from at most the buffered bytes + this piece
+        cap = self._ctx.max_cuts(len(data) + 2 * self._ctx.max_size + (96 << 20)) + 1
+        cuts = np.zeros(cap, dtype=np.uint64)
+        n = ctypes.c_uint64(0)
+        st = L.rcdc_stream_feed(self._h, a.ctypes.data if a.size else None, a.size,
+                                int(is_final), cuts.ctypes.data, cap, ctypes.byref(n))
+        if st:
+            raise status_error(st, _lib.last_error())
+        return cuts[:n.value]
+
+    def close(self):
+        if self._h:
+            _lib.lib().rcdc_stream_close(self._h)
+            self._h = None
+
+    __del__ = close
+
+
+def _read(reader, n: int) -> bytes:
+    """One reader.read(n) with the reference's error mapping (rabin.rs:162-181)."""
+    while True:
+        try:
+            b = reader.read(n)
+        except InterruptedError:
+            continue  # ErrorKind::Interrupted -> retry (rabin.rs:173)
+        except OSError as e:
+            raise RusticError(ErrorKind.InputOutput,
+                              f"Failed to read from reader in iterator: {e}") from e
+        return b if b is not None else b""
+
+
+class RabinChunkIter:
+    """rabin.rs ChunkIter with device-computed cut points.
+
+    Yields ``bytes`` chunks; raises ``RusticError`` like the reference's
+    ``Some(Err(..))`` items (after which iteration stops).
+    """
+
+    def __init__(self, ctx: Context, reader, size_hint: int = 0):
+        check_rabin_params(ctx.avg, ctx.min_size, ctx.max_size)
+        self._ctx = ctx
+        self._reader = reader
+        self.size_hint = size_hint  # capacity hint only; never affects cuts
+        self._stream = _Stream(ctx)
+        self._buf = bytearray()      # bytes not yet yielded
+        self._base = 0               # absolute offset of _buf[0]
+        self._cuts: list = []
+        self._eof = False
+        self._finished = False
+
+    def __iter__(self) -> Iterator[bytes]:
+        return self
+
+    def _fill(self) -> None:
+        while not self._cuts and not self._eof:
+            data = _read(self._reader, READ_SIZE)
+            if not data:
+                self._eof = True
+            self._buf += data
+            self._cuts.extend(int(c) for c in self._stream.feed(data, self._eof))
+
+    def __next__(self) -> bytes:
+        if self._finished:
+            raise StopIteration
+        try:
+            self._fill()
+        except RusticError:
+            self._finished = True
+            raise
+        if not self._cuts:
+            self._finished = True
+            self._stream.close()
+            raise StopIteration
+        end = self._cuts.pop(0)
+        k = end - self._base
+        chunk = bytes(self._buf[:k])
+        del self._buf[:k]
+        self._base = end
+        self.size_hint = max(self.size_hint - len(chunk), 0)
+        return chunk
+
+
+class FixedSizeChunkIter:
+    """fixed_size.rs:41-70 -- cuts every ``size`` bytes (no hashing: host only)."""
+
+    def __init__(self, size: int, reader, size_hint: int = 0):
+        self._size = size
+        self._reader = reader
+        self.size_hint = size_hint
+        self._finished = False
+
+    def __iter__(self):
+        return self
+
+    def __next__(self) -> bytes:
+        if self._finished:
+            raise StopIteration
+        out = bytearray()
+        while len(out) < self._size:
+            try:
+                b = _read(self._reader, self._size - len(out))
+            except RusticError:
+                self._finished = True
+                raise
+            if not b:
+                break
+            out += b
+        if len(out) < self._size:
+            self._finished = True
+        if not out:
+            raise StopIteration
+        self.size_hint = max(self.size_hint - len(out), 0)
+        return bytes(out)
+
+
+class ChunkIter:
+    """chunker.rs:16-59 -- dispatch on ``ConfigFile.chunker``."""
+
+    @staticmethod
+    def from_config(config: ConfigFile, reader, size_hint: int = 0,
+                    device: Optional[int] = None):
+        if isinstance(reader, (bytes, bytearray, memoryview)):
+            reader = io.BytesIO(bytes(reader))
+        if config.get_chunker() == Chunker.Rabin:
+            poly = config.poly()
+            check_rabin_params(config.chunk_size(), config.chunk_min_size(),
+                               config.chunk_max_size())
+            ctx = Context.get(poly, config.chunk_min_size(), config.chunk_size(),
+                              config.chunk_max_size(), device)
+            return RabinChunkIter(ctx, reader, size_hint)
+        return FixedSizeChunkIter(config.chunk_size(), reader, size_hint)
+
+
+def fixed_cuts(n: int, size: int) -> np.ndarray:
+    """Cut offsets of the FixedSize chunker via the C ABI (rcdc_fixed_cuts)."""
+    cap = n // max(size, 1) + 1
+    cuts = np.zeros(max(cap, 1), dtype=np.uint64)
+    k = _lib.lib().rcdc_fixed_cuts(n, size, cuts.ctypes.data, cap)
+    return cuts[:k]

@@ -1,0 +1,67 @@
+// rcdc_internal.h -- types shared by the HIP kernels and the host runtime.
+//
+// Data layout in HBM (see DESIGN.md "Data layout"):
+//   arena      : caller's bytes; stream i = arena[off_i, off_i + N_i)
+//   ScanItem[] : one per 64 consecutive segments of one stream (one wave)
+//   Summary[]  : one uint4 per segment {first, last, count, 0}; first/last
+//                are positions relative to the segment's first position,
+//                0xFFFFFFFF = no candidate
+//   item_mask[]: one u64 per ScanItem, bit l = segment l has a candidate
+//   StreamDesc[]: resolver input per stream; cuts[] / counts[] its output
+#pragma once
+#include <stdint.h>
+
+namespace rcdc {
+
+constexpr uint32_t kNone = 0xFFFFFFFFu;
+constexpr int kWindow = 64;          // Rabin64::new_with_polynom(6, ..) -> 2^6
+constexpr int kScanThreads = 1024;   // 16 waves; one workgroup per CU
+constexpr int kScanWaves = kScanThreads / 64;
+constexpr int kTableRepl = 32;       // per-lane table copies: bank = lane % 32
+constexpr uint32_t kTableBytes = 256u * kTableRepl * 8u;  // 64 KiB per table
+constexpr uint32_t kLdsBytes = 2u * kTableBytes;          // OUT + MOD
+constexpr uint32_t kUnit = 64;       // bytes per register unit (16 dwords)
+
+// One wave of work: segments [sum_idx, sum_idx + nvalid) of one stream.
+// Lane l scans bytes [q0 + l*S, q0 + l*S + 64 + S) of the arena and tests
+// stream-relative positions pos0 + l*S + r, r in [0, S).
+struct ScanItem {
+    uint64_t q0;        // arena byte offset of lane 0's first byte (16-aligned)
+    uint64_t pos0;      // stream position tested at r = 0 by lane 0
+    uint64_t lo, hi;    // positions that matter: [lo, hi)
+    uint64_t sum_idx;   // summary index of lane 0
+    uint64_t rec_bytes; // buffer-descriptor range from q0 (<= 2^32 - 1)
+    uint32_t nvalid;    // lanes with a segment (1..64)
+    uint32_t stream;
+    uint64_t pad;
+};
+static_assert(sizeof(ScanItem) == 64, "ScanItem is 64 B");
+
+struct StreamDesc {
+    uint64_t off;       // arena offset of byte 0
+    uint64_t n;         // stream length
+    uint64_t pos0;      // position of segment 0, r = 0
+    uint64_t sum_base;  // summary index of segment 0
+    uint64_t item_base; // item index of segment 0's item
+    uint64_t nseg;      // segments of this stream
+    uint64_t cut_base;  // first output slot
+    uint64_t cut_cap;   // output slots
+};
+static_assert(sizeof(StreamDesc) == 64, "StreamDesc is 64 B");
+
+struct ScanParams {
+    uint32_t seg_bytes;  // S, multiple of 64
+    uint32_t mask;       // avg - 1 (avg <= 2^32)
+    uint32_t idx_shift;  // deg - 32: top-byte index from the high word
+    uint32_t pad;
+};
+
+struct ResolveParams {
+    uint64_t min_size, max_size;
+    uint32_t seg_bytes;
+    uint32_t mask;
+    uint32_t shift;  // deg - 8
+    uint32_t pad;
+};
+
+}  // namespace rcdc

@@ -1,0 +1,605 @@
+// rcdc_runtime.cpp -- host runtime behind include/rcdc.h.
+//
+// Owns the device (tables, work lists, summaries, cut lists, pinned staging)
+// and maps the reference's chunker surface onto the two kernels:
+//   rcdc_check_params  <- crates/core/src/chunker/rabin.rs:17-42
+//   rcdc_parse_poly    <- crates/core/src/repofile/configfile.rs:165-175
+//   rcdc_ctx_create    <- crates/core/src/chunker.rs:29-38 (Rabin64 tables once)
+//   rcdc_chunk_batch   <- per-file parallel ChunkIter (archiver.rs:195)
+//   rcdc_stream_*      <- one ChunkIter over a Read (rabin.rs:110-191)
+//   rcdc_plan_*        <- device-resident batches (the measured path)
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cerrno>
+#include <cstdarg>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/rcdc.h"
+#include "rcdc_internal.h"
+
+namespace rcdc {
+hipError_t launch_scan(const uint8_t *arena, const ScanItem *items, uint32_t nitems,
+                       const uint64_t *gtab, const ScanParams &prm, uint4 *sums,
+                       uint64_t *item_masks, uint32_t blocks, hipStream_t stream);
+hipError_t launch_resolve(const uint8_t *arena, const StreamDesc *sds, uint32_t nstreams,
+                          const uint64_t *gtab, const ResolveParams &prm, const uint4 *sums,
+                          const uint64_t *item_masks, uint64_t *cuts, uint64_t *counts,
+                          hipStream_t stream);
+}  // namespace rcdc
+
+using namespace rcdc;
+
+// ---------------------------------------------------------------------------
+// errors
+// ---------------------------------------------------------------------------
+namespace {
+thread_local std::string g_err;
+
+rcdc_status fail(rcdc_status st, const char *fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    g_err = buf;
+    return st;
+}
+
+#define HIP_TRY(expr)                                                                   \
+    do {                                                                                \
+        hipError_t e_ = (expr);                                                         \
+        if (e_ != hipSuccess)                                                           \
+            return fail(RCDC_ERR_INTERNAL, "%s failed: %s", #expr, hipGetErrorString(e_)); \
+    } while (0)
+
+// ---------------------------------------------------------------------------
+// GF(2) polynomial arithmetic for the Rabin64 tables (rustic_cdc Polynom64)
+// ---------------------------------------------------------------------------
+int poly_degree(uint64_t p) { return p ? 63 - __builtin_clzll(p) : -1; }
+
+uint64_t poly_mod(uint64_t p, uint64_t m) {
+    const int dm = poly_degree(m);
+    while (p) {
+        const int dp = poly_degree(p);
+        if (dp < dm) break;
+        p ^= m << (dp - dm);
+    }
+    return p;
+}
+
+// Device table image: [0,256) out[b] << 8, [256,512) mod[i]
+// out[b] = b * x^(8*63) mod P;  mod[i] = ((i << deg) mod P) | (i << deg).
+void build_tables(uint64_t poly, uint64_t *img) {
+    const int deg = poly_degree(poly);
+    for (uint64_t b = 0; b < 256; b++) {
+        uint64_t h = poly_mod(b, poly);
+        for (int i = 0; i < kWindow - 1; i++) h = poly_mod(h << 8, poly);
+        img[b] = h << 8;
+        const uint64_t p = b << deg;
+        img[256 + b] = poly_mod(p, poly) | p;
+    }
+}
+
+uint64_t round_up(uint64_t x, uint64_t a) { return (x + a - 1) / a * a; }
+}  // namespace
+
+// ---------------------------------------------------------------------------
+// context / plan objects
+// ---------------------------------------------------------------------------
+struct rcdc_plan {
+    rcdc_ctx *ctx = nullptr;
+    uint32_t n = 0;
+    uint64_t arena_len = 0;
+    uint32_t seg_bytes = 0;
+    uint32_t blocks = 0;
+    uint64_t nseg = 0, ncuts = 0, scanned = 0;
+    std::vector<ScanItem> items;
+    std::vector<StreamDesc> sds;
+    std::vector<uint64_t> cut_base;
+    // device
+    ScanItem *d_items = nullptr;
+    StreamDesc *d_sds = nullptr;
+    uint4 *d_sums = nullptr;
+    uint64_t *d_masks = nullptr;
+    uint64_t *d_cuts = nullptr;
+    uint64_t *d_counts = nullptr;
+    uint64_t cap_items = 0, cap_sds = 0, cap_sums = 0, cap_cuts = 0, cap_masks = 0,
+             cap_counts = 0;
+    hipEvent_t done = nullptr;
+    bool ran = false;
+};
+
+struct rcdc_ctx {
+    int device = 0;
+    uint64_t poly = 0, min = 0, avg = 0, max = 0;
+    int deg = 0;
+    int num_cus = 0;
+    hipStream_t stream = nullptr;
+    uint64_t *d_tables = nullptr;
+    std::mutex mu;
+    // host-buffer batch path
+    uint8_t *pinned = nullptr;
+    uint64_t pinned_cap = 0;
+    uint8_t *d_arena = nullptr;
+    uint64_t arena_cap = 0;
+    rcdc_plan *batch_plan = nullptr;
+};
+
+struct rcdc_stream {
+    rcdc_ctx *ctx = nullptr;
+    std::vector<uint8_t> pending;  // bytes from the current chunk start
+    uint64_t base = 0;             // absolute offset of pending[0]
+    bool done = false;
+    rcdc_plan *plan = nullptr;
+};
+
+namespace {
+
+struct DeviceGuard {
+    int prev = 0;
+    explicit DeviceGuard(int dev) {
+        (void)hipGetDevice(&prev);
+        (void)hipSetDevice(dev);
+    }
+    ~DeviceGuard() { (void)hipSetDevice(prev); }
+};
+
+template <typename T>
+rcdc_status ensure_dev(T **p, uint64_t *cap, uint64_t need) {
+    if (need <= *cap && *p) return RCDC_OK;
+    if (*p) HIP_TRY(hipFree(*p));
+    *p = nullptr;
+    *cap = 0;
+    const uint64_t n = std::max<uint64_t>(need, 1);
+    HIP_TRY(hipMalloc((void **)p, n * sizeof(T)));
+    *cap = n;
+    return RCDC_OK;
+}
+
+// Choose the per-lane segment S so that a batch covers the chip once:
+// roughly (scanned bytes) / (CUs * 1024 lanes), 512 <= S <= 4096.
+uint32_t choose_segment(uint64_t scanned, int cus) {
+    const uint64_t lanes = (uint64_t)std::max(cus, 1) * kScanThreads;
+    uint64_t s = round_up((scanned + lanes - 1) / lanes, kUnit);
+    return (uint32_t)std::min<uint64_t>(std::max<uint64_t>(s, 512), 4096);
+}
+
+rcdc_status plan_build(rcdc_ctx *ctx, rcdc_plan *pl, const uint64_t *offs, const uint64_t *lens,
+                       uint32_t n, uint64_t arena_len) {
+    const uint64_t pos_lo = ctx->min + kWindow;  // first pure-window test position
+    pl->ctx = ctx;
+    pl->n = n;
+    pl->arena_len = arena_len;
+    uint64_t scanned = 0;
+    for (uint32_t i = 0; i < n; i++) {
+        if (offs[i] > arena_len || lens[i] > arena_len - offs[i])
+            return fail(RCDC_ERR_INVALID_INPUT, "stream %u [%llu,+%llu) outside arena of %llu B", i,
+                        (unsigned long long)offs[i], (unsigned long long)lens[i],
+                        (unsigned long long)arena_len);
+        if (lens[i] > pos_lo) scanned += lens[i] - pos_lo + kWindow;
+    }
+    const uint32_t S = choose_segment(scanned, ctx->num_cus);
+    pl->seg_bytes = S;
+    pl->items.clear();
+    pl->sds.assign(n, StreamDesc{});
+    pl->cut_base.assign(n, 0);
+    uint64_t nseg = 0, ncut = 0;
+    pl->scanned = 0;
+    for (uint32_t i = 0; i < n; i++) {
+        StreamDesc &d = pl->sds[i];
+        const uint64_t N = lens[i], off = offs[i];
+        d.off = off;
+        d.n = N;
+        d.cut_base = ncut;
+        d.cut_cap = N / ctx->min + 1;
+        pl->cut_base[i] = ncut;
+        ncut += d.cut_cap;
+        d.sum_base = nseg;
+        d.item_base = pl->items.size();
+        if (N <= pos_lo) continue;
+        // lane start q (arena offset) 16-aligned; tests positions q+65 ..
+        const uint64_t q0 = (off + pos_lo - 65) & ~(uint64_t)15;
+        const uint64_t p0 = q0 - off + 65;
+        const uint64_t segs = (N - p0 + S - 1) / S;
+        d.pos0 = p0;
+        d.nseg = segs;
+        pl->scanned += segs * (uint64_t)S;
+        for (uint64_t j = 0; j < segs; j += 64) {
+            ScanItem it{};
+            it.q0 = q0 + j * S;
+            it.pos0 = p0 + j * S;
+            it.lo = pos_lo;
+            it.hi = N;
+            it.sum_idx = nseg + j;
+            const uint64_t rest = arena_len > it.q0 ? arena_len - it.q0 : 0;
+            it.rec_bytes = std::min<uint64_t>(rest, 0xFFFFFFFFull);
+            it.nvalid = (uint32_t)std::min<uint64_t>(64, segs - j);
+            it.stream = i;
+            pl->items.push_back(it);
+        }
+        nseg += segs;
+    }
+    pl->nseg = nseg;
+    pl->ncuts = ncut;
+    const uint64_t waves_needed = (pl->items.size() + kScanWaves - 1) / kScanWaves;
+    pl->blocks = (uint32_t)std::min<uint64_t>(waves_needed, (uint64_t)std::max(ctx->num_cus, 1));
+
+    DeviceGuard g(ctx->device);
+    rcdc_status st;
+    if ((st = ensure_dev(&pl->d_items, &pl->cap_items, pl->items.size()))) return st;
+    if ((st = ensure_dev(&pl->d_sds, &pl->cap_sds, n))) return st;
+    if ((st = ensure_dev(&pl->d_sums, &pl->cap_sums, nseg))) return st;
+    if ((st = ensure_dev(&pl->d_masks, &pl->cap_masks, pl->items.size()))) return st;
+    if ((st = ensure_dev(&pl->d_cuts, &pl->cap_cuts, ncut))) return st;
+    if ((st = ensure_dev(&pl->d_counts, &pl->cap_counts, n))) return st;
+    if (!pl->items.empty())
+        HIP_TRY(hipMemcpy(pl->d_items, pl->items.data(), pl->items.size() * sizeof(ScanItem),
+                          hipMemcpyHostToDevice));
+    if (n)
+        HIP_TRY(hipMemcpy(pl->d_sds, pl->sds.data(), n * sizeof(StreamDesc),
+                          hipMemcpyHostToDevice));
+    if (!pl->done) HIP_TRY(hipEventCreateWithFlags(&pl->done, hipEventDisableTiming));
+    pl->ran = false;
+    return RCDC_OK;
+}
+
+rcdc_status plan_run(rcdc_plan *pl, const void *d_arena, hipStream_t stream) {
+    rcdc_ctx *ctx = pl->ctx;
+    if (((uintptr_t)d_arena & 255u) != 0)
+        return fail(RCDC_ERR_INVALID_INPUT, "device arena %p is not 256-byte aligned", d_arena);
+    if (!stream) stream = ctx->stream;
+    DeviceGuard g(ctx->device);
+    ScanParams sp{};
+    sp.seg_bytes = pl->seg_bytes;
+    sp.mask = (uint32_t)(ctx->avg - 1);
+    sp.idx_shift = (uint32_t)(ctx->deg - 32);
+    HIP_TRY(launch_scan((const uint8_t *)d_arena, pl->d_items, (uint32_t)pl->items.size(),
+                        ctx->d_tables, sp, pl->d_sums, pl->d_masks, pl->blocks, stream));
+    ResolveParams rp{};
+    rp.min_size = ctx->min;
+    rp.max_size = ctx->max;
+    rp.seg_bytes = pl->seg_bytes;
+    rp.mask = (uint32_t)(ctx->avg - 1);
+    rp.shift = (uint32_t)(ctx->deg - 8);
+    HIP_TRY(launch_resolve((const uint8_t *)d_arena, pl->d_sds, pl->n, ctx->d_tables, rp,
+                           pl->d_sums, pl->d_masks, pl->d_cuts, pl->d_counts, stream));
+    HIP_TRY(hipEventRecord(pl->done, stream));
+    pl->ran = true;
+    return RCDC_OK;
+}
+
+rcdc_status plan_results(rcdc_plan *pl, uint64_t *cuts, uint64_t cap, uint64_t *counts) {
+    if (!pl->ran) return fail(RCDC_ERR_INVALID_INPUT, "plan has not been run");
+    DeviceGuard g(pl->ctx->device);
+    HIP_TRY(hipEventSynchronize(pl->done));
+    std::vector<uint64_t> cnt(pl->n);
+    if (pl->n)
+        HIP_TRY(hipMemcpy(cnt.data(), pl->d_counts, pl->n * 8, hipMemcpyDeviceToHost));
+    uint64_t total = 0;
+    for (uint32_t i = 0; i < pl->n; i++) {
+        if (cnt[i] > pl->sds[i].cut_cap)
+            return fail(RCDC_ERR_INTERNAL, "stream %u produced %llu cuts > bound %llu", i,
+                        (unsigned long long)cnt[i], (unsigned long long)pl->sds[i].cut_cap);
+        counts[i] = cnt[i];
+        total += cnt[i];
+    }
+    if (total > cap) return fail(RCDC_ERR_CAPACITY, "need %llu cut slots, have %llu",
+                                 (unsigned long long)total, (unsigned long long)cap);
+    std::vector<uint64_t> all(pl->ncuts);
+    if (pl->ncuts)
+        HIP_TRY(hipMemcpy(all.data(), pl->d_cuts, pl->ncuts * 8, hipMemcpyDeviceToHost));
+    uint64_t o = 0;
+    for (uint32_t i = 0; i < pl->n; i++) {
+        memcpy(cuts + o, all.data() + pl->cut_base[i], cnt[i] * 8);
+        o += cnt[i];
+    }
+    return RCDC_OK;
+}
+
+void plan_free(rcdc_plan *pl) {
+    if (!pl) return;
+    DeviceGuard g(pl->ctx ? pl->ctx->device : 0);
+    (void)hipFree(pl->d_items);
+    (void)hipFree(pl->d_sds);
+    (void)hipFree(pl->d_sums);
+    (void)hipFree(pl->d_masks);
+    (void)hipFree(pl->d_cuts);
+    (void)hipFree(pl->d_counts);
+    if (pl->done) (void)hipEventDestroy(pl->done);
+    delete pl;
+}
+
+// Host bytes -> (pinned staging) -> device arena -> plan -> cuts.
+rcdc_status run_host_batch(rcdc_ctx *ctx, rcdc_plan **cache, const rcdc_buf *bufs, uint32_t n,
+                           uint64_t *cuts, uint64_t cap, uint64_t *counts) {
+    std::vector<uint64_t> offs(n), lens(n);
+    uint64_t total = 0;
+    for (uint32_t i = 0; i < n; i++) {
+        offs[i] = total;
+        lens[i] = bufs[i].len;
+        total = round_up(total + bufs[i].len, 256);
+    }
+    const uint64_t arena_len = total + 256;
+    DeviceGuard g(ctx->device);
+    if (arena_len > ctx->pinned_cap) {
+        if (ctx->pinned) HIP_TRY(hipHostFree(ctx->pinned));
+        ctx->pinned = nullptr;
+        ctx->pinned_cap = 0;
+        HIP_TRY(hipHostMalloc((void **)&ctx->pinned, arena_len, hipHostMallocDefault));
+        ctx->pinned_cap = arena_len;
+    }
+    rcdc_status st;
+    if ((st = ensure_dev(&ctx->d_arena, &ctx->arena_cap, arena_len))) return st;
+    for (uint32_t i = 0; i < n; i++) {
+        if (bufs[i].len && !bufs[i].data)
+            return fail(RCDC_ERR_INVALID_INPUT, "buffer %u is NULL with length %llu", i,
+                        (unsigned long long)bufs[i].len);
+        if (bufs[i].len) memcpy(ctx->pinned + offs[i], bufs[i].data, bufs[i].len);
+    }
+    HIP_TRY(hipMemcpyAsync(ctx->d_arena, ctx->pinned, arena_len, hipMemcpyHostToDevice,
+                           ctx->stream));
+    if (!*cache) *cache = new rcdc_plan();
+    if ((st = plan_build(ctx, *cache, offs.data(), lens.data(), n, arena_len))) return st;
+    if ((st = plan_run(*cache, ctx->d_arena, ctx->stream))) return st;
+    return plan_results(*cache, cuts, cap, counts);
+}
+
+bool valid_ctx(const rcdc_ctx *c) { return c != nullptr; }
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
+// C ABI
+// ---------------------------------------------------------------------------
+extern "C" {
+
+uint32_t rcdc_abi_version(void) { return RCDC_ABI_VERSION; }
+
+const char *rcdc_last_error(void) { return g_err.c_str(); }
+
+rcdc_status rcdc_check_params(uint64_t avg, uint64_t min, uint64_t max) {
+    // rabin.rs:21-40, same order and same ErrorKind
+    if (avg == 0 || (avg & (avg - 1)) != 0)
+        return fail(RCDC_ERR_UNSUPPORTED,
+                    "Chunk size must be a power of 2 for the rabin chunker. chunk size = %llu.",
+                    (unsigned long long)avg);
+    if (min > avg)
+        return fail(RCDC_ERR_UNSUPPORTED,
+                    "Chunk min size must be smaller or equal than the chunk size.");
+    if (max < avg)
+        return fail(RCDC_ERR_UNSUPPORTED,
+                    "Chunk max size must be larger or equal than the chunk size.");
+    if (min < (uint64_t)kWindow)
+        return fail(RCDC_ERR_UNSUPPORTED, "Chunk min size must be at least 64 bytes (window).");
+    if (avg > (1ull << 32) || max > (1ull << 40))
+        return fail(RCDC_ERR_UNSUPPORTED, "chunk size > 4 GiB or max size > 1 TiB");
+    return RCDC_OK;
+}
+
+rcdc_status rcdc_parse_poly(const char *hex, uint64_t *poly) {
+    // u64::from_str_radix(s, 16): optional leading '+', hex digits only, no
+    // prefix, no whitespace, non-empty, must fit in 64 bits.
+    if (!hex || !poly) return fail(RCDC_ERR_INVALID_INPUT, "null argument");
+    const char *p = hex;
+    if (*p == '+') p++;
+    if (!*p)
+        return fail(RCDC_ERR_INVALID_INPUT,
+                    "Parsing u64 from hex failed for polynomial `%s`, the value must be a valid "
+                    "hexadecimal string.", hex);
+    uint64_t v = 0;
+    for (; *p; p++) {
+        int d;
+        if (*p >= '0' && *p <= '9') d = *p - '0';
+        else if (*p >= 'a' && *p <= 'f') d = *p - 'a' + 10;
+        else if (*p >= 'A' && *p <= 'F') d = *p - 'A' + 10;
+        else
+            return fail(RCDC_ERR_INVALID_INPUT,
+                        "Parsing u64 from hex failed for polynomial `%s`, the value must be a "
+                        "valid hexadecimal string.", hex);
+        if (v >> 60)
+            return fail(RCDC_ERR_INVALID_INPUT,
+                        "Parsing u64 from hex failed for polynomial `%s`, the value must be a "
+                        "valid hexadecimal string.", hex);
+        v = (v << 4) | (uint64_t)d;
+    }
+    *poly = v;
+    return RCDC_OK;
+}
+
+rcdc_status rcdc_ctx_create(uint64_t poly, uint64_t min, uint64_t avg_pow2, uint64_t max,
+                            int device, rcdc_ctx **out) {
+    if (!out) return fail(RCDC_ERR_INVALID_INPUT, "out is NULL");
+    *out = nullptr;
+    rcdc_status st = rcdc_check_params(avg_pow2, min, max);
+    if (st) return st;
+    const int deg = poly_degree(poly);
+    if (deg < 33 || deg > 56)
+        return fail(RCDC_ERR_UNSUPPORTED, "polynomial %#llx has degree %d; supported 33..56",
+                    (unsigned long long)poly, deg);
+    int ndev = 0;
+    HIP_TRY(hipGetDeviceCount(&ndev));
+    if (device < 0 || device >= ndev)
+        return fail(RCDC_ERR_INVALID_INPUT, "device %d not present (%d devices)", device, ndev);
+    rcdc_ctx *c = new rcdc_ctx();
+    c->device = device;
+    c->poly = poly;
+    c->min = min;
+    c->avg = avg_pow2;
+    c->max = max;
+    c->deg = deg;
+    DeviceGuard g(device);
+    hipDeviceProp_t prop;
+    hipError_t e = hipGetDeviceProperties(&prop, device);
+    if (e != hipSuccess) {
+        delete c;
+        return fail(RCDC_ERR_INTERNAL, "hipGetDeviceProperties: %s", hipGetErrorString(e));
+    }
+    c->num_cus = prop.multiProcessorCount;
+    uint64_t img[512];
+    build_tables(poly, img);
+    if ((e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking)) != hipSuccess ||
+        (e = hipMalloc((void **)&c->d_tables, sizeof img)) != hipSuccess ||
+        (e = hipMemcpy(c->d_tables, img, sizeof img, hipMemcpyHostToDevice)) != hipSuccess) {
+        rcdc_ctx_destroy(c);
+        return fail(RCDC_ERR_INTERNAL, "context setup: %s", hipGetErrorString(e));
+    }
+    *out = c;
+    return RCDC_OK;
+}
+
+void rcdc_ctx_destroy(rcdc_ctx *c) {
+    if (!c) return;
+    {
+        DeviceGuard g(c->device);
+        if (c->stream) (void)hipStreamSynchronize(c->stream);
+        plan_free(c->batch_plan);
+        (void)hipFree(c->d_tables);
+        (void)hipFree(c->d_arena);
+        if (c->pinned) (void)hipHostFree(c->pinned);
+        if (c->stream) (void)hipStreamDestroy(c->stream);
+    }
+    delete c;
+}
+
+uint64_t rcdc_max_cuts(const rcdc_ctx *c, uint64_t n) { return c ? n / c->min + 1 : 0; }
+
+rcdc_status rcdc_chunk_batch(rcdc_ctx *ctx, const rcdc_buf *bufs, uint32_t n, uint64_t *cuts,
+                             uint64_t cuts_cap, uint64_t *cut_counts) {
+    if (!valid_ctx(ctx)) return fail(RCDC_ERR_INVALID_INPUT, "ctx is NULL");
+    if (n && (!bufs || !cut_counts)) return fail(RCDC_ERR_INVALID_INPUT, "null argument");
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    return run_host_batch(ctx, &ctx->batch_plan, bufs, n, cuts, cuts_cap, cut_counts);
+}
+
+rcdc_status rcdc_plan_create(rcdc_ctx *ctx, const uint64_t *offs, const uint64_t *lens,
+                             uint32_t n, uint64_t arena_len, rcdc_plan **out) {
+    if (!valid_ctx(ctx) || !out || (n && (!offs || !lens)))
+        return fail(RCDC_ERR_INVALID_INPUT, "null argument");
+    rcdc_plan *pl = new rcdc_plan();
+    rcdc_status st = plan_build(ctx, pl, offs, lens, n, arena_len);
+    if (st) {
+        plan_free(pl);
+        return st;
+    }
+    *out = pl;
+    return RCDC_OK;
+}
+
+void rcdc_plan_destroy(rcdc_plan *plan) { plan_free(plan); }
+
+rcdc_status rcdc_plan_run(rcdc_plan *plan, const void *d_arena, void *hip_stream) {
+    if (!plan || (!d_arena && plan->arena_len))
+        return fail(RCDC_ERR_INVALID_INPUT, "null argument");
+    return plan_run(plan, d_arena, (hipStream_t)hip_stream);
+}
+
+rcdc_status rcdc_plan_results(rcdc_plan *plan, uint64_t *cuts, uint64_t cuts_cap,
+                              uint64_t *cut_counts) {
+    if (!plan || (plan->n && !cut_counts)) return fail(RCDC_ERR_INVALID_INPUT, "null argument");
+    return plan_results(plan, cuts, cuts_cap, cut_counts);
+}
+
+rcdc_status rcdc_plan_device_results(rcdc_plan *plan, uint64_t *d_cuts, uint64_t *d_counts,
+                                     const uint64_t **cut_base) {
+    if (!plan || !d_cuts || !d_counts || !cut_base)
+        return fail(RCDC_ERR_INVALID_INPUT, "null argument");
+    *d_cuts = (uint64_t)(uintptr_t)plan->d_cuts;
+    *d_counts = (uint64_t)(uintptr_t)plan->d_counts;
+    *cut_base = plan->cut_base.data();
+    return RCDC_OK;
+}
+
+rcdc_status rcdc_plan_get_info(const rcdc_plan *plan, rcdc_plan_info *info) {
+    if (!plan || !info) return fail(RCDC_ERR_INVALID_INPUT, "null argument");
+    info->scanned_bytes = plan->scanned;
+    info->segments = plan->nseg;
+    info->segment_bytes = plan->seg_bytes;
+    info->work_items = (uint32_t)plan->items.size();
+    info->scan_blocks = plan->blocks;
+    info->reserved = 0;
+    return RCDC_OK;
+}
+
+uint64_t rcdc_fixed_cuts(uint64_t n, uint64_t size, uint64_t *cuts, uint64_t cap) {
+    // fixed_size.rs:41-70: `take(size).read_to_end`, short final chunk, none if empty
+    if (size == 0) return 0;
+    uint64_t k = 0;
+    for (uint64_t s = 0; s < n;) {
+        const uint64_t e = (n - s < size) ? n : s + size;
+        if (k < cap) cuts[k] = e;
+        k++;
+        s = e;
+    }
+    return k;
+}
+
+// ---- streaming: one file fed in pieces -------------------------------------
+
+rcdc_status rcdc_stream_open(rcdc_ctx *ctx, rcdc_stream **out) {
+    if (!valid_ctx(ctx) || !out) return fail(RCDC_ERR_INVALID_INPUT, "null argument");
+    rcdc_stream *s = new rcdc_stream();
+    s->ctx = ctx;
+    *out = s;
+    return RCDC_OK;
+}
+
+void rcdc_stream_close(rcdc_stream *st) {
+    if (!st) return;
+    plan_free(st->plan);
+    delete st;
+}
+
+rcdc_status rcdc_stream_feed(rcdc_stream *st, const uint8_t *data, uint64_t len, int is_final,
+                             uint64_t *cuts, uint64_t cap, uint64_t *n_cuts) {
+    if (!st || !n_cuts || (len && !data)) return fail(RCDC_ERR_INVALID_INPUT, "null argument");
+    *n_cuts = 0;
+    if (st->done) {
+        if (len) return fail(RCDC_ERR_INVALID_INPUT, "stream already finished");
+        return RCDC_OK;
+    }
+    rcdc_ctx *ctx = st->ctx;
+    st->pending.insert(st->pending.end(), data, data + len);
+    // Process once enough bytes are buffered that a cut is guaranteed
+    // (every chunk ends by chunk start + max), or at EOF.
+    const uint64_t batch = std::max<uint64_t>(64ull << 20, 2 * ctx->max + 256);
+    if (!is_final && st->pending.size() < batch) return RCDC_OK;
+
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    // One device pass over everything buffered: every cut except the one at
+    // the end of the buffer depends only on bytes before it, so it is final;
+    // the end-of-buffer cut is final only at EOF.  The unfinished tail
+    // (< max bytes, from the last final cut) is re-chunked with more data.
+    uint64_t produced = 0;
+    const uint64_t N = st->pending.size();
+    if (N) {
+        std::vector<uint64_t> tmp(rcdc_max_cuts(ctx, N));
+        rcdc_buf b{st->pending.data(), N};
+        uint64_t cnt = 0;
+        rcdc_status s2 = run_host_batch(ctx, &st->plan, &b, 1, tmp.data(), tmp.size(), &cnt);
+        if (s2) return s2;
+        uint64_t keep = cnt;
+        if (!is_final && cnt && tmp[cnt - 1] == N) keep = cnt - 1;
+        if (keep > cap)
+            return fail(RCDC_ERR_CAPACITY, "need %llu cut slots, have %llu",
+                        (unsigned long long)keep, (unsigned long long)cap);
+        for (uint64_t i = 0; i < keep; i++) cuts[i] = st->base + tmp[i];
+        produced = keep;
+        const uint64_t consumed = keep ? tmp[keep - 1] : 0;
+        st->pending.erase(st->pending.begin(), st->pending.begin() + (long)consumed);
+        st->base += consumed;
+    }
+    if (is_final) {
+        st->pending.clear();
+        st->done = true;
+    }
+    *n_cuts = produced;
+    return RCDC_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,102 @@
+"""Device-resident batches: the measured hot path (rcdc_plan_* in include/rcdc.h).
+
+A batch is a set of independent streams laid out in one device arena (a torch
+``uint8`` CUDA tensor, i.e. HIP memory on ROCm).  ``DevicePlan`` fixes the
+layout once (work lists, summaries and cut slots live in HBM) and ``run()``
+enqueues the scan and resolve kernels on a HIP stream.  torch is only the
+allocator / stream provider here; the C ABI sees plain pointers.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Optional, Sequence
+
+import numpy as np
+
+from . import _lib
+from .chunker import Context
+from .errors import status_error
+
+
+def align_up(x: int, a: int = 256) -> int:
+    return (x + a - 1) // a * a
+
+
+def pack_offsets(lens: Sequence[int], align: int = 256):
+    """Offsets of streams packed back to back (each ``align``-aligned)."""
+    offs, o = [], 0
+    for n in lens:
+        offs.append(o)
+        o = align_up(o + int(n), align)
+    return np.array(offs, dtype=np.uint64), o + align
+
+
+class DevicePlan:
+    def __init__(self, ctx: Context, offs, lens, arena_len: int):
+        self.ctx = ctx
+        self.offs = np.ascontiguousarray(offs, dtype=np.uint64)
+        self.lens = np.ascontiguousarray(lens, dtype=np.uint64)
+        self.n = int(self.lens.size)
+        self.arena_len = int(arena_len)
+        h = ctypes.c_void_p()
+        st = _lib.lib().rcdc_plan_create(ctx.handle, self.offs.ctypes.data,
+                                         self.lens.ctypes.data, self.n, self.arena_len,
+                                         ctypes.byref(h))
+        if st:
+            raise status_error(st, _lib.last_error())
+        self._h = h
+        self.cap = sum(ctx.max_cuts(int(n)) for n in self.lens)
+
+    def info(self) -> dict:
+        inf = _lib.PlanInfo()
+        st = _lib.lib().rcdc_plan_get_info(self._h, ctypes.byref(inf))
+        if st:
+            raise status_error(st, _lib.last_error())
+        return {k: getattr(inf, k) for k, _ in _lib.PlanInfo._fields_ if k != "reserved"}
+
+    def run(self, d_arena_ptr: int, hip_stream: Optional[int] = None) -> None:
+        st = _lib.lib().rcdc_plan_run(self._h, ctypes.c_void_p(d_arena_ptr),
+                                      ctypes.c_void_p(hip_stream or 0))
+        if st:
+            raise status_error(st, _lib.last_error())
+
+    def results(self) -> list:
+        cuts = np.zeros(max(self.cap, 1), dtype=np.uint64)
+        counts = np.zeros(max(self.n, 1), dtype=np.uint64)
+        st = _lib.lib().rcdc_plan_results(self._h, cuts.ctypes.data, self.cap,
+                                          counts.ctypes.data)
+        if st:
+            raise status_error(st, _lib.last_error())
+        out, o = [], 0
+        for i in range(self.n):
+            k = int(counts[i])
+            out.append(cuts[o:o + k].copy())
+            o += k
+        return out
+
+    def device_results(self):
+        """(d_cuts_ptr, d_counts_ptr, cut_base[n]) -- raw device pointers."""
+        dc, dn = ctypes.c_uint64(0), ctypes.c_uint64(0)
+        base = ctypes.POINTER(ctypes.c_uint64)()
+        st = _lib.lib().rcdc_plan_device_results(self._h, ctypes.byref(dc), ctypes.byref(dn),
+                                                 ctypes.byref(base))
+        if st:
+            raise status_error(st, _lib.last_error())
+        return dc.value, dn.value, np.ctypeslib.as_array(base, shape=(max(self.n, 1),))[:self.n]
+
+    def close(self):
+        if getattr(self, "_h", None):
+            _lib.lib().rcdc_plan_destroy(self._h)
+            self._h = None
+
+    __del__ = close
+
+
+def chunk_device(ctx: Context, arena_tensor, offs, lens, stream=None) -> list:
+    """One-shot: plan + run + results over a torch CUDA uint8 arena."""
+    plan = DevicePlan(ctx, offs, lens, arena_tensor.numel())
+    plan.run(arena_tensor.data_ptr(), stream)
+    try:
+        return plan.results()
+    finally:
+        plan.close()

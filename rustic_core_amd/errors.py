@@ -1,0 +1,41 @@
+"""Error surface of the chunker, mirroring rustic_core's ``RusticError``.
+
+``ErrorKind`` follows crates/core/src/error.rs:108-124 (only the kinds the
+chunking path can raise); ``status_error`` maps the C ABI's ``rcdc_status``
+(include/rcdc.h) onto it.
+"""
+from __future__ import annotations
+
+import enum
+
+
+class ErrorKind(enum.Enum):
+    Unsupported = "Unsupported"      # rabin.rs:22-40 (check_rabin_params)
+    InvalidInput = "InvalidInput"    # configfile.rs:166-171 (poly hex)
+    Internal = "Internal"            # device / runtime failure
+    InputOutput = "InputOutput"      # rabin.rs:131-138,174-180 (reader errors)
+
+
+class RusticError(Exception):
+    def __init__(self, kind: ErrorKind, message: str):
+        super().__init__(f"{kind.value}: {message}")
+        self.kind = kind
+        self.message = message
+
+
+class CapacityError(RusticError):
+    """The caller's cut buffer was too small (rcdc_status RCDC_ERR_CAPACITY)."""
+
+
+_STATUS = {
+    1: ErrorKind.Unsupported,
+    2: ErrorKind.InvalidInput,
+    3: ErrorKind.Internal,
+    4: ErrorKind.InputOutput,
+}
+
+
+def status_error(status: int, message: str) -> RusticError:
+    if status == 5:
+        return CapacityError(ErrorKind.Internal, message)
+    return RusticError(_STATUS.get(status, ErrorKind.Internal), message)

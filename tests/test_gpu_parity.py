@@ -1,0 +1,224 @@
+"""Device parity: librcdc (HIP, gfx950) vs the CPU oracle and the reference's
+golden snapshots.  Bit-exact cut offsets are the bar (integer work).
+
+Every case runs through the C ABI (rcdc_plan_*, rcdc_chunk_batch,
+rcdc_stream_feed); the oracle is only the checker.
+"""
+import hashlib
+import json
+import os
+
+import numpy as np
+import pytest
+
+from oracle import oracle
+
+pytestmark = pytest.mark.gpu
+
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden", "reference_snapshots.json")
+MiB = 1 << 20
+KiB = 1 << 10
+
+
+def _torch():
+    import torch
+    return torch
+
+
+def _device_cuts(ctx, bufs, offsets=None, align=256):
+    """Chunk host buffers via a device-resident plan; returns per-buffer cuts."""
+    torch = _torch()
+    from rustic_core_amd.device import DevicePlan, pack_offsets
+    lens = [len(b) for b in bufs]
+    if offsets is None:
+        offs, arena_len = pack_offsets(lens, align)
+    else:
+        offs = np.array(offsets, dtype=np.uint64)
+        arena_len = int(max([o + n for o, n in zip(offsets, lens)] + [0])) + 256
+    host = np.zeros(arena_len, dtype=np.uint8)
+    for o, b in zip(offs, bufs):
+        host[int(o):int(o) + len(b)] = np.frombuffer(bytes(b), np.uint8) if not isinstance(
+            b, np.ndarray) else b
+    dev = torch.from_numpy(host).to("cuda:0")
+    plan = DevicePlan(ctx, offs, lens, arena_len)
+    plan.run(dev.data_ptr())
+    out = plan.results()
+    plan.close()
+    return out
+
+
+def _ctx(min_size, avg, max_size, poly=oracle.DEFAULT_POLY):
+    from rustic_core_amd.chunker import Context
+    return Context.get(poly, min_size, avg, max_size, device=0)
+
+
+# ---------------------------------------------------------------- golden pins
+def test_chunk_random_snapshot(gpu_ctx):
+    """rabin.rs:341-358 + chunk_random.snap: all 29 (len, sha256) exact."""
+    from rustic_core_amd import ChunkIter, ConfigFile
+    g = json.load(open(GOLDEN))["rabin_chunk_random"]
+    data = oracle.stdrng_bytes(g["seed"], g["size"]).tobytes()
+    cfg = ConfigFile.new(2, int(g["poly"], 16))
+    chunks = [(len(c), hashlib.sha256(c).hexdigest())
+              for c in ChunkIter.from_config(cfg, data, 0)]
+    assert chunks == [tuple(x) for x in g["chunks"]]
+
+
+def test_chunk_empty(gpu_ctx):
+    """rabin.rs:360-376: empty input -> no chunk, whatever the size hint."""
+    from rustic_core_amd import ChunkIter, ConfigFile
+    cfg = ConfigFile.new(2, oracle.DEFAULT_POLY)
+    assert list(ChunkIter.from_config(cfg, b"", 0)) == []
+    assert list(ChunkIter.from_config(cfg, b"", 100)) == []
+
+
+def test_chunk_zeros(gpu_ctx):
+    """rabin.rs:378-385: zeros -> first chunk is exactly MIN_SIZE."""
+    from rustic_core_amd import ChunkIter, ConfigFile
+    cfg = ConfigFile.new(2, oracle.DEFAULT_POLY)
+    it = ChunkIter.from_config(cfg, bytes(3 * MiB + 12345), 2 ** 63)
+    first = next(it)
+    assert len(first) == 512 * KiB
+    rest = [len(c) for c in it]
+    assert rest == [512 * KiB] * 5 + [12345]
+
+
+# ---------------------------------------------------------------- C2 workload
+def test_c2_random_1mib_buffers(gpu_ctx):
+    """Config #2 sample: 1 MiB random buffers (StdRng seed 1000+i), every cut diffed."""
+    bufs = [oracle.stdrng_bytes(1000 + i, MiB) for i in range(256)]
+    got = _device_cuts(gpu_ctx, bufs)
+    for i, b in enumerate(bufs):
+        assert np.array_equal(got[i], oracle.chunk_cuts(b)), i
+
+
+def test_batch_host_api(gpu_ctx):
+    bufs = [oracle.stdrng_bytes(7 + i, n) for i, n in
+            enumerate([0, 1, 63, 4096, 512 * KiB, 512 * KiB + 64, 512 * KiB + 65, 3 * MiB + 7])]
+    got = gpu_ctx.chunk_batch(bufs)
+    for i, b in enumerate(bufs):
+        assert np.array_equal(got[i], oracle.chunk_cuts(b)), i
+
+
+# ---------------------------------------------------------------- edge sizes
+@pytest.mark.parametrize("n", [0, 1, 64, 4095, 512 * KiB - 1, 512 * KiB, 512 * KiB + 1,
+                               512 * KiB + 63, 512 * KiB + 64, 512 * KiB + 65,
+                               512 * KiB + 200, MiB, 8 * MiB, 8 * MiB + 1, 17 * MiB + 3])
+def test_edge_lengths(gpu_ctx, n):
+    b = oracle.stdrng_bytes(99, n)
+    got = _device_cuts(gpu_ctx, [b])[0]
+    assert np.array_equal(got, oracle.chunk_cuts(b))
+
+
+def test_unaligned_offsets(gpu_ctx):
+    bufs = [oracle.stdrng_bytes(300 + i, MiB + 17 * i) for i in range(6)]
+    offsets, o = [], 0
+    for b in bufs:
+        o += 1 + 37 * len(offsets)
+        offsets.append(o)
+        o += len(b)
+    got = _device_cuts(gpu_ctx, bufs, offsets=offsets)
+    for i, b in enumerate(bufs):
+        assert np.array_equal(got[i], oracle.chunk_cuts(b)), i
+
+
+# ---------------------------------------------------------------- small params
+def _mixed(seed, n, zero_frac=0.5):
+    rng = np.random.default_rng(seed)
+    out = np.empty(n, dtype=np.uint8)
+    i = 0
+    while i < n:
+        k = int(rng.integers(1, 40000))
+        if rng.random() < zero_frac:
+            out[i:i + k] = 0
+        else:
+            out[i:i + k] = rng.integers(0, 256, size=len(out[i:i + k]), dtype=np.uint8)
+        i += k
+    return out
+
+
+@pytest.mark.parametrize("params", [(4096, 8192, 16384), (4096, 4096, 4096),
+                                    (4096, 16384, 65536), (8192, 65536, 1 << 20),
+                                    (64, 256, 1024), (100, 128, 300)])
+@pytest.mark.parametrize("kind", ["random", "zeros", "mixed", "lowent"])
+def test_small_params(params, kind):
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    mn, avg, mx = params
+    ctx = _ctx(mn, avg, mx)
+    n = 3 * MiB + 1234
+    if kind == "random":
+        b = oracle.stdrng_bytes(5, n)
+    elif kind == "zeros":
+        b = np.zeros(n, np.uint8)
+    elif kind == "mixed":
+        b = _mixed(11, n)
+    else:
+        b = np.random.default_rng(3).integers(0, 2, size=n, dtype=np.uint8)
+    got = _device_cuts(ctx, [b, b[:n // 3], b[7:]])
+    for g, x in zip(got, [b, b[:n // 3], b[7:]]):
+        exp = oracle.chunk_cuts(x, min_size=mn, avg=avg, max_size=mx)
+        assert np.array_equal(g, exp)
+
+
+def test_other_polynomial():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    for poly in (0x3DA3358B4DC173 ^ (1 << 20), (1 << 40) | 0x1B, (1 << 56) | 0x95):
+        ctx = _ctx(4096, 8192, 65536, poly)
+        b = oracle.stdrng_bytes(17, 2 * MiB)
+        got = _device_cuts(ctx, [b])[0]
+        exp = oracle.chunk_cuts(b, poly=poly, min_size=4096, avg=8192, max_size=65536)
+        assert np.array_equal(got, exp), hex(poly)
+
+
+# ---------------------------------------------------------------- min-zone (V1)
+def test_min_zone_v1_semantics():
+    """Inputs crafted so that a min-zone position hits under V1 only or A only."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from tests.zone_craft import craft_zone_cases
+    mn, avg, mx = 4096, 1 << 16, 1 << 20
+    ctx = _ctx(mn, avg, mx)
+    cases = craft_zone_cases(mn, avg, count=24)
+    bufs = [c for c, _ in cases]
+    got = _device_cuts(ctx, bufs)
+    n_diff = 0
+    for g, b in zip(got, bufs):
+        v1 = oracle.chunk_cuts(b, min_size=mn, avg=avg, max_size=mx)
+        a = oracle.chunk_cuts(b, min_size=mn, avg=avg, max_size=mx, prefill64=True)
+        n_diff += not np.array_equal(v1, a)
+        assert np.array_equal(g, v1)
+    assert n_diff >= len(bufs) // 2
+
+
+# ---------------------------------------------------------------- streaming
+def test_stream_split_invariance(gpu_ctx):
+    """Cuts do not depend on how the file is split into reads (rabin.rs:162-181)."""
+    from rustic_core_amd.chunker import _Stream
+    b = _mixed(21, 40 * MiB, 0.3)
+    exp = oracle.chunk_cuts(b)
+    rng = np.random.default_rng(5)
+    for trial in range(3):
+        st = _Stream(gpu_ctx)
+        cuts, i = [], 0
+        while i < b.size:
+            k = int(rng.integers(1, 24 * MiB))
+            piece = b[i:i + k].tobytes()
+            i += len(piece)
+            cuts.extend(st.feed(piece, i >= b.size).tolist())
+        if b.size == 0:
+            cuts.extend(st.feed(b"", True).tolist())
+        st.close()
+        assert np.array_equal(np.array(cuts, np.uint64), exp), trial
+
+
+def test_chunkiter_large_mixed(gpu_ctx):
+    from rustic_core_amd import ChunkIter, ConfigFile
+    b = _mixed(8, 70 * MiB, 0.5)
+    cfg = ConfigFile.new(2, oracle.DEFAULT_POLY)
+    lens = [len(c) for c in ChunkIter.from_config(cfg, b.tobytes(), 0)]
+    assert np.array_equal(np.cumsum(lens, dtype=np.uint64), oracle.chunk_cuts(b))
