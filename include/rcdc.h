@@ -146,6 +146,15 @@ typedef struct {
 } rcdc_plan_info;
 rcdc_status rcdc_plan_get_info(const rcdc_plan *plan, rcdc_plan_info *info);
 
+/* Kernel timing (HIP events recorded on the launch stream around the scan
+ * and the resolve kernel of every run while enabled).  enable = 1 starts a
+ * fresh accumulation, 0 stops recording.  rcdc_plan_kernel_times waits for
+ * the recorded runs and returns their count and summed device times.      */
+rcdc_status rcdc_plan_set_timing(rcdc_plan *plan, int enable);
+rcdc_status rcdc_plan_kernel_times(rcdc_plan *plan, uint64_t *runs,
+                                   double *scan_ms_total,
+                                   double *resolve_ms_total);
+
 /* ---- FixedSize chunker (crates/core/src/chunker/fixed_size.rs:41-70) ---- */
 /* Cuts every `size` bytes, last chunk short; returns the count.           */
 uint64_t rcdc_fixed_cuts(uint64_t n, uint64_t size, uint64_t *cuts,

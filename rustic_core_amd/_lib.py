@@ -21,7 +21,7 @@ EXPORTS = (
     "rcdc_ctx_create", "rcdc_ctx_destroy", "rcdc_max_cuts", "rcdc_chunk_batch",
     "rcdc_stream_open", "rcdc_stream_feed", "rcdc_stream_close", "rcdc_plan_create",
     "rcdc_plan_destroy", "rcdc_plan_run", "rcdc_plan_results", "rcdc_plan_device_results",
-    "rcdc_plan_get_info", "rcdc_fixed_cuts",
+    "rcdc_plan_get_info", "rcdc_plan_set_timing", "rcdc_plan_kernel_times", "rcdc_fixed_cuts",
 )
 ABI_VERSION = 1
 
@@ -118,6 +118,10 @@ def lib() -> ctypes.CDLL:
     L.rcdc_plan_device_results.argtypes = [vp, P(u64), P(u64), P(P(u64))]
     L.rcdc_plan_get_info.restype = st
     L.rcdc_plan_get_info.argtypes = [vp, P(PlanInfo)]
+    L.rcdc_plan_set_timing.restype = st
+    L.rcdc_plan_set_timing.argtypes = [vp, ctypes.c_int]
+    L.rcdc_plan_kernel_times.restype = st
+    L.rcdc_plan_kernel_times.argtypes = [vp, P(u64), P(ctypes.c_double), P(ctypes.c_double)]
     L.rcdc_fixed_cuts.restype = u64
     L.rcdc_fixed_cuts.argtypes = [u64, u64, vp, u64]
     _lib = L

@@ -24,7 +24,9 @@
 #include "rcdc_internal.h"
 
 namespace rcdc {
-hipError_t launch_scan(const uint8_t *arena, const ScanItem *items, uint32_t nitems,
+int scan_variant_chains(int variant);
+int scan_variant_threads(int variant);
+hipError_t launch_scan(int variant, const uint8_t *arena, const ScanItem *items, uint32_t nitems,
                        const uint64_t *gtab, const ScanParams &prm, uint4 *sums,
                        uint64_t *item_masks, uint32_t blocks, hipStream_t stream);
 hipError_t launch_resolve(const uint8_t *arena, const StreamDesc *sds, uint32_t nstreams,
@@ -113,6 +115,10 @@ struct rcdc_plan {
              cap_counts = 0;
     hipEvent_t done = nullptr;
     bool ran = false;
+    // optional per-run kernel timing
+    bool timing = false;
+    std::vector<hipEvent_t> tev;  // 3 per run: before scan, after scan, after resolve
+    uint64_t truns = 0;
 };
 
 struct rcdc_ctx {
@@ -120,6 +126,7 @@ struct rcdc_ctx {
     uint64_t poly = 0, min = 0, avg = 0, max = 0;
     int deg = 0;
     int num_cus = 0;
+    int variant = 0;  // scan-kernel variant (RCDC_SCAN_VARIANT), see launch_scan
     hipStream_t stream = nullptr;
     uint64_t *d_tables = nullptr;
     std::mutex mu;
@@ -164,8 +171,8 @@ rcdc_status ensure_dev(T **p, uint64_t *cap, uint64_t need) {
 
 // Choose the per-lane segment S so that a batch covers the chip once:
 // roughly (scanned bytes) / (CUs * 1024 lanes), 512 <= S <= 4096.
-uint32_t choose_segment(uint64_t scanned, int cus) {
-    const uint64_t lanes = (uint64_t)std::max(cus, 1) * kScanThreads;
+uint32_t choose_segment(uint64_t scanned, int cus, int chains, int threads) {
+    const uint64_t lanes = (uint64_t)std::max(cus, 1) * threads * chains;
     uint64_t s = round_up((scanned + lanes - 1) / lanes, kUnit);
     return (uint32_t)std::min<uint64_t>(std::max<uint64_t>(s, 512), 4096);
 }
@@ -184,7 +191,10 @@ rcdc_status plan_build(rcdc_ctx *ctx, rcdc_plan *pl, const uint64_t *offs, const
                         (unsigned long long)arena_len);
         if (lens[i] > pos_lo) scanned += lens[i] - pos_lo + kWindow;
     }
-    const uint32_t S = choose_segment(scanned, ctx->num_cus);
+    const int nc = scan_variant_chains(ctx->variant);
+    const int nthreads = scan_variant_threads(ctx->variant);
+    uint32_t S = choose_segment(scanned, ctx->num_cus, nc, nthreads);
+    if (const char *e = getenv("RCDC_SEG_BYTES")) S = (uint32_t)(atoi(e) / 64 * 64);  // experiments
     pl->seg_bytes = S;
     pl->items.clear();
     pl->sds.assign(n, StreamDesc{});
@@ -227,7 +237,8 @@ rcdc_status plan_build(rcdc_ctx *ctx, rcdc_plan *pl, const uint64_t *offs, const
     }
     pl->nseg = nseg;
     pl->ncuts = ncut;
-    const uint64_t waves_needed = (pl->items.size() + kScanWaves - 1) / kScanWaves;
+    const uint64_t supers = (pl->items.size() + nc - 1) / nc;
+    const uint64_t waves_needed = (supers + nthreads / 64 - 1) / (nthreads / 64);
     pl->blocks = (uint32_t)std::min<uint64_t>(waves_needed, (uint64_t)std::max(ctx->num_cus, 1));
 
     DeviceGuard g(ctx->device);
@@ -259,8 +270,22 @@ rcdc_status plan_run(rcdc_plan *pl, const void *d_arena, hipStream_t stream) {
     sp.seg_bytes = pl->seg_bytes;
     sp.mask = (uint32_t)(ctx->avg - 1);
     sp.idx_shift = (uint32_t)(ctx->deg - 32);
-    HIP_TRY(launch_scan((const uint8_t *)d_arena, pl->d_items, (uint32_t)pl->items.size(),
+    hipEvent_t *ev = nullptr;
+    if (pl->timing) {
+        if (pl->tev.size() < 3 * (pl->truns + 1)) {
+            for (int k = 0; k < 3; k++) {
+                hipEvent_t e;
+                HIP_TRY(hipEventCreate(&e));
+                pl->tev.push_back(e);
+            }
+        }
+        ev = &pl->tev[3 * pl->truns];
+        pl->truns++;
+        HIP_TRY(hipEventRecord(ev[0], stream));
+    }
+    HIP_TRY(launch_scan(ctx->variant, (const uint8_t *)d_arena, pl->d_items, (uint32_t)pl->items.size(),
                         ctx->d_tables, sp, pl->d_sums, pl->d_masks, pl->blocks, stream));
+    if (ev) HIP_TRY(hipEventRecord(ev[1], stream));
     ResolveParams rp{};
     rp.min_size = ctx->min;
     rp.max_size = ctx->max;
@@ -269,6 +294,7 @@ rcdc_status plan_run(rcdc_plan *pl, const void *d_arena, hipStream_t stream) {
     rp.shift = (uint32_t)(ctx->deg - 8);
     HIP_TRY(launch_resolve((const uint8_t *)d_arena, pl->d_sds, pl->n, ctx->d_tables, rp,
                            pl->d_sums, pl->d_masks, pl->d_cuts, pl->d_counts, stream));
+    if (ev) HIP_TRY(hipEventRecord(ev[2], stream));
     HIP_TRY(hipEventRecord(pl->done, stream));
     pl->ran = true;
     return RCDC_OK;
@@ -312,6 +338,7 @@ void plan_free(rcdc_plan *pl) {
     (void)hipFree(pl->d_cuts);
     (void)hipFree(pl->d_counts);
     if (pl->done) (void)hipEventDestroy(pl->done);
+    for (hipEvent_t e : pl->tev) (void)hipEventDestroy(e);
     delete pl;
 }
 
@@ -441,6 +468,7 @@ rcdc_status rcdc_ctx_create(uint64_t poly, uint64_t min, uint64_t avg_pow2, uint
         return fail(RCDC_ERR_INTERNAL, "hipGetDeviceProperties: %s", hipGetErrorString(e));
     }
     c->num_cus = prop.multiProcessorCount;
+    if (const char *v = getenv("RCDC_SCAN_VARIANT")) c->variant = atoi(v);
     uint64_t img[512];
     build_tables(poly, img);
     if ((e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking)) != hipSuccess ||
@@ -523,6 +551,34 @@ rcdc_status rcdc_plan_get_info(const rcdc_plan *plan, rcdc_plan_info *info) {
     info->work_items = (uint32_t)plan->items.size();
     info->scan_blocks = plan->blocks;
     info->reserved = 0;
+    return RCDC_OK;
+}
+
+rcdc_status rcdc_plan_set_timing(rcdc_plan *plan, int enable) {
+    if (!plan) return fail(RCDC_ERR_INVALID_INPUT, "null argument");
+    plan->timing = enable != 0;
+    if (enable) plan->truns = 0;
+    return RCDC_OK;
+}
+
+rcdc_status rcdc_plan_kernel_times(rcdc_plan *plan, uint64_t *runs, double *scan_ms,
+                                   double *resolve_ms) {
+    if (!plan || !runs || !scan_ms || !resolve_ms)
+        return fail(RCDC_ERR_INVALID_INPUT, "null argument");
+    DeviceGuard g(plan->ctx->device);
+    double s = 0, r = 0;
+    for (uint64_t i = 0; i < plan->truns; i++) {
+        hipEvent_t *ev = &plan->tev[3 * i];
+        HIP_TRY(hipEventSynchronize(ev[2]));
+        float a = 0, b = 0;
+        HIP_TRY(hipEventElapsedTime(&a, ev[0], ev[1]));
+        HIP_TRY(hipEventElapsedTime(&b, ev[1], ev[2]));
+        s += a;
+        r += b;
+    }
+    *runs = plan->truns;
+    *scan_ms = s;
+    *resolve_ms = r;
     return RCDC_OK;
 }
 

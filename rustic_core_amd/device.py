@@ -84,12 +84,30 @@ class DevicePlan:
             raise status_error(st, _lib.last_error())
         return dc.value, dn.value, np.ctypeslib.as_array(base, shape=(max(self.n, 1),))[:self.n]
 
+    def set_timing(self, enable: bool) -> None:
+        st = _lib.lib().rcdc_plan_set_timing(self._h, int(enable))
+        if st:
+            raise status_error(st, _lib.last_error())
+
+    def kernel_times(self):
+        """(runs, summed scan ms, summed resolve ms) since set_timing(True)."""
+        n, a, b = ctypes.c_uint64(0), ctypes.c_double(0), ctypes.c_double(0)
+        st = _lib.lib().rcdc_plan_kernel_times(self._h, ctypes.byref(n), ctypes.byref(a),
+                                               ctypes.byref(b))
+        if st:
+            raise status_error(st, _lib.last_error())
+        return n.value, a.value, b.value
+
     def close(self):
         if getattr(self, "_h", None):
             _lib.lib().rcdc_plan_destroy(self._h)
             self._h = None
 
-    __del__ = close
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # interpreter shutdown
+            pass
 
 
 def chunk_device(ctx: Context, arena_tensor, offs, lens, stream=None) -> list:
