@@ -24,9 +24,8 @@
 #include "rcdc_internal.h"
 
 namespace rcdc {
-int scan_variant_chains(int variant);
-int scan_variant_threads(int variant);
-hipError_t launch_scan(int variant, const uint8_t *arena, const ScanItem *items, uint32_t nitems,
+int scan_threads(int code);
+hipError_t launch_scan(int code, const uint8_t *arena, const ScanItem *items, uint32_t nitems,
                        const uint64_t *gtab, const ScanParams &prm, uint4 *sums,
                        uint64_t *item_masks, uint32_t blocks, hipStream_t stream);
 hipError_t launch_resolve(const uint8_t *arena, const StreamDesc *sds, uint32_t nstreams,
@@ -126,7 +125,7 @@ struct rcdc_ctx {
     uint64_t poly = 0, min = 0, avg = 0, max = 0;
     int deg = 0;
     int num_cus = 0;
-    int variant = 0;  // scan-kernel variant (RCDC_SCAN_VARIANT), see launch_scan
+    int variant = kDefaultScanCode;  // scan-kernel configuration (RCDC_SCAN_VARIANT)
     hipStream_t stream = nullptr;
     uint64_t *d_tables = nullptr;
     std::mutex mu;
@@ -169,12 +168,40 @@ rcdc_status ensure_dev(T **p, uint64_t *cap, uint64_t need) {
     return RCDC_OK;
 }
 
-// Choose the per-lane segment S so that a batch covers the chip once:
-// roughly (scanned bytes) / (CUs * 1024 lanes), 512 <= S <= 4096.
-uint32_t choose_segment(uint64_t scanned, int cus, int chains, int threads) {
-    const uint64_t lanes = (uint64_t)std::max(cus, 1) * threads * chains;
-    uint64_t s = round_up((scanned + lanes - 1) / lanes, kUnit);
-    return (uint32_t)std::min<uint64_t>(std::max<uint64_t>(s, 512), 4096);
+// Choose the per-lane segment S (multiple of 128 in [512, 4096]): the scan
+// runs ceil(items / wave_slots) rounds of S + 64 slides per lane (64 = the
+// warm-up window), items = sum over streams of ceil(ceil(span / S) / 64).
+// Minimise rounds * (S + 64); ties go to the smaller S (finer summaries).
+uint32_t choose_segment(const std::vector<uint64_t> &spans, int cus, int chains, int threads) {
+    const uint64_t slots = (uint64_t)std::max(cus, 1) * (threads / 64) * chains;
+    uint64_t best_cost = ~0ull;
+    uint32_t best = 2048;
+    for (uint32_t S = 512; S <= 4096; S += 128) {
+        uint64_t items = 0;
+        for (uint64_t sp : spans) items += ((sp + S - 1) / S + 63) / 64;
+        const uint64_t rounds = std::max<uint64_t>((items + slots - 1) / slots, 1);
+        const uint64_t cost = rounds * (S + kWindow);
+        if (cost < best_cost) {
+            best_cost = cost;
+            best = S;
+        }
+    }
+    return best;
+}
+
+// Arena offset of lane 0's first byte for a stream at `off`: 16-aligned, or
+// aligned to `align` (a power of two <= 128) when that does not start
+// before the stream's first byte - 64.
+static inline uint64_t stream_q0(uint64_t off, uint64_t pos_lo, uint64_t align) {
+    const uint64_t x = off + pos_lo - 65;
+    const uint64_t q = x & ~(align - 1);
+    return q + 64 >= off ? q : (x & ~(uint64_t)15);
+}
+
+static uint64_t q0_align() {
+    const char *e = getenv("RCDC_Q0_ALIGN");  // experiments: 16 .. 128
+    const uint64_t v = e ? (uint64_t)atoll(e) : 16;
+    return (v == 128 || v == 64 || v == 32) ? v : (uint64_t)16;
 }
 
 rcdc_status plan_build(rcdc_ctx *ctx, rcdc_plan *pl, const uint64_t *offs, const uint64_t *lens,
@@ -183,18 +210,19 @@ rcdc_status plan_build(rcdc_ctx *ctx, rcdc_plan *pl, const uint64_t *offs, const
     pl->ctx = ctx;
     pl->n = n;
     pl->arena_len = arena_len;
-    uint64_t scanned = 0;
+    std::vector<uint64_t> spans;
+    spans.reserve(n);
     for (uint32_t i = 0; i < n; i++) {
         if (offs[i] > arena_len || lens[i] > arena_len - offs[i])
             return fail(RCDC_ERR_INVALID_INPUT, "stream %u [%llu,+%llu) outside arena of %llu B", i,
                         (unsigned long long)offs[i], (unsigned long long)lens[i],
                         (unsigned long long)arena_len);
-        if (lens[i] > pos_lo) scanned += lens[i] - pos_lo + kWindow;
+        if (lens[i] > pos_lo) spans.push_back(lens[i] - (stream_q0(offs[i], pos_lo, q0_align()) - offs[i] + 65));
     }
-    const int nc = scan_variant_chains(ctx->variant);
-    const int nthreads = scan_variant_threads(ctx->variant);
-    uint32_t S = choose_segment(scanned, ctx->num_cus, nc, nthreads);
-    if (const char *e = getenv("RCDC_SEG_BYTES")) S = (uint32_t)(atoi(e) / 64 * 64);  // experiments
+    const int nc = 1;
+    const int nthreads = scan_threads(ctx->variant);
+    uint32_t S = choose_segment(spans, ctx->num_cus, nc, nthreads);
+    if (const char *e = getenv("RCDC_SEG_BYTES")) S = (uint32_t)(atoi(e) / 128 * 128);  // experiments
     pl->seg_bytes = S;
     pl->items.clear();
     pl->sds.assign(n, StreamDesc{});
@@ -214,7 +242,7 @@ rcdc_status plan_build(rcdc_ctx *ctx, rcdc_plan *pl, const uint64_t *offs, const
         d.item_base = pl->items.size();
         if (N <= pos_lo) continue;
         // lane start q (arena offset) 16-aligned; tests positions q+65 ..
-        const uint64_t q0 = (off + pos_lo - 65) & ~(uint64_t)15;
+        const uint64_t q0 = stream_q0(off, pos_lo, q0_align());
         const uint64_t p0 = q0 - off + 65;
         const uint64_t segs = (N - p0 + S - 1) / S;
         d.pos0 = p0;

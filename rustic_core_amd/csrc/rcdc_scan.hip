@@ -1,24 +1,24 @@
-// rcdc_scan.hip -- the candidate-scan kernel (gfx950), v3.
+// rcdc_scan.hip -- scan kernel of the rcdc chunker (gfx950).
 //
-// Replaces the per-byte loop of crates/core/src/chunker/rabin.rs:153-188
+// Replaces the per-byte hot loop of crates/core/src/chunker/rabin.rs:153-188
 // (rustic_cdc Rabin64::slide + `hash & split_mask == 0`): every lane owns one
 // S-byte segment of one stream, rolls the 64-byte-window Rabin64 fingerprint
-// over it and records first / last / number of candidate positions.
+// over it and records the first / last / number of candidate positions
+// (fp(b[p-64, p)) & mask == 0).  Output format as rcdc_internal.h.
 //
-// Design points (measured on MI355X, see DESIGN.md "Scan kernel"):
-//  * VALU-issue bound: wave64 v_xor/v_and/v_or/shift-by-constant and
-//    v_bitop3 (VGPR operands) issue at ~2 cycles per SIMD, v_perm /
-//    v_alignbit / v_cmp / any SGPR-operand op at ~4.  The byte step uses
-//    2 v_perm + 1 v_alignbit + 1 v_cmp + 6 fast ops; constants live in VGPRs.
-//  * Loads: lanes l and l+32 read the two 16-byte halves of one 32-byte piece
-//    of segment (l mod 32) -- one instruction covers 32 x 32 contiguous bytes
-//    instead of 64 scattered lines -- and one v_permlane32_swap per dword
-//    gives every lane its own segment's bytes back.
-//  * NC independent segments ("chains") per lane interleave their dependency
-//    chains (LDS lookup -> 4 VALU -> LDS lookup) for latency hiding.
-//  * Tables: 32 lane-private copies of OUT' (out[b] << 8) and MOD in LDS
-//    (128 KiB), entry e of copy c at e*256 + c*8: ds_read_b64 is conflict-free
-//    whatever the data.
+// Cost model (profiles/r01_slide_bench*.txt): the loop is VALU-issue bound at
+// ~8 VALU + 2 ds_read_b64 per byte; the LDS array is at ~40 % and HBM at
+// ~45 % of their peaks.  Choices that follow from it:
+//   * candidate test: a v_min3_u16 over the low halves of 16 consecutive
+//     fingerprints (0.5 VALU/byte) and ONE wave ballot per 16 bytes; the
+//     exact test (h & mask) == 0 runs only on the rare groups whose minimum
+//     is 0 (P ~ 2^-12 per lane-group for mask >= 0xFFFF).  The per-byte
+//     and + v_cmp + s_or form it replaces cost 2-3x as much.
+//   * every operand of the hot loop is a VGPR or an inline constant (SGPR
+//     operands and 64-bit shifts issue at half rate on gfx950).
+//   * loads: each lane streams its own segment in 64-B units (4 x
+//     buffer_load_dwordx4, or 8 = one 128-B line with PAIR), a ring of R
+//     units so loads run R-2 units ahead; no load beyond the segment.
 #include <hip/hip_runtime.h>
 
 #include "rcdc_internal.h"
@@ -29,10 +29,12 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 namespace {
 
-constexpr uint32_t kLutA = 0xF0, kLutB = 0xCC, kLutC = 0xAA;  // v_bitop3 operand LUTs
+constexpr uint32_t kOpA = 0xF0, kOpB = 0xCC, kOpC = 0xAA;  // v_bitop3 operand truth tables
+constexpr uint32_t kXor3 = kOpA ^ kOpB ^ kOpC;
+constexpr uint32_t kAndOr = (kOpA & kOpB) | kOpC;
 
-// Materialise a value in a VGPR the compiler cannot turn back into an SGPR
-// or an inline constant (SGPR operands halve the VALU issue rate).
+// Materialise a wave-uniform value in a VGPR once (keeps the compiler from
+// folding it back into an SGPR operand of every use).
 __device__ __forceinline__ uint32_t in_vgpr(uint32_t x) {
     uint32_t r;
     asm volatile("v_mov_b32 %0, %1" : "=v"(r) : "s"(x));
@@ -43,129 +45,75 @@ __device__ __forceinline__ uint2 lds_u2(const uint8_t *tab, uint32_t byte_addr) 
     return *reinterpret_cast<const uint2 *>(tab + byte_addr);
 }
 
-// 32 bytes of one lane's segment: dwords 0..3 then 4..7.
-struct Unit32 {
-    u32x4 a, b;
+struct Unit {
+    u32x4 v[4];
 };
-template <int D>
-__device__ __forceinline__ uint32_t dw(const Unit32 &u) {
-    if constexpr (D < 4) return u.a[D];
-    else return u.b[D - 4];
-}
-
-// Issue the two paired loads of a 32-byte unit (see header).
-__device__ __forceinline__ void load_unit(Unit32 &u, __amdgpu_buffer_rsrc_t rsrc, uint32_t voffa,
-                                          uint32_t pair_stride, uint32_t off) {
-    u.a = __builtin_amdgcn_raw_buffer_load_b128(rsrc, (int)(voffa + off), 0, 0);
-    u.b = __builtin_amdgcn_raw_buffer_load_b128(rsrc, (int)(voffa + pair_stride + off), 0, 0);
-}
-
-// After the loads land: lane l < 32 holds (seg l: bytes 0-15, seg l+32: 0-15),
-// lane l+32 holds (seg l: 16-31, seg l+32: 16-31); swap the cross halves.
-__device__ __forceinline__ void fix_unit(Unit32 &u) {
-#pragma unroll
-    for (int i = 0; i < 4; i++) {
-        auto r = __builtin_amdgcn_permlane32_swap(u.a[i], u.b[i], false, false);
-        u.a[i] = r[0];
-        u.b[i] = r[1];
-    }
-}
-
-// Adjacent-lane pairing: lanes 2p and 2p+1 read the two 16-byte halves of a
-// 32-byte piece of segment 2p (first load) and of segment 2p+1 (second load);
-// the 2x2 exchange is one DPP (quad_perm swap) v_cndmask per dword.
-__device__ __forceinline__ void fix_unit_adjacent(Unit32 &u, uint64_t even, uint64_t odd) {
-    uint32_t c0, c1, c2, c3, d0, d1, d2, d3;
-    asm volatile(
-        "s_mov_b64 vcc, %16\n\t"
-        "s_nop 1\n\t"
-        "v_cndmask_b32_dpp %0, %12, %8, vcc quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
-        "v_cndmask_b32_dpp %1, %13, %9, vcc quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
-        "v_cndmask_b32_dpp %2, %14, %10, vcc quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
-        "v_cndmask_b32_dpp %3, %15, %11, vcc quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
-        "s_mov_b64 vcc, %17\n\t"
-        "s_nop 1\n\t"
-        "v_cndmask_b32_dpp %4, %8, %12, vcc quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
-        "v_cndmask_b32_dpp %5, %9, %13, vcc quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
-        "v_cndmask_b32_dpp %6, %10, %14, vcc quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
-        "v_cndmask_b32_dpp %7, %11, %15, vcc quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf"
-        : "=&v"(c0), "=&v"(c1), "=&v"(c2), "=&v"(c3), "=&v"(d0), "=&v"(d1), "=&v"(d2), "=&v"(d3)
-        : "v"(u.a[0]), "v"(u.a[1]), "v"(u.a[2]), "v"(u.a[3]), "v"(u.b[0]), "v"(u.b[1]),
-          "v"(u.b[2]), "v"(u.b[3]), "s"(even), "s"(odd)
-        : "vcc");
-    u.a[0] = c0; u.a[1] = c1; u.a[2] = c2; u.a[3] = c3;
-    u.b[0] = d0; u.b[1] = d1; u.b[2] = d2; u.b[3] = d3;
-}
+#define UDW(u, d) ((u).v[(d) >> 2][(d) & 3])
 
 struct Consts {
-    uint32_t lwo, lwm;  // lane part of the OUT / MOD table addresses
+    uint32_t lwo, lwm;  // lane's table-copy offset in OUT / MOD
     uint32_t kff00;     // 0xFF00 in a VGPR
-    uint32_t mask;      // split mask (avg - 1) in a VGPR
-    uint32_t tsh;       // deg - 40: top byte of h from hi32(h << 8) >> tsh
-    uint64_t even, odd; // lane masks for the adjacent-pair exchange
+    uint32_t mask;      // avg - 1 in a VGPR
+    uint32_t tsh;       // deg - 32 (generic-degree path only)
 };
 
-// Warm-up slide (window still filling: nothing leaves).
-template <int K>
-__device__ __forceinline__ void slide_warm(uint32_t &h0, uint32_t &h1, uint32_t dnew,
-                                           const uint8_t *tab, const Consts &k) {
+// MOD table address of the top byte of a1x = hi32(h << 8 ^ out << 8).
+// TSH >= 0: compile-time deg - 40 (v_lshrrev by an inline constant + one
+// v_bitop3 (x & 0xFF00) | lwm); TSH < 0: any degree, runtime shift.
+template <int TSH>
+__device__ __forceinline__ uint32_t mod_addr(uint32_t a1x, const Consts &k) {
+    if constexpr (TSH >= 0) return __builtin_amdgcn_bitop3_b32(a1x >> TSH, k.kff00, k.lwm, kAndOr);
+    else return ((a1x >> k.tsh) << 8) | k.lwm;
+}
+
+// One slide: h ^= out[o]; i = top byte; h = ((h<<8)|n) ^ mod[i]
+// with h = h1:h0, OUT table pre-shifted by 8 (see rcdc_kernels.hip).
+template <int K, int TSH>
+__device__ __forceinline__ void slide(uint32_t &h0, uint32_t &h1, uint32_t dnew, uint32_t dold,
+                                      const uint8_t *tab, const Consts &k) {
+    const uint2 o = lds_u2(tab, __builtin_amdgcn_perm(dold, k.lwo, 0x0C0C0000u | ((4u + K) << 8)));
+    const uint32_t a1x = __builtin_amdgcn_alignbit(h1, h0, 24) ^ o.y;
+    const uint2 m = lds_u2(tab, mod_addr<TSH>(a1x, k));
+    h0 = __builtin_amdgcn_bitop3_b32(__builtin_amdgcn_perm(h0, dnew, 0x06050400u | K), o.x, m.x, kXor3);
+    h1 = a1x ^ m.y;
+}
+
+// Warm-up slide (the window is still filling: nothing leaves it).
+template <int K, int TSH>
+__device__ __forceinline__ void slide_in(uint32_t &h0, uint32_t &h1, uint32_t dnew,
+                                         const uint8_t *tab, const Consts &k) {
     const uint32_t a1 = __builtin_amdgcn_alignbit(h1, h0, 24);
-    const uint32_t am = __builtin_amdgcn_bitop3_b32(a1 >> k.tsh, k.kff00, k.lwm,
-                                                    (kLutA & kLutB) | kLutC);
-    const uint2 m = lds_u2(tab, am);
+    const uint2 m = lds_u2(tab, mod_addr<TSH>(a1, k));
     h0 = __builtin_amdgcn_perm(h0, dnew, 0x06050400u | K) ^ m.x;
     h1 = a1 ^ m.y;
 }
 
-// One Rabin64 slide: h ^= out[o]; i = top byte; h = ((h<<8)|n) ^ mod[i].
-//   a1x = hi32(h << 8) ^ hi32(out[o] << 8)        v_alignbit, v_xor
-//   am  = ((a1x >> (deg-40)) & 0xFF00) | lwm       v_lshrrev, v_bitop3   (MOD address)
-//   h1  = a1x ^ hi32(mod[i])                       v_xor   (mod[i] carries i << deg)
-//   h0  = ((h0 << 8) | n) ^ lo32(out<<8) ^ lo32(mod[i])   v_perm, v_bitop3
-// ABL (timing-only ablations, wrong results): bit 1 = no LDS lookups.
-template <int ABL>
-__device__ __forceinline__ uint2 lookup(const uint8_t *tab, uint32_t a) {
-    if constexpr (ABL & 2) {
-        return make_uint2(a * 0x9E3779B1u, a ^ 0x7F4A7C15u);
-    } else {
-        return lds_u2(tab, a);
+template <int TSH>
+__device__ __forceinline__ void slide_b(int b, uint32_t &h0, uint32_t &h1, uint32_t dn,
+                                        uint32_t d_o, const uint8_t *tab, const Consts &k) {
+    switch (b & 3) {
+        case 0: slide<0, TSH>(h0, h1, dn, d_o, tab, k); break;
+        case 1: slide<1, TSH>(h0, h1, dn, d_o, tab, k); break;
+        case 2: slide<2, TSH>(h0, h1, dn, d_o, tab, k); break;
+        default: slide<3, TSH>(h0, h1, dn, d_o, tab, k); break;
     }
-}
-
-template <int K, int ABL = 0>
-__device__ __forceinline__ void slide(uint32_t &h0, uint32_t &h1, uint32_t dnew, uint32_t dold,
-                                      const uint8_t *tab, const Consts &k) {
-    const uint2 o = lookup<ABL>(tab, __builtin_amdgcn_perm(dold, k.lwo, 0x0C0C0000u | ((4u + K) << 8)));
-    const uint32_t a1x = __builtin_amdgcn_alignbit(h1, h0, 24) ^ o.y;
-    const uint32_t am = __builtin_amdgcn_bitop3_b32(a1x >> k.tsh, k.kff00, k.lwm,
-                                                    (kLutA & kLutB) | kLutC);
-    const uint2 m = lookup<ABL>(tab, am);
-    h0 = __builtin_amdgcn_bitop3_b32(__builtin_amdgcn_perm(h0, dnew, 0x06050400u | K), o.x, m.x,
-                                     kLutA ^ kLutB ^ kLutC);
-    h1 = a1x ^ m.y;
 }
 
 struct Chain {
     uint32_t h0, h1;
-    uint32_t first, last, count;  // candidates, relative positions
-    uint32_t rlo, rhi;            // relative positions that count
-    Unit32 u[4];                  // rotating 32-byte units
+    uint32_t first, last, count;  // candidate summary (segment-relative)
+    uint32_t rlo, rhi;            // relative positions that count: [rlo, rhi)
 };
 
-// hb = 2*hb + (this lane's bit of m)
-__device__ __forceinline__ uint32_t shift_in(uint32_t hb, uint64_t m) {
-    uint32_t r;
-    asm("v_addc_co_u32 %0, vcc, %1, %1, %2" : "=v"(r) : "v"(hb), "s"(m) : "vcc");
-    return r;
-}
-
-// Rare path: lanes of this chain saw candidates at rb + j, j < 8 (m[j]).
-__device__ __forceinline__ void record_hits(Chain &c, const uint64_t (&m)[8], uint32_t rb) {
+// Rare path: exact test of the G fingerprints of group rb .. rb + G - 1.
+template <int G>
+__device__ __forceinline__ void record_group(Chain &c, const uint32_t (&hk)[G], uint32_t mask,
+                                             uint32_t rb) {
     uint32_t hb = 0;
 #pragma unroll
-    for (int j = 7; j >= 0; j--) hb = shift_in(hb, m[j]);  // bit j <-> position rb + j
-    const int lo = min(max((int)c.rlo - (int)rb, 0), 8);
-    const int hi = min(max((int)c.rhi - (int)rb, 0), 8);
+    for (int j = 0; j < G; j++) hb |= (uint32_t)((hk[j] & mask) == 0u) << j;
+    const int lo = min(max((int)c.rlo - (int)rb, 0), G);
+    const int hi = min(max((int)c.rhi - (int)rb, 0), G);
     hb &= ((1u << hi) - 1u) & ~((1u << lo) - 1u);
     if (hb) {
         c.count += __builtin_popcount(hb);
@@ -174,165 +122,129 @@ __device__ __forceinline__ void record_hits(Chain &c, const uint64_t (&m)[8], ui
     }
 }
 
-template <int NC, int B, int IN, int IO, int ABL>
-__device__ __forceinline__ void step_all(Chain (&ch)[NC], const uint8_t *tab, const Consts &k,
-                                         uint64_t (&m)[NC][8], int j) {
+// 64 slides over unit `un` (bytes 64 back in `uo`), 64 / G groups of G.
+// SMALL: mask < 0xFFFF, the prefilter then runs on h & mask (exact).
+template <int TSH, bool SMALL, int G>
+__device__ __forceinline__ void scan_unit(Chain &c, const Unit &un, const Unit &uo,
+                                          const uint8_t *tab, const Consts &k, uint64_t valid,
+                                          uint32_t lane, uint32_t rb) {
 #pragma unroll
-    for (int c = 0; c < NC; c++) {
-        const uint32_t dn = dw<(B >> 2)>(ch[c].u[IN]);
-        const uint32_t d_o = dw<(B >> 2)>(ch[c].u[IO]);
-        slide<(B & 3), ABL>(ch[c].h0, ch[c].h1, dn, d_o, tab, k);
-        if constexpr (ABL & 4) m[c][j] = 0;  // ablation: no test
-        else m[c][j] = __builtin_amdgcn_ballot_w64((ch[c].h0 & k.mask) == 0u);
-    }
-}
-
-// Bytes [B, E) of the current unit for every chain (compile-time unrolled).
-template <int NC, int B, int E, int IN, int IO, int ABL>
-__device__ __forceinline__ void steps(Chain (&ch)[NC], const uint8_t *tab, const Consts &k,
-                                      uint64_t (&m)[NC][8]) {
-    if constexpr (B < E) {
-        step_all<NC, B, IN, IO, ABL>(ch, tab, k, m, B & 7);
-        steps<NC, B + 1, E, IN, IO, ABL>(ch, tab, k, m);
-    }
-}
-
-template <int NC, int G, int IN, int IO, int ABL>
-__device__ __forceinline__ void scan_group(Chain (&ch)[NC], const uint8_t *tab, const Consts &k,
-                                           const uint64_t (&valid)[NC], uint32_t rb) {
-    uint64_t m[NC][8];
-    steps<NC, G * 8, G * 8 + 8, IN, IO, ABL>(ch, tab, k, m);
+    for (int g = 0; g < 64 / G; g++) {
+        uint32_t hk[G];
+        uint16_t acc = 0xFFFFu;
 #pragma unroll
-    for (int c = 0; c < NC; c++) {
-        uint64_t any = m[c][0];
-#pragma unroll
-        for (int j = 1; j < 8; j++) any |= m[c][j];
-        if (any & valid[c]) record_hits(ch[c], m[c], rb + G * 8);
-    }
-}
-
-// 32 slides per chain: new bytes in unit IN, bytes 64 earlier in unit IO.
-template <int NC, int IN, int IO, int ABL>
-__device__ __forceinline__ void scan_unit(Chain (&ch)[NC], const uint8_t *tab, const Consts &k,
-                                          const uint64_t (&valid)[NC], uint32_t rb) {
-    if constexpr (!(ABL & 8)) {
-#pragma unroll
-        for (int c = 0; c < NC; c++) {
-            if constexpr (ABL & 16) fix_unit(ch[c].u[IN]);
-            else fix_unit_adjacent(ch[c].u[IN], k.even, k.odd);
+        for (int j = 0; j < G; j++) {
+            const int b = g * G + j;
+            slide_b<TSH>(b, c.h0, c.h1, UDW(un, b >> 2), UDW(uo, b >> 2), tab, k);
+            hk[j] = c.h0;
+            const uint16_t t = SMALL ? (uint16_t)(c.h0 & k.mask) : (uint16_t)c.h0;
+            acc = __builtin_elementwise_min(acc, t);
+        }
+        // one ballot per group; the prefilter is necessary, not sufficient:
+        // flagged lanes run the exact test
+        const uint64_t flagged = __builtin_amdgcn_ballot_w64(acc == 0) & valid;
+        if (flagged) {
+            if ((flagged >> lane) & 1u) record_group<G>(c, hk, k.mask, rb + g * G);
         }
     }
-    scan_group<NC, 0, IN, IO, ABL>(ch, tab, k, valid, rb);
-    scan_group<NC, 1, IN, IO, ABL>(ch, tab, k, valid, rb);
-    scan_group<NC, 2, IN, IO, ABL>(ch, tab, k, valid, rb);
-    scan_group<NC, 3, IN, IO, ABL>(ch, tab, k, valid, rb);
 }
 
-template <int NC, int IN, int ABL>
-__device__ __forceinline__ void warm_unit(Chain (&ch)[NC], const uint8_t *tab, const Consts &k) {
+template <int TSH>
+__device__ __forceinline__ void warm_unit(Chain &c, const Unit &u, const uint8_t *tab,
+                                          const Consts &k) {
 #pragma unroll
-    for (int c = 0; c < NC; c++) {
-        if constexpr (ABL & 16) fix_unit(ch[c].u[IN]);
-        else fix_unit_adjacent(ch[c].u[IN], k.even, k.odd);
+    for (int b = 0; b < 64; b++) {
+        const uint32_t dn = UDW(u, b >> 2);
+        switch (b & 3) {
+            case 0: slide_in<0, TSH>(c.h0, c.h1, dn, tab, k); break;
+            case 1: slide_in<1, TSH>(c.h0, c.h1, dn, tab, k); break;
+            case 2: slide_in<2, TSH>(c.h0, c.h1, dn, tab, k); break;
+            default: slide_in<3, TSH>(c.h0, c.h1, dn, tab, k); break;
+        }
     }
+}
+
+__device__ __forceinline__ void load_unit(Unit &u, __amdgpu_buffer_rsrc_t rsrc, uint32_t voff) {
 #pragma unroll
-    for (int b = 0; b < 32; b++) {
-#pragma unroll
-        for (int c = 0; c < NC; c++) {
-            const Unit32 &u = ch[c].u[IN];
-            const uint32_t dn = (b >> 2) < 4 ? u.a[(b >> 2) & 3] : u.b[(b >> 2) & 3];
-            switch (b & 3) {
-                case 0: slide_warm<0>(ch[c].h0, ch[c].h1, dn, tab, k); break;
-                case 1: slide_warm<1>(ch[c].h0, ch[c].h1, dn, tab, k); break;
-                case 2: slide_warm<2>(ch[c].h0, ch[c].h1, dn, tab, k); break;
-                default: slide_warm<3>(ch[c].h0, ch[c].h1, dn, tab, k); break;
+    for (int i = 0; i < 4; i++)
+        u.v[i] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, (int)(voff + 16u * i), 0, 0);
+}
+
+// Ring step: process unit i (buffer B = i % R, old = (i-1) % R), then refill
+// the freed buffer(s) with unit i - 1 + R (PAIR: units i-2+R, i-1+R after
+// even i, one 128-B line per lane).  Returns false after the last unit.
+template <int R, bool PAIR, int TSH, bool SMALL, int G, int B>
+__device__ __forceinline__ bool ring_step(Chain &c, Unit (&u)[R], uint32_t &i, uint32_t nunits,
+                                          __amdgpu_buffer_rsrc_t rsrc, uint32_t voff,
+                                          const uint8_t *tab, const Consts &k, uint64_t valid,
+                                          uint32_t lane) {
+    scan_unit<TSH, SMALL, G>(c, u[B], u[(B + R - 1) % R], tab, k, valid, lane, (i - 1) * 64u);
+    if constexpr (PAIR) {
+        if ((B & 1) == 0) {  // i even (R even, so B = i % R has i's parity)
+            const uint32_t nxt = i - 2 + R;  // units nxt, nxt + 1 -> buffers B-2, B-1
+            if (nxt <= nunits) {
+                load_unit(u[(B + R - 2) % R], rsrc, voff + nxt * 64u);
+                load_unit(u[(B + R - 1) % R], rsrc, voff + (nxt + 1) * 64u);
             }
         }
+    } else {
+        const uint32_t nxt = i - 1 + R;
+        if (nxt <= nunits) load_unit(u[(B + R - 1) % R], rsrc, voff + nxt * 64u);
     }
+    return ++i <= nunits;
 }
 
-// Scan NC items (64 segments each) with one wave; lane l owns segment l.
-template <int NC, int ABL = 0>
-__device__ __forceinline__ void scan_items(const uint8_t *__restrict__ arena,
-                                           const ScanItem *__restrict__ items, uint32_t it0,
-                                           uint32_t lane, const uint8_t *tab, const Consts &k,
-                                           uint32_t S, uint4 *__restrict__ sums,
-                                           uint64_t *__restrict__ item_masks) {
-    Chain ch[NC];
-    __amdgpu_buffer_rsrc_t rsrc[NC];
-    uint64_t valid[NC];
-    uint64_t sum_idx[NC];
-    // ABL & 16 (old scheme): lane l reads half (l >> 5) of segment (l & 31)
-    // and of segment (l & 31) + 32.  Default: lanes 2p, 2p+1 read the halves
-    // of segment 2p, then of segment 2p+1.
-    const uint32_t voffa = (ABL & 16) ? (lane & 31u) * S + (lane >> 5) * 16u
-                                      : (lane & ~1u) * S + (lane & 1u) * 16u;
-    const uint32_t pstride = (ABL & 16) ? 32u * S : S;
-    const uint32_t nunits = S / 32u;
-#pragma unroll
-    for (int c = 0; c < NC; c++) {
-        const ScanItem item = items[it0 + c];
-        const uint64_t segpos = item.pos0 + (uint64_t)lane * S;
-        const bool lv = lane < item.nvalid;
-        valid[c] = __builtin_amdgcn_ballot_w64(lv);
-        ch[c].h0 = ch[c].h1 = 0;
-        ch[c].first = ch[c].last = kNone;
-        ch[c].count = 0;
-        ch[c].rlo = (lv && item.lo > segpos) ? (uint32_t)min(item.lo - segpos, (uint64_t)S) : 0u;
-        ch[c].rhi = (lv && item.hi > segpos) ? (uint32_t)min(item.hi - segpos, (uint64_t)S) : 0u;
-        sum_idx[c] = item.sum_idx;
-        rsrc[c] = __builtin_amdgcn_make_buffer_rsrc((void *)(arena + item.q0), (short)0,
-                                                    (int)(uint32_t)item.rec_bytes, 0x00020000);
-        load_unit(ch[c].u[0], rsrc[c], voffa, pstride, 0u);    // warm-up bytes 0-31
-        load_unit(ch[c].u[1], rsrc[c], voffa, pstride, 32u);   // warm-up bytes 32-63
-        load_unit(ch[c].u[2], rsrc[c], voffa, pstride, 64u);   // first tested unit
-        load_unit(ch[c].u[3], rsrc[c], voffa, pstride, 96u);
-    }
-    warm_unit<NC, 0, ABL>(ch, tab, k);
-    warm_unit<NC, 1, ABL>(ch, tab, k);
+template <int R, bool PAIR, int TSH, bool SMALL, int G, int B = 1>
+__device__ __forceinline__ bool ring_pass(Chain &c, Unit (&u)[R], uint32_t &i, uint32_t nunits,
+                                          __amdgpu_buffer_rsrc_t rsrc, uint32_t voff,
+                                          const uint8_t *tab, const Consts &k, uint64_t valid,
+                                          uint32_t lane) {
+    if (!ring_step<R, PAIR, TSH, SMALL, G, B % R>(c, u, i, nunits, rsrc, voff, tab, k, valid, lane))
+        return false;
+    if constexpr (B < R) return ring_pass<R, PAIR, TSH, SMALL, G, B + 1>(c, u, i, nunits, rsrc,
+                                                                        voff, tab, k, valid, lane);
+    else return true;
+}
 
-    // unit u (u >= 2) uses new = u[u%4], old = u[(u-2)%4]; afterwards the old
-    // buffer takes unit u+2.
-    uint32_t u = 2, rb = 0;
-    for (;;) {
-        scan_unit<NC, 2, 0, ABL>(ch, tab, k, valid, rb);
+// One wave scans one item (64 segments): lane l owns segment l.
+template <int R, bool PAIR, int TSH, bool SMALL, int G>
+__device__ __forceinline__ void scan_item(const uint8_t *__restrict__ arena, const ScanItem &item,
+                                          uint32_t lane, const uint8_t *tab, const Consts &k,
+                                          uint32_t S, uint4 *__restrict__ sums,
+                                          uint64_t *__restrict__ item_mask) {
+    const uint32_t nunits = S / kUnit;  // plus unit 0 = the 64-byte warm-up window
+    const uint64_t segpos = item.pos0 + (uint64_t)lane * S;
+    const bool lv = lane < item.nvalid;
+    const uint64_t valid = __builtin_amdgcn_ballot_w64(lv);
+    Chain c;
+    c.h0 = c.h1 = 0;
+    c.first = c.last = kNone;
+    c.count = 0;
+    c.rlo = (lv && item.lo > segpos) ? (uint32_t)min(item.lo - segpos, (uint64_t)S) : 0u;
+    c.rhi = (lv && item.hi > segpos) ? (uint32_t)min(item.hi - segpos, (uint64_t)S) : 0u;
+    const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
+        (void *)(arena + item.q0), (short)0, (int)(uint32_t)item.rec_bytes, 0x00020000);
+    const uint32_t voff = lane * S;
+
+    Unit u[R];
 #pragma unroll
-        for (int c = 0; c < NC; c++)
-            if constexpr (!(ABL & 1)) load_unit(ch[c].u[0], rsrc[c], voffa, pstride, (u + 2) * 32u);
-        rb += 32;
-        if (++u >= nunits + 2) break;
-        scan_unit<NC, 3, 1, ABL>(ch, tab, k, valid, rb);
-#pragma unroll
-        for (int c = 0; c < NC; c++)
-            if constexpr (!(ABL & 1)) load_unit(ch[c].u[1], rsrc[c], voffa, pstride, (u + 2) * 32u);
-        rb += 32;
-        if (++u >= nunits + 2) break;
-        scan_unit<NC, 0, 2, ABL>(ch, tab, k, valid, rb);
-#pragma unroll
-        for (int c = 0; c < NC; c++)
-            if constexpr (!(ABL & 1)) load_unit(ch[c].u[2], rsrc[c], voffa, pstride, (u + 2) * 32u);
-        rb += 32;
-        if (++u >= nunits + 2) break;
-        scan_unit<NC, 1, 3, ABL>(ch, tab, k, valid, rb);
-#pragma unroll
-        for (int c = 0; c < NC; c++)
-            if constexpr (!(ABL & 1)) load_unit(ch[c].u[3], rsrc[c], voffa, pstride, (u + 2) * 32u);
-        rb += 32;
-        if (++u >= nunits + 2) break;
+    for (int j = 0; j < R; j++)
+        if ((uint32_t)j <= nunits) load_unit(u[j], rsrc, voff + j * 64u);
+    warm_unit<TSH>(c, u[0], tab, k);
+    uint32_t i = 1;
+    while (ring_pass<R, PAIR, TSH, SMALL, G>(c, u, i, nunits, rsrc, voff, tab, k, valid, lane)) {
     }
-#pragma unroll
-    for (int c = 0; c < NC; c++) {
-        if ((valid[c] >> lane) & 1)
-            sums[sum_idx[c] + lane] = make_uint4(ch[c].first, ch[c].last, ch[c].count, 0u);
-        const uint64_t hits = __builtin_amdgcn_ballot_w64(ch[c].count != 0u) & valid[c];
-        if (lane == 0) item_masks[it0 + c] = hits;
-    }
+    if (lv) sums[item.sum_idx + lane] = make_uint4(c.first, c.last, c.count, 0u);
+    const uint64_t hits = __builtin_amdgcn_ballot_w64(c.count != 0u) & valid;
+    if (lane == 0) *item_mask = hits;
 }
 
 }  // namespace
 
-template <int NC, int THREADS, int ABL = 0>
-__global__ __launch_bounds__(THREADS, 1) void rcdc_scan3_kernel(
+// One workgroup of THREADS lanes per CU; 128 KiB of LDS tables (32
+// lane-private copies of OUT' and MOD: ds_read_b64 never bank-conflicts).
+template <int R, bool PAIR, int THREADS, int TSH, bool SMALL, int G>
+__global__ __launch_bounds__(THREADS, 1) void rcdc_scan_kernel(
     const uint8_t *__restrict__ arena, const ScanItem *__restrict__ items, uint32_t nitems,
     const uint64_t *__restrict__ gtab, ScanParams prm, uint4 *__restrict__ sums,
     uint64_t *__restrict__ item_masks) {
@@ -349,62 +261,63 @@ __global__ __launch_bounds__(THREADS, 1) void rcdc_scan3_kernel(
 
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = threadIdx.x >> 6;
-    constexpr uint32_t waves = THREADS / 64;
+    constexpr uint32_t kWaves = THREADS / 64;
     Consts k;
     k.lwo = (lane & 31u) * 8u;
     k.lwm = k.lwo | kTableBytes;
     k.kff00 = in_vgpr(0xFF00u);
     k.mask = in_vgpr(prm.mask);
-    k.tsh = prm.idx_shift - 8u;  // (deg - 32) - 8: idx lands in bits 8..15
-    k.even = 0x5555555555555555ull;
-    k.odd = 0xAAAAAAAAAAAAAAAAull;
-    const uint32_t nsuper = (nitems + NC - 1) / NC;
-    for (uint32_t sp = blockIdx.x * waves + wave; sp < nsuper; sp += gridDim.x * waves) {
-        const uint32_t it0 = __builtin_amdgcn_readfirstlane(sp * NC);
-        if (it0 + NC <= nitems) {
-            scan_items<NC, ABL>(arena, items, it0, lane, s_tab, k, prm.seg_bytes, sums, item_masks);
-        } else {
-            for (uint32_t it = it0; it < nitems; it++)
-                scan_items<1>(arena, items, it, lane, s_tab, k, prm.seg_bytes, sums, item_masks);
-        }
+    k.tsh = prm.idx_shift;
+    for (uint32_t it = blockIdx.x * kWaves + wave; it < nitems; it += gridDim.x * kWaves) {
+        const uint32_t iu = __builtin_amdgcn_readfirstlane(it);
+        scan_item<R, PAIR, TSH, SMALL, G>(arena, items[iu], lane, s_tab, k, prm.seg_bytes, sums,
+                                       item_masks + iu);
     }
 }
 
 namespace rcdc {
 
-// variant 12 + (NC - 1): v3 kernels
-hipError_t launch_scan3(int nc, const uint8_t *arena, const ScanItem *items, uint32_t nitems,
+// Kernel configuration `code` (RCDC_SCAN_VARIANT, default kDefaultScanCode):
+// 100 * (group == 8) + 10 * ring + pair; + 1000: 768 threads.  Measured on
+// the C2 workload (profiles/r01_scan4_ab.txt): 41 = ring of 4 64-B units,
+// 128-B loads, groups of 16, 1024 threads is the fastest.  deg 53 uses the compile-time index shift, other degrees the
+// generic path; avg < 2^16 the masked prefilter.
+template <int R, bool PAIR, int THREADS, int G>
+static hipError_t launch4(const uint8_t *arena, const ScanItem *items, uint32_t nitems,
+                          const uint64_t *gtab, const ScanParams &prm, uint4 *sums,
+                          uint64_t *item_masks, uint32_t blocks, hipStream_t stream) {
+    const bool small = prm.mask < 0xFFFFu;
+    if (prm.idx_shift == 21 && !small)
+        hipLaunchKernelGGL((rcdc_scan_kernel<R, PAIR, THREADS, 13, false, G>), dim3(blocks),
+                           dim3(THREADS), 0, stream, arena, items, nitems, gtab, prm, sums,
+                           item_masks);
+    else if (small)
+        hipLaunchKernelGGL((rcdc_scan_kernel<R, PAIR, THREADS, -1, true, G>), dim3(blocks),
+                           dim3(THREADS), 0, stream, arena, items, nitems, gtab, prm, sums,
+                           item_masks);
+    else
+        hipLaunchKernelGGL((rcdc_scan_kernel<R, PAIR, THREADS, -1, false, G>), dim3(blocks),
+                           dim3(THREADS), 0, stream, arena, items, nitems, gtab, prm, sums,
+                           item_masks);
+    return hipGetLastError();
+}
+
+int scan_threads(int code) { return code >= 1000 ? 768 : 1024; }
+
+hipError_t launch_scan(int code, const uint8_t *arena, const ScanItem *items, uint32_t nitems,
                         const uint64_t *gtab, const ScanParams &prm, uint4 *sums,
                         uint64_t *item_masks, uint32_t blocks, hipStream_t stream) {
     if (nitems == 0) return hipSuccess;
-#define RCDC_ABL(NC_, T_, A_)                                                                  \
-    case (NC_) + 10 * (A_):                                                                  \
-        hipLaunchKernelGGL((rcdc_scan3_kernel<NC_, T_, A_>), dim3(blocks), dim3(T_), 0, stream, \
-                           arena, items, nitems, gtab, prm, sums, item_masks);                \
-        return hipGetLastError();
-    switch (nc) {
-        RCDC_ABL(1, 1024, 1) RCDC_ABL(1, 1024, 3) RCDC_ABL(1, 1024, 7) RCDC_ABL(1, 1024, 15)
-        RCDC_ABL(1, 1024, 4) RCDC_ABL(1, 1024, 9)
-        RCDC_ABL(2, 1024, 1) RCDC_ABL(2, 1024, 3) RCDC_ABL(2, 1024, 7) RCDC_ABL(2, 1024, 15)
-        RCDC_ABL(1, 1024, 16) RCDC_ABL(2, 1024, 16)
-        default: break;
+    switch (code) {
+        case 30: return launch4<3, false, 1024, 16>(arena, items, nitems, gtab, prm, sums, item_masks, blocks, stream);
+        case 50: return launch4<5, false, 1024, 16>(arena, items, nitems, gtab, prm, sums, item_masks, blocks, stream);
+        case 150: return launch4<5, false, 1024, 8>(arena, items, nitems, gtab, prm, sums, item_masks, blocks, stream);
+        case 130: return launch4<3, false, 1024, 8>(arena, items, nitems, gtab, prm, sums, item_masks, blocks, stream);
+        case 41: return launch4<4, true, 1024, 16>(arena, items, nitems, gtab, prm, sums, item_masks, blocks, stream);
+        case 141: return launch4<4, true, 1024, 8>(arena, items, nitems, gtab, prm, sums, item_masks, blocks, stream);
+        case 1161: return launch4<6, true, 768, 8>(arena, items, nitems, gtab, prm, sums, item_masks, blocks, stream);
+        default: return hipErrorInvalidValue;
     }
-#undef RCDC_ABL
-    switch (nc) {
-        case 1:
-            hipLaunchKernelGGL((rcdc_scan3_kernel<1, 1024>), dim3(blocks), dim3(1024), 0, stream,
-                               arena, items, nitems, gtab, prm, sums, item_masks);
-            break;
-        case 2:
-            hipLaunchKernelGGL((rcdc_scan3_kernel<2, 1024>), dim3(blocks), dim3(1024), 0, stream,
-                               arena, items, nitems, gtab, prm, sums, item_masks);
-            break;
-        default:
-            hipLaunchKernelGGL((rcdc_scan3_kernel<3, 768>), dim3(blocks), dim3(768), 0, stream,
-                               arena, items, nitems, gtab, prm, sums, item_masks);
-            break;
-    }
-    return hipGetLastError();
 }
 
 }  // namespace rcdc

@@ -1,0 +1,89 @@
+"""Multi-GPU sharding of independent streams.
+
+rustic chunks every file independently, one ChunkIter per file on pariter
+workers (crates/core/src/archiver.rs:195, file_archiver.rs:144-160), so the
+path shards by file with no data exchange: each rank (one process per GPU,
+torch.distributed) chunks the files assigned to it and only the cut lists
+travel, once, to the rank that hands them on (the packer side).
+
+  assign_lpt(lens, world)          largest-first onto the least-loaded rank
+  local_streams(lens, rank, world) this rank's stream indices (deterministic)
+  gather_cuts(local, rank, world)  all ranks' {index: cuts} -> input order
+"""
+from __future__ import annotations
+
+import heapq
+from typing import Callable, Dict, List, Optional, Sequence
+
+import numpy as np
+
+
+def assign_lpt(lens: Sequence[int], world: int) -> List[List[int]]:
+    """Longest-processing-time-first assignment of streams to `world` ranks.
+
+    Streams sorted by length (descending, index breaks ties) each go to the
+    rank with the fewest bytes so far (lowest rank breaks ties).  The result
+    is a pure function of (lens, world), so every rank computes the same
+    assignment without communication.  Max load <= 4/3 of optimal.
+    """
+    if world < 1:
+        raise ValueError("world size must be >= 1")
+    order = sorted(range(len(lens)), key=lambda i: (-int(lens[i]), i))
+    heap = [(0, r) for r in range(world)]
+    out: List[List[int]] = [[] for _ in range(world)]
+    for i in order:
+        load, r = heapq.heappop(heap)
+        out[r].append(i)
+        heapq.heappush(heap, (load + int(lens[i]), r))
+    for r in range(world):
+        out[r].sort()
+    return out
+
+
+def local_streams(lens: Sequence[int], rank: int, world: int) -> List[int]:
+    return assign_lpt(lens, world)[rank]
+
+
+def gather_cuts(local: Dict[int, np.ndarray], n_streams: int, group=None,
+                dst: Optional[int] = None) -> Optional[List[np.ndarray]]:
+    """Collect every rank's {stream index: cut offsets} into input order.
+
+    One all_gather_object (or gather_object to `dst`) of the per-rank
+    results; this is the only collective of the sharded path and it moves
+    the outputs (8 B per cut), never the stream bytes.  Returns the full
+    list on every rank (dst None) or on `dst` only.
+    """
+    import torch.distributed as dist
+    payload = {int(k): np.asarray(v, dtype=np.uint64) for k, v in local.items()}
+    world = dist.get_world_size(group)
+    if dst is None:
+        parts: list = [None] * world
+        dist.all_gather_object(parts, payload, group=group)
+    else:
+        parts = [None] * world if dist.get_rank(group) == dst else None
+        dist.gather_object(payload, parts, dst=dst, group=group)
+        if parts is None:
+            return None
+    out: List[Optional[np.ndarray]] = [None] * n_streams
+    for p in parts:
+        for k, v in p.items():
+            if out[k] is not None:
+                raise RuntimeError(f"stream {k} chunked by two ranks")
+            out[k] = v
+    missing = [i for i, v in enumerate(out) if v is None]
+    if missing:
+        raise RuntimeError(f"streams {missing[:8]} not chunked by any rank")
+    return out  # type: ignore[return-value]
+
+
+def chunk_sharded(lens: Sequence[int], rank: int, world: int,
+                  chunk_local: Callable[[List[int]], Dict[int, np.ndarray]],
+                  group=None) -> List[np.ndarray]:
+    """Chunk all streams over `world` ranks: this rank runs `chunk_local` on
+    its LPT share (the device path: rustic_core_amd.device.chunk_device over
+    an arena holding those streams) and all ranks receive every cut list."""
+    mine = local_streams(lens, rank, world)
+    local = chunk_local(mine)
+    if set(local) != set(mine):
+        raise RuntimeError("chunk_local returned a different stream set")
+    return gather_cuts(local, len(lens), group=group)

@@ -1,0 +1,110 @@
+"""CPU: pin the oracle (oracle/cdc_ref.c, oracle/pyref.py) to the reference's
+own golden vectors before anything is compared against it.
+
+Fixtures (tests/golden/reference_snapshots.json, made by make_golden.py from
+the reference's insta snapshots):
+  crates/core/src/chunker/rabin.rs:341-358      chunk_random (29 x (len, sha256))
+  crates/core/src/chunker/rabin.rs:360-385      chunk_empty / _wrong_hint / chunk_zeros
+  crates/core/src/chunker/fixed_size.rs:82-102  chunk-size1048576 / chunk-size1045504
+The random input is rand 0.10 StdRng::seed_from_u64(23) (ChaCha12), restated
+in cdc_ref_stdrng_fill; the FixedSize snapshots pin that stream on their own.
+"""
+import hashlib
+import json
+import os
+
+import numpy as np
+import pytest
+
+GOLD = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "reference_snapshots.json")))
+
+
+def _lens_hashes(data: np.ndarray, cuts) -> list:
+    out, s = [], 0
+    for c in cuts:
+        c = int(c)
+        out.append([c - s, hashlib.sha256(data[s:c].tobytes()).hexdigest()])
+        s = c
+    return out
+
+
+@pytest.fixture(scope="module")
+def random32(oracle_mod):
+    g = GOLD["rabin_chunk_random"]
+    return oracle_mod.stdrng_bytes(g["seed"], g["size"])
+
+
+def test_rabin_chunk_random_snapshot(oracle_mod, random32):
+    g = GOLD["rabin_chunk_random"]
+    cuts = oracle_mod.chunk_cuts(random32, int(g["poly"], 16), g["min"], g["avg"], g["max"])
+    assert _lens_hashes(random32, cuts) == g["chunks"]
+
+
+def test_rabin_chunk_random_owned_mode(oracle_mod, random32):
+    """Reference-equivalent mode (owned chunks, 4 KiB reads) = same cuts."""
+    g = GOLD["rabin_chunk_random"]
+    a = oracle_mod.chunk_cuts(random32, int(g["poly"], 16), g["min"], g["avg"], g["max"])
+    b = oracle_mod.chunk_cuts_owned(random32, int(g["poly"], 16), g["min"], g["avg"], g["max"])
+    assert np.array_equal(a, b)
+
+
+@pytest.mark.parametrize("entry", GOLD["fixed_chunk_random"], ids=lambda e: str(e["chunk_size"]))
+def test_fixed_size_snapshots(oracle_mod, random32, entry):
+    assert entry["seed"] == GOLD["rabin_chunk_random"]["seed"]
+    cuts = oracle_mod.fixed_cuts(entry["size"], entry["chunk_size"])
+    assert _lens_hashes(random32[: entry["size"]], cuts) == entry["chunks"]
+
+
+def test_known_answers(oracle_mod):
+    ka = GOLD["known_answers"]
+    assert len(oracle_mod.chunk_cuts(np.zeros(0, np.uint8))) == ka["chunk_empty"]["chunks"] == 0
+    zeros = np.zeros(4 << 20, np.uint8)
+    cuts = oracle_mod.chunk_cuts(zeros)
+    assert int(cuts[0]) == ka["chunk_zeros"]["first_chunk_len"]
+    # every zero chunk is exactly min long (fp(0...0) = 0 hits at s + min)
+    assert np.all(np.diff(np.concatenate([[0], cuts])) == 512 * 1024)
+
+
+def test_stdrng_skip_consistent(oracle_mod):
+    full = oracle_mod.stdrng_bytes(7, 1 << 16)
+    for skip in (0, 64, 128, 4096, 4096 + 64 * 7):
+        part = oracle_mod.stdrng_bytes(7, 1000, skip=skip)
+        assert np.array_equal(part, full[skip:skip + 1000])
+
+
+@pytest.mark.parametrize("params", [(256, 64, 1024), (512, 128, 2048), (1024, 512, 1024)])
+def test_c_oracle_matches_pure_python(oracle_mod, params):
+    """Two independent restatements of rabin.rs:107-191 agree: the C oracle
+    (literal ring-window Rabin64) and pyref (closed-form fp per window)."""
+    from oracle import pyref
+    avg, mn, mx = params
+    rng = np.random.default_rng(avg)
+    parts = [rng.integers(0, 256, 3000, dtype=np.uint8), np.zeros(1500, np.uint8),
+             rng.integers(0, 4, 2500, dtype=np.uint8)]
+    data = np.concatenate(parts)
+    c = oracle_mod.chunk_cuts(data, oracle_mod.DEFAULT_POLY, mn, avg, mx)
+    p = pyref.chunk_cuts(data.tobytes(), oracle_mod.DEFAULT_POLY, mn, avg, mx)
+    assert list(map(int, c)) == list(p)
+
+
+def test_candidates_match_window_fp(oracle_mod):
+    """cand(p) = fp(b[p-64, p)) & mask == 0 per position."""
+    from oracle import pyref
+    rng = np.random.default_rng(5)
+    data = rng.integers(0, 256, 3000, dtype=np.uint8)
+    mask = 15  # dense candidates
+    flags = oracle_mod.candidates(data, 64, 2900, oracle_mod.DEFAULT_POLY, mask)
+    want = [(pyref.fp(data[p - 64:p].tobytes(), oracle_mod.DEFAULT_POLY) & mask) == 0
+            for p in range(64, 2964)]
+    assert list(map(bool, flags)) == want
+
+
+@pytest.mark.parametrize("avg,mn,mx,ok", [
+    (1 << 20, 1 << 19, 1 << 23, True),
+    (1 << 20, 1 << 20, 1 << 20, True),
+    ((1 << 20) + 1, 1 << 19, 1 << 23, False),   # not a power of 2 (rabin.rs:22)
+    (1 << 20, (1 << 20) + 1, 1 << 23, False),   # min > avg (rabin.rs:29)
+    (1 << 20, 1 << 19, (1 << 20) - 1, False),   # max < avg (rabin.rs:35)
+])
+def test_check_params(oracle_mod, avg, mn, mx, ok):
+    assert oracle_mod.check_params(avg, mn, mx) == ok
