@@ -102,8 +102,9 @@ def _cpu_model() -> str:
 
 def pmc_traffic():
     """Per-launch HBM bytes of the scan kernel from the committed rocprofv3
-    PMC summary (profiles/pmc_scan.json), corrected per MI355X_MICROARCH.md
-    (FETCH_SIZE x 2 on gfx950 streaming reads); None if absent."""
+    PMC summary (profiles/pmc_scan.json: FETCH_SIZE + WRITE_SIZE converted
+    with the calibration for this access pattern, profiles/r01_pmc_hbm.txt);
+    (None, None) if absent."""
     p = os.path.join(ROOT, "profiles", "pmc_scan.json")
     try:
         d = json.load(open(p))
@@ -169,12 +170,16 @@ def main():
     total_bytes = step_bytes * args.steps * world
     value = total_bytes / el_max / GiB
 
-    # dominant kernel (scan): algorithmic bytes per launch = bytes it must
-    # hash = sum(N - min) (the reference never hashes a chunk's first min
-    # bytes; DESIGN.md "Roofline"), over its mean event-timed duration.
+    # dominant kernel (scan), HIP events on its launch stream over the timed
+    # region.  Algorithmic bytes per launch:
+    # 1 byte read per INPUT byte -> achieved = input bytes / scan time.  The
+    # kernel physically reads only the bytes it must hash, sum(N - min) (the
+    # reference never hashes a chunk's first min bytes), plus 64 B of warm-up
+    # per segment: that rate and the PMC-measured HBM traffic are reported
+    # beside it.
     hashed = int(sum(max(int(x) - MIN, 0) for x in lens))
     scan_s = scan_ms / max(runs, 1) / 1e3
-    achieved = hashed / scan_s / 1e9
+    achieved = step_bytes / scan_s / 1e9
     traffic, pmc = pmc_traffic()
     roofline = {
         "bound": "hbm",
@@ -184,12 +189,15 @@ def main():
         "unit": "GB/s",
         "frac": round(achieved / HBM_PEAK_GBS, 4),
         "traffic": traffic,
-        "algorithmic_bytes_per_launch": hashed,
+        "algorithmic_bytes_per_launch": step_bytes,
         "scan_us_per_launch": round(scan_s * 1e6, 2),
         "resolve_us_per_launch": round(resolve_ms / max(runs, 1) * 1e3, 2),
-        "achieved_input_gbs": round(step_bytes / scan_s / 1e9, 1),
+        "hashed_bytes_per_launch": hashed,
+        "achieved_hashed_gbs": round(hashed / scan_s / 1e9, 1),
+        "frac_hashed": round(hashed / scan_s / 1e9 / HBM_PEAK_GBS, 4),
         "segment_bytes": info["segment_bytes"],
         "bytes_read_by_lanes": info["scanned_bytes"] + 64 * info["segments"],
+        "limiter": "VALU issue (DESIGN.md 3: ~95% of the measured compute ceiling)",
     }
     if pmc:
         roofline["traffic_source"] = pmc.get("source")

@@ -21,7 +21,7 @@ constexpr int kTableRepl = 32;       // per-lane table copies: bank = lane % 32
 constexpr uint32_t kTableBytes = 256u * kTableRepl * 8u;  // 64 KiB per table
 constexpr uint32_t kLdsBytes = 2u * kTableBytes;          // OUT + MOD
 constexpr uint32_t kUnit = 64;       // bytes per register unit (16 dwords)
-constexpr int kDefaultScanCode = 41; // rcdc_scan.hip launch_scan configuration
+constexpr int kDefaultScanCode = 30; // rcdc_scan.hip launch_scan configuration
 
 // One wave of work: segments [sum_idx, sum_idx + nvalid) of one stream.
 // Lane l scans bytes [q0 + l*S, q0 + l*S + 64 + S) of the arena and tests

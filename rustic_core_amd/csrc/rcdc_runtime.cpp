@@ -189,9 +189,12 @@ uint32_t choose_segment(const std::vector<uint64_t> &spans, int cus, int chains,
     return best;
 }
 
-// Arena offset of lane 0's first byte for a stream at `off`: 16-aligned, or
-// aligned to `align` (a power of two <= 128) when that does not start
-// before the stream's first byte - 64.
+// Arena offset of lane 0's first byte for a stream at `off`: aligned to
+// `align` (a power of two, 16..128) unless that would start before the
+// stream's first byte - 64, then 16-aligned.  64 (default) puts every 64-B
+// register unit of every lane in one cache-line half: the unaligned layout
+// fetched each line twice (profiles/r01_pmc_hbm.txt).  128 adds up to 63
+// bytes per stream, which on 1 MiB streams costs an extra segment.
 static inline uint64_t stream_q0(uint64_t off, uint64_t pos_lo, uint64_t align) {
     const uint64_t x = off + pos_lo - 65;
     const uint64_t q = x & ~(align - 1);
@@ -199,9 +202,9 @@ static inline uint64_t stream_q0(uint64_t off, uint64_t pos_lo, uint64_t align) 
 }
 
 static uint64_t q0_align() {
-    const char *e = getenv("RCDC_Q0_ALIGN");  // experiments: 16 .. 128
-    const uint64_t v = e ? (uint64_t)atoll(e) : 16;
-    return (v == 128 || v == 64 || v == 32) ? v : (uint64_t)16;
+    const char *e = getenv("RCDC_Q0_ALIGN");  // experiments: 16, 32, 64, 128
+    const uint64_t v = e ? (uint64_t)atoll(e) : 64;
+    return (v == 128 || v == 64 || v == 32 || v == 16) ? v : (uint64_t)64;
 }
 
 rcdc_status plan_build(rcdc_ctx *ctx, rcdc_plan *pl, const uint64_t *offs, const uint64_t *lens,

@@ -17,8 +17,10 @@
 //   * every operand of the hot loop is a VGPR or an inline constant (SGPR
 //     operands and 64-bit shifts issue at half rate on gfx950).
 //   * loads: each lane streams its own segment in 64-B units (4 x
-//     buffer_load_dwordx4, or 8 = one 128-B line with PAIR), a ring of R
-//     units so loads run R-2 units ahead; no load beyond the segment.
+//     buffer_load_dwordx4 into one cache-line half: the runtime aligns lane
+//     starts to 64 B), a ring of R units so loads run R-2 units ahead; no
+//     load beyond the segment.  PAIR issues two units (one 128-B line) at
+//     once; it only paid off while lane starts were unaligned.
 #include <hip/hip_runtime.h>
 
 #include "rcdc_internal.h"
@@ -279,8 +281,9 @@ namespace rcdc {
 
 // Kernel configuration `code` (RCDC_SCAN_VARIANT, default kDefaultScanCode):
 // 100 * (group == 8) + 10 * ring + pair; + 1000: 768 threads.  Measured on
-// the C2 workload (profiles/r01_scan4_ab.txt): 41 = ring of 4 64-B units,
-// 128-B loads, groups of 16, 1024 threads is the fastest.  deg 53 uses the compile-time index shift, other degrees the
+// the C2 workload (profiles/r01_scan4_ab.txt) with 64-B aligned lane starts:
+// 30 (ring of 3 64-B units, groups of 16, 1024 threads) 174 us, 130 (groups
+// of 8) the same, 41 (ring of 4, 128-B loads) 193 us, 50 (ring of 5) 204 us.  deg 53 uses the compile-time index shift, other degrees the
 // generic path; avg < 2^16 the masked prefilter.
 template <int R, bool PAIR, int THREADS, int G>
 static hipError_t launch4(const uint8_t *arena, const ScanItem *items, uint32_t nitems,
