@@ -57,6 +57,24 @@ struct ScanParams {
     uint32_t pad;
 };
 
+// Resolver work: one wave hops from `start` until its first cut >= `stop`.
+// direct: a whole stream, cuts straight to the stream's output slots;
+// otherwise a speculative piece of a long stream (piece_cuts[out_base ..]).
+struct ResolveUnit {
+    uint64_t start, stop;
+    uint64_t out_base;
+    uint32_t out_cap;
+    uint32_t stream;
+    uint32_t direct;
+    uint32_t pad;
+};
+static_assert(sizeof(ResolveUnit) == 40, "ResolveUnit is 40 B");
+
+// One long stream: pieces units[unit0 .. unit0 + npieces).
+struct StitchDesc {
+    uint32_t stream, unit0, npieces, pad;
+};
+
 struct ResolveParams {
     uint64_t min_size, max_size;
     uint32_t seg_bytes;

@@ -11,6 +11,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cmath>
 #include <cerrno>
 #include <cstdarg>
 #include <cstdio>
@@ -28,9 +29,11 @@ int scan_threads(int code);
 hipError_t launch_scan(int code, const uint8_t *arena, const ScanItem *items, uint32_t nitems,
                        const uint64_t *gtab, const ScanParams &prm, uint4 *sums,
                        uint64_t *item_masks, uint32_t blocks, hipStream_t stream);
-hipError_t launch_resolve(const uint8_t *arena, const StreamDesc *sds, uint32_t nstreams,
+hipError_t launch_resolve(const uint8_t *arena, const StreamDesc *sds, const ResolveUnit *units,
+                          uint32_t nunits, const StitchDesc *stitches, uint32_t nstitch,
                           const uint64_t *gtab, const ResolveParams &prm, const uint4 *sums,
                           const uint64_t *item_masks, uint64_t *cuts, uint64_t *counts,
+                          uint64_t *piece_cuts, uint64_t *piece_counts, uint64_t *stats,
                           hipStream_t stream);
 }  // namespace rcdc
 
@@ -103,9 +106,17 @@ struct rcdc_plan {
     std::vector<ScanItem> items;
     std::vector<StreamDesc> sds;
     std::vector<uint64_t> cut_base;
+    std::vector<ResolveUnit> units;
+    std::vector<StitchDesc> stitches;
+    uint64_t npiece_cuts = 0;
     // device
     ScanItem *d_items = nullptr;
     StreamDesc *d_sds = nullptr;
+    ResolveUnit *d_units = nullptr;
+    StitchDesc *d_stitches = nullptr;
+    uint64_t *d_piece_cuts = nullptr;
+    uint64_t *d_piece_counts = nullptr;
+    uint64_t cap_units = 0, cap_stitches = 0, cap_piece_cuts = 0, cap_piece_counts = 0;
     uint4 *d_sums = nullptr;
     uint64_t *d_masks = nullptr;
     uint64_t *d_cuts = nullptr;
@@ -207,6 +218,61 @@ static uint64_t q0_align() {
     return (v == 128 || v == 64 || v == 32 || v == 16) ? v : (uint64_t)64;
 }
 
+// Resolver work list.  A stream of N >= kPieceStreams * min bytes is cut into
+// pieces of Lp bytes (a multiple of min, >= 16 min), resolved speculatively in
+// parallel and stitched (rcdc_resolve.hip).  Lp ~ sqrt(N * min / 2) balances
+// the hops of one piece (Lp / chunk) against the stitch's per-piece step.
+constexpr uint64_t kPieceStreams = 64;  // in units of min
+
+static uint64_t piece_bytes(uint64_t N, uint64_t mn) {
+    if (const char *e = getenv("RCDC_PIECE_BYTES")) {  // experiments; 0 disables
+        const uint64_t v = (uint64_t)atoll(e);
+        return v ? std::max<uint64_t>(v / mn, 1) * mn : 0;
+    }
+    if (N < kPieceStreams * mn) return 0;
+    const double lp = std::sqrt((double)N * (double)mn / 2.0);
+    return std::max<uint64_t>((uint64_t)(lp / (double)mn), 16) * mn;
+}
+
+void build_resolve_units(rcdc_plan *pl, uint64_t mn) {
+    pl->units.clear();
+    pl->stitches.clear();
+    pl->npiece_cuts = 0;
+    for (uint32_t i = 0; i < pl->n; i++) {
+        const StreamDesc &d = pl->sds[i];
+        const uint64_t N = d.n;
+        const uint64_t Lp = piece_bytes(N, mn);
+        if (Lp == 0 || N <= 2 * Lp) {
+            ResolveUnit u{};
+            u.start = 0;
+            u.stop = N;
+            u.out_base = d.cut_base;
+            u.out_cap = (uint32_t)std::min<uint64_t>(d.cut_cap, 0xFFFFFFFFu);
+            u.stream = i;
+            u.direct = 1;
+            pl->units.push_back(u);
+            continue;
+        }
+        StitchDesc sd{};
+        sd.stream = i;
+        sd.unit0 = (uint32_t)pl->units.size();
+        for (uint64_t a = 0; a < N; a += Lp) {
+            ResolveUnit u{};
+            u.start = a;
+            u.stop = std::min(a + Lp, N);
+            u.out_base = pl->npiece_cuts;
+            // chunks >= min except the last: (stop - start) / min + the crossing cut
+            u.out_cap = (uint32_t)((u.stop - u.start) / mn + 3);
+            u.stream = i;
+            u.direct = 0;
+            pl->npiece_cuts += u.out_cap;
+            pl->units.push_back(u);
+        }
+        sd.npieces = (uint32_t)pl->units.size() - sd.unit0;
+        pl->stitches.push_back(sd);
+    }
+}
+
 rcdc_status plan_build(rcdc_ctx *ctx, rcdc_plan *pl, const uint64_t *offs, const uint64_t *lens,
                        uint32_t n, uint64_t arena_len) {
     const uint64_t pos_lo = ctx->min + kWindow;  // first pure-window test position
@@ -268,6 +334,7 @@ rcdc_status plan_build(rcdc_ctx *ctx, rcdc_plan *pl, const uint64_t *offs, const
     }
     pl->nseg = nseg;
     pl->ncuts = ncut;
+    build_resolve_units(pl, ctx->min);
     const uint64_t supers = (pl->items.size() + nc - 1) / nc;
     const uint64_t waves_needed = (supers + nthreads / 64 - 1) / (nthreads / 64);
     pl->blocks = (uint32_t)std::min<uint64_t>(waves_needed, (uint64_t)std::max(ctx->num_cus, 1));
@@ -280,6 +347,16 @@ rcdc_status plan_build(rcdc_ctx *ctx, rcdc_plan *pl, const uint64_t *offs, const
     if ((st = ensure_dev(&pl->d_masks, &pl->cap_masks, pl->items.size()))) return st;
     if ((st = ensure_dev(&pl->d_cuts, &pl->cap_cuts, ncut))) return st;
     if ((st = ensure_dev(&pl->d_counts, &pl->cap_counts, n))) return st;
+    if ((st = ensure_dev(&pl->d_units, &pl->cap_units, pl->units.size()))) return st;
+    if ((st = ensure_dev(&pl->d_stitches, &pl->cap_stitches, pl->stitches.size()))) return st;
+    if ((st = ensure_dev(&pl->d_piece_cuts, &pl->cap_piece_cuts, pl->npiece_cuts))) return st;
+    if ((st = ensure_dev(&pl->d_piece_counts, &pl->cap_piece_counts, pl->units.size()))) return st;
+    if (!pl->units.empty())
+        HIP_TRY(hipMemcpy(pl->d_units, pl->units.data(), pl->units.size() * sizeof(ResolveUnit),
+                          hipMemcpyHostToDevice));
+    if (!pl->stitches.empty())
+        HIP_TRY(hipMemcpy(pl->d_stitches, pl->stitches.data(),
+                          pl->stitches.size() * sizeof(StitchDesc), hipMemcpyHostToDevice));
     if (!pl->items.empty())
         HIP_TRY(hipMemcpy(pl->d_items, pl->items.data(), pl->items.size() * sizeof(ScanItem),
                           hipMemcpyHostToDevice));
@@ -323,8 +400,11 @@ rcdc_status plan_run(rcdc_plan *pl, const void *d_arena, hipStream_t stream) {
     rp.seg_bytes = pl->seg_bytes;
     rp.mask = (uint32_t)(ctx->avg - 1);
     rp.shift = (uint32_t)(ctx->deg - 8);
-    HIP_TRY(launch_resolve((const uint8_t *)d_arena, pl->d_sds, pl->n, ctx->d_tables, rp,
-                           pl->d_sums, pl->d_masks, pl->d_cuts, pl->d_counts, stream));
+    HIP_TRY(launch_resolve((const uint8_t *)d_arena, pl->d_sds, pl->d_units,
+                           (uint32_t)pl->units.size(), pl->d_stitches,
+                           (uint32_t)pl->stitches.size(), ctx->d_tables, rp, pl->d_sums,
+                           pl->d_masks, pl->d_cuts, pl->d_counts, pl->d_piece_cuts,
+                           pl->d_piece_counts, nullptr, stream));
     if (ev) HIP_TRY(hipEventRecord(ev[2], stream));
     HIP_TRY(hipEventRecord(pl->done, stream));
     pl->ran = true;
@@ -368,6 +448,10 @@ void plan_free(rcdc_plan *pl) {
     (void)hipFree(pl->d_masks);
     (void)hipFree(pl->d_cuts);
     (void)hipFree(pl->d_counts);
+    (void)hipFree(pl->d_units);
+    (void)hipFree(pl->d_stitches);
+    (void)hipFree(pl->d_piece_cuts);
+    (void)hipFree(pl->d_piece_counts);
     if (pl->done) (void)hipEventDestroy(pl->done);
     for (hipEvent_t e : pl->tev) (void)hipEventDestroy(e);
     delete pl;

@@ -222,3 +222,56 @@ def test_chunkiter_large_mixed(gpu_ctx):
     cfg = ConfigFile.new(2, oracle.DEFAULT_POLY)
     lens = [len(c) for c in ChunkIter.from_config(cfg, b.tobytes(), 0)]
     assert np.array_equal(np.cumsum(lens, dtype=np.uint64), oracle.chunk_cuts(b))
+
+
+# ------------------------------------------------------- long streams: pieces
+def _phase_zeros(n, phase, seed):
+    """random prefix of `phase` bytes, then zeros: the speculative chains from
+    piece starts (multiples of min) run out of phase with the true chain."""
+    rng = np.random.default_rng(seed)
+    a = np.zeros(n, np.uint8)
+    a[:phase] = rng.integers(0, 256, phase, dtype=np.uint8)
+    return a
+
+
+@pytest.mark.parametrize("kind", ["random", "zeros", "mixed", "phase_zeros", "lowent"])
+def test_long_stream_pieces_small_params(kind, monkeypatch):
+    """Speculative pieces + stitch (rcdc_resolve.hip) on long streams with
+    many pieces: bit-exact whatever the merge behaviour."""
+    mn, avg, mx = 4096, 16384, 65536
+    monkeypatch.setenv("RCDC_PIECE_BYTES", str(16 * mn))
+    rng = np.random.default_rng(11)
+    n = 6 * MiB + 777
+    if kind == "random":
+        data = rng.integers(0, 256, n, dtype=np.uint8)
+    elif kind == "zeros":
+        data = np.zeros(n, np.uint8)
+    elif kind == "mixed":
+        data = _mixed(5, n)
+    elif kind == "phase_zeros":
+        data = _phase_zeros(n, 1234, 3)
+    else:
+        data = rng.integers(0, 3, n, dtype=np.uint8)
+    ctx = _ctx(mn, avg, mx)
+    got = _device_cuts(ctx, [data, data[: n // 3], data[5:]])
+    for g, b in zip(got, [data, data[: n // 3], data[5:]]):
+        assert np.array_equal(g, oracle.chunk_cuts(b, oracle.DEFAULT_POLY, mn, avg, mx))
+
+
+@pytest.mark.parametrize("kind", ["random", "zeros", "phase_zeros", "mixed"])
+def test_long_stream_default_params(gpu_ctx, kind, monkeypatch):
+    """Default parameters, 160 MiB streams: the automatic piece size (and a
+    forced small one) give the oracle's cuts."""
+    n = 160 * MiB + 4097
+    if kind == "random":
+        data = oracle.stdrng_bytes(77, n)
+    elif kind == "zeros":
+        data = np.zeros(n, np.uint8)
+    elif kind == "phase_zeros":
+        data = _phase_zeros(n, 3 * MiB + 99, 4)
+    else:
+        data = _mixed(9, n)
+    want = oracle.chunk_cuts(data)
+    assert np.array_equal(_device_cuts(gpu_ctx, [data])[0], want)
+    monkeypatch.setenv("RCDC_PIECE_BYTES", str(8 * MiB))
+    assert np.array_equal(_device_cuts(gpu_ctx, [data])[0], want)
