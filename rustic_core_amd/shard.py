@@ -87,3 +87,89 @@ def chunk_sharded(lens: Sequence[int], rank: int, world: int,
     if set(local) != set(mine):
         raise RuntimeError("chunk_local returned a different stream set")
     return gather_cuts(local, len(lens), group=group)
+
+
+# ---------------------------------------------------------------- one long stream
+def slice_bounds(total: int, world: int, min_size: int, max_size: int):
+    """Split one stream of `total` bytes into `world` slices [a_r, b_r) whose
+    starts are multiples of min (long zero runs then stay in phase, every
+    chunk there being exactly min), plus each rank's readable extent
+    [a_r, e_r): the slice and a halo of max + 64 bytes from the next slice,
+    enough for the chain that starts before b_r to reach its crossing cut
+    exactly (no hop from s < b_r looks past s + max + 63).
+    """
+    per = -(-total // world)
+    per = -(-per // min_size) * min_size
+    out = []
+    for r in range(world):
+        a = min(r * per, total)
+        b = min(a + per, total)
+        e = min(b + max_size + 64, total)
+        out.append((a, b, e))
+    return out
+
+
+def _stitch_lists(bounds, lists, total):
+    """Walk the ranks in order.  lists[r] = (entry, cuts): cuts of the chain
+    that starts at `entry` (absolute), ending with its first cut >= b_r (or
+    total).  Returns (true cut lists per rank, first rank that could not be
+    merged and the true entry it needs, or None)."""
+    true = []
+    x = 0  # true chain position entering slice r
+    for r, (a, b, _) in enumerate(bounds):
+        entry, cuts = lists[r]
+        if x >= b or a >= b:
+            true.append(np.zeros(0, np.uint64))
+            continue
+        cuts = np.asarray(cuts, dtype=np.uint64)
+        if x == entry:
+            keep = cuts
+        else:
+            i = int(np.searchsorted(cuts, x))
+            if i < len(cuts) and int(cuts[i]) == x:
+                keep = cuts[i + 1:]
+            else:
+                return true, (r, x)
+        true.append(keep)
+        if len(keep):
+            x = int(keep[-1])
+    return true, None
+
+
+def chunk_long_stream_sharded(total: int, rank: int, world: int, min_size: int,
+                              max_size: int, chunk_from: Callable[[int], np.ndarray],
+                              group=None) -> np.ndarray:
+    """Chunk ONE stream of `total` bytes split over `world` ranks
+    (SURVEY.md 8(e), C5).  Rank r owns bytes [a_r, e_r) (slice_bounds);
+    `chunk_from(s)` must return the absolute cuts of the chain that starts at
+    absolute position s, computed on this rank's bytes and truncated after
+    the first cut >= b_r (the device path: a plan over arena[s - a_r, e_r -
+    a_r) as an independent stream; its cuts up to the crossing are exact
+    because the halo covers s + max + 63).
+
+    Every rank chunks its slice speculatively from a_r; one all_gather of
+    the cut lists lets every rank walk the chain in order; a rank whose list
+    does not contain the true entry cut re-chunks from that entry (another
+    round).  Returns this rank's true cuts (absolute; rank 0 starts at 0).
+    """
+    import torch.distributed as dist
+    bounds = slice_bounds(total, world, min_size, max_size)
+    a, b, _ = bounds[rank]
+    entry = a
+    mine = np.asarray(chunk_from(a), dtype=np.uint64) if a < b else np.zeros(0, np.uint64)
+    distributed = world > 1 and dist.is_available() and dist.is_initialized()
+    if world > 1 and not distributed:
+        raise RuntimeError("chunk_long_stream_sharded: world > 1 needs torch.distributed")
+    while True:
+        parts: list = [None] * world
+        if distributed:
+            dist.all_gather_object(parts, (entry, mine), group=group)
+        else:
+            parts[0] = (entry, mine)
+        true, todo = _stitch_lists(bounds, parts, total)
+        if todo is None:
+            return true[rank]
+        r, x = todo
+        if r == rank:
+            entry = x
+            mine = np.asarray(chunk_from(x), dtype=np.uint64)

@@ -87,3 +87,93 @@ def test_chunk_sharded_gloo_world2(tmp_path):
     err = str(tmp_path / "err.txt")
     mp.spawn(_worker, args=(2, _free_port(), err), nprocs=2, join=True)
     assert not os.path.exists(err)
+
+
+# ------------------------------------------------- one long stream over ranks
+LPARAMS = dict(min_size=4096, avg=16384, max_size=65536)
+
+
+def _long_data(kind):
+    rng = np.random.default_rng(21)
+    n = 1_000_003
+    if kind == "zeros":
+        return np.zeros(n, np.uint8)
+    if kind == "phase_zeros":   # true chain out of phase with the slice starts
+        a = np.zeros(n, np.uint8)
+        a[:777] = rng.integers(0, 256, 777, dtype=np.uint8)
+        return a
+    if kind == "random":
+        return rng.integers(0, 256, n, dtype=np.uint8)
+    out = np.zeros(n, np.uint8)
+    i = 0
+    while i < n:
+        k = int(rng.integers(1000, 60000))
+        if rng.random() < 0.5:
+            out[i:i + k] = rng.integers(0, 256, len(out[i:i + k]), dtype=np.uint8)
+        i += k
+    return out
+
+
+def _long_worker(rank, world, port, errfile, kind):
+    import torch.distributed as dist
+    from oracle import oracle
+    from rustic_core_amd.shard import chunk_long_stream_sharded, slice_bounds
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        data = _long_data(kind)
+        total = len(data)
+        bounds = slice_bounds(total, world, LPARAMS["min_size"], LPARAMS["max_size"])
+        a, b, e = bounds[rank]
+        local = data[a:e]  # this rank's bytes only: slice + halo
+
+        def chunk_from(s):
+            cuts = oracle.chunk_cuts(local[s - a:], oracle.DEFAULT_POLY, **LPARAMS) + s
+            if e < total:  # truncate after the crossing cut (the rest sees a fake end)
+                k = int(np.searchsorted(cuts, b))
+                cuts = cuts[:k + 1]
+                assert len(cuts) and int(cuts[-1]) >= b
+            return cuts
+
+        mine = chunk_long_stream_sharded(total, rank, world, LPARAMS["min_size"],
+                                         LPARAMS["max_size"], chunk_from)
+        parts = [None] * world
+        dist.all_gather_object(parts, mine)
+        got = np.concatenate([np.asarray(p, np.uint64) for p in parts])
+        want = oracle.chunk_cuts(data, oracle.DEFAULT_POLY, **LPARAMS)
+        assert np.array_equal(got, want), (kind, len(got), len(want))
+        dist.barrier()
+    except Exception as ex:  # pragma: no cover
+        with open(errfile, "a") as f:
+            f.write(f"rank {rank}: {ex!r}\n")
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("kind", ["zeros", "phase_zeros", "random", "mixed"])
+@pytest.mark.parametrize("world", [2, 3])
+def test_long_stream_sharded_gloo(tmp_path, kind, world):
+    import torch.multiprocessing as mp
+    err = str(tmp_path / "err.txt")
+    mp.spawn(_long_worker, args=(world, _free_port(), err, kind), nprocs=world, join=True)
+    assert not os.path.exists(err)
+
+
+def test_slice_bounds():
+    from rustic_core_amd.shard import slice_bounds
+    b = slice_bounds(10_000_000, 4, 4096, 65536)
+    assert b[0][0] == 0 and b[-1][1] == 10_000_000
+    for (a, bb, e), nxt in zip(b, b[1:] + [(10_000_000, 0, 0)]):
+        assert a % 4096 == 0 and bb == nxt[0] and e == min(bb + 65536 + 64, 10_000_000)
+
+
+def test_long_stream_single_rank_no_process_group():
+    """world 1 needs no process group (bench.py C5 at N=1)."""
+    from oracle import oracle
+    from rustic_core_amd.shard import chunk_long_stream_sharded
+    data = _long_data("mixed")
+    cuts = chunk_long_stream_sharded(
+        len(data), 0, 1, LPARAMS["min_size"], LPARAMS["max_size"],
+        lambda s: oracle.chunk_cuts(data[s:], oracle.DEFAULT_POLY, **LPARAMS) + s)
+    assert np.array_equal(cuts, oracle.chunk_cuts(data, oracle.DEFAULT_POLY, **LPARAMS))
