@@ -11,6 +11,10 @@ Other SURVEY.md 8(d) configurations (--workload, not the driver's line):
   C3  64 streams x 1 GiB per GPU, mixed entropy (random runs 64 KiB-16 MiB,
       zero runs 4 KiB-16 MiB, 50/50 by bytes); --e2e adds the pinned-H2D
       rate with the copy of the next batch overlapped on a side stream.
+  C4  8192 files, sizes log-uniform in [4, 256] MiB (seed 4000, ~485 GiB),
+      LPT-sharded over the ranks (shard.assign_lpt); a step is one pass over
+      the rank's share, in HBM-resident batches when it exceeds --c4-batch
+      (each batch generated on device before its timed chunking).
   C5  one all-zero stream of 12.5 GiB per GPU (100 GiB at 8 GPUs) split
       across ranks (shard.slice_bounds, max + 64 B halos); a step includes
       the cross-rank stitch (shard.chunk_long_stream_sharded).
@@ -51,7 +55,9 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--workload", choices=["C2", "C3", "C5"], default="C2")
+    ap.add_argument("--workload", choices=["C2", "C3", "C4", "C5"], default="C2")
+    ap.add_argument("--c4-files", type=int, default=8192)
+    ap.add_argument("--c4-batch", type=float, default=96.0, help="C4: GiB per resident batch")
     ap.add_argument("--streams", type=int, default=None, help="C2: 1024, C3: 64")
     ap.add_argument("--stream-bytes", type=int, default=None,
                     help="C2: 1 MiB, C3: 1 GiB, C5: 12.5 GiB per GPU")
@@ -195,6 +201,135 @@ def pmc_traffic():
         return None, None
 
 
+def c4_files(n: int):
+    """sizes log-uniform in [4, 256] MiB, seed 4000."""
+    rng = np.random.default_rng(4000)
+    return [int(np.exp(rng.uniform(np.log(4 * MiB), np.log(256 * MiB)))) for _ in range(n)]
+
+
+def c4_fill(torch, arena, offs, files, sizes, dev):
+    """File f = uniform random bytes from a generator seeded 4000 + f."""
+    g = torch.Generator(device=dev)
+    for o, f in zip(offs, files):
+        g.manual_seed(4000 + f)
+        arena[int(o):int(o) + sizes[f]] = torch.randint(0, 256, (sizes[f],), dtype=torch.uint8,
+                                                        device=dev, generator=g)
+
+
+def run_c4(args, torch, dist, dev, rank, world, local):
+    """C4: the rank's LPT share of 8192 files, chunked in resident batches."""
+    from rustic_core_amd.chunker import Context
+    from rustic_core_amd.device import DevicePlan, pack_offsets
+    from rustic_core_amd.shard import assign_lpt
+    sizes = c4_files(args.c4_files)
+    mine = assign_lpt(sizes, world)[rank]
+    cap = int(args.c4_batch * GiB)
+    batches, cur, acc = [], [], 0
+    for f in sorted(mine, key=lambda f: -sizes[f]):
+        if cur and acc + sizes[f] > cap:
+            batches.append(cur)
+            cur, acc = [], 0
+        cur.append(f)
+        acc += sizes[f]
+    if cur:
+        batches.append(cur)
+    ctx = Context.get(POLY, MIN, AVG, MAX, device=local)
+    arena_len = max(pack_offsets([sizes[f] for f in b])[1] for b in batches) if batches else 256
+    arena = torch.empty(arena_len, dtype=torch.uint8, device=dev)
+    layouts = []
+    for b in batches:
+        offs, alen = pack_offsets([sizes[f] for f in b])
+        layouts.append((b, offs, DevicePlan(ctx, offs, [sizes[f] for f in b], alen)))
+    sptr = torch.cuda.current_stream(dev).cuda_stream
+    scan_ms = resolve_ms = 0.0
+    runs = 0
+    # warmup on the first batch
+    if layouts:
+        b, offs, plan = layouts[0]
+        c4_fill(torch, arena, offs, b, sizes, dev)
+        for _ in range(args.warmup):
+            plan.run(arena.data_ptr(), sptr)
+    torch.cuda.synchronize(dev)
+    el = 0.0
+    sample_cuts = {}
+    rng = np.random.default_rng(4001)
+    sample = set(int(x) for x in rng.choice(args.c4_files, size=min(64, args.c4_files),
+                                             replace=False))
+    for step in range(args.steps):
+        for b, offs, plan in layouts:
+            if len(layouts) > 1 or step == 0:
+                c4_fill(torch, arena, offs, b, sizes, dev)  # outside the timed span
+            if world > 1:
+                dist.barrier()
+            torch.cuda.synchronize(dev)
+            plan.set_timing(True)
+            t0 = time.perf_counter()
+            plan.run(arena.data_ptr(), sptr)
+            torch.cuda.synchronize(dev)
+            el += time.perf_counter() - t0
+            plan.set_timing(False)
+            r, sm, rm = plan.kernel_times()
+            runs += r
+            scan_ms += sm
+            resolve_ms += rm
+            if step == 0 and not args.no_parity:
+                got = plan.results()
+                for i, f in enumerate(b):
+                    if f in sample:
+                        o = int(offs[i])
+                        sample_cuts[f] = (got[i], arena[o:o + sizes[f]].cpu().numpy())
+    t = torch.tensor([el], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    el_max = float(t.item())
+    total = sum(sizes) * args.steps
+    share = sum(sizes[f] for f in mine)
+    bad = 0
+    for f, (cuts, host) in sample_cuts.items():
+        from oracle import oracle
+        bad += not np.array_equal(cuts, oracle.chunk_cuts(host, POLY, MIN, AVG, MAX))
+    checked = torch.tensor([len(sample_cuts), bad], dtype=torch.int64, device=dev)
+    if world > 1:
+        dist.all_reduce(checked)
+    if rank == 0:
+        line = {
+            "metric": METRIC, "value": round(total / el_max / GiB, 2), "unit": "GiB/s",
+            "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(el_max / args.steps * 1e3, 4), "higher_is_better": True,
+            "scaling": "strong", "vs_baseline": None, "dtype": "u8",
+            "data": "synthetic: uniform random bytes per file (torch.randint, seed 4000+file)",
+            "config": {"workload": f"C4: {args.c4_files} files, log-uniform 4-256 MiB "
+                                   f"({sum(sizes) / GiB:.1f} GiB), LPT-sharded over {world} GPU(s) "
+                                   "(BASELINE.json configs[3])",
+                       "batches_on_rank0": len(batches), "rank0_share_gib": round(share / GiB, 2),
+                       "poly": hex(POLY), "min": MIN, "avg": AVG, "max": MAX,
+                       "parallelism": f"per-file LPT sharding over {world} GPU(s), no collectives"},
+            "roofline": {"bound": "hbm", "kernel": "rcdc_scan_kernel",
+                         "achieved": round(share / (scan_ms / max(runs, 1) * len(layouts) / 1e3)
+                                           / 1e9, 1) if runs else None,
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(share / (scan_ms / max(runs, 1) * len(layouts) / 1e3) / 1e9
+                                       / HBM_PEAK_GBS, 4) if runs else None,
+                         "traffic": None,
+                         "scan_ms_per_pass": round(scan_ms / max(args.steps, 1), 3),
+                         "resolve_ms_per_pass": round(resolve_ms / max(args.steps, 1), 3)},
+            "parity": {"files_checked": int(checked[0]), "mismatches": int(checked[1]),
+                       "checker": "oracle/cdc_ref on a seeded sample of 64 files"},
+        }
+        if world == 1 and not args.no_cpu_baseline and sample_cuts:
+            from rustic_core_amd.device import pack_offsets
+            hosts = [h for _, h in sample_cuts.values()]
+            offs, alen = pack_offsets([len(h) for h in hosts])
+            buf = np.zeros(alen, np.uint8)
+            for o, h in zip(offs, hosts):
+                buf[int(o):int(o) + len(h)] = h
+            line["cpu_baseline"] = cpu_baseline(buf, offs, np.array([len(h) for h in hosts],
+                                                                    np.uint64), args.cpu_seconds)
+        print(json.dumps(line), flush=True)
+    for _, _, p in layouts:
+        p.close()
+
+
 def main():
     args = parse()
     import torch
@@ -210,6 +345,12 @@ def main():
 
     from rustic_core_amd.chunker import Context
     from rustic_core_amd.device import DevicePlan
+
+    if args.workload == "C4":
+        run_c4(args, torch, dist, dev, rank, world, local)
+        if world > 1:
+            dist.destroy_process_group()
+        return
 
     arena, offs, lens, desc = build_workload(args, torch, dev, rank, world)
     ctx = Context.get(POLY, MIN, AVG, MAX, device=local)
