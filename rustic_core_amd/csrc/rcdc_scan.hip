@@ -59,25 +59,40 @@ struct Consts {
     uint32_t tsh;       // deg - 32 (generic-degree path only)
 };
 
-// MOD table address of the top byte of a1x = hi32(h << 8 ^ out << 8).
-// TSH >= 0: compile-time deg - 40 (v_lshrrev by an inline constant + one
-// v_bitop3 (x & 0xFF00) | lwm); TSH < 0: any degree, runtime shift.
+// MOD table address of the top byte of h (h1 = hi32(h), a1 = hi32(h << 8)).
+// TSH >= 100: compile-time shift TSH - 100 = deg - 48 straight from h1, so the
+//   address does not wait for the v_alignbit (critical path per byte:
+//   v_lshrrev, v_bitop3, ds_read_b64, v_bitop3);
+// 0 <= TSH < 100: compile-time deg - 40 from a1 (v_lshrrev by an inline
+//   constant + one v_bitop3 (x & 0xFF00) | lwm);
+// TSH < 0: any degree, runtime shift of a1.
 template <int TSH>
-__device__ __forceinline__ uint32_t mod_addr(uint32_t a1x, const Consts &k) {
-    if constexpr (TSH >= 0) return __builtin_amdgcn_bitop3_b32(a1x >> TSH, k.kff00, k.lwm, kAndOr);
-    else return ((a1x >> k.tsh) << 8) | k.lwm;
+__device__ __forceinline__ uint32_t mod_addr(uint32_t h1, uint32_t a1, const Consts &k) {
+    if constexpr (TSH >= 100)
+        return __builtin_amdgcn_bitop3_b32(h1 >> (TSH - 100), k.kff00, k.lwm, kAndOr);
+    else if constexpr (TSH >= 0)
+        return __builtin_amdgcn_bitop3_b32(a1 >> TSH, k.kff00, k.lwm, kAndOr);
+    else
+        return ((a1 >> k.tsh) << 8) | k.lwm;
 }
 
 // One slide: h ^= out[o]; i = top byte; h = ((h<<8)|n) ^ mod[i]
-// with h = h1:h0, OUT table pre-shifted by 8 (see rcdc_kernels.hip).
+// with h = h1:h0 (53 bits for deg 53).
+//
+// The LDS "OUT" table holds OM[b] = b * x^512 mod P = (out[b] << 8) reduced
+// (built in the kernel prologue).  MOD is linear in its index, so
+//   mod[top(h ^ out[o])] = mod[top(h)] ^ mod[top(out[o])]
+// and the slide becomes h' = ((h << 8) | n) ^ mod[top(h)] ^ OM[o]: the MOD
+// index no longer waits for the OUT lookup, and h1 takes one v_bitop3
+// (xor3) instead of two XORs -- 7 VALU + 2 ds_read_b64 per byte.
 template <int K, int TSH>
 __device__ __forceinline__ void slide(uint32_t &h0, uint32_t &h1, uint32_t dnew, uint32_t dold,
                                       const uint8_t *tab, const Consts &k) {
     const uint2 o = lds_u2(tab, __builtin_amdgcn_perm(dold, k.lwo, 0x0C0C0000u | ((4u + K) << 8)));
-    const uint32_t a1x = __builtin_amdgcn_alignbit(h1, h0, 24) ^ o.y;
-    const uint2 m = lds_u2(tab, mod_addr<TSH>(a1x, k));
+    const uint32_t a1 = __builtin_amdgcn_alignbit(h1, h0, 24);
+    const uint2 m = lds_u2(tab, mod_addr<TSH>(h1, a1, k));
     h0 = __builtin_amdgcn_bitop3_b32(__builtin_amdgcn_perm(h0, dnew, 0x06050400u | K), o.x, m.x, kXor3);
-    h1 = a1x ^ m.y;
+    h1 = __builtin_amdgcn_bitop3_b32(a1, o.y, m.y, kXor3);
 }
 
 // Warm-up slide (the window is still filling: nothing leaves it).
@@ -85,7 +100,7 @@ template <int K, int TSH>
 __device__ __forceinline__ void slide_in(uint32_t &h0, uint32_t &h1, uint32_t dnew,
                                          const uint8_t *tab, const Consts &k) {
     const uint32_t a1 = __builtin_amdgcn_alignbit(h1, h0, 24);
-    const uint2 m = lds_u2(tab, mod_addr<TSH>(a1, k));
+    const uint2 m = lds_u2(tab, mod_addr<TSH>(h1, a1, k));
     h0 = __builtin_amdgcn_perm(h0, dnew, 0x06050400u | K) ^ m.x;
     h1 = a1 ^ m.y;
 }
@@ -138,10 +153,49 @@ __device__ __forceinline__ void record_group(Chain &c, const uint32_t (&hk)[G], 
 
 // 64 slides over unit `un` (bytes 64 back in `uo`), 64 / G groups of G.
 // SMALL: mask < 0xFFFF, the prefilter then runs on h & mask (exact).
+// G >= 100: groups of G - 100 that keep no fingerprints: a flagged lane
+// re-rolls its group from the saved state (P ~ 2^-12 per lane-group).
+template <int TSH, int G>
+__device__ __forceinline__ void rescan_group(Chain &c, uint32_t h0, uint32_t h1, const Unit &un,
+                                             const Unit &uo, const uint8_t *tab, const Consts &k,
+                                             uint32_t rb, int g) {
+#pragma unroll
+    for (int j = 0; j < G; j++) {
+        const int b = g * G + j;
+        slide_b<TSH>(b, h0, h1, UDW(un, b >> 2), UDW(uo, b >> 2), tab, k);
+        const uint32_t rel = rb + (uint32_t)j;
+        if ((h0 & k.mask) == 0u && rel >= c.rlo && rel < c.rhi) {
+            c.count++;
+            c.last = rel;
+            if (c.first == kNone) c.first = rel;
+        }
+    }
+}
+
 template <int TSH, bool SMALL, int G>
 __device__ __forceinline__ void scan_unit(Chain &c, const Unit &un, const Unit &uo,
                                           const uint8_t *tab, const Consts &k, uint64_t valid,
                                           uint32_t lane, uint32_t rb) {
+    if constexpr (G >= 100) {
+        constexpr int GG = G - 100;
+#pragma unroll
+        for (int g = 0; g < 64 / GG; g++) {
+            const uint32_t h0s = c.h0, h1s = c.h1;
+            uint16_t acc = 0xFFFFu;
+#pragma unroll
+            for (int j = 0; j < GG; j++) {
+                const int b = g * GG + j;
+                slide_b<TSH>(b, c.h0, c.h1, UDW(un, b >> 2), UDW(uo, b >> 2), tab, k);
+                const uint16_t t = SMALL ? (uint16_t)(c.h0 & k.mask) : (uint16_t)c.h0;
+                acc = __builtin_elementwise_min(acc, t);
+            }
+            const uint64_t flagged = __builtin_amdgcn_ballot_w64(acc == 0) & valid;
+            if (flagged) {
+                if ((flagged >> lane) & 1u)
+                    rescan_group<TSH, GG>(c, h0s, h1s, un, uo, tab, k, rb + g * GG, g);
+            }
+        }
+    } else {
 #pragma unroll
     for (int g = 0; g < 64 / G; g++) {
         uint32_t hk[G];
@@ -160,6 +214,7 @@ __device__ __forceinline__ void scan_unit(Chain &c, const Unit &un, const Unit &
         if (flagged) {
             if ((flagged >> lane) & 1u) record_group<G>(c, hk, k.mask, rb + g * G);
         }
+    }
     }
 }
 
@@ -265,7 +320,10 @@ __global__ __launch_bounds__(THREADS, 1) void rcdc_scan_kernel(
     __shared__ __attribute__((aligned(16))) uint8_t s_tab[kLdsBytes];
     for (uint32_t i = threadIdx.x; i < 256u * kTableRepl; i += THREADS) {
         const uint32_t e = i / kTableRepl, c = i % kTableRepl;
-        const uint64_t o = gtab[e], m = gtab[256 + e];
+        // OM[e] = OUT'[e] reduced: the top byte of out << 8 sits at bits
+        // deg .. deg + 7 and MOD's (i << deg) term cancels it
+        const uint64_t ot = gtab[e], m = gtab[256 + e];
+        const uint64_t o = ot ^ gtab[256 + ((ot >> (prm.idx_shift + 32u)) & 255u)];
         *reinterpret_cast<uint2 *>(s_tab + e * 256u + c * 8u) =
             make_uint2((uint32_t)o, (uint32_t)(o >> 32));
         *reinterpret_cast<uint2 *>(s_tab + kTableBytes + e * 256u + c * 8u) =
@@ -292,18 +350,24 @@ __global__ __launch_bounds__(THREADS, 1) void rcdc_scan_kernel(
 namespace rcdc {
 
 // Kernel configuration `code` (RCDC_SCAN_VARIANT, default kDefaultScanCode):
-// 100 * (group == 8) + 10 * ring + pair; + 1000: 768 threads.  Measured on
-// the C2 workload (profiles/r01_scan4_ab.txt) with 64-B aligned lane starts:
-// 30 (ring of 3 64-B units, groups of 16, 1024 threads) 174 us, 130 (groups
-// of 8) the same, 41 (ring of 4, 128-B loads) 193 us, 50 (ring of 5) 204 us.  deg 53 uses the compile-time index shift, other degrees the
-// generic path; avg < 2^16 the masked prefilter.
-template <int R, bool PAIR, int THREADS, int G>
+// 100 * (group == 8) + 10 * ring + pair; + 1000: 768 threads; 3116: groups of
+// 16 re-rolled on a flag instead of kept; 930: MOD index from hi32(h << 8)
+// (the pre-OM form's index).  Measured on the C2 workload with 64-B aligned
+// lane starts, HIP-event medians in one process (tools/variants.py,
+// profiles/r01_scan_variants.txt):
+//   before the OM table: 30 174 us, 130 the same, 41 193 us, 50 204 us;
+//   OM table, MOD index from hi32(h << 8) (930): 164 us;
+//   OM table, MOD index from h1 (30, default): 161-165 us; 130 170 us;
+//   3116 168 us; no candidate test at all (cost floor, wrong output) 157 us.
+// deg 53 uses the compile-time index shift, other degrees the generic path;
+// avg < 2^16 the masked prefilter.
+template <int R, bool PAIR, int THREADS, int G, bool HIDX = true>
 static hipError_t launch4(const uint8_t *arena, const ScanItem *items, uint32_t nitems,
                           const uint64_t *gtab, const ScanParams &prm, uint4 *sums,
                           uint64_t *item_masks, uint32_t blocks, hipStream_t stream) {
     const bool small = prm.mask < 0xFFFFu;
     if (prm.idx_shift == 21 && !small)
-        hipLaunchKernelGGL((rcdc_scan_kernel<R, PAIR, THREADS, 13, false, G>), dim3(blocks),
+        hipLaunchKernelGGL((rcdc_scan_kernel<R, PAIR, THREADS, HIDX ? 105 : 13, false, G>), dim3(blocks),
                            dim3(THREADS), 0, stream, arena, items, nitems, gtab, prm, sums,
                            item_masks);
     else if (small)
@@ -317,7 +381,7 @@ static hipError_t launch4(const uint8_t *arena, const ScanItem *items, uint32_t 
     return hipGetLastError();
 }
 
-int scan_threads(int code) { return code >= 1000 ? 768 : 1024; }
+int scan_threads(int code) { return (code >= 1000 && code < 2000) ? 768 : 1024; }
 
 hipError_t launch_scan(int code, const uint8_t *arena, const ScanItem *items, uint32_t nitems,
                         const uint64_t *gtab, const ScanParams &prm, uint4 *sums,
@@ -325,6 +389,8 @@ hipError_t launch_scan(int code, const uint8_t *arena, const ScanItem *items, ui
     if (nitems == 0) return hipSuccess;
     switch (code) {
         case 30: return launch4<3, false, 1024, 16>(arena, items, nitems, gtab, prm, sums, item_masks, blocks, stream);
+        case 3116: return launch4<3, false, 1024, 116>(arena, items, nitems, gtab, prm, sums, item_masks, blocks, stream);
+        case 930: return launch4<3, false, 1024, 16, false>(arena, items, nitems, gtab, prm, sums, item_masks, blocks, stream);
         case 50: return launch4<5, false, 1024, 16>(arena, items, nitems, gtab, prm, sums, item_masks, blocks, stream);
         case 150: return launch4<5, false, 1024, 8>(arena, items, nitems, gtab, prm, sums, item_masks, blocks, stream);
         case 130: return launch4<3, false, 1024, 8>(arena, items, nitems, gtab, prm, sums, item_masks, blocks, stream);
