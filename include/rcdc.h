@@ -142,14 +142,16 @@ typedef struct {
     uint32_t segment_bytes;   /* S                                        */
     uint32_t work_items;      /* 64-segment wave work items               */
     uint32_t scan_blocks;     /* workgroups of the scan launch            */
-    uint32_t reserved;
+    uint32_t walk_pieces;     /* pieces of long streams on the walk path  */
 } rcdc_plan_info;
 rcdc_status rcdc_plan_get_info(const rcdc_plan *plan, rcdc_plan_info *info);
 
 /* Kernel timing (HIP events recorded on the launch stream around the scan
- * and the resolve kernel of every run while enabled).  enable = 1 starts a
- * fresh accumulation, 0 stops recording.  rcdc_plan_kernel_times waits for
- * the recorded runs and returns their count and summed device times.      */
+ * and the resolve kernel while enabled).  enable = P >= 1 starts a fresh
+ * accumulation and times every P-th run from the next one on (P = 1: every
+ * run; a larger P samples the runs and keeps the events' own inter-kernel
+ * gaps out of most of them); 0 stops recording.  rcdc_plan_kernel_times
+ * waits for the timed runs and returns their count and summed device times. */
 rcdc_status rcdc_plan_set_timing(rcdc_plan *plan, int enable);
 rcdc_status rcdc_plan_kernel_times(rcdc_plan *plan, uint64_t *runs,
                                    double *scan_ms_total,

@@ -41,7 +41,7 @@ class PlanInfo(ctypes.Structure):
         ("segment_bytes", ctypes.c_uint32),
         ("work_items", ctypes.c_uint32),
         ("scan_blocks", ctypes.c_uint32),
-        ("reserved", ctypes.c_uint32),
+        ("walk_pieces", ctypes.c_uint32),
     ]
 
 

@@ -83,4 +83,67 @@ struct ResolveParams {
     uint32_t pad;
 };
 
+// ---- walk path (long streams; rcdc_walk.hip) --------------------------------
+// A long stream is split into pieces [start, stop).  One wave walks the chunk
+// chain of each piece from its start, hashing only what the reference hashes:
+// per chunk the 64 min-zone positions and the pure windows from s + min + 64
+// to the cut (rabin.rs:127-188 never hashes a chunk's first min bytes).  Piece
+// starts other than 0 are assumptions; rcdc_walk_check_kernel finds where the
+// true chain meets each piece's chain, rcdc_walk_fixup_kernel walks the rare
+// stretches where it does not, rcdc_walk_assemble_kernel writes the result.
+
+// Cut value | kind << 62 in piece lists: what the walker verified before it.
+constexpr uint64_t kCutVal = (1ull << 62) - 1;
+constexpr uint64_t kKindHit = 0;   // first pure-window hit >= s + min + 64
+constexpr uint64_t kKindMax = 1;   // s + max: no hit in [s + min + 64, s + max)
+constexpr uint64_t kKindEof = 2;   // N: no hit in [s + min + 64, N) (or N - s <= min)
+constexpr uint64_t kKindZone = 3;  // a min-zone / all-zero-prefill cut: nothing scanned
+constexpr uint64_t kOpenFlag = 1ull << 32;  // piece status: walk stopped "open"
+
+struct WalkUnit {
+    uint64_t start, stop;  // assumed chunk start (exact for piece 0); next piece's start or N
+    uint64_t out_base;     // first slot in piece_cuts
+    uint32_t out_cap;
+    uint32_t stream;
+    uint32_t piece;        // index within the stream
+    uint32_t unit0;        // unit index of the stream's piece 0
+    uint32_t npieces;
+    uint32_t pad;
+};
+static_assert(sizeof(WalkUnit) == 48, "WalkUnit is 48 B");
+
+struct WalkParams {
+    uint64_t min_size, max_size;
+    uint64_t arena_len;
+    uint64_t piece_bytes;  // Lp: piece j starts at j * Lp
+    uint32_t seg_bytes;    // S: bytes per lane per round
+    uint32_t mask;         // avg - 1
+    uint32_t idx_shift;    // deg - 32
+    uint32_t shift;        // deg - 8
+    uint32_t nunits;
+    uint32_t fix_cap;      // fixup cut slots per boundary
+};
+
+constexpr int kMaxHops = 13;  // chain steps the check kernel resolves itself
+
+// Per boundary (indexed by the unit of the later piece).
+struct BoundRes {
+    uint32_t kind;         // kBoundNone / Merged / Fixup / Bad
+    uint32_t nhops;        // hops[] cuts before the merge
+    uint32_t merge_unit;   // Merged: continue in this unit's list
+    int32_t merge_idx;     //   after this index (-1: the whole list)
+    uint64_t fix_from;     // Fixup: exact cut the fixup walk starts from
+    uint64_t hops[kMaxHops];
+};
+static_assert(sizeof(BoundRes) == 16 * 8, "BoundRes is 128 B");
+constexpr uint32_t kBoundNone = 0, kBoundMerged = 1, kBoundFixup = 2, kBoundEnd = 3;
+
+// Per fixup boundary: cuts in fix_cuts[unit * fix_cap ..].
+struct FixRes {
+    uint32_t count;
+    uint32_t merge_unit;   // 0xFFFFFFFF: ran to N (or overflowed: count > fix_cap)
+    int32_t merge_idx;
+    uint32_t pad;
+};
+
 }  // namespace rcdc

@@ -35,6 +35,16 @@ hipError_t launch_resolve(const uint8_t *arena, const StreamDesc *sds, const Res
                           const uint64_t *item_masks, uint64_t *cuts, uint64_t *counts,
                           uint64_t *piece_cuts, uint64_t *piece_counts, uint64_t *stats,
                           hipStream_t stream);
+hipError_t launch_walk(const uint8_t *arena, const StreamDesc *sds, const WalkUnit *units,
+                       const WalkParams &prm, const uint64_t *gtab, uint64_t *piece_cuts,
+                       uint64_t *pstatus, uint32_t *ctr, uint32_t blocks, hipStream_t stream);
+hipError_t launch_walk_chain(const uint8_t *arena, const StreamDesc *sds, const WalkUnit *units,
+                             const uint32_t *stream_unit0, uint32_t nstreams,
+                             const WalkParams &prm, const uint64_t *gtab,
+                             const uint64_t *piece_cuts, const uint64_t *pstatus, BoundRes *bres,
+                             uint32_t *ctr, uint32_t *fixlist, uint64_t *fix_cuts,
+                             FixRes *fixres, uint64_t *cuts, uint64_t *counts,
+                             uint32_t fix_blocks, hipStream_t stream);
 }  // namespace rcdc
 
 using namespace rcdc;
@@ -123,11 +133,33 @@ struct rcdc_plan {
     uint64_t *d_counts = nullptr;
     uint64_t cap_items = 0, cap_sds = 0, cap_sums = 0, cap_cuts = 0, cap_masks = 0,
              cap_counts = 0;
+    // walk path (long streams, rcdc_walk.hip)
+    bool no_walk = false;             // force the scan path (fallback re-runs)
+    std::vector<WalkUnit> wunits;
+    std::vector<uint32_t> wstream_u0;  // unit0 of every walked stream
+    std::vector<uint8_t> walked;       // per stream: on the walk path
+    uint64_t nwpiece_cuts = 0;
+    WalkParams wprm{};
+    WalkUnit *d_wunits = nullptr;
+    uint32_t *d_wsu0 = nullptr;
+    uint64_t *d_wpiece = nullptr;
+    uint64_t *d_pstatus = nullptr;
+    BoundRes *d_bres = nullptr;
+    uint32_t *d_ctr = nullptr;
+    uint32_t *d_fixlist = nullptr;
+    uint64_t *d_fixcuts = nullptr;
+    FixRes *d_fixres = nullptr;
+    uint64_t cap_wunits = 0, cap_wsu0 = 0, cap_wpiece = 0, cap_pstatus = 0, cap_bres = 0,
+             cap_ctr = 0, cap_fixlist = 0, cap_fixcuts = 0, cap_fixres = 0;
+    const void *last_arena = nullptr;  // of the last run (fallback re-runs)
+    hipStream_t last_stream = nullptr;
     hipEvent_t done = nullptr;
     bool ran = false;
     // optional per-run kernel timing
     bool timing = false;
-    std::vector<hipEvent_t> tev;  // 3 per run: before scan, after scan, after resolve
+    uint32_t tperiod = 1;         // record every tperiod-th run (rcdc_plan_set_timing)
+    uint64_t tcalls = 0;          // runs since timing was enabled
+    std::vector<hipEvent_t> tev;  // 3 per timed run: before scan, after scan, after resolve
     uint64_t truns = 0;
 };
 
@@ -239,6 +271,7 @@ void build_resolve_units(rcdc_plan *pl, uint64_t mn) {
     pl->stitches.clear();
     pl->npiece_cuts = 0;
     for (uint32_t i = 0; i < pl->n; i++) {
+        if (pl->walked[i]) continue;
         const StreamDesc &d = pl->sds[i];
         const uint64_t N = d.n;
         const uint64_t Lp = piece_bytes(N, mn);
@@ -273,21 +306,54 @@ void build_resolve_units(rcdc_plan *pl, uint64_t mn) {
     }
 }
 
+// Walk-path selection (rcdc_walk.hip).  The walk hashes what the reference
+// hashes (~2/3 of random bytes, ~nothing of zero runs) but parallelises only
+// over pieces of Lp bytes, so it needs many of them to fill the chip: a
+// stream of N >= 2 Lp is walked when the plan's walkable bytes give at least
+// kWalkMinPieces pieces.  Lp ~ walkable / (4 x 4096 wave slots), so the
+// dynamic queue balances cheap (zero) and expensive (random) pieces, clamped
+// to [4 MiB, 32 MiB] and a multiple of min.  RCDC_WALK_PIECE (bytes; 0 = scan
+// path only) and RCDC_WALK_MIN_PIECES override.
+constexpr uint64_t kWalkMinPieces = 1024;
+
+static uint64_t walk_piece_bytes(const uint64_t *lens, uint32_t n, uint64_t mn, uint64_t mx) {
+    uint64_t lp_env = ~0ull, min_pieces = kWalkMinPieces;
+    if (const char *e = getenv("RCDC_WALK_PIECE")) lp_env = (uint64_t)atoll(e);
+    if (const char *e = getenv("RCDC_WALK_MIN_PIECES")) min_pieces = (uint64_t)atoll(e);
+    if (lp_env == 0) return 0;
+    const uint64_t lo = 4ull << 20, hi = 32ull << 20;
+    uint64_t total = 0;
+    for (uint32_t i = 0; i < n; i++)
+        if (lens[i] >= 2 * lo) total += lens[i];
+    uint64_t lp = lp_env != ~0ull ? lp_env : std::min(std::max(total / 16384, lo), hi);
+    lp = std::max<uint64_t>(lp / mn, 1) * mn;
+    (void)mx;
+    uint64_t walkable = 0;
+    for (uint32_t i = 0; i < n; i++)
+        if (lens[i] >= 2 * lp) walkable += lens[i];
+    if (walkable / lp < min_pieces) return 0;
+    return lp;
+}
+
 rcdc_status plan_build(rcdc_ctx *ctx, rcdc_plan *pl, const uint64_t *offs, const uint64_t *lens,
                        uint32_t n, uint64_t arena_len) {
     const uint64_t pos_lo = ctx->min + kWindow;  // first pure-window test position
     pl->ctx = ctx;
     pl->n = n;
     pl->arena_len = arena_len;
-    std::vector<uint64_t> spans;
-    spans.reserve(n);
-    for (uint32_t i = 0; i < n; i++) {
+    for (uint32_t i = 0; i < n; i++)
         if (offs[i] > arena_len || lens[i] > arena_len - offs[i])
             return fail(RCDC_ERR_INVALID_INPUT, "stream %u [%llu,+%llu) outside arena of %llu B", i,
                         (unsigned long long)offs[i], (unsigned long long)lens[i],
                         (unsigned long long)arena_len);
-        if (lens[i] > pos_lo) spans.push_back(lens[i] - (stream_q0(offs[i], pos_lo, q0_align()) - offs[i] + 65));
-    }
+    const uint64_t Lp = pl->no_walk ? 0 : walk_piece_bytes(lens, n, ctx->min, ctx->max);
+    pl->walked.assign(n, 0);
+    for (uint32_t i = 0; i < n; i++) pl->walked[i] = Lp && lens[i] >= 2 * Lp;
+    std::vector<uint64_t> spans;
+    spans.reserve(n);
+    for (uint32_t i = 0; i < n; i++)
+        if (!pl->walked[i] && lens[i] > pos_lo)
+            spans.push_back(lens[i] - (stream_q0(offs[i], pos_lo, q0_align()) - offs[i] + 65));
     const int nc = 1;
     const int nthreads = scan_threads(ctx->variant);
     uint32_t S = choose_segment(spans, ctx->num_cus, nc, nthreads);
@@ -309,7 +375,7 @@ rcdc_status plan_build(rcdc_ctx *ctx, rcdc_plan *pl, const uint64_t *offs, const
         ncut += d.cut_cap;
         d.sum_base = nseg;
         d.item_base = pl->items.size();
-        if (N <= pos_lo) continue;
+        if (N <= pos_lo || pl->walked[i]) continue;
         // lane start q (arena offset) 16-aligned; tests positions q+65 ..
         const uint64_t q0 = stream_q0(off, pos_lo, q0_align());
         const uint64_t p0 = q0 - off + 65;
@@ -335,6 +401,48 @@ rcdc_status plan_build(rcdc_ctx *ctx, rcdc_plan *pl, const uint64_t *offs, const
     pl->nseg = nseg;
     pl->ncuts = ncut;
     build_resolve_units(pl, ctx->min);
+    // walk units: pieces [j Lp, (j+1) Lp) of every walked stream, the last
+    // one to N (between Lp and 2 Lp)
+    pl->wunits.clear();
+    pl->wstream_u0.clear();
+    pl->nwpiece_cuts = 0;
+    for (uint32_t i = 0; i < n && Lp; i++) {
+        if (!pl->walked[i]) continue;
+        const uint64_t N = lens[i];
+        const uint32_t P = (uint32_t)std::max<uint64_t>(N / Lp, 1);
+        const uint32_t u0 = (uint32_t)pl->wunits.size();
+        pl->wstream_u0.push_back(u0);
+        for (uint32_t j = 0; j < P; j++) {
+            WalkUnit u{};
+            u.start = (uint64_t)j * Lp;
+            u.stop = j + 1 < P ? (uint64_t)(j + 1) * Lp : N;
+            u.out_base = pl->nwpiece_cuts;
+            // cuts in [start, first cut >= stop]: >= min apart, plus the crossing and EOF cuts
+            u.out_cap = (uint32_t)((u.stop - u.start) / ctx->min + ctx->max / ctx->min + 4);
+            u.stream = i;
+            u.piece = j;
+            u.unit0 = u0;
+            u.npieces = P;
+            pl->nwpiece_cuts += u.out_cap;
+            pl->wunits.push_back(u);
+        }
+    }
+    WalkParams &wp = pl->wprm;
+    wp = WalkParams{};
+    wp.min_size = ctx->min;
+    wp.max_size = ctx->max;
+    wp.arena_len = arena_len;
+    wp.piece_bytes = Lp ? Lp : 1;
+    wp.seg_bytes = 2048;
+    if (const char *e = getenv("RCDC_WALK_SEG")) wp.seg_bytes = (uint32_t)std::max(atoi(e) / 128 * 128, 128);
+    wp.mask = (uint32_t)(ctx->avg - 1);
+    wp.idx_shift = (uint32_t)(ctx->deg - 32);
+    wp.shift = (uint32_t)(ctx->deg - 8);
+    wp.nunits = (uint32_t)pl->wunits.size();
+    // a fixup walks until it meets a piece's chain: a few chunks, longer only
+    // through phase-shifted zero runs (min-sized chunks); more -> host redo
+    wp.fix_cap = (uint32_t)(4 * (Lp ? Lp : 1) / ctx->min + ctx->max / ctx->min + 64);
+    if (const char *e = getenv("RCDC_WALK_FIXCAP")) wp.fix_cap = (uint32_t)std::max(atoi(e), 1);  // tests
     const uint64_t supers = (pl->items.size() + nc - 1) / nc;
     const uint64_t waves_needed = (supers + nthreads / 64 - 1) / (nthreads / 64);
     pl->blocks = (uint32_t)std::min<uint64_t>(waves_needed, (uint64_t)std::max(ctx->num_cus, 1));
@@ -351,6 +459,22 @@ rcdc_status plan_build(rcdc_ctx *ctx, rcdc_plan *pl, const uint64_t *offs, const
     if ((st = ensure_dev(&pl->d_stitches, &pl->cap_stitches, pl->stitches.size()))) return st;
     if ((st = ensure_dev(&pl->d_piece_cuts, &pl->cap_piece_cuts, pl->npiece_cuts))) return st;
     if ((st = ensure_dev(&pl->d_piece_counts, &pl->cap_piece_counts, pl->units.size()))) return st;
+    const uint64_t nw = pl->wunits.size();
+    if (nw) {
+        if ((st = ensure_dev(&pl->d_wunits, &pl->cap_wunits, nw))) return st;
+        if ((st = ensure_dev(&pl->d_wsu0, &pl->cap_wsu0, pl->wstream_u0.size()))) return st;
+        if ((st = ensure_dev(&pl->d_wpiece, &pl->cap_wpiece, pl->nwpiece_cuts))) return st;
+        if ((st = ensure_dev(&pl->d_pstatus, &pl->cap_pstatus, nw))) return st;
+        if ((st = ensure_dev(&pl->d_bres, &pl->cap_bres, nw))) return st;
+        if ((st = ensure_dev(&pl->d_ctr, &pl->cap_ctr, 4))) return st;
+        if ((st = ensure_dev(&pl->d_fixlist, &pl->cap_fixlist, nw))) return st;
+        if ((st = ensure_dev(&pl->d_fixcuts, &pl->cap_fixcuts, nw * pl->wprm.fix_cap))) return st;
+        if ((st = ensure_dev(&pl->d_fixres, &pl->cap_fixres, nw))) return st;
+        HIP_TRY(hipMemcpy(pl->d_wunits, pl->wunits.data(), nw * sizeof(WalkUnit),
+                          hipMemcpyHostToDevice));
+        HIP_TRY(hipMemcpy(pl->d_wsu0, pl->wstream_u0.data(),
+                          pl->wstream_u0.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+    }
     if (!pl->units.empty())
         HIP_TRY(hipMemcpy(pl->d_units, pl->units.data(), pl->units.size() * sizeof(ResolveUnit),
                           hipMemcpyHostToDevice));
@@ -379,7 +503,7 @@ rcdc_status plan_run(rcdc_plan *pl, const void *d_arena, hipStream_t stream) {
     sp.mask = (uint32_t)(ctx->avg - 1);
     sp.idx_shift = (uint32_t)(ctx->deg - 32);
     hipEvent_t *ev = nullptr;
-    if (pl->timing) {
+    if (pl->timing && (pl->tcalls++ % pl->tperiod) == 0) {
         if (pl->tev.size() < 3 * (pl->truns + 1)) {
             for (int k = 0; k < 3; k++) {
                 hipEvent_t e;
@@ -393,6 +517,19 @@ rcdc_status plan_run(rcdc_plan *pl, const void *d_arena, hipStream_t stream) {
     }
     HIP_TRY(launch_scan(ctx->variant, (const uint8_t *)d_arena, pl->d_items, (uint32_t)pl->items.size(),
                         ctx->d_tables, sp, pl->d_sums, pl->d_masks, pl->blocks, stream));
+    const uint32_t cus = (uint32_t)std::max(ctx->num_cus, 1);
+    static const bool dbg = getenv("RCDC_DEBUG_SYNC") != nullptr;  // stage-by-stage sync
+    if (dbg) {
+        HIP_TRY(hipStreamSynchronize(stream));
+        fprintf(stderr, "rcdc: scan done\n");
+    }
+    HIP_TRY(launch_walk((const uint8_t *)d_arena, pl->d_sds, pl->d_wunits, pl->wprm, ctx->d_tables,
+                        pl->d_wpiece, pl->d_pstatus, pl->d_ctr,
+                        (uint32_t)std::min<uint64_t>(cus, (pl->wunits.size() + 15) / 16), stream));
+    if (dbg) {
+        HIP_TRY(hipStreamSynchronize(stream));
+        fprintf(stderr, "rcdc: walk done (%zu units)\n", pl->wunits.size());
+    }
     if (ev) HIP_TRY(hipEventRecord(ev[1], stream));
     ResolveParams rp{};
     rp.min_size = ctx->min;
@@ -405,11 +542,23 @@ rcdc_status plan_run(rcdc_plan *pl, const void *d_arena, hipStream_t stream) {
                            (uint32_t)pl->stitches.size(), ctx->d_tables, rp, pl->d_sums,
                            pl->d_masks, pl->d_cuts, pl->d_counts, pl->d_piece_cuts,
                            pl->d_piece_counts, nullptr, stream));
+    if (dbg) {
+        HIP_TRY(hipStreamSynchronize(stream));
+        fprintf(stderr, "rcdc: resolve done\n");
+    }
+    HIP_TRY(launch_walk_chain((const uint8_t *)d_arena, pl->d_sds, pl->d_wunits, pl->d_wsu0,
+                              (uint32_t)pl->wstream_u0.size(), pl->wprm, ctx->d_tables,
+                              pl->d_wpiece, pl->d_pstatus, pl->d_bres, pl->d_ctr, pl->d_fixlist,
+                              pl->d_fixcuts, pl->d_fixres, pl->d_cuts, pl->d_counts, cus, stream));
     if (ev) HIP_TRY(hipEventRecord(ev[2], stream));
+    pl->last_arena = d_arena;
+    pl->last_stream = stream;
     HIP_TRY(hipEventRecord(pl->done, stream));
     pl->ran = true;
     return RCDC_OK;
 }
+
+void plan_release(rcdc_plan *pl);
 
 rcdc_status plan_results(rcdc_plan *pl, uint64_t *cuts, uint64_t cap, uint64_t *counts) {
     if (!pl->ran) return fail(RCDC_ERR_INVALID_INPUT, "plan has not been run");
@@ -418,6 +567,27 @@ rcdc_status plan_results(rcdc_plan *pl, uint64_t *cuts, uint64_t cap, uint64_t *
     std::vector<uint64_t> cnt(pl->n);
     if (pl->n)
         HIP_TRY(hipMemcpy(cnt.data(), pl->d_counts, pl->n * 8, hipMemcpyDeviceToHost));
+    // a walked stream whose fixup overflowed (count ~0): redo it on the scan
+    // path over the same device bytes
+    std::vector<std::vector<uint64_t>> redo(pl->n);
+    for (uint32_t i = 0; i < pl->n; i++) {
+        if (cnt[i] != ~0ull) continue;
+        rcdc_plan tmp;
+        tmp.no_walk = true;
+        const uint64_t off = pl->sds[i].off, len = pl->sds[i].n;
+        rcdc_status st = plan_build(pl->ctx, &tmp, &off, &len, 1, pl->arena_len);
+        if (!st) st = plan_run(&tmp, pl->last_arena, pl->last_stream);
+        if (!st) HIP_TRY(hipEventSynchronize(tmp.done));
+        uint64_t c1 = 0;
+        if (!st) HIP_TRY(hipMemcpy(&c1, tmp.d_counts, 8, hipMemcpyDeviceToHost));
+        if (!st) {
+            redo[i].resize(c1);
+            if (c1) HIP_TRY(hipMemcpy(redo[i].data(), tmp.d_cuts, c1 * 8, hipMemcpyDeviceToHost));
+        }
+        plan_release(&tmp);
+        if (st) return st;
+        cnt[i] = c1;
+    }
     uint64_t total = 0;
     for (uint32_t i = 0; i < pl->n; i++) {
         if (cnt[i] > pl->sds[i].cut_cap)
@@ -433,15 +603,24 @@ rcdc_status plan_results(rcdc_plan *pl, uint64_t *cuts, uint64_t cap, uint64_t *
         HIP_TRY(hipMemcpy(all.data(), pl->d_cuts, pl->ncuts * 8, hipMemcpyDeviceToHost));
     uint64_t o = 0;
     for (uint32_t i = 0; i < pl->n; i++) {
-        memcpy(cuts + o, all.data() + pl->cut_base[i], cnt[i] * 8);
+        memcpy(cuts + o, redo[i].empty() ? all.data() + pl->cut_base[i] : redo[i].data(),
+               cnt[i] * 8);
         o += cnt[i];
     }
     return RCDC_OK;
 }
 
-void plan_free(rcdc_plan *pl) {
-    if (!pl) return;
+void plan_release(rcdc_plan *pl) {
     DeviceGuard g(pl->ctx ? pl->ctx->device : 0);
+    (void)hipFree(pl->d_wunits);
+    (void)hipFree(pl->d_wsu0);
+    (void)hipFree(pl->d_wpiece);
+    (void)hipFree(pl->d_pstatus);
+    (void)hipFree(pl->d_bres);
+    (void)hipFree(pl->d_ctr);
+    (void)hipFree(pl->d_fixlist);
+    (void)hipFree(pl->d_fixcuts);
+    (void)hipFree(pl->d_fixres);
     (void)hipFree(pl->d_items);
     (void)hipFree(pl->d_sds);
     (void)hipFree(pl->d_sums);
@@ -454,6 +633,11 @@ void plan_free(rcdc_plan *pl) {
     (void)hipFree(pl->d_piece_counts);
     if (pl->done) (void)hipEventDestroy(pl->done);
     for (hipEvent_t e : pl->tev) (void)hipEventDestroy(e);
+}
+
+void plan_free(rcdc_plan *pl) {
+    if (!pl) return;
+    plan_release(pl);
     delete pl;
 }
 
@@ -665,14 +849,18 @@ rcdc_status rcdc_plan_get_info(const rcdc_plan *plan, rcdc_plan_info *info) {
     info->segment_bytes = plan->seg_bytes;
     info->work_items = (uint32_t)plan->items.size();
     info->scan_blocks = plan->blocks;
-    info->reserved = 0;
+    info->walk_pieces = (uint32_t)plan->wunits.size();
     return RCDC_OK;
 }
 
 rcdc_status rcdc_plan_set_timing(rcdc_plan *plan, int enable) {
     if (!plan) return fail(RCDC_ERR_INVALID_INPUT, "null argument");
-    plan->timing = enable != 0;
-    if (enable) plan->truns = 0;
+    plan->timing = enable > 0;
+    if (enable > 0) {
+        plan->truns = 0;
+        plan->tcalls = 0;
+        plan->tperiod = (uint32_t)enable;
+    }
     return RCDC_OK;
 }
 

@@ -1,0 +1,707 @@
+// rcdc_walk.hip -- walk path of the rcdc chunker for long streams (gfx950).
+//
+// The scan path (rcdc_scan.hip) hashes every byte after a stream's first
+// min bytes.  The reference hashes less: ChunkIter::next
+// (crates/core/src/chunker/rabin.rs:110-191) copies each chunk's first min
+// bytes unhashed (:127-139), prefills the window with the 64 bytes before
+// s + min (:149-151) and slides only from there to the cut (:153-188).  On
+// random data that skips a third of the bytes; in zero runs (every chunk
+// exactly min, decided by the all-zero prefill) it skips almost all of them.
+// The walk path does the same on the device:
+//
+//   rcdc_walk_kernel         one wave per piece [start, stop) of a long
+//                            stream (dynamic queue): hops chunk to chunk from
+//                            `start` like the reference loop; the pure-window
+//                            search of a chunk runs in rounds of 64 lanes x S
+//                            bytes (the scan kernel's per-lane segment code),
+//                            the 64 min-zone hashes lane-parallel, zero runs
+//                            64 chunks per step.  A piece other than the
+//                            first assumes a chunk starts at `start`; it
+//                            stops at its first cut >= stop, or "open" once
+//                            its search passes stop + min + 64, so adjacent
+//                            pieces never hash the same bytes.
+//   rcdc_walk_check_kernel   one wave per piece boundary: from the previous
+//                            piece's end state, finds where the true chain
+//                            meets this piece's chain, using what the walker
+//                            verified (each cut's kind: the window it searched
+//                            was hit-free); rarely it needs bytes nobody
+//                            hashed and hands the boundary to
+//   rcdc_walk_fixup_kernel   one workgroup per such boundary (rounds of 1024
+//                            lanes): walks the exact chain until it meets a
+//                            piece's chain;
+//   rcdc_walk_assemble_kernel one wave per stream: concatenates.
+//
+// The result is exact for any input and any piece size; the piece size only
+// moves work between the walk and the (rare) fixups.
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+
+#include "rcdc_internal.h"
+
+using namespace rcdc;
+
+#include "rcdc_slide.h"
+
+namespace {
+
+constexpr int kWR = 3, kWG = 16;   // ring of 3 register units, groups of 16 (scan default)
+constexpr uint64_t kNoCut = ~0ull;
+constexpr uint64_t kOpen = ~0ull - 1;
+constexpr uint32_t kNoUnit = 0xFFFFFFFFu;
+
+__device__ __forceinline__ uint64_t readlane64(uint64_t v, uint32_t l) {
+    const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)v, l);
+    const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)(v >> 32), l);
+    return ((uint64_t)hi << 32) | lo;
+}
+
+// A value every lane holds, made provably wave-uniform (an SGPR): branches on
+// it are scalar and barriers around them stay matched across waves
+// (cdna_hip_programming.md Guideline 5).
+__device__ __forceinline__ uint64_t uni64(uint64_t v) {
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+    return ((uint64_t)hi << 32) | lo;
+}
+
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+}
+
+// MOD-table access in the two LDS layouts: the scan layout (32 lane copies,
+// entry e at kTableBytes + e * 256 + copy * 8) and a plain 256-entry table.
+struct ModRepl {
+    const uint8_t *tab;
+    uint32_t lwm;
+    __device__ uint64_t operator()(uint32_t e) const {
+        const uint2 v = *reinterpret_cast<const uint2 *>(tab + lwm + e * 256u);
+        return ((uint64_t)v.y << 32) | v.x;
+    }
+};
+struct ModPlain {
+    const uint64_t *mod;
+    __device__ uint64_t operator()(uint32_t e) const { return mod[e]; }
+};
+
+// The min-zone of the chunk starting at pos (z = pos + min), one wave:
+// position z + k (k < 64) hashes the last 64 bytes of
+// b[z-64, z-1) ++ b[z, z+k) (rustic_cdc prefills 63 bytes).
+// Returns the first zone cut below `limit`, or kNoCut; *zero: the cut came
+// from the all-zero prefill (its hash is 0, which passes any mask).
+template <typename Mod>
+__device__ uint64_t zone_wave(const uint8_t *s, uint64_t N, uint64_t z, uint64_t limit,
+                              uint32_t mask, uint32_t shift, const Mod &mod, uint8_t *win,
+                              uint32_t lane, bool *zero) {
+    const uint32_t w0 = s[z - 64 + lane];
+    const uint32_t w1 = (z + lane < N) ? s[z + lane] : 0u;
+    *zero = false;
+    if (__builtin_amdgcn_ballot_w64(lane < 63 && w0 != 0) == 0) {
+        *zero = true;
+        return z;
+    }
+    // X = 0 ++ b[z-64, z-1) ++ b[z, z+64): lane k hashes X[k, k+64)
+    wave_sync();
+    if (lane < 63) win[lane + 1] = (uint8_t)w0;
+    else win[0] = 0;
+    win[64 + lane] = (uint8_t)w1;
+    wave_sync();
+    uint64_t h = 0;
+    for (uint32_t i = 0; i < 64; i++) {
+        const uint32_t b = win[lane + i];
+        h = ((h << 8) | b) ^ mod((uint32_t)(h >> shift) & 255u);
+    }
+    wave_sync();
+    const uint64_t hit = __builtin_amdgcn_ballot_w64(z + lane < limit && (h & mask) == 0);
+    return hit ? z + (uint64_t)__builtin_ctzll(hit) : kNoCut;
+}
+
+// Consecutive chunks of exactly min bytes from `pos` by the all-zero prefill
+// rule: lane i checks the chunk starting at pos + i*min.  Returns how many
+// leading lanes qualify (0..64).  (As rcdc_resolve.hip zero_hops.)
+__device__ uint32_t zero_run(const uint8_t *s, uint64_t N, uint64_t mn, uint64_t mx, uint64_t pos,
+                             uint32_t lane) {
+    if (mn >= mx) return 0;
+    const uint64_t si = pos + (uint64_t)lane * mn;
+    bool ok = si + mn <= N;
+    if (ok) {
+        const uint64_t w = si + mn - 64, e = w + 63;
+        uint32_t acc = 0;
+        const uintptr_t aw = (reinterpret_cast<uintptr_t>(s + w) + 3) & ~(uintptr_t)3;
+        const uintptr_t ae = reinterpret_cast<uintptr_t>(s + e) & ~(uintptr_t)3;
+        const uint8_t *p = s + w;
+        for (; reinterpret_cast<uintptr_t>(p) < aw && p < s + e; p++) acc |= *p;
+        for (; reinterpret_cast<uintptr_t>(p) + 4 <= ae; p += 4) acc |= *reinterpret_cast<const uint32_t *>(p);
+        for (; p < s + e; p++) acc |= *p;
+        ok = acc == 0;
+    }
+    const uint64_t bad = __builtin_amdgcn_ballot_w64(!ok);
+    return bad ? (uint32_t)__builtin_ctzll(bad) : 64u;
+}
+
+// A walker over one stream: one wave (LANES = 64) or one workgroup of 1024.
+struct Walk {
+    const uint8_t *arena;
+    uint64_t arena_len;
+    uint64_t off, N, mn, mx;
+    uint32_t S, mask, shift;
+    const uint8_t *tab;
+    Consts k;
+    uint8_t *win;      // 128 B of LDS (the zone window)
+    uint64_t *red;     // LDS: 16 reduction slots (workgroup walker)
+    uint32_t lane, wave, tid;
+};
+
+// First pure-window candidate p in [q, end) among the positions of one round
+// [A, A + LANES*S) (A: stream position with off + A 64-byte aligned); kNoCut
+// if none.  Lane t scans [A + t*S, A + (t+1)*S) after a 64-byte warm-up.
+template <int LANES, int TSH, bool SMALL>
+__device__ uint64_t round_first(const Walk &W, uint64_t A, uint64_t q, uint64_t end) {
+    const uint64_t P0 = A + (uint64_t)W.tid * W.S;
+    const uint32_t rlo = q > P0 ? (uint32_t)min(q - P0, (uint64_t)W.S) : 0u;
+    const uint32_t rhi = end > P0 ? (uint32_t)min(end - P0, (uint64_t)W.S) : 0u;
+    const uint64_t valid = __builtin_amdgcn_ballot_w64(rlo < rhi);
+    uint64_t best = kNoCut;
+    if (valid) {
+        const uint64_t base = W.off + A - 64;  // >= off: A >= q - 63 >= pos + min + 1
+        const uint64_t wbase = base + (uint64_t)W.wave * 64u * W.S;
+        const uint64_t rest = W.arena_len > wbase ? W.arena_len - wbase : 0;
+        const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
+            (void *)(W.arena + wbase), (short)0, (int)(uint32_t)min(rest, 0xFFFFFFFFull),
+            0x00020000);
+        const Chain c = scan_segment<kWR, false, TSH, SMALL, kWG>(rsrc, W.lane * W.S, W.S / kUnit,
+                                                                   rlo, rhi, W.tab, W.k, valid,
+                                                                   W.lane);
+        const uint64_t hits = __builtin_amdgcn_ballot_w64(c.first != kNone) & valid;
+        if (hits) {
+            const uint32_t L = (uint32_t)__builtin_ctzll(hits);
+            best = readlane64(P0 + c.first, L);
+        }
+    }
+    if constexpr (LANES > 64) {
+        if (W.lane == 0) W.red[W.wave] = best;
+        __syncthreads();
+        best = kNoCut;
+        for (int w = 0; w < LANES / 64; w++) best = min(best, W.red[w]);
+        best = uni64(best);
+        __syncthreads();
+    }
+    return best;
+}
+
+// The end of the chunk starting at pos (rabin.rs:110-191), or kOpen if no
+// cut was found below stop_scan (the search stopped there).  *kind: what the
+// walker verified (rcdc_internal.h kKind*); *zero: all-zero prefill cut.
+template <int LANES, int TSH, bool SMALL>
+__device__ uint64_t walk_next(const Walk &W, uint64_t pos, uint64_t stop_scan, uint64_t *kind,
+                              bool *zero) {
+    *zero = false;
+    if (W.N - pos <= W.mn) {  // rabin.rs:141-147: the rest is the last chunk
+        *kind = kKindEof;
+        return W.N;
+    }
+    const uint64_t z = pos + W.mn;
+    const uint64_t limit = min(pos + W.mx, W.N);  // rabin.rs:154 / EOF
+    uint64_t zc;
+    bool zz;
+    const ModRepl mod{W.tab, W.k.lwm};
+    if constexpr (LANES == 64) {
+        zc = zone_wave(W.arena + W.off, W.N, z, limit, W.mask, W.shift, mod, W.win, W.lane, &zz);
+    } else {
+        if (W.wave == 0) {
+            zc = zone_wave(W.arena + W.off, W.N, z, limit, W.mask, W.shift, mod, W.win, W.lane,
+                           &zz);
+            if (W.lane == 0) {
+                W.red[0] = zc;
+                W.red[1] = zz;
+            }
+        }
+        __syncthreads();
+        zc = uni64(W.red[0]);
+        zz = uni64(W.red[1]) != 0;
+        __syncthreads();
+    }
+    if (zc != kNoCut) {
+        *kind = kKindZone;
+        *zero = zz;
+        return zc;
+    }
+    if (limit <= z + 64) {
+        *kind = limit == W.N ? kKindEof : kKindMax;
+        return limit;
+    }
+    const uint64_t q = z + 64;
+    const uint64_t end = min(limit, stop_scan);
+    uint64_t A = ((W.off + q) & ~63ull) - W.off;
+    while (A < end) {
+        const uint64_t p = round_first<LANES, TSH, SMALL>(W, A, q, end);
+        if (p != kNoCut) {
+            *kind = kKindHit;
+            return p;
+        }
+        A += (uint64_t)LANES * W.S;
+    }
+    if (end == limit) {
+        *kind = limit == W.N ? kKindEof : kKindMax;
+        return limit;
+    }
+    return kOpen;
+}
+
+// Index of cut value c in the sorted piece list L[0, n) (kind bits masked),
+// or -2; one wave.
+__device__ int64_t find_cut(const uint64_t *L, uint64_t n, uint64_t c, uint32_t lane) {
+    for (uint64_t i0 = 0; i0 < n; i0 += 64) {
+        const uint64_t i = i0 + lane;
+        const uint64_t v = i < n ? (L[i] & kCutVal) : ~0ull;
+        const uint64_t eq = __builtin_amdgcn_ballot_w64(v == c);
+        if (eq) return (int64_t)(i0 + __builtin_ctzll(eq));
+        if (__builtin_amdgcn_ballot_w64(v > c)) break;
+    }
+    return -2;
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
+// Walk: one wave per unit, units pulled from ctr[0].
+template <int TSH, bool SMALL>
+__global__ __launch_bounds__(1024, 1) void rcdc_walk_kernel(
+    const uint8_t *__restrict__ arena, const StreamDesc *__restrict__ sds,
+    const WalkUnit *__restrict__ units, WalkParams prm, const uint64_t *__restrict__ gtab,
+    uint64_t *__restrict__ piece_cuts, uint64_t *__restrict__ pstatus, uint32_t *ctr) {
+    __shared__ __attribute__((aligned(16))) uint8_t s_tab[kLdsBytes];
+    __shared__ __attribute__((aligned(16))) uint8_t s_win[16][128];
+    fill_tables(s_tab, gtab, prm.idx_shift, threadIdx.x, 1024);
+    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+    Walk W;
+    W.arena = arena;
+    W.arena_len = prm.arena_len;
+    W.mn = prm.min_size;
+    W.mx = prm.max_size;
+    W.S = prm.seg_bytes;
+    W.mask = prm.mask;
+    W.shift = prm.shift;
+    W.tab = s_tab;
+    W.k = make_consts(lane, prm.mask, prm.idx_shift);
+    W.win = s_win[wave];
+    W.red = nullptr;
+    W.lane = lane;
+    W.wave = 0;  // a wave walker: lane t of the round is t
+    W.tid = lane;
+    for (;;) {
+        uint32_t u = 0;
+        if (lane == 0) u = atomicAdd(&ctr[0], 1u);
+        u = __builtin_amdgcn_readfirstlane(u);
+        if (u >= prm.nunits) break;
+        const WalkUnit U = units[u];
+        const StreamDesc d = sds[U.stream];
+        W.off = d.off;
+        W.N = d.n;
+        const uint8_t *s = arena + d.off;
+        uint64_t *out = piece_cuts + U.out_base;
+        const uint64_t stop_scan = U.stop < d.n ? U.stop + W.mn + 64 : ~0ull;
+        uint64_t pos = U.start, n = 0;
+        bool open = false;
+        while (pos < d.n) {
+            uint64_t kind;
+            bool zero;
+            const uint64_t c = walk_next<64, TSH, SMALL>(W, pos, stop_scan, &kind, &zero);
+            if (c == kOpen) {
+                open = true;
+                break;
+            }
+            if (lane == 0 && n < U.out_cap) out[n] = c | (kind << 62);
+            n++;
+            pos = c;
+            if (pos >= U.stop) break;
+            // inside a zero run: up to 64 further min-sized chunks per step
+            while (zero && pos < d.n) {
+                uint32_t m = zero_run(s, d.n, W.mn, W.mx, pos, lane);
+                if (m == 0) break;
+                if (pos + (uint64_t)m * W.mn >= U.stop)
+                    m = (uint32_t)((U.stop - pos + W.mn - 1) / W.mn);
+                if (lane < m && n + lane < U.out_cap)
+                    out[n + lane] = (pos + (lane + 1) * W.mn) | (kKindZone << 62);
+                n += m;
+                pos += (uint64_t)m * W.mn;
+                if (pos >= U.stop || m < 64) break;
+            }
+            if (pos >= U.stop) break;
+        }
+        if (lane == 0)
+            pstatus[u] = min(n, (uint64_t)U.out_cap) | (open ? kOpenFlag : 0ull) |
+                         (n > U.out_cap ? (kOpenFlag << 1) : 0ull);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Check: one wave per unit with piece >= 1 (the boundary at its start).
+__global__ __launch_bounds__(64) void rcdc_walk_check_kernel(
+    const uint8_t *__restrict__ arena, const StreamDesc *__restrict__ sds,
+    const WalkUnit *__restrict__ units, WalkParams prm, const uint64_t *__restrict__ gtab,
+    const uint64_t *__restrict__ piece_cuts, const uint64_t *__restrict__ pstatus,
+    BoundRes *__restrict__ bres, uint32_t *ctr, uint32_t *__restrict__ fixlist) {
+    __shared__ uint64_t s_mod[256];
+    __shared__ uint8_t s_win[128];
+    const uint32_t lane = threadIdx.x;
+    for (uint32_t i = lane; i < 256; i += 64) s_mod[i] = gtab[256 + i];
+    __syncthreads();
+    const uint32_t u = blockIdx.x;
+    if (u >= prm.nunits) return;
+    const WalkUnit U = units[u];
+    if (U.piece == 0) return;
+    const WalkUnit Up = units[u - 1];
+    const StreamDesc d = sds[U.stream];
+    const uint8_t *s = arena + d.off;
+    const uint64_t N = d.n, mn = prm.min_size, mx = prm.max_size;
+    const ModPlain mod{s_mod};
+    BoundRes R;
+    R.kind = kBoundNone;
+    R.nhops = 0;
+    R.merge_unit = u;
+    R.merge_idx = -1;
+    R.fix_from = 0;
+
+    const uint64_t sp = pstatus[u - 1];
+    const uint64_t np = sp & 0xFFFFFFFFu;
+    const bool open_prev = (sp & kOpenFlag) != 0;
+    const uint64_t *Lprev = piece_cuts + Up.out_base;
+    const uint64_t sj = pstatus[u];
+    const uint64_t nj = sj & 0xFFFFFFFFu;
+    const bool open_j = (sj & kOpenFlag) != 0;
+    const uint64_t *L = piece_cuts + U.out_base;
+    const uint64_t aj = U.start;
+    const uint64_t open_end = U.stop + mn + 64;  // open_j: searched hit-free below this
+
+    // Exact state at the previous piece's end (exact if that piece is):
+    // closed at c, or open at c with [c+min+64, aj+min+64) hit-free and no
+    // zone cut in c's zone.
+    uint64_t c;
+    bool pending = false;
+    if (open_prev) {
+        c = np ? (Lprev[np - 1] & kCutVal) : Up.start;
+        pending = true;
+    } else {
+        c = np ? (Lprev[np - 1] & kCutVal) : N;
+    }
+    if (!pending && c >= N) {
+        if (lane == 0) bres[u] = R;  // the stream ended before this piece
+        return;
+    }
+    // region lookup in L: first pure hit >= lo below lim as far as the walker
+    // verified it; kNoCut = unknown.
+    auto region = [&](uint64_t lo, uint64_t lim) -> uint64_t {
+        uint64_t res = kNoCut;
+        bool found = false;
+        for (uint64_t t0 = 0; t0 < nj && !found; t0 += 64) {
+            const uint64_t t = t0 + lane;
+            bool mine = false;
+            uint64_t r = kNoCut;
+            if (t < nj) {
+                const uint64_t prev = t == 0 ? aj : (L[t - 1] & kCutVal);
+                const uint64_t v = L[t] & kCutVal, kd = L[t] >> 62;
+                const uint64_t base = prev + mn + 64;
+                if (kd != kKindZone && base <= lo && lo <= v) {
+                    mine = true;
+                    if (kd == kKindHit) r = min(v, lim);
+                    else if (kd == kKindMax) r = lim <= v ? lim : kNoCut;
+                    else r = lim;  // EOF: hit-free to N >= lim
+                }
+            }
+            const uint64_t b = __builtin_amdgcn_ballot_w64(mine);
+            if (b) {
+                found = true;
+                res = readlane64(r, (uint32_t)__builtin_ctzll(b));
+            }
+        }
+        if (!found && open_j) {
+            const uint64_t base = (nj ? (L[nj - 1] & kCutVal) : aj) + mn + 64;
+            if (base <= lo && lo < open_end && lim <= open_end) res = lim;
+        }
+        return res;
+    };
+
+    for (int step = 0; step <= kMaxHops; step++) {
+        if (!pending) {
+            if (c == aj) {
+                R.kind = kBoundMerged;
+                R.merge_idx = -1;
+                break;
+            }
+            const int64_t at = find_cut(L, nj, c, lane);
+            if (at >= 0) {
+                R.kind = kBoundMerged;
+                R.merge_idx = (int32_t)at;
+                break;
+            }
+            if (step == kMaxHops) {
+                R.kind = kBoundFixup;
+                R.fix_from = c;
+                break;
+            }
+        }
+        uint64_t nxt;
+        if (pending) {
+            pending = false;
+            nxt = region(aj + mn + 64, min(c + mx, N));
+        } else if (N - c <= mn) {
+            nxt = N;
+        } else {
+            const uint64_t z = c + mn, lim = min(c + mx, N);
+            bool zz;
+            const uint64_t zc = zone_wave(s, N, z, lim, prm.mask, prm.shift, mod, s_win, lane, &zz);
+            if (zc != kNoCut) nxt = zc;
+            else if (lim <= z + 64) nxt = lim;
+            else nxt = region(z + 64, lim);
+        }
+        if (nxt == kNoCut) {
+            R.kind = kBoundFixup;
+            R.fix_from = c;
+            break;
+        }
+        R.hops[R.nhops++] = nxt;
+        c = nxt;
+        if (c >= N) {
+            R.kind = kBoundEnd;
+            break;
+        }
+    }
+    if (lane == 0) {
+        bres[u] = R;
+        if (R.kind == kBoundFixup) fixlist[atomicAdd(&ctr[1], 1u)] = u;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Fixup: persistent workgroups over the boundaries the check could not
+// resolve; each walks the exact chain with 1024-lane rounds until a cut lies
+// on a piece's chain (that piece's list, or the previous one's crossing cut).
+template <int TSH, bool SMALL>
+__global__ __launch_bounds__(1024, 1) void rcdc_walk_fixup_kernel(
+    const uint8_t *__restrict__ arena, const StreamDesc *__restrict__ sds,
+    const WalkUnit *__restrict__ units, WalkParams prm, const uint64_t *__restrict__ gtab,
+    const uint64_t *__restrict__ piece_cuts, const uint64_t *__restrict__ pstatus,
+    const BoundRes *__restrict__ bres, uint32_t *ctr, const uint32_t *__restrict__ fixlist,
+    uint64_t *__restrict__ fix_cuts, FixRes *__restrict__ fixres) {
+    const uint32_t nfix = __atomic_load_n(&ctr[1], __ATOMIC_RELAXED);
+    if (blockIdx.x >= nfix) return;
+    __shared__ __attribute__((aligned(16))) uint8_t s_tab[kLdsBytes];
+    __shared__ __attribute__((aligned(16))) uint8_t s_win[128];
+    __shared__ uint64_t s_red[16];
+    __shared__ uint64_t s_bc[4];
+    fill_tables(s_tab, gtab, prm.idx_shift, threadIdx.x, 1024);
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    Walk W;
+    W.arena = arena;
+    W.arena_len = prm.arena_len;
+    W.mn = prm.min_size;
+    W.mx = prm.max_size;
+    W.S = prm.seg_bytes;
+    W.mask = prm.mask;
+    W.shift = prm.shift;
+    W.tab = s_tab;
+    W.k = make_consts(lane, prm.mask, prm.idx_shift);
+    W.win = s_win;
+    W.red = s_red;
+    W.lane = lane;
+    W.wave = wave;
+    W.tid = threadIdx.x;
+    for (uint32_t idx = blockIdx.x; idx < nfix; idx += gridDim.x) {
+        const uint32_t u = fixlist[idx];
+        const WalkUnit U = units[u];
+        const StreamDesc d = sds[U.stream];
+        W.off = d.off;
+        W.N = d.n;
+        const uint8_t *s = arena + d.off;
+        uint64_t *out = fix_cuts + (uint64_t)u * prm.fix_cap;
+        uint64_t c = bres[u].fix_from, n = 0;
+        uint32_t munit = kNoUnit;
+        int32_t midx = -1;
+        while (c < d.n && n <= prm.fix_cap) {
+            uint64_t kind;
+            bool zero;
+            uint64_t nxt = walk_next<1024, TSH, SMALL>(W, c, ~0ull, &kind, &zero);
+            uint32_t m = 1;
+            if (zero && nxt < d.n) {  // zero run: this cut and up to 63 more
+                if (wave == 0) {
+                    const uint32_t zr = zero_run(s, d.n, W.mn, W.mx, nxt, lane);
+                    if (lane == 0) s_bc[1] = zr;
+                }
+                __syncthreads();
+                m = 1 + (uint32_t)min(uni64(s_bc[1]), (uint64_t)63);
+                __syncthreads();
+            }
+            // emit the m cuts nxt, nxt + min, ...; stop at the first on a chain
+            bool merged = false;
+            for (uint32_t i = 0; i < m && !merged; i++) {
+                const uint64_t cut = nxt + (uint64_t)i * W.mn;
+                if (threadIdx.x == 0 && n < prm.fix_cap) out[n] = cut;
+                n++;
+                c = cut;
+                if (cut >= d.n) break;
+                // which piece's range holds cut; also the previous piece's crossing cut
+                if (wave == 0) {
+                    uint64_t k = min(cut / prm.piece_bytes, (uint64_t)U.npieces - 1);
+                    uint32_t mu = kNoUnit;
+                    int64_t at = -2;
+                    for (int back = 0; back < 2 && mu == kNoUnit; back++) {
+                        if (back == 1 && k == 0) break;
+                        const uint32_t uk = U.unit0 + (uint32_t)(k - back);
+                        if (uk < u) break;  // never before the boundary's own piece
+                        const WalkUnit Uk = units[uk];
+                        const uint64_t nk = pstatus[uk] & 0xFFFFFFFFu;
+                        if (back == 0 && cut == Uk.start) {
+                            mu = uk;
+                            at = -1;
+                        } else {
+                            at = find_cut(piece_cuts + Uk.out_base, nk, cut, lane);
+                            if (at >= 0) mu = uk;
+                        }
+                    }
+                    if (lane == 0) {
+                        s_bc[2] = mu;
+                        s_bc[3] = (uint64_t)(int64_t)at;
+                    }
+                }
+                __syncthreads();
+                const uint32_t mu_all = (uint32_t)uni64(s_bc[2]);
+                if (mu_all != kNoUnit) {
+                    merged = true;
+                    munit = mu_all;
+                    midx = (int32_t)(int64_t)uni64(s_bc[3]);
+                }
+                __syncthreads();
+            }
+            if (merged) break;
+        }
+        if (threadIdx.x == 0) {
+            FixRes F;
+            F.count = (uint32_t)min(n, (uint64_t)prm.fix_cap + 1);
+            F.merge_unit = munit;
+            F.merge_idx = midx;
+            F.pad = 0;
+            fixres[u] = F;
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Assemble: one wave per walked stream (units[unit0 .. unit0 + npieces)).
+// counts[stream] = ~0 flags a stream whose fixup overflowed (the host redoes
+// it on the scan path).
+__global__ __launch_bounds__(64) void rcdc_walk_assemble_kernel(
+    const StreamDesc *__restrict__ sds, const WalkUnit *__restrict__ units,
+    const uint32_t *__restrict__ stream_unit0, uint32_t nstreams, WalkParams prm,
+    const uint64_t *__restrict__ piece_cuts, const uint64_t *__restrict__ pstatus,
+    const BoundRes *__restrict__ bres, const uint64_t *__restrict__ fix_cuts,
+    const FixRes *__restrict__ fixres, uint64_t *__restrict__ cuts,
+    uint64_t *__restrict__ counts) {
+    const uint32_t lane = threadIdx.x;
+    if (blockIdx.x >= nstreams) return;
+    const uint32_t u0 = stream_unit0[blockIdx.x];
+    const WalkUnit U0 = units[u0];
+    const StreamDesc d = sds[U0.stream];
+    uint64_t *out = cuts + d.cut_base;
+    const uint64_t cap = d.cut_cap;
+    uint64_t nc = 0;
+    bool bad = false;
+    auto append = [&](const uint64_t *src, uint64_t a, uint64_t b, uint64_t vmask) {
+        for (uint64_t i = a + lane; i < b; i += 64)
+            if (nc + (i - a) < cap) out[nc + (i - a)] = src[i] & vmask;
+        nc += b - a;
+    };
+    auto list_n = [&](uint32_t uu) { return pstatus[uu] & 0xFFFFFFFFu; };
+    append(piece_cuts + units[u0].out_base, 0, list_n(u0), kCutVal);
+    uint32_t j = 1;
+    while (j < U0.npieces) {
+        const uint32_t u = u0 + j;
+        const BoundRes &B = bres[u];
+        if (B.kind == kBoundNone) break;
+        append(B.hops, 0, B.nhops, ~0ull);
+        if (B.kind == kBoundEnd) break;
+        uint32_t mu;
+        int32_t mi;
+        if (B.kind == kBoundMerged) {
+            mu = B.merge_unit;
+            mi = B.merge_idx;
+        } else {
+            const FixRes F = fixres[u];
+            if (F.count > prm.fix_cap) {
+                bad = true;
+                break;
+            }
+            append(fix_cuts + (uint64_t)u * prm.fix_cap, 0, F.count, ~0ull);
+            if (F.merge_unit == kNoUnit) break;  // ran to N
+            mu = F.merge_unit;
+            mi = F.merge_idx;
+        }
+        append(piece_cuts + units[mu].out_base, (uint64_t)(mi + 1), list_n(mu), kCutVal);
+        j = units[mu].piece + 1;
+    }
+    if (nc > cap) bad = true;
+    if (lane == 0) counts[U0.stream] = bad ? ~0ull : nc;
+}
+
+// ---------------------------------------------------------------------------
+namespace rcdc {
+
+// The hashing part: counters reset + the walk kernel.
+hipError_t launch_walk(const uint8_t *arena, const StreamDesc *sds, const WalkUnit *units,
+                       const WalkParams &prm, const uint64_t *gtab, uint64_t *piece_cuts,
+                       uint64_t *pstatus, uint32_t *ctr, uint32_t blocks, hipStream_t stream) {
+    if (prm.nunits == 0) return hipSuccess;
+    hipError_t e = hipMemsetAsync(ctr, 0, 4 * sizeof(uint32_t), stream);
+    if (e != hipSuccess) return e;
+    const bool small = prm.mask < 0xFFFFu;
+#define RCDC_WALK_LAUNCH(TSH, SM)                                                                  \
+    hipLaunchKernelGGL((rcdc_walk_kernel<TSH, SM>), dim3(blocks), dim3(1024), 0, stream, arena,   \
+                       sds, units, prm, gtab, piece_cuts, pstatus, ctr)
+    if (prm.idx_shift == 21 && !small) RCDC_WALK_LAUNCH(105, false);
+    else if (small) RCDC_WALK_LAUNCH(-1, true);
+    else RCDC_WALK_LAUNCH(-1, false);
+#undef RCDC_WALK_LAUNCH
+    return hipGetLastError();
+}
+
+// The chain part: boundary checks, fixups, assembly into cuts / counts.
+hipError_t launch_walk_chain(const uint8_t *arena, const StreamDesc *sds, const WalkUnit *units,
+                             const uint32_t *stream_unit0, uint32_t nstreams,
+                             const WalkParams &prm, const uint64_t *gtab,
+                             const uint64_t *piece_cuts, const uint64_t *pstatus, BoundRes *bres,
+                             uint32_t *ctr, uint32_t *fixlist, uint64_t *fix_cuts,
+                             FixRes *fixres, uint64_t *cuts, uint64_t *counts,
+                             uint32_t fix_blocks, hipStream_t stream) {
+    if (prm.nunits == 0) return hipSuccess;
+    static const bool dbg = getenv("RCDC_DEBUG_SYNC") != nullptr;
+    hipLaunchKernelGGL(rcdc_walk_check_kernel, dim3(prm.nunits), dim3(64), 0, stream, arena, sds,
+                       units, prm, gtab, piece_cuts, pstatus, bres, ctr, fixlist);
+    if (dbg) {
+        (void)hipStreamSynchronize(stream);
+        uint32_t h[4];
+        (void)hipMemcpy(h, ctr, 16, hipMemcpyDeviceToHost);
+        fprintf(stderr, "rcdc: check done, %u fixups\n", h[1]);
+    }
+    const bool small = prm.mask < 0xFFFFu;
+#define RCDC_FIX_LAUNCH(TSH, SM)                                                                   \
+    hipLaunchKernelGGL((rcdc_walk_fixup_kernel<TSH, SM>), dim3(fix_blocks), dim3(1024), 0, stream, \
+                       arena, sds, units, prm, gtab, piece_cuts, pstatus, bres, ctr, fixlist,      \
+                       fix_cuts, fixres)
+    if (prm.idx_shift == 21 && !small) RCDC_FIX_LAUNCH(105, false);
+    else if (small) RCDC_FIX_LAUNCH(-1, true);
+    else RCDC_FIX_LAUNCH(-1, false);
+#undef RCDC_FIX_LAUNCH
+    if (dbg) {
+        (void)hipStreamSynchronize(stream);
+        fprintf(stderr, "rcdc: fixup done\n");
+    }
+    hipLaunchKernelGGL(rcdc_walk_assemble_kernel, dim3(nstreams), dim3(64), 0, stream, sds, units,
+                       stream_unit0, nstreams, prm, piece_cuts, pstatus, bres, fix_cuts, fixres,
+                       cuts, counts);
+    return hipGetLastError();
+}
+
+}  // namespace rcdc

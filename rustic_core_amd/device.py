@@ -52,7 +52,7 @@ class DevicePlan:
         st = _lib.lib().rcdc_plan_get_info(self._h, ctypes.byref(inf))
         if st:
             raise status_error(st, _lib.last_error())
-        return {k: getattr(inf, k) for k, _ in _lib.PlanInfo._fields_ if k != "reserved"}
+        return {k: getattr(inf, k) for k, _ in _lib.PlanInfo._fields_}
 
     def run(self, d_arena_ptr: int, hip_stream: Optional[int] = None) -> None:
         st = _lib.lib().rcdc_plan_run(self._h, ctypes.c_void_p(d_arena_ptr),
@@ -84,8 +84,10 @@ class DevicePlan:
             raise status_error(st, _lib.last_error())
         return dc.value, dn.value, np.ctypeslib.as_array(base, shape=(max(self.n, 1),))[:self.n]
 
-    def set_timing(self, enable: bool) -> None:
-        st = _lib.lib().rcdc_plan_set_timing(self._h, int(enable))
+    def set_timing(self, enable: bool, every: int = 1) -> None:
+        """HIP events around the kernels of every ``every``-th run (see
+        ``rcdc_plan_set_timing``); ``enable=False`` stops recording."""
+        st = _lib.lib().rcdc_plan_set_timing(self._h, int(every) if enable else 0)
         if st:
             raise status_error(st, _lib.last_error())
 

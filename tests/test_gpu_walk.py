@@ -1,0 +1,179 @@
+"""Device parity of the walk path (rcdc_walk.hip) for long streams.
+
+The walk hashes only what the reference hashes (rabin.rs:127-188 skips each
+chunk's first min bytes) and splits long streams into pieces whose chains are
+stitched where they meet the true chain.  Small pieces (RCDC_WALK_PIECE) and
+small chunk parameters put many piece boundaries, merge failures and fixup
+walks into every case; every cut list is diffed against the CPU oracle.
+"""
+import numpy as np
+import pytest
+
+from oracle import oracle
+
+pytestmark = pytest.mark.gpu
+
+KiB = 1 << 10
+MiB = 1 << 20
+
+
+@pytest.fixture
+def walk_env(monkeypatch, gpu_ctx):
+    def set_(piece, min_pieces=1, fixcap=None):
+        monkeypatch.setenv("RCDC_WALK_PIECE", str(piece))
+        monkeypatch.setenv("RCDC_WALK_MIN_PIECES", str(min_pieces))
+        if fixcap is not None:
+            monkeypatch.setenv("RCDC_WALK_FIXCAP", str(fixcap))
+    return set_
+
+
+def _run(params, bufs, offsets=None, expect_walk=True, poly=oracle.DEFAULT_POLY):
+    import torch
+    from rustic_core_amd.chunker import Context
+    from rustic_core_amd.device import DevicePlan, pack_offsets
+    mn, avg, mx = params
+    ctx = Context.get(poly, mn, avg, mx, device=0)
+    lens = [len(b) for b in bufs]
+    if offsets is None:
+        offs, alen = pack_offsets(lens)
+    else:
+        offs = np.array(offsets, np.uint64)
+        alen = int(max(o + n for o, n in zip(offsets, lens))) + 256
+    host = np.zeros(alen, np.uint8)
+    for o, b in zip(offs, bufs):
+        host[int(o):int(o) + len(b)] = b
+    dev = torch.from_numpy(host).to("cuda:0")
+    plan = DevicePlan(ctx, offs, lens, alen)
+    if expect_walk:
+        assert plan.info()["walk_pieces"] > 0, "walk path not selected"
+    plan.run(dev.data_ptr())
+    got = plan.results()
+    plan.close()
+    for i, b in enumerate(bufs):
+        exp = oracle.chunk_cuts(b, poly, mn, avg, mx)
+        assert np.array_equal(got[i], exp), (i, len(got[i]), len(exp),
+                                             _first_diff(got[i], exp))
+    return got
+
+
+def _first_diff(a, b):
+    n = min(len(a), len(b))
+    d = np.nonzero(a[:n] != b[:n])[0]
+    i = int(d[0]) if len(d) else n
+    return i, a[max(i - 2, 0):i + 2], b[max(i - 2, 0):i + 2]
+
+
+def _rand(seed, n):
+    return np.random.default_rng(seed).integers(0, 256, n, dtype=np.uint8)
+
+
+def _mixed(seed, n, rmin, rmax, zmin, zmax):
+    rng = np.random.default_rng(seed)
+    out = np.zeros(n, np.uint8)
+    p = 0
+    while p < n:
+        r = int(rng.integers(rmin, rmax))
+        out[p:p + r] = rng.integers(0, 256, min(r, n - p), dtype=np.uint8)
+        p += r + int(rng.integers(zmin, zmax))
+    return out
+
+
+SMALL = (8 * KiB, 16 * KiB, 64 * KiB)
+DEFAULT = (512 * KiB, 1 * MiB, 8 * MiB)
+
+
+def test_walk_random_small_params(walk_env):
+    walk_env(256 * KiB)
+    _run(SMALL, [_rand(10 + i, 6 * MiB + 1013 * i) for i in range(6)])
+
+
+def test_walk_random_default_params(walk_env):
+    walk_env(4 * MiB)
+    _run(DEFAULT, [_rand(20 + i, 96 * MiB + 777 * i) for i in range(3)])
+
+
+def test_walk_zeros_in_and_out_of_phase(walk_env):
+    walk_env(256 * KiB)
+    z = np.zeros(8 * MiB, np.uint8)
+    shifted = np.concatenate([_rand(3, 12345), np.zeros(8 * MiB, np.uint8), _rand(4, 3 * MiB)])
+    _run(SMALL, [z, shifted])
+
+
+def test_walk_mixed_entropy(walk_env):
+    walk_env(256 * KiB)
+    bufs = [_mixed(30 + i, 8 * MiB, 4 * KiB, 512 * KiB, 1 * KiB, 600 * KiB) for i in range(4)]
+    _run(SMALL, bufs)
+
+
+def test_walk_mixed_default_params(walk_env):
+    walk_env(4 * MiB)
+    bufs = [_mixed(40 + i, 128 * MiB, 64 * KiB, 16 * MiB, 4 * KiB, 16 * MiB) for i in range(2)]
+    _run(DEFAULT, bufs)
+
+
+def test_walk_low_entropy(walk_env):
+    """Periodic data: either no candidate at all (max cuts everywhere) or a
+    candidate in every period."""
+    walk_env(256 * KiB)
+    pat3 = np.resize(np.frombuffer(b"abc", np.uint8), 5 * MiB)
+    pat7 = np.resize(np.frombuffer(b"rustic!", np.uint8), 5 * MiB)
+    ones = np.full(5 * MiB, 1, np.uint8)
+    _run(SMALL, [pat3, pat7, ones])
+
+
+def test_walk_unaligned_offsets_and_short_streams(walk_env):
+    """Walked and scan-path streams in one plan, at odd arena offsets."""
+    walk_env(256 * KiB)
+    bufs = [_rand(50, 5 * MiB), _rand(51, 100 * KiB), _rand(52, 3 * MiB + 7), np.zeros(0, np.uint8),
+            _mixed(53, 4 * MiB, 4 * KiB, 300 * KiB, 1 * KiB, 200 * KiB)]
+    offs, o = [], 3
+    for b in bufs:
+        offs.append(o)
+        o += len(b) + 13
+    _run(SMALL, bufs, offsets=offs)
+
+
+@pytest.mark.parametrize("poly", [(1 << 40) | 0x1B, 0x3DA3358B4DC173 ^ (1 << 20),
+                                  (1 << 56) | 0x95])
+def test_walk_other_degrees(walk_env, poly):
+    walk_env(256 * KiB)
+    _run(SMALL, [_rand(60, 4 * MiB), _mixed(61, 4 * MiB, 4 * KiB, 300 * KiB, 1 * KiB, 200 * KiB)],
+         poly=poly)
+
+
+def test_walk_small_mask(walk_env):
+    """avg < 2^16: the masked (SMALL) prefilter instantiation."""
+    walk_env(64 * KiB)
+    _run((1 * KiB, 4 * KiB, 16 * KiB), [_rand(70, 2 * MiB), _mixed(71, 2 * MiB, 1024, 64 * KiB,
+                                                                     256, 64 * KiB)])
+
+
+def test_walk_fixup_overflow_falls_back(walk_env):
+    """Fixup capacity 1 forces the host re-run of a stream on the scan path."""
+    walk_env(128 * KiB, fixcap=1)
+    _run(SMALL, [_rand(80, 4 * MiB), np.concatenate([_rand(81, 999), np.zeros(3 * MiB, np.uint8),
+                                                     _rand(82, MiB)])])
+
+
+def test_walk_selected_by_default_for_large_batches():
+    """Without overrides a plan over >= 1024 pieces' worth of long streams
+    walks (64 x 64 MiB = 1024 pieces of 4 MiB); parity on two of them."""
+    import torch
+    from rustic_core_amd.chunker import Context
+    from rustic_core_amd.device import DevicePlan, pack_offsets
+    mn, avg, mx = DEFAULT
+    ctx = Context.get(oracle.DEFAULT_POLY, mn, avg, mx, device=0)
+    lens = [64 * MiB] * 64
+    offs, alen = pack_offsets(lens)
+    g = torch.Generator(device="cuda:0")
+    g.manual_seed(90)
+    arena = torch.randint(0, 256, (alen,), dtype=torch.uint8, device="cuda:0", generator=g)
+    plan = DevicePlan(ctx, offs, lens, alen)
+    assert plan.info()["walk_pieces"] == 1024
+    plan.run(arena.data_ptr())
+    got = plan.results()
+    plan.close()
+    for i in (0, 63):
+        o = int(offs[i])
+        host = arena[o:o + lens[i]].cpu().numpy()
+        assert np.array_equal(got[i], oracle.chunk_cuts(host, oracle.DEFAULT_POLY, mn, avg, mx))
