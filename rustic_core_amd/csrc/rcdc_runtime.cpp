@@ -567,6 +567,44 @@ rcdc_status plan_results(rcdc_plan *pl, uint64_t *cuts, uint64_t cap, uint64_t *
     std::vector<uint64_t> cnt(pl->n);
     if (pl->n)
         HIP_TRY(hipMemcpy(cnt.data(), pl->d_counts, pl->n * 8, hipMemcpyDeviceToHost));
+    if (const char *e = getenv("RCDC_WALK_DUMP"); e && !pl->wunits.empty()) {  // debugging aid
+        const uint32_t want = (uint32_t)atoi(e);
+        const size_t nw = pl->wunits.size();
+        std::vector<uint64_t> ps(nw), pc(pl->nwpiece_cuts);
+        std::vector<BoundRes> br(nw);
+        std::vector<FixRes> fr(nw);
+        std::vector<uint64_t> fc(nw * pl->wprm.fix_cap);
+        HIP_TRY(hipMemcpy(ps.data(), pl->d_pstatus, nw * 8, hipMemcpyDeviceToHost));
+        HIP_TRY(hipMemcpy(pc.data(), pl->d_wpiece, pc.size() * 8, hipMemcpyDeviceToHost));
+        HIP_TRY(hipMemcpy(br.data(), pl->d_bres, nw * sizeof(BoundRes), hipMemcpyDeviceToHost));
+        HIP_TRY(hipMemcpy(fr.data(), pl->d_fixres, nw * sizeof(FixRes), hipMemcpyDeviceToHost));
+        HIP_TRY(hipMemcpy(fc.data(), pl->d_fixcuts, fc.size() * 8, hipMemcpyDeviceToHost));
+        for (size_t u = 0; u < nw; u++) {
+            const WalkUnit &U = pl->wunits[u];
+            if (U.stream != want) continue;
+            fprintf(stderr, "unit %zu piece %u [%llu,%llu) n=%llu open=%d:", u, U.piece,
+                    (unsigned long long)U.start, (unsigned long long)U.stop,
+                    (unsigned long long)(ps[u] & 0xFFFFFFFFu), (int)((ps[u] >> 32) & 1));
+            for (uint64_t i = 0; i < (ps[u] & 0xFFFFFFFFu); i++) {
+                const uint64_t v = pc[U.out_base + i];
+                fprintf(stderr, " %llu%c", (unsigned long long)(v & kCutVal), "hmez"[v >> 62]);
+            }
+            if (U.piece) {
+                const BoundRes &B = br[u];
+                fprintf(stderr, "\n   bound kind %u nhops %u merge %u/%d fix_from %llu hops:", B.kind,
+                        B.nhops, B.merge_unit, B.merge_idx, (unsigned long long)B.fix_from);
+                for (uint32_t i = 0; i < B.nhops && i < (uint32_t)kMaxHops; i++)
+                    fprintf(stderr, " %llu", (unsigned long long)B.hops[i]);
+                if (B.kind == kBoundFixup) {
+                    fprintf(stderr, "\n   fix count %u merge %u/%d:", fr[u].count, fr[u].merge_unit,
+                            fr[u].merge_idx);
+                    for (uint32_t i = 0; i < fr[u].count && i < pl->wprm.fix_cap; i++)
+                        fprintf(stderr, " %llu", (unsigned long long)fc[u * pl->wprm.fix_cap + i]);
+                }
+            }
+            fprintf(stderr, "\n");
+        }
+    }
     // a walked stream whose fixup overflowed (count ~0): redo it on the scan
     // path over the same device bytes
     std::vector<std::vector<uint64_t>> redo(pl->n);

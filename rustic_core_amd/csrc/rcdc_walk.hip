@@ -155,22 +155,33 @@ struct Walk {
 };
 
 // First pure-window candidate p in [q, end) among the positions of one round
-// [A, A + LANES*S) (A: stream position with off + A 64-byte aligned); kNoCut
-// if none.  Lane t scans [A + t*S, A + (t+1)*S) after a 64-byte warm-up.
+// (A: stream position with off + A 64-byte aligned); kNoCut if none.  Lane t
+// hashes bytes [A - 64 + t*S, A + (t+1)*S): after the 64-byte warm-up the
+// first slide gives the window of position A + t*S + 1, so lane t tests
+// [A + 1 + t*S, A + 1 + (t+1)*S) (the scan kernel's r = 0 <-> lane start + 65).
 template <int LANES, int TSH, bool SMALL>
 __device__ uint64_t round_first(const Walk &W, uint64_t A, uint64_t q, uint64_t end) {
-    const uint64_t P0 = A + (uint64_t)W.tid * W.S;
-    const uint32_t rlo = q > P0 ? (uint32_t)min(q - P0, (uint64_t)W.S) : 0u;
-    const uint32_t rhi = end > P0 ? (uint32_t)min(end - P0, (uint64_t)W.S) : 0u;
+    const uint64_t P0 = A + 1 + (uint64_t)W.tid * W.S;
+    // signed clamps: hipcc (ROCm 7.2) dropped the `end > P0 ?` guard of the
+    // unsigned form in the workgroup instantiation (lanes past `end` then
+    // counted a full segment; seen in the .s and on the device)
+    const int64_t dlo = (int64_t)q - (int64_t)P0, dhi = (int64_t)end - (int64_t)P0;
+    const uint32_t rlo = (uint32_t)min(max(dlo, (int64_t)0), (int64_t)W.S);
+    const uint32_t rhi = (uint32_t)min(max(dhi, (int64_t)0), (int64_t)W.S);
     const uint64_t valid = __builtin_amdgcn_ballot_w64(rlo < rhi);
     uint64_t best = kNoCut;
     if (valid) {
-        const uint64_t base = W.off + A - 64;  // >= off: A >= q - 63 >= pos + min + 1
+        const uint64_t base = W.off + A - 64;  // >= off: A >= q - 64 >= pos + min
         const uint64_t wbase = base + (uint64_t)W.wave * 64u * W.S;
         const uint64_t rest = W.arena_len > wbase ? W.arena_len - wbase : 0;
+        // integer clamp, made provably uniform: a descriptor hipcc cannot
+        // prove uniform costs a waterfall loop per buffer load
+        // (cdna_hip_programming.md T20); min(uint64_t, unsigned long long)
+        // had resolved to the double overload
+        const uint32_t rec = __builtin_amdgcn_readfirstlane(
+            (uint32_t)(rest < 0xFFFFFFFFull ? rest : 0xFFFFFFFFull));
         const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
-            (void *)(W.arena + wbase), (short)0, (int)(uint32_t)min(rest, 0xFFFFFFFFull),
-            0x00020000);
+            (void *)(W.arena + wbase), (short)0, (int)rec, 0x00020000);
         const Chain c = scan_segment<kWR, false, TSH, SMALL, kWG>(rsrc, W.lane * W.S, W.S / kUnit,
                                                                    rlo, rhi, W.tab, W.k, valid,
                                                                    W.lane);
@@ -178,6 +189,13 @@ __device__ uint64_t round_first(const Walk &W, uint64_t A, uint64_t q, uint64_t 
         if (hits) {
             const uint32_t L = (uint32_t)__builtin_ctzll(hits);
             best = readlane64(P0 + c.first, L);
+#ifdef RCDC_WALK_PRINTF
+            if (LANES > 64 && W.lane == L)
+                printf("round wave %u lane %u A %llu q %llu end %llu P0 %llu first %u rlo %u rhi %u -> %llu\n",
+                       W.wave, L, (unsigned long long)A, (unsigned long long)q,
+                       (unsigned long long)end, (unsigned long long)P0, c.first, rlo, rhi,
+                       (unsigned long long)(P0 + c.first));
+#endif
         }
     }
     if constexpr (LANES > 64) {
@@ -234,7 +252,7 @@ __device__ uint64_t walk_next(const Walk &W, uint64_t pos, uint64_t stop_scan, u
     }
     const uint64_t q = z + 64;
     const uint64_t end = min(limit, stop_scan);
-    uint64_t A = ((W.off + q) & ~63ull) - W.off;
+    uint64_t A = ((W.off + q - 1) & ~63ull) - W.off;  // A + 1 <= q: q is tested
     while (A < end) {
         const uint64_t p = round_first<LANES, TSH, SMALL>(W, A, q, end);
         if (p != kNoCut) {

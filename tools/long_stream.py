@@ -1,6 +1,6 @@
 """Scan / resolve timing on long streams (C3 / C5 shapes), parity vs oracle.
 
-usage: python tools/long_stream.py [GiB_per_stream] [n_streams]
+usage: python tools/long_stream.py [GiB_per_stream] [n_streams] [case,case..]
 Cases: random, zeros, mixed (random runs 64 KiB-16 MiB + zero runs 4 KiB-16 MiB).
 """
 import os, sys, time
@@ -30,7 +30,8 @@ def mixed(dev_arr, off, length, rng):
         pos += L
 
 
-for case in ("random", "zeros", "mixed"):
+cases = sys.argv[3].split(",") if len(sys.argv) > 3 else ["random", "zeros", "mixed"]
+for case in cases:
     lens = [n] * ns
     offs, alen = pack_offsets(lens)
     arena = torch.zeros(alen, dtype=torch.uint8, device="cuda")
