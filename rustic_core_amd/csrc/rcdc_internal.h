@@ -122,6 +122,8 @@ struct WalkParams {
     uint32_t shift;        // deg - 8
     uint32_t nunits;
     uint32_t fix_cap;      // fixup cut slots per boundary
+    uint32_t fix_seg;      // S for the fixup walker (latency-bound: smaller rounds)
+    uint32_t pad;
 };
 
 constexpr int kMaxHops = 13;  // chain steps the check kernel resolves itself

@@ -442,6 +442,8 @@ rcdc_status plan_build(rcdc_ctx *ctx, rcdc_plan *pl, const uint64_t *offs, const
     // a fixup walks until it meets a piece's chain: a few chunks, longer only
     // through phase-shifted zero runs (min-sized chunks); more -> host redo
     wp.fix_cap = (uint32_t)(4 * (Lp ? Lp : 1) / ctx->min + ctx->max / ctx->min + 64);
+    wp.fix_seg = 512;
+    if (const char *e = getenv("RCDC_FIX_SEG")) wp.fix_seg = (uint32_t)std::max(atoi(e) / 128 * 128, 128);
     if (const char *e = getenv("RCDC_WALK_FIXCAP")) wp.fix_cap = (uint32_t)std::max(atoi(e), 1);  // tests
     const uint64_t supers = (pl->items.size() + nc - 1) / nc;
     const uint64_t waves_needed = (supers + nthreads / 64 - 1) / (nthreads / 64);

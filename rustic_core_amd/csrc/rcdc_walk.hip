@@ -281,6 +281,17 @@ __device__ int64_t find_cut(const uint64_t *L, uint64_t n, uint64_t c, uint32_t 
     return -2;
 }
 
+// Per-lane form of find_cut: binary search in the sorted list.
+__device__ int64_t find_cut_lane(const uint64_t *L, uint64_t n, uint64_t c) {
+    uint64_t lo = 0, hi = n;
+    while (lo < hi) {
+        const uint64_t mid = (lo + hi) >> 1;
+        if ((L[mid] & kCutVal) < c) lo = mid + 1;
+        else hi = mid;
+    }
+    return (lo < n && (L[lo] & kCutVal) == c) ? (int64_t)lo : -2;
+}
+
 }  // namespace
 
 // ---------------------------------------------------------------------------
@@ -518,7 +529,7 @@ __global__ __launch_bounds__(1024, 1) void rcdc_walk_fixup_kernel(
     W.arena_len = prm.arena_len;
     W.mn = prm.min_size;
     W.mx = prm.max_size;
-    W.S = prm.seg_bytes;
+    W.S = prm.fix_seg;
     W.mask = prm.mask;
     W.shift = prm.shift;
     W.tab = s_tab;
@@ -543,57 +554,59 @@ __global__ __launch_bounds__(1024, 1) void rcdc_walk_fixup_kernel(
             uint64_t kind;
             bool zero;
             uint64_t nxt = walk_next<1024, TSH, SMALL>(W, c, ~0ull, &kind, &zero);
-            uint32_t m = 1;
-            if (zero && nxt < d.n) {  // zero run: this cut and up to 63 more
-                if (wave == 0) {
-                    const uint32_t zr = zero_run(s, d.n, W.mn, W.mx, nxt, lane);
-                    if (lane == 0) s_bc[1] = zr;
-                }
-                __syncthreads();
-                m = 1 + (uint32_t)min(uni64(s_bc[1]), (uint64_t)63);
-                __syncthreads();
-            }
-            // emit the m cuts nxt, nxt + min, ...; stop at the first on a chain
-            bool merged = false;
-            for (uint32_t i = 0; i < m && !merged; i++) {
-                const uint64_t cut = nxt + (uint64_t)i * W.mn;
-                if (threadIdx.x == 0 && n < prm.fix_cap) out[n] = cut;
-                n++;
-                c = cut;
-                if (cut >= d.n) break;
-                // which piece's range holds cut; also the previous piece's crossing cut
-                if (wave == 0) {
-                    uint64_t k = min(cut / prm.piece_bytes, (uint64_t)U.npieces - 1);
-                    uint32_t mu = kNoUnit;
-                    int64_t at = -2;
-                    for (int back = 0; back < 2 && mu == kNoUnit; back++) {
-                        if (back == 1 && k == 0) break;
-                        const uint32_t uk = U.unit0 + (uint32_t)(k - back);
-                        if (uk < u) break;  // never before the boundary's own piece
-                        const WalkUnit Uk = units[uk];
-                        const uint64_t nk = pstatus[uk] & 0xFFFFFFFFu;
-                        if (back == 0 && cut == Uk.start) {
-                            mu = uk;
-                            at = -1;
-                        } else {
-                            at = find_cut(piece_cuts + Uk.out_base, nk, cut, lane);
-                            if (at >= 0) mu = uk;
+            // The cuts nxt, nxt + min, ... (m > 1 inside a zero run); wave 0
+            // checks them lane-parallel and the first one on a piece chain (or
+            // at N) ends the run of cuts.
+            if (wave == 0) {
+                uint32_t m = 1;
+                if (zero && nxt < d.n)
+                    m = 1 + min(zero_run(s, d.n, W.mn, W.mx, nxt, lane), 63u);
+                const uint64_t cut = nxt + (uint64_t)lane * W.mn;
+                uint32_t mu = kNoUnit;
+                int64_t at = -2;
+                bool stop = false;
+                if (lane < m) {
+                    if (cut >= d.n) {
+                        stop = true;
+                    } else {
+                        const uint64_t k = min(cut / prm.piece_bytes, (uint64_t)U.npieces - 1);
+                        for (int back = 0; back < 2 && mu == kNoUnit; back++) {
+                            if (back == 1 && k == 0) break;
+                            const uint32_t uk = U.unit0 + (uint32_t)(k - back);
+                            if (uk < u) break;  // never before the boundary's own piece
+                            const WalkUnit Uk = units[uk];
+                            if (back == 0 && cut == Uk.start) {
+                                mu = uk;
+                                at = -1;
+                            } else {
+                                at = find_cut_lane(piece_cuts + Uk.out_base,
+                                                   pstatus[uk] & 0xFFFFFFFFu, cut);
+                                if (at >= 0) mu = uk;
+                            }
                         }
-                    }
-                    if (lane == 0) {
-                        s_bc[2] = mu;
-                        s_bc[3] = (uint64_t)(int64_t)at;
+                        stop = mu != kNoUnit;
                     }
                 }
-                __syncthreads();
-                const uint32_t mu_all = (uint32_t)uni64(s_bc[2]);
-                if (mu_all != kNoUnit) {
-                    merged = true;
-                    munit = mu_all;
-                    midx = (int32_t)(int64_t)uni64(s_bc[3]);
+                const uint64_t hit = __builtin_amdgcn_ballot_w64(stop);
+                const uint32_t first = hit ? (uint32_t)__builtin_ctzll(hit) : m - 1;
+                if (lane <= first && n + lane < prm.fix_cap) out[n + lane] = cut;
+                if (lane == first) {
+                    s_bc[0] = cut;
+                    s_bc[1] = first + 1;
+                    s_bc[2] = mu;
+                    s_bc[3] = (uint64_t)at;
                 }
-                __syncthreads();
             }
+            __syncthreads();
+            c = uni64(s_bc[0]);
+            n += uni64(s_bc[1]);
+            const uint32_t mu_all = (uint32_t)uni64(s_bc[2]);
+            const bool merged = mu_all != kNoUnit && c < d.n;
+            if (merged) {
+                munit = mu_all;
+                midx = (int32_t)(int64_t)uni64(s_bc[3]);
+            }
+            __syncthreads();
             if (merged) break;
         }
         if (threadIdx.x == 0) {
