@@ -621,60 +621,173 @@ __global__ __launch_bounds__(1024, 1) void rcdc_walk_fixup_kernel(
 }
 
 // ---------------------------------------------------------------------------
-// Assemble: one wave per walked stream (units[unit0 .. unit0 + npieces)).
+// Assemble: one workgroup per walked stream (units[unit0 .. unit0 + npieces)).
+// Node j >= 1 is the boundary at piece j's start; on the exact chain it adds
+// its hops, its fixup cuts and the tail of the list it merged into, then the
+// chain goes on at node next(j) = piece(merge unit) + 1 > j.  Nodes are taken
+// kAsmB at a time: every thread prepares one node, thread 0 follows the chain
+// through the block by runs of "simple" nodes (next = j + 1, the common case),
+// and a block prefix sum places each on-chain node's segment.
 // counts[stream] = ~0 flags a stream whose fixup overflowed (the host redoes
 // it on the scan path).
-__global__ __launch_bounds__(64) void rcdc_walk_assemble_kernel(
+constexpr int kAsmB = 1024;
+
+__global__ __launch_bounds__(kAsmB) void rcdc_walk_assemble_kernel(
     const StreamDesc *__restrict__ sds, const WalkUnit *__restrict__ units,
     const uint32_t *__restrict__ stream_unit0, uint32_t nstreams, WalkParams prm,
     const uint64_t *__restrict__ piece_cuts, const uint64_t *__restrict__ pstatus,
     const BoundRes *__restrict__ bres, const uint64_t *__restrict__ fix_cuts,
     const FixRes *__restrict__ fixres, uint64_t *__restrict__ cuts,
     uint64_t *__restrict__ counts) {
-    const uint32_t lane = threadIdx.x;
+    constexpr int NW = kAsmB / 64;
+    __shared__ uint64_t s_ns[NW];          // bitmap: node is not simple
+    __shared__ uint32_t s_next[kAsmB];     // next node (stream piece index)
+    __shared__ uint8_t s_term[kAsmB];      // node ends the chain
+    __shared__ uint32_t s_rng[2 * kAsmB];  // on-chain ranges [lo, hi) of this block
+    __shared__ uint64_t s_wsum[NW];
+    __shared__ uint32_t s_st[4];           // cur, done, nranges
     if (blockIdx.x >= nstreams) return;
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
     const uint32_t u0 = stream_unit0[blockIdx.x];
     const WalkUnit U0 = units[u0];
     const StreamDesc d = sds[U0.stream];
     uint64_t *out = cuts + d.cut_base;
     const uint64_t cap = d.cut_cap;
-    uint64_t nc = 0;
-    bool bad = false;
-    auto append = [&](const uint64_t *src, uint64_t a, uint64_t b, uint64_t vmask) {
-        for (uint64_t i = a + lane; i < b; i += 64)
-            if (nc + (i - a) < cap) out[nc + (i - a)] = src[i] & vmask;
-        nc += b - a;
-    };
+    const uint32_t P = U0.npieces;
     auto list_n = [&](uint32_t uu) { return pstatus[uu] & 0xFFFFFFFFu; };
-    append(piece_cuts + units[u0].out_base, 0, list_n(u0), kCutVal);
-    uint32_t j = 1;
-    while (j < U0.npieces) {
+
+    const uint64_t n0 = list_n(u0);
+    for (uint64_t i = tid; i < n0 && i < cap; i += kAsmB)
+        out[i] = piece_cuts[U0.out_base + i] & kCutVal;
+    uint64_t nc = n0;
+    bool bad = false;
+    uint32_t cur = 1, done = P <= 1;
+    for (uint32_t b = 1; !done && b < P; b += kAsmB) {
+        if (cur >= b + kAsmB) continue;
+        // ---- this thread's node
+        const uint32_t j = b + tid;
+        const bool valid = j < P;
+        bool term = true, nbad = false;
+        uint32_t nh = 0, fc = 0, mu = kNoUnit, nxt = P;
+        uint64_t tail_lo = 0, tail_hi = 0;
         const uint32_t u = u0 + j;
-        const BoundRes &B = bres[u];
-        if (B.kind == kBoundNone) break;
-        append(B.hops, 0, B.nhops, ~0ull);
-        if (B.kind == kBoundEnd) break;
-        uint32_t mu;
-        int32_t mi;
-        if (B.kind == kBoundMerged) {
-            mu = B.merge_unit;
-            mi = B.merge_idx;
-        } else {
-            const FixRes F = fixres[u];
-            if (F.count > prm.fix_cap) {
-                bad = true;
-                break;
+        if (valid) {
+            const uint32_t kind = bres[u].kind;
+            if (kind != kBoundNone) {
+                nh = bres[u].nhops;
+                if (kind == kBoundMerged || kind == kBoundFixup) {
+                    int32_t mi = bres[u].merge_idx;
+                    mu = bres[u].merge_unit;
+                    if (kind == kBoundFixup) {
+                        const FixRes F = fixres[u];
+                        mu = F.merge_unit;
+                        mi = F.merge_idx;
+                        if (F.count > prm.fix_cap) {
+                            nbad = true;
+                            mu = kNoUnit;
+                        } else {
+                            fc = F.count;
+                        }
+                    }
+                    if (mu != kNoUnit) {
+                        term = false;
+                        tail_lo = (uint64_t)(mi + 1);
+                        tail_hi = list_n(mu);
+                        nxt = units[mu].piece + 1;
+                    }
+                }
             }
-            append(fix_cuts + (uint64_t)u * prm.fix_cap, 0, F.count, ~0ull);
-            if (F.merge_unit == kNoUnit) break;  // ran to N
-            mu = F.merge_unit;
-            mi = F.merge_idx;
         }
-        append(piece_cuts + units[mu].out_base, (uint64_t)(mi + 1), list_n(mu), kCutVal);
-        j = units[mu].piece + 1;
+        const uint64_t len = nbad ? 0 : nh + fc + (tail_hi - tail_lo);
+        s_next[tid] = nxt;
+        s_term[tid] = term;
+        const uint64_t ns = __builtin_amdgcn_ballot_w64(!(valid && !term && nxt == j + 1));
+        if (lane == 0) s_ns[wave] = ns;
+        __syncthreads();
+        // ---- the chain through this block (thread 0)
+        if (tid == 0) {
+            uint32_t c = cur - b, nr = 0, dn = 0, cu = cur;
+            while (true) {
+                // first non-simple node f >= c
+                uint32_t f = kAsmB;
+                for (uint32_t w = c >> 6; w < (uint32_t)NW; w++) {
+                    uint64_t m = s_ns[w];
+                    if (w == (c >> 6)) m &= ~0ull << (c & 63u);
+                    if (m) {
+                        f = w * 64u + (uint32_t)__builtin_ctzll(m);
+                        break;
+                    }
+                }
+                if (f == (uint32_t)kAsmB) {  // runs through the block
+                    s_rng[2 * nr] = c;
+                    s_rng[2 * nr + 1] = kAsmB;
+                    nr++;
+                    cu = b + kAsmB;
+                    break;
+                }
+                if (b + f >= P) {  // past the last piece
+                    s_rng[2 * nr] = c;
+                    s_rng[2 * nr + 1] = f;
+                    nr++;
+                    dn = 1;
+                    break;
+                }
+                s_rng[2 * nr] = c;
+                s_rng[2 * nr + 1] = f + 1;
+                nr++;
+                if (s_term[f] || s_next[f] >= P) {
+                    dn = 1;
+                    break;
+                }
+                cu = s_next[f];
+                if (cu >= b + kAsmB) break;
+                c = cu - b;
+            }
+            s_st[0] = cu;
+            s_st[1] = dn;
+            s_st[2] = nr;
+        }
+        __syncthreads();
+        const uint32_t nr = __builtin_amdgcn_readfirstlane(s_st[2]);
+        bool on = false;
+        for (uint32_t r = 0; r < nr; r++)
+            on |= tid >= s_rng[2 * r] && tid < s_rng[2 * r + 1];
+        on = on && valid;
+        bad |= on && nbad;
+        // ---- block exclusive prefix sum of the on-chain segment lengths
+        uint64_t v = on ? len : 0;
+        for (uint32_t o = 1; o < 64; o <<= 1) {
+            const uint64_t t = __shfl_up(v, o, 64);
+            if (lane >= o) v += t;
+        }
+        if (lane == 63) s_wsum[wave] = v;
+        __syncthreads();
+        uint64_t base = 0, total = 0;
+        for (uint32_t w = 0; w < (uint32_t)NW; w++) {
+            const uint64_t t = s_wsum[w];
+            if (w < wave) base += t;
+            total += t;
+        }
+        if (on) {
+            uint64_t o = nc + base + v - len;
+            for (uint32_t i = 0; i < nh; i++, o++)
+                if (o < cap) out[o] = bres[u].hops[i];
+            const uint64_t *fsrc = fix_cuts + (uint64_t)u * prm.fix_cap;
+            for (uint32_t i = 0; i < fc; i++, o++)
+                if (o < cap) out[o] = fsrc[i];
+            if (mu != kNoUnit) {
+                const uint64_t *L = piece_cuts + units[mu].out_base;
+                for (uint64_t i = tail_lo; i < tail_hi; i++, o++)
+                    if (o < cap) out[o] = L[i] & kCutVal;
+            }
+        }
+        nc += total;
+        cur = __builtin_amdgcn_readfirstlane(s_st[0]);
+        done = __builtin_amdgcn_readfirstlane(s_st[1]);
+        __syncthreads();
     }
-    if (nc > cap) bad = true;
-    if (lane == 0) counts[U0.stream] = bad ? ~0ull : nc;
+    const bool any_bad = __syncthreads_or(bad);
+    if (tid == 0) counts[U0.stream] = (any_bad || nc > cap) ? ~0ull : nc;
 }
 
 // ---------------------------------------------------------------------------
@@ -729,7 +842,7 @@ hipError_t launch_walk_chain(const uint8_t *arena, const StreamDesc *sds, const 
         (void)hipStreamSynchronize(stream);
         fprintf(stderr, "rcdc: fixup done\n");
     }
-    hipLaunchKernelGGL(rcdc_walk_assemble_kernel, dim3(nstreams), dim3(64), 0, stream, sds, units,
+    hipLaunchKernelGGL(rcdc_walk_assemble_kernel, dim3(nstreams), dim3(kAsmB), 0, stream, sds, units,
                        stream_unit0, nstreams, prm, piece_cuts, pstatus, bres, fix_cuts, fixres,
                        cuts, counts);
     return hipGetLastError();

@@ -177,3 +177,13 @@ def test_walk_selected_by_default_for_large_batches():
         o = int(offs[i])
         host = arena[o:o + lens[i]].cpu().numpy()
         assert np.array_equal(got[i], oracle.chunk_cuts(host, oracle.DEFAULT_POLY, mn, avg, mx))
+
+
+def test_walk_many_pieces_per_stream(walk_env):
+    # > 1024 pieces per stream: the assembler follows the chain over several
+    # node blocks, and the phase-shifted 40 MiB zero run's fixup merges more
+    # than a block (2560 pieces) later
+    walk_env(16 * KiB, fixcap=8192)
+    shifted = np.concatenate([_rand(90, 999), np.zeros(40 * MiB, np.uint8), _rand(91, 3 * MiB)])
+    _run(SMALL, [_rand(92, 40 * MiB), np.zeros(40 * MiB, np.uint8), shifted,
+                 _mixed(93, 40 * MiB, 4 * KiB, 1 * MiB, 1 * KiB, 4 * MiB)])
