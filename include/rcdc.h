@@ -162,6 +162,36 @@ rcdc_status rcdc_plan_kernel_times(rcdc_plan *plan, uint64_t *runs,
 uint64_t rcdc_fixed_cuts(uint64_t n, uint64_t size, uint64_t *cuts,
                          uint64_t cap);
 
+/* ---- SHA-256 blob ids: crypto/hasher.rs:17-19 `hash(&chunk)`, called per
+ * chunk by FileArchiver::backup_reader (archiver/file_archiver.rs:151) ---- */
+
+/* One chunk of a device arena: bytes [off, off + len). */
+typedef struct {
+    uint64_t off;
+    uint64_t len;
+} rcdc_chunk_ref;
+
+/* SHA-256 of n chunks of a device arena.  d_refs (16-B aligned) and
+ * d_digests (32 bytes per chunk, 4-B aligned) are device pointers.
+ * Asynchronous on hip_stream (0: the context's stream).                    */
+rcdc_status rcdc_sha256_chunks(rcdc_ctx *ctx, const void *d_arena,
+                               const rcdc_chunk_ref *d_refs, uint32_t n,
+                               uint8_t *d_digests, void *hip_stream);
+
+/* Fused blob ids of a plan: after rcdc_plan_run over d_arena (the same
+ * pointer), enqueue the SHA-256 of every chunk it found, on the device
+ * cut list (no host round trip).  Asynchronous.                           */
+rcdc_status rcdc_plan_hash(rcdc_plan *plan, const void *d_arena,
+                           void *hip_stream);
+
+/* Synchronise and copy the digests to the host: 32 bytes per chunk, in the
+ * order of rcdc_plan_results' cuts (whose counts it also writes).          */
+rcdc_status rcdc_plan_digests(rcdc_plan *plan, uint8_t *digests,
+                              uint64_t cap_chunks, uint64_t *cut_counts);
+
+/* Device view: slot-indexed like rcdc_plan_device_results' d_cuts. */
+rcdc_status rcdc_plan_device_digests(rcdc_plan *plan, uint64_t *d_digests);
+
 /* ABI version of the loaded library (== RCDC_ABI_VERSION). */
 uint32_t rcdc_abi_version(void);
 

@@ -22,6 +22,7 @@ EXPORTS = (
     "rcdc_stream_open", "rcdc_stream_feed", "rcdc_stream_close", "rcdc_plan_create",
     "rcdc_plan_destroy", "rcdc_plan_run", "rcdc_plan_results", "rcdc_plan_device_results",
     "rcdc_plan_get_info", "rcdc_plan_set_timing", "rcdc_plan_kernel_times", "rcdc_fixed_cuts",
+    "rcdc_sha256_chunks", "rcdc_plan_hash", "rcdc_plan_digests", "rcdc_plan_device_digests",
 )
 ABI_VERSION = 1
 
@@ -124,6 +125,14 @@ def lib() -> ctypes.CDLL:
     L.rcdc_plan_kernel_times.argtypes = [vp, P(u64), P(ctypes.c_double), P(ctypes.c_double)]
     L.rcdc_fixed_cuts.restype = u64
     L.rcdc_fixed_cuts.argtypes = [u64, u64, vp, u64]
+    L.rcdc_sha256_chunks.restype = st
+    L.rcdc_sha256_chunks.argtypes = [vp, vp, vp, u32, vp, vp]
+    L.rcdc_plan_hash.restype = st
+    L.rcdc_plan_hash.argtypes = [vp, vp, vp]
+    L.rcdc_plan_digests.restype = st
+    L.rcdc_plan_digests.argtypes = [vp, vp, u64, vp]
+    L.rcdc_plan_device_digests.restype = st
+    L.rcdc_plan_device_digests.argtypes = [vp, P(u64)]
     _lib = L
     return L
 

@@ -45,6 +45,11 @@ hipError_t launch_walk_chain(const uint8_t *arena, const StreamDesc *sds, const 
                              uint32_t *ctr, uint32_t *fixlist, uint64_t *fix_cuts,
                              FixRes *fixres, uint64_t *cuts, uint64_t *counts,
                              uint32_t fix_blocks, hipStream_t stream);
+hipError_t launch_sha256_list(const uint8_t *arena, const ulonglong2 *refs, uint32_t n,
+                              uint32_t *digests, hipStream_t stream);
+hipError_t launch_sha256_plan(const uint8_t *arena, const StreamDesc *sds, uint32_t nstreams,
+                              const uint64_t *cuts, const uint64_t *counts, uint64_t nslots,
+                              uint32_t *digests, hipStream_t stream);
 }  // namespace rcdc
 
 using namespace rcdc;
@@ -155,6 +160,10 @@ struct rcdc_plan {
     hipStream_t last_stream = nullptr;
     hipEvent_t done = nullptr;
     bool ran = false;
+    // SHA-256 of every chunk (rcdc_plan_hash), slot-indexed like d_cuts
+    uint32_t *d_dig = nullptr;
+    uint64_t cap_dig = 0;
+    bool hashed = false;
     // optional per-run kernel timing
     bool timing = false;
     uint32_t tperiod = 1;         // record every tperiod-th run (rcdc_plan_set_timing)
@@ -557,6 +566,7 @@ rcdc_status plan_run(rcdc_plan *pl, const void *d_arena, hipStream_t stream) {
     pl->last_stream = stream;
     HIP_TRY(hipEventRecord(pl->done, stream));
     pl->ran = true;
+    pl->hashed = false;
     return RCDC_OK;
 }
 
@@ -667,6 +677,7 @@ void plan_release(rcdc_plan *pl) {
     (void)hipFree(pl->d_masks);
     (void)hipFree(pl->d_cuts);
     (void)hipFree(pl->d_counts);
+    (void)hipFree(pl->d_dig);
     (void)hipFree(pl->d_units);
     (void)hipFree(pl->d_stitches);
     (void)hipFree(pl->d_piece_cuts);
@@ -936,6 +947,109 @@ uint64_t rcdc_fixed_cuts(uint64_t n, uint64_t size, uint64_t *cuts, uint64_t cap
         s = e;
     }
     return k;
+}
+
+// ---- SHA-256 blob ids (crypto/hasher.rs:17-19, file_archiver.rs:151) -----
+
+rcdc_status rcdc_sha256_chunks(rcdc_ctx *ctx, const void *d_arena, const rcdc_chunk_ref *d_refs,
+                               uint32_t n, uint8_t *d_digests, void *hip_stream) {
+    if (!valid_ctx(ctx) || (n && (!d_arena || !d_refs || !d_digests)))
+        return fail(RCDC_ERR_INVALID_INPUT, "null argument");
+    if (((uintptr_t)d_digests & 3) || ((uintptr_t)d_refs & 15))
+        return fail(RCDC_ERR_INVALID_INPUT, "digests must be 4-byte and refs 16-byte aligned");
+    DeviceGuard g(ctx->device);
+    hipStream_t st = hip_stream ? (hipStream_t)hip_stream : ctx->stream;
+    HIP_TRY(launch_sha256_list((const uint8_t *)d_arena, (const ulonglong2 *)d_refs, n,
+                               (uint32_t *)d_digests, st));
+    return RCDC_OK;
+}
+
+rcdc_status rcdc_plan_hash(rcdc_plan *plan, const void *d_arena, void *hip_stream) {
+    if (!plan || (!d_arena && plan->arena_len)) return fail(RCDC_ERR_INVALID_INPUT, "null argument");
+    if (!plan->ran) return fail(RCDC_ERR_INVALID_INPUT, "plan has not been run");
+    if (d_arena != plan->last_arena)
+        return fail(RCDC_ERR_INVALID_INPUT, "arena differs from the last rcdc_plan_run");
+    DeviceGuard g(plan->ctx->device);
+    hipStream_t st = hip_stream ? (hipStream_t)hip_stream : plan->last_stream;
+    if (!st) st = plan->ctx->stream;
+    rcdc_status rs;
+    if ((rs = ensure_dev(&plan->d_dig, &plan->cap_dig, plan->ncuts * 8))) return rs;
+    if (st != plan->last_stream) HIP_TRY(hipStreamWaitEvent(st, plan->done, 0));
+    HIP_TRY(launch_sha256_plan((const uint8_t *)d_arena, plan->d_sds, plan->n, plan->d_cuts,
+                               plan->d_counts, plan->ncuts, plan->d_dig, st));
+    HIP_TRY(hipEventRecord(plan->done, st));
+    plan->hashed = true;
+    return RCDC_OK;
+}
+
+rcdc_status rcdc_plan_digests(rcdc_plan *plan, uint8_t *digests, uint64_t cap_chunks,
+                              uint64_t *cut_counts) {
+    if (!plan || (plan->n && !cut_counts)) return fail(RCDC_ERR_INVALID_INPUT, "null argument");
+    if (!plan->hashed) return fail(RCDC_ERR_INVALID_INPUT, "rcdc_plan_hash has not been run");
+    DeviceGuard g(plan->ctx->device);
+    std::vector<uint64_t> dcnt(plan->n);
+    HIP_TRY(hipEventSynchronize(plan->done));
+    if (plan->n)
+        HIP_TRY(hipMemcpy(dcnt.data(), plan->d_counts, plan->n * 8, hipMemcpyDeviceToHost));
+    uint64_t total_cap = 0;
+    for (uint32_t i = 0; i < plan->n; i++) total_cap += plan->sds[i].cut_cap;
+    std::vector<uint64_t> cuts(total_cap);
+    rcdc_status rs = plan_results(plan, cuts.data(), total_cap, cut_counts);
+    if (rs) return rs;
+    uint64_t total = 0;
+    for (uint32_t i = 0; i < plan->n; i++) total += cut_counts[i];
+    if (total > cap_chunks)
+        return fail(RCDC_ERR_CAPACITY, "need %llu digest slots, have %llu",
+                    (unsigned long long)total, (unsigned long long)cap_chunks);
+    std::vector<uint8_t> all(plan->ncuts * 32);
+    if (plan->ncuts)
+        HIP_TRY(hipMemcpy(all.data(), plan->d_dig, all.size(), hipMemcpyDeviceToHost));
+    // streams the walk path handed back to the scan path (device count ~0):
+    // their cuts came from the host-side redo, so hash them from that list
+    std::vector<ulonglong2> refs;
+    std::vector<uint64_t> ref_slot;
+    uint64_t o = 0;
+    for (uint32_t i = 0; i < plan->n; i++) {
+        if (dcnt[i] == ~0ull) {
+            uint64_t prev = 0;
+            for (uint64_t j = 0; j < cut_counts[i]; j++) {
+                refs.push_back({plan->sds[i].off + prev, cuts[o + j] - prev});
+                ref_slot.push_back(o + j);
+                prev = cuts[o + j];
+            }
+        } else if (cut_counts[i]) {
+            memcpy(digests + o * 32, all.data() + plan->cut_base[i] * 32, cut_counts[i] * 32);
+        }
+        o += cut_counts[i];
+    }
+    if (!refs.empty()) {
+        ulonglong2 *d_refs = nullptr;
+        uint32_t *d_out = nullptr;
+        std::vector<uint8_t> out(refs.size() * 32);
+        hipError_t e = hipMalloc((void **)&d_refs, refs.size() * sizeof(ulonglong2));
+        if (e == hipSuccess) e = hipMalloc((void **)&d_out, out.size());
+        if (e == hipSuccess)
+            e = hipMemcpy(d_refs, refs.data(), refs.size() * sizeof(ulonglong2),
+                          hipMemcpyHostToDevice);
+        if (e == hipSuccess)
+            e = launch_sha256_list((const uint8_t *)plan->last_arena, d_refs,
+                                   (uint32_t)refs.size(), d_out, plan->ctx->stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(plan->ctx->stream);
+        if (e == hipSuccess) e = hipMemcpy(out.data(), d_out, out.size(), hipMemcpyDeviceToHost);
+        (void)hipFree(d_refs);
+        (void)hipFree(d_out);
+        HIP_TRY(e);
+        for (size_t r = 0; r < refs.size(); r++)
+            memcpy(digests + ref_slot[r] * 32, out.data() + r * 32, 32);
+    }
+    return RCDC_OK;
+}
+
+rcdc_status rcdc_plan_device_digests(rcdc_plan *plan, uint64_t *d_digests) {
+    if (!plan || !d_digests) return fail(RCDC_ERR_INVALID_INPUT, "null argument");
+    if (!plan->hashed) return fail(RCDC_ERR_INVALID_INPUT, "rcdc_plan_hash has not been run");
+    *d_digests = (uint64_t)(uintptr_t)plan->d_dig;
+    return RCDC_OK;
 }
 
 // ---- streaming: one file fed in pieces -------------------------------------

@@ -1,0 +1,194 @@
+// rcdc_sha256.hip -- SHA-256 of every chunk, on the bytes already in HBM.
+//
+// Reference: the blob id of a chunk is `hash(&chunk)` = SHA-256
+// (crates/core/src/crypto/hasher.rs:17-19), computed by
+// FileArchiver::backup_reader right after the chunker yields the chunk
+// (crates/core/src/archiver/file_archiver.rs:151).  The chunker test
+// snapshot (src/chunker/snapshots/*chunk_random.snap) pins (len, sha256)
+// pairs, so the digests are checked against it directly.
+//
+// SHA-256 (FIPS 180-4) is a strict Merkle-Damgard chain: a chunk's 64-byte
+// blocks must be compressed in order, so the only parallelism is across
+// chunks.  One lane owns one chunk.  Per 64-byte block the lane issues 16
+// dword loads at its (4-aligned-down) address, realigns them with
+// v_alignbyte and byte-swaps with v_perm, expands the message schedule in a
+// 16-word register ring and runs the 64 rounds: ~1.4k VALU ops per block,
+// ~21 per byte, so the kernel is VALU-bound (not HBM-bound) and reaches its
+// throughput only with >= ~4 waves per SIMD of chunks in flight (C3/C4
+// scale), not on 1409 chunks (C2).
+#include <hip/hip_runtime.h>
+
+#include "rcdc_internal.h"
+
+namespace rcdc {
+
+namespace {
+
+__device__ __forceinline__ uint32_t rotr(uint32_t x, uint32_t n) {
+    return __builtin_amdgcn_alignbit(x, x, n);
+}
+
+__device__ __forceinline__ uint32_t bswap(uint32_t x) {
+    return __builtin_bswap32(x);  // one v_perm_b32
+}
+
+constexpr uint32_t kK[64] = {
+    0x428a2f98u, 0x71374491u, 0xb5c0fbcfu, 0xe9b5dba5u, 0x3956c25bu, 0x59f111f1u, 0x923f82a4u,
+    0xab1c5ed5u, 0xd807aa98u, 0x12835b01u, 0x243185beu, 0x550c7dc3u, 0x72be5d74u, 0x80deb1feu,
+    0x9bdc06a7u, 0xc19bf174u, 0xe49b69c1u, 0xefbe4786u, 0x0fc19dc6u, 0x240ca1ccu, 0x2de92c6fu,
+    0x4a7484aau, 0x5cb0a9dcu, 0x76f988dau, 0x983e5152u, 0xa831c66du, 0xb00327c8u, 0xbf597fc7u,
+    0xc6e00bf3u, 0xd5a79147u, 0x06ca6351u, 0x14292967u, 0x27b70a85u, 0x2e1b2138u, 0x4d2c6dfcu,
+    0x53380d13u, 0x650a7354u, 0x766a0abbu, 0x81c2c92eu, 0x92722c85u, 0xa2bfe8a1u, 0xa81a664bu,
+    0xc24b8b70u, 0xc76c51a3u, 0xd192e819u, 0xd6990624u, 0xf40e3585u, 0x106aa070u, 0x19a4c116u,
+    0x1e376c08u, 0x2748774cu, 0x34b0bcb5u, 0x391c0cb3u, 0x4ed8aa4au, 0x5b9cca4fu, 0x682e6ff3u,
+    0x748f82eeu, 0x78a5636fu, 0x84c87814u, 0x8cc70208u, 0x90befffau, 0xa4506cebu, 0xbef9a3f7u,
+    0xc67178f2u};
+
+struct Sha {
+    uint32_t s[8];
+    __device__ __forceinline__ void init() {
+        s[0] = 0x6a09e667u; s[1] = 0xbb67ae85u; s[2] = 0x3c6ef372u; s[3] = 0xa54ff53au;
+        s[4] = 0x510e527fu; s[5] = 0x9b05688cu; s[6] = 0x1f83d9abu; s[7] = 0x5be0cd19u;
+    }
+    // w[]: the block as 16 big-endian words (consumed: becomes the schedule)
+    __device__ __forceinline__ void compress(uint32_t w[16]) {
+        uint32_t a = s[0], b = s[1], c = s[2], d = s[3], e = s[4], f = s[5], g = s[6], h = s[7];
+#pragma unroll
+        for (int t = 0; t < 64; t++) {
+            uint32_t wt;
+            if (t < 16) {
+                wt = w[t];
+            } else {
+                const uint32_t w15 = w[(t - 15) & 15], w2 = w[(t - 2) & 15];
+                const uint32_t s0 = rotr(w15, 7) ^ rotr(w15, 18) ^ (w15 >> 3);
+                const uint32_t s1 = rotr(w2, 17) ^ rotr(w2, 19) ^ (w2 >> 10);
+                wt = w[t & 15] = w[t & 15] + s0 + w[(t - 7) & 15] + s1;
+            }
+            const uint32_t S1 = rotr(e, 6) ^ rotr(e, 11) ^ rotr(e, 25);
+            const uint32_t ch = (e & f) ^ (~e & g);
+            const uint32_t t1 = h + S1 + ch + kK[t] + wt;
+            const uint32_t S0 = rotr(a, 2) ^ rotr(a, 13) ^ rotr(a, 22);
+            const uint32_t maj = (a & b) | (c & (a | b));
+            const uint32_t t2 = S0 + maj;
+            h = g; g = f; f = e; e = d + t1;
+            d = c; c = b; b = a; a = t1 + t2;
+        }
+        s[0] += a; s[1] += b; s[2] += c; s[3] += d;
+        s[4] += e; s[5] += f; s[6] += g; s[7] += h;
+    }
+};
+
+// SHA-256 of arena[p, p + len) into out[0..8) (digest words, big-endian
+// byte order when stored as bytes: out bytes = digest bytes).
+__device__ __forceinline__ void sha256_range(const uint8_t *__restrict__ arena, uint64_t p,
+                                             uint64_t len, uint32_t *__restrict__ out) {
+    Sha sh;
+    sh.init();
+    const uint32_t k = (uint32_t)(p & 3);  // byte misalignment
+    const uint32_t *q = (const uint32_t *)(arena + (p - k));
+    const uint64_t nfull = len >> 6;
+    // carried dword: q[16] of block i is q[0] of block i + 1
+    uint32_t carry = nfull ? q[0] : 0;
+    for (uint64_t blk = 0; blk < nfull; blk++) {
+        uint32_t d[17];
+        d[0] = carry;
+#pragma unroll
+        for (int i = 1; i < 16; i++) d[i] = q[i];
+        // q[16] holds a byte of the chunk unless the chunk ends exactly here
+        d[16] = (64 < k + (len - (blk << 6))) ? q[16] : 0;
+        carry = d[16];
+        uint32_t w[16];
+#pragma unroll
+        for (int i = 0; i < 16; i++) w[i] = bswap(__builtin_amdgcn_alignbyte(d[i + 1], d[i], k));
+        sh.compress(w);
+        q += 16;
+    }
+    // tail: r < 64 data bytes, 0x80, zeros, 64-bit big-endian bit length
+    const uint32_t r = (uint32_t)(len & 63);
+    // last valid byte relative to q (aligned base): k + r - 1; dword j holds
+    // a valid byte iff 4j <= k + r - 1
+    uint32_t w[16];
+#pragma unroll
+    for (int i = 0; i < 16; i++) {
+        const uint32_t j0 = (uint32_t)i, j1 = (uint32_t)i + 1;
+        const uint32_t lo = (4 * j0 < k + r) ? q[j0] : 0;
+        const uint32_t hi = (4 * j1 < k + r) ? q[j1] : 0;
+        uint32_t v = __builtin_amdgcn_alignbyte(hi, lo, k);  // little-endian bytes 4i..4i+3
+        const int nv = (int)r - 4 * i;                         // valid bytes in this word
+        if (nv <= 0) v = 0;
+        else if (nv < 4) v &= (1u << (8 * nv)) - 1u;
+        if (nv >= 0 && nv < 4) v |= 0x80u << (8 * nv);
+        w[i] = bswap(v);
+    }
+    const uint64_t bits = len << 3;
+    if (r < 56) {
+        w[14] = (uint32_t)(bits >> 32);
+        w[15] = (uint32_t)bits;
+        sh.compress(w);
+    } else {
+        sh.compress(w);
+#pragma unroll
+        for (int i = 0; i < 14; i++) w[i] = 0;
+        w[14] = (uint32_t)(bits >> 32);
+        w[15] = (uint32_t)bits;
+        sh.compress(w);
+    }
+#pragma unroll
+    for (int i = 0; i < 8; i++) out[i] = bswap(sh.s[i]);
+}
+
+// Chunk list: chunk c = arena[refs[c].x, refs[c].x + refs[c].y).
+__global__ __launch_bounds__(64) void rcdc_sha256_list_kernel(const uint8_t *__restrict__ arena,
+                                                              const ulonglong2 *__restrict__ refs,
+                                                              uint32_t n,
+                                                              uint32_t *__restrict__ digests) {
+    const uint32_t c = blockIdx.x * 64 + threadIdx.x;
+    if (c >= n) return;
+    const ulonglong2 ref = refs[c];
+    sha256_range(arena, ref.x, ref.y, digests + 8ull * c);
+}
+
+// A plan's results: slot g in [0, nslots) belongs to the stream i with
+// cut_base <= g < cut_base + cut_cap; it is chunk j = g - cut_base of that
+// stream when j < counts[i] (a count of ~0 marks a stream the host redoes).
+__global__ __launch_bounds__(64) void rcdc_sha256_plan_kernel(
+    const uint8_t *__restrict__ arena, const StreamDesc *__restrict__ sds, uint32_t nstreams,
+    const uint64_t *__restrict__ cuts, const uint64_t *__restrict__ counts, uint64_t nslots,
+    uint32_t *__restrict__ digests) {
+    const uint64_t g = (uint64_t)blockIdx.x * 64 + threadIdx.x;
+    if (g >= nslots) return;
+    uint32_t lo = 0, hi = nstreams;  // last stream with cut_base <= g
+    while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (sds[mid].cut_base <= g) lo = mid;
+        else hi = mid;
+    }
+    const StreamDesc sd = sds[lo];
+    const uint64_t j = g - sd.cut_base;
+    const uint64_t cnt = counts[lo];
+    if (cnt == ~0ull || j >= cnt) return;
+    const uint64_t start = j ? cuts[g - 1] : 0;
+    const uint64_t end = cuts[g];
+    sha256_range(arena, sd.off + start, end - start, digests + 8ull * g);
+}
+
+}  // namespace
+
+hipError_t launch_sha256_list(const uint8_t *arena, const ulonglong2 *refs, uint32_t n,
+                              uint32_t *digests, hipStream_t stream) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(rcdc_sha256_list_kernel, dim3((n + 63) / 64), dim3(64), 0, stream, arena,
+                       refs, n, digests);
+    return hipGetLastError();
+}
+
+hipError_t launch_sha256_plan(const uint8_t *arena, const StreamDesc *sds, uint32_t nstreams,
+                              const uint64_t *cuts, const uint64_t *counts, uint64_t nslots,
+                              uint32_t *digests, hipStream_t stream) {
+    if (nslots == 0 || nstreams == 0) return hipSuccess;
+    hipLaunchKernelGGL(rcdc_sha256_plan_kernel, dim3((uint32_t)((nslots + 63) / 64)), dim3(64), 0,
+                       stream, arena, sds, nstreams, cuts, counts, nslots, digests);
+    return hipGetLastError();
+}
+
+}  // namespace rcdc

@@ -84,6 +84,29 @@ class DevicePlan:
             raise status_error(st, _lib.last_error())
         return dc.value, dn.value, np.ctypeslib.as_array(base, shape=(max(self.n, 1),))[:self.n]
 
+    def hash(self, d_arena_ptr: int, hip_stream: Optional[int] = None) -> None:
+        """Enqueue the SHA-256 blob id of every chunk of the last ``run``
+        (``rcdc_plan_hash``; crypto/hasher.rs:17-19, file_archiver.rs:151)."""
+        st = _lib.lib().rcdc_plan_hash(self._h, ctypes.c_void_p(d_arena_ptr),
+                                       ctypes.c_void_p(hip_stream or 0))
+        if st:
+            raise status_error(st, _lib.last_error())
+
+    def digests(self) -> list:
+        """Per stream, a ``(k, 32)`` uint8 array of chunk digests in cut order."""
+        cap = max(self.cap, 1)
+        dig = np.zeros((cap, 32), dtype=np.uint8)
+        counts = np.zeros(max(self.n, 1), dtype=np.uint64)
+        st = _lib.lib().rcdc_plan_digests(self._h, dig.ctypes.data, cap, counts.ctypes.data)
+        if st:
+            raise status_error(st, _lib.last_error())
+        out, o = [], 0
+        for i in range(self.n):
+            k = int(counts[i])
+            out.append(dig[o:o + k].copy())
+            o += k
+        return out
+
     def set_timing(self, enable: bool, every: int = 1) -> None:
         """HIP events around the kernels of every ``every``-th run (see
         ``rcdc_plan_set_timing``); ``enable=False`` stops recording."""
@@ -110,6 +133,29 @@ class DevicePlan:
             self.close()
         except Exception:  # interpreter shutdown
             pass
+
+
+def sha256_device(ctx: Context, arena_tensor, refs, out_tensor=None, stream=None):
+    """SHA-256 of chunks ``refs`` (an ``(n, 2)`` int64 CUDA tensor of
+    ``(offset, length)`` rows) of a device arena; returns an ``(n, 32)``
+    uint8 CUDA tensor (``rcdc_sha256_chunks``)."""
+    import torch
+
+    refs = refs.contiguous()
+    n = int(refs.shape[0])
+    if refs.dtype != torch.int64 or refs.dim() != 2 or refs.shape[1] != 2:
+        raise ValueError("refs must be an (n, 2) int64 tensor")
+    if out_tensor is None:
+        out_tensor = torch.empty((n, 32), dtype=torch.uint8, device=arena_tensor.device)
+    if not stream:  # order after torch's producers of arena / refs
+        stream = torch.cuda.current_stream(arena_tensor.device).cuda_stream
+    st = _lib.lib().rcdc_sha256_chunks(ctx.handle, ctypes.c_void_p(arena_tensor.data_ptr()),
+                                       ctypes.c_void_p(refs.data_ptr()), n,
+                                       ctypes.c_void_p(out_tensor.data_ptr()),
+                                       ctypes.c_void_p(stream or 0))
+    if st:
+        raise status_error(st, _lib.last_error())
+    return out_tensor
 
 
 def chunk_device(ctx: Context, arena_tensor, offs, lens, stream=None) -> list:
