@@ -68,6 +68,10 @@ def parse():
                     help="untimed seconds of steps after the W warmup steps (clock ramp)")
     ap.add_argument("--time-every", type=int, default=4,
                     help="HIP-event timing of the kernels on every n-th timed step")
+    ap.add_argument("--sha256", action="store_true",
+                    help="also measure the fused blob ids (rcdc_plan_hash, SURVEY 8(f) row 1), "
+                         "reported as a separate object; the headline value is unchanged")
+    ap.add_argument("--sha-steps", type=int, default=5)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-parity", action="store_true")
     ap.add_argument("--e2e", action="store_true",
@@ -474,6 +478,9 @@ def main():
     if rank == 0 and not args.no_cpu_baseline and world == 1:
         out_extra["cpu_baseline"] = cpu_baseline(arena.cpu().numpy(), offs, lens,
                                                  args.cpu_seconds)
+    if args.sha256:
+        out_extra["sha256"] = sha_measure(torch, plan, ptr, sptr, dev, args, arena, offs, lens,
+                                          rank == 0 and world == 1 and not args.no_cpu_baseline)
     if args.e2e and rank == 0:
         out_extra["e2e"] = e2e_rate(torch, arena, offs, lens, plan, args.workload)
 
@@ -507,6 +514,70 @@ def main():
     plan.close()
     if world > 1:
         dist.destroy_process_group()
+
+
+def sha_measure(torch, plan, ptr, sptr, dev, args, arena, offs, lens, cpu: bool) -> dict:
+    """Blob ids (SHA-256 per chunk, crypto/hasher.rs:17-19) on the device:
+    hash-only kernel time over the plan's cut list (HIP events on the launch
+    stream), the fused chunk + hash step rate, a hashlib spot check and a
+    hashlib CPU rate.  The kernel is VALU-bound (~21 VALU ops per byte,
+    DESIGN.md 3c), so its roofline is the measured VALU issue rate, not HBM."""
+    import hashlib
+
+    # a stream of our own: torch's current stream may be the null stream
+    # (cuda_stream == 0), which the C ABI maps to the context's stream, and
+    # the events must be on the stream the kernel is launched on
+    side = torch.cuda.Stream(dev)
+    sptr = side.cuda_stream
+    plan.run(ptr, sptr)
+    plan.hash(ptr, sptr)
+    torch.cuda.synchronize(dev)
+    cuts = plan.results()
+    nchunks = int(sum(len(c) for c in cuts))
+    in_bytes = int(lens.sum())
+    k = max(args.sha_steps, 1)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(side)
+    for _ in range(k):
+        plan.hash(ptr, sptr)
+    e1.record(side)
+    torch.cuda.synchronize(dev)
+    hash_ms = e0.elapsed_time(e1) / k
+    t0 = time.perf_counter()
+    for _ in range(k):
+        plan.run(ptr, sptr)
+        plan.hash(ptr, sptr)
+    torch.cuda.synchronize(dev)
+    fused_s = (time.perf_counter() - t0) / k
+    # spot check: the first chunks of up to 4 streams against hashlib
+    digs = plan.digests()
+    checked = mism = 0
+    for i in range(min(4, len(lens))):
+        o = int(offs[i])
+        prev = 0
+        for j, c in enumerate(cuts[i][:8]):
+            b = arena[o + prev:o + int(c)].cpu().numpy().tobytes()
+            mism += hashlib.sha256(b).digest() != bytes(digs[i][j])
+            checked += 1
+            prev = int(c)
+    out = {
+        "kernel": "rcdc_sha256_plan_kernel",
+        "chunks_per_launch": nchunks,
+        "hash_ms_per_launch": round(hash_ms, 3),
+        "hash_gibs": round(in_bytes / (hash_ms / 1e3) / GiB, 2),
+        "fused_chunk_and_hash_gibs": round(in_bytes / fused_s / GiB, 2),
+        "bound": "valu (one lane per chunk; SHA-256 is a sequential chain per chunk)",
+        "spot_check": {"chunks": checked, "mismatches": mism, "checker": "hashlib"},
+    }
+    if cpu:
+        sample = arena[int(offs[0]):int(offs[0]) + min(int(lens[0]), 256 << 20)].cpu().numpy()
+        sample = sample.tobytes()
+        t0, n = time.perf_counter(), 0
+        while time.perf_counter() - t0 < 2.0:
+            hashlib.sha256(sample).digest()
+            n += len(sample)
+        out["cpu_hashlib_gibs_1thread"] = round(n / (time.perf_counter() - t0) / GiB, 3)
+    return out
 
 
 def parity_check(args, arena, offs, lens, plan, last, desc) -> dict:

@@ -28,6 +28,49 @@ __device__ __forceinline__ uint32_t rotr(uint32_t x, uint32_t n) {
     return __builtin_amdgcn_alignbit(x, x, n);
 }
 
+// x ^ y ^ z in one v_bitop3_b32 (truth table 0xF0 ^ 0xCC ^ 0xAA)
+__device__ __forceinline__ uint32_t xor3(uint32_t x, uint32_t y, uint32_t z) {
+    return __builtin_amdgcn_bitop3_b32(x, y, z, 0x96);
+}
+
+// Prefetch of the next block: 4 x global_load_dwordx4 (4-byte aligned
+// addresses are accepted) + 1 dword, issued as inline asm.  Plain loads of
+// read-only bytes get rematerialised next to their use by the compiler,
+// which re-exposes the full HBM latency every block; volatile loads become
+// uncached (sc0 sc1) with a wait after each.  The compiler does not track
+// these loads, so wait_loads() must run before any use of their results;
+// its "+v" operands order every use (and copy) after the wait.
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+struct Blk {
+    u32x4 v0, v1, v2, v3;
+    uint32_t x16;
+};
+__device__ __forceinline__ void issue_loads(const uint32_t *p, uint32_t o16, Blk &b) {
+    const uint32_t *p16 = p + o16;
+    asm volatile(
+        "global_load_dwordx4 %0, %5, off\n\t"
+        "global_load_dwordx4 %1, %5, off offset:16\n\t"
+        "global_load_dwordx4 %2, %5, off offset:32\n\t"
+        "global_load_dwordx4 %3, %5, off offset:48\n\t"
+        "global_load_dword %4, %6, off"
+        : "=&v"(b.v0), "=&v"(b.v1), "=&v"(b.v2), "=&v"(b.v3), "=&v"(b.x16)
+        : "v"(p), "v"(p16)
+        : "memory");
+}
+__device__ __forceinline__ void wait_loads(Blk &b) {
+    asm volatile("s_waitcnt vmcnt(0)"
+                 : "+v"(b.v0), "+v"(b.v1), "+v"(b.v2), "+v"(b.v3), "+v"(b.x16)
+                 :
+                 : "memory");
+}
+__device__ __forceinline__ void unpack(const Blk &b, uint32_t (&x)[17]) {
+    x[0] = b.v0.x; x[1] = b.v0.y; x[2] = b.v0.z; x[3] = b.v0.w;
+    x[4] = b.v1.x; x[5] = b.v1.y; x[6] = b.v1.z; x[7] = b.v1.w;
+    x[8] = b.v2.x; x[9] = b.v2.y; x[10] = b.v2.z; x[11] = b.v2.w;
+    x[12] = b.v3.x; x[13] = b.v3.y; x[14] = b.v3.z; x[15] = b.v3.w;
+    x[16] = b.x16;
+}
+
 __device__ __forceinline__ uint32_t bswap(uint32_t x) {
     return __builtin_bswap32(x);  // one v_perm_b32
 }
@@ -60,14 +103,14 @@ struct Sha {
                 wt = w[t];
             } else {
                 const uint32_t w15 = w[(t - 15) & 15], w2 = w[(t - 2) & 15];
-                const uint32_t s0 = rotr(w15, 7) ^ rotr(w15, 18) ^ (w15 >> 3);
-                const uint32_t s1 = rotr(w2, 17) ^ rotr(w2, 19) ^ (w2 >> 10);
+                const uint32_t s0 = xor3(rotr(w15, 7), rotr(w15, 18), w15 >> 3);
+                const uint32_t s1 = xor3(rotr(w2, 17), rotr(w2, 19), w2 >> 10);
                 wt = w[t & 15] = w[t & 15] + s0 + w[(t - 7) & 15] + s1;
             }
-            const uint32_t S1 = rotr(e, 6) ^ rotr(e, 11) ^ rotr(e, 25);
+            const uint32_t S1 = xor3(rotr(e, 6), rotr(e, 11), rotr(e, 25));
             const uint32_t ch = (e & f) ^ (~e & g);
             const uint32_t t1 = h + S1 + ch + kK[t] + wt;
-            const uint32_t S0 = rotr(a, 2) ^ rotr(a, 13) ^ rotr(a, 22);
+            const uint32_t S0 = xor3(rotr(a, 2), rotr(a, 13), rotr(a, 22));
             const uint32_t maj = (a & b) | (c & (a | b));
             const uint32_t t2 = S0 + maj;
             h = g; g = f; f = e; e = d + t1;
@@ -87,20 +130,30 @@ __device__ __forceinline__ void sha256_range(const uint8_t *__restrict__ arena, 
     const uint32_t k = (uint32_t)(p & 3);  // byte misalignment
     const uint32_t *q = (const uint32_t *)(arena + (p - k));
     const uint64_t nfull = len >> 6;
-    // carried dword: q[16] of block i is q[0] of block i + 1
-    uint32_t carry = nfull ? q[0] : 0;
+    // Block i is dwords q[16i .. 16i + 16] (17: the misaligned last word).
+    // The next block's dwords are loaded before this block is compressed,
+    // so HBM latency hides behind ~1.4k VALU ops of the current block.
+    // q[16] is read from q[15] when k == 0 (unused then, and q[16] may lie
+    // past the chunk's last dword); past the last full block the prefetch
+    // re-reads the current block.
+    const uint32_t o16 = k ? 16u : 15u;
+    Blk cur, nxt;
+    if (nfull) {
+        issue_loads(q, o16, cur);
+        wait_loads(cur);
+    }
     for (uint64_t blk = 0; blk < nfull; blk++) {
+        const uint32_t *qn = (blk + 1 < nfull) ? q + 16 : q;
+        issue_loads(qn, o16, nxt);
+        __builtin_amdgcn_sched_barrier(0);  // keep the prefetch at the top
         uint32_t d[17];
-        d[0] = carry;
-#pragma unroll
-        for (int i = 1; i < 16; i++) d[i] = q[i];
-        // q[16] holds a byte of the chunk unless the chunk ends exactly here
-        d[16] = (64 < k + (len - (blk << 6))) ? q[16] : 0;
-        carry = d[16];
+        unpack(cur, d);
         uint32_t w[16];
 #pragma unroll
         for (int i = 0; i < 16; i++) w[i] = bswap(__builtin_amdgcn_alignbyte(d[i + 1], d[i], k));
         sh.compress(w);
+        wait_loads(nxt);
+        cur = nxt;
         q += 16;
     }
     // tail: r < 64 data bytes, 0x80, zeros, 64-bit big-endian bit length
