@@ -72,6 +72,9 @@ def parse():
                     help="also measure the fused blob ids (rcdc_plan_hash, SURVEY 8(f) row 1), "
                          "reported as a separate object; the headline value is unchanged")
     ap.add_argument("--sha-steps", type=int, default=5)
+    ap.add_argument("--pipeline", action="store_true",
+                    help="overlap run k's resolve with run k+1's scan (rcdc_plan_set_pipeline; "
+                         "measured slower on C2: the resolve waves starve behind the scan)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-parity", action="store_true")
     ap.add_argument("--e2e", action="store_true",
@@ -277,6 +280,14 @@ def run_c4(args, torch, dist, dev, rank, world, local):
             el += time.perf_counter() - t0
             plan.set_timing(False)
             r, sm, rm = plan.kernel_times()
+            if os.environ.get("RCDC_C4_VERBOSE") and rank == 0:
+                inf = plan.info()
+                print(f"c4 batch files={len(b)} gib={sum(sizes[f] for f in b) / GiB:.1f} "
+                      f"min_mib={min(sizes[f] for f in b) / 2**20:.1f} "
+                      f"wall_ms={(time.perf_counter() - t0) * 1e3:.2f} scan_ms={sm:.2f} "
+                      f"chain_ms={rm:.2f} walk_pieces={inf['walk_pieces']} "
+                      f"seg={inf['segment_bytes']} scanned_gib={inf['scanned_bytes'] / GiB:.1f}",
+                      file=sys.stderr, flush=True)
             runs += r
             scan_ms += sm
             resolve_ms += rm
@@ -364,6 +375,10 @@ def main():
     ctx = Context.get(POLY, MIN, AVG, MAX, device=local)
     plan = DevicePlan(ctx, offs, lens, int(arena.numel()))
     info = plan.info()
+    pipelined = False
+    if args.pipeline and args.workload != "C5" and info.get("walk_pieces", 0) == 0:
+        plan.set_pipeline(True)  # rcdc_plan_set_pipeline: resolve k overlaps scan k+1
+        pipelined = True
     stream = torch.cuda.current_stream(dev)
     sptr = stream.cuda_stream
     ptr = arena.data_ptr()
@@ -468,6 +483,7 @@ def main():
         "segment_bytes": info["segment_bytes"],
         "bytes_read_by_lanes": info["scanned_bytes"] + 64 * info["segments"],
         "limiter": "VALU issue (DESIGN.md 3: ~95% of the measured compute ceiling)",
+        "pipelined": pipelined,
     }
     if pmc:
         roofline["traffic_source"] = pmc.get("source")

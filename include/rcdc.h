@@ -135,6 +135,15 @@ rcdc_status rcdc_plan_device_results(rcdc_plan *plan, uint64_t *d_cuts,
                                      uint64_t *d_counts,
                                      const uint64_t **cut_base);
 
+/* Pipelined runs: with enable = 1, run k's resolve goes to a stream of the
+ * plan's own (after run k's scan) and run k + 1's scan, on the caller's
+ * stream, overlaps it; the per-segment summaries alternate between two
+ * buffer sets.  rcdc_plan_results / rcdc_plan_hash wait for the resolve;
+ * a caller that reuses the arena must synchronise the device (or call
+ * rcdc_plan_results) first.  RCDC_ERR_UNSUPPORTED for plans with walked
+ * (long) streams.  enable = 0 restores serial runs.                       */
+rcdc_status rcdc_plan_set_pipeline(rcdc_plan *plan, int enable);
+
 /* Scan-kernel geometry chosen by the plan (for profiling / roofline). */
 typedef struct {
     uint64_t scanned_bytes;   /* bytes the scan kernel must hash         */

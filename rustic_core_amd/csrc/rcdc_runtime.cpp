@@ -160,6 +160,17 @@ struct rcdc_plan {
     hipStream_t last_stream = nullptr;
     hipEvent_t done = nullptr;
     bool ran = false;
+    // pipelined runs (rcdc_plan_set_pipeline): scan k + 1 overlaps resolve k;
+    // summaries ping-pong between two buffer sets, resolve on its own stream
+    bool pipelined = false;
+    uint32_t pp = 0;                  // buffer set of the next run
+    uint4 *d_sums2 = nullptr;
+    uint64_t *d_masks2 = nullptr;
+    uint64_t cap_sums2 = 0, cap_masks2 = 0;
+    hipStream_t rstream = nullptr;
+    hipEvent_t ev_scan[2] = {nullptr, nullptr};
+    hipEvent_t ev_res[2] = {nullptr, nullptr};
+    bool res_pending[2] = {false, false};
     // SHA-256 of every chunk (rcdc_plan_hash), slot-indexed like d_cuts
     uint32_t *d_dig = nullptr;
     uint64_t cap_dig = 0;
@@ -526,8 +537,13 @@ rcdc_status plan_run(rcdc_plan *pl, const void *d_arena, hipStream_t stream) {
         pl->truns++;
         HIP_TRY(hipEventRecord(ev[0], stream));
     }
+    const uint32_t set = pl->pipelined ? pl->pp : 0;
+    uint4 *sums = set ? pl->d_sums2 : pl->d_sums;
+    uint64_t *masks = set ? pl->d_masks2 : pl->d_masks;
+    if (pl->pipelined && pl->res_pending[set])  // resolve k - 2 read this set
+        HIP_TRY(hipStreamWaitEvent(stream, pl->ev_res[set], 0));
     HIP_TRY(launch_scan(ctx->variant, (const uint8_t *)d_arena, pl->d_items, (uint32_t)pl->items.size(),
-                        ctx->d_tables, sp, pl->d_sums, pl->d_masks, pl->blocks, stream));
+                        ctx->d_tables, sp, sums, masks, pl->blocks, stream));
     const uint32_t cus = (uint32_t)std::max(ctx->num_cus, 1);
     static const bool dbg = getenv("RCDC_DEBUG_SYNC") != nullptr;  // stage-by-stage sync
     if (dbg) {
@@ -542,6 +558,12 @@ rcdc_status plan_run(rcdc_plan *pl, const void *d_arena, hipStream_t stream) {
         fprintf(stderr, "rcdc: walk done (%zu units)\n", pl->wunits.size());
     }
     if (ev) HIP_TRY(hipEventRecord(ev[1], stream));
+    const hipStream_t scan_stream = stream;
+    if (pl->pipelined) {  // resolve on the plan's own stream, after this scan
+        HIP_TRY(hipEventRecord(pl->ev_scan[set], stream));
+        stream = pl->rstream;
+        HIP_TRY(hipStreamWaitEvent(stream, pl->ev_scan[set], 0));
+    }
     ResolveParams rp{};
     rp.min_size = ctx->min;
     rp.max_size = ctx->max;
@@ -550,8 +572,8 @@ rcdc_status plan_run(rcdc_plan *pl, const void *d_arena, hipStream_t stream) {
     rp.shift = (uint32_t)(ctx->deg - 8);
     HIP_TRY(launch_resolve((const uint8_t *)d_arena, pl->d_sds, pl->d_units,
                            (uint32_t)pl->units.size(), pl->d_stitches,
-                           (uint32_t)pl->stitches.size(), ctx->d_tables, rp, pl->d_sums,
-                           pl->d_masks, pl->d_cuts, pl->d_counts, pl->d_piece_cuts,
+                           (uint32_t)pl->stitches.size(), ctx->d_tables, rp, sums,
+                           masks, pl->d_cuts, pl->d_counts, pl->d_piece_cuts,
                            pl->d_piece_counts, nullptr, stream));
     if (dbg) {
         HIP_TRY(hipStreamSynchronize(stream));
@@ -562,6 +584,12 @@ rcdc_status plan_run(rcdc_plan *pl, const void *d_arena, hipStream_t stream) {
                               pl->d_wpiece, pl->d_pstatus, pl->d_bres, pl->d_ctr, pl->d_fixlist,
                               pl->d_fixcuts, pl->d_fixres, pl->d_cuts, pl->d_counts, cus, stream));
     if (ev) HIP_TRY(hipEventRecord(ev[2], stream));
+    if (pl->pipelined) {
+        HIP_TRY(hipEventRecord(pl->ev_res[set], stream));
+        pl->res_pending[set] = true;
+        pl->pp ^= 1u;
+    }
+    (void)scan_stream;
     pl->last_arena = d_arena;
     pl->last_stream = stream;
     HIP_TRY(hipEventRecord(pl->done, stream));
@@ -675,6 +703,13 @@ void plan_release(rcdc_plan *pl) {
     (void)hipFree(pl->d_sds);
     (void)hipFree(pl->d_sums);
     (void)hipFree(pl->d_masks);
+    (void)hipFree(pl->d_sums2);
+    (void)hipFree(pl->d_masks2);
+    for (int k = 0; k < 2; k++) {
+        if (pl->ev_scan[k]) (void)hipEventDestroy(pl->ev_scan[k]);
+        if (pl->ev_res[k]) (void)hipEventDestroy(pl->ev_res[k]);
+    }
+    if (pl->rstream) (void)hipStreamDestroy(pl->rstream);
     (void)hipFree(pl->d_cuts);
     (void)hipFree(pl->d_counts);
     (void)hipFree(pl->d_dig);
@@ -890,6 +925,30 @@ rcdc_status rcdc_plan_device_results(rcdc_plan *plan, uint64_t *d_cuts, uint64_t
     *d_cuts = (uint64_t)(uintptr_t)plan->d_cuts;
     *d_counts = (uint64_t)(uintptr_t)plan->d_counts;
     *cut_base = plan->cut_base.data();
+    return RCDC_OK;
+}
+
+rcdc_status rcdc_plan_set_pipeline(rcdc_plan *plan, int enable) {
+    if (!plan) return fail(RCDC_ERR_INVALID_INPUT, "null argument");
+    if (!enable) {
+        plan->pipelined = false;
+        return RCDC_OK;
+    }
+    if (!plan->wunits.empty())
+        return fail(RCDC_ERR_UNSUPPORTED, "pipelined runs need a plan without walked streams");
+    DeviceGuard g(plan->ctx->device);
+    rcdc_status st;
+    if ((st = ensure_dev(&plan->d_sums2, &plan->cap_sums2, plan->cap_sums))) return st;
+    if ((st = ensure_dev(&plan->d_masks2, &plan->cap_masks2, plan->cap_masks))) return st;
+    if (!plan->rstream)
+        HIP_TRY(hipStreamCreateWithFlags(&plan->rstream, hipStreamNonBlocking));
+    for (int k = 0; k < 2; k++) {
+        if (!plan->ev_scan[k])
+            HIP_TRY(hipEventCreateWithFlags(&plan->ev_scan[k], hipEventDisableTiming));
+        if (!plan->ev_res[k])
+            HIP_TRY(hipEventCreateWithFlags(&plan->ev_res[k], hipEventDisableTiming));
+    }
+    plan->pipelined = true;
     return RCDC_OK;
 }
 

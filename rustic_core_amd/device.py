@@ -107,6 +107,12 @@ class DevicePlan:
             o += k
         return out
 
+    def set_pipeline(self, enable: bool) -> None:
+        """Overlap run k's resolve with run k + 1's scan (rcdc_plan_set_pipeline)."""
+        st = _lib.lib().rcdc_plan_set_pipeline(self._h, 1 if enable else 0)
+        if st:
+            raise status_error(st, _lib.last_error())
+
     def set_timing(self, enable: bool, every: int = 1) -> None:
         """HIP events around the kernels of every ``every``-th run (see
         ``rcdc_plan_set_timing``); ``enable=False`` stops recording."""

@@ -275,3 +275,44 @@ def test_long_stream_default_params(gpu_ctx, kind, monkeypatch):
     assert np.array_equal(_device_cuts(gpu_ctx, [data])[0], want)
     monkeypatch.setenv("RCDC_PIECE_BYTES", str(8 * MiB))
     assert np.array_equal(_device_cuts(gpu_ctx, [data])[0], want)
+
+
+def test_pipelined_runs(gpu_ctx):
+    """rcdc_plan_set_pipeline: resolve k on the plan's stream overlaps scan
+    k + 1 (ping-pong summaries); alternating arenas must give each run's own
+    cuts, and the fused hash must follow the last run."""
+    import hashlib
+    torch = _torch()
+    from rustic_core_amd.device import DevicePlan, pack_offsets
+    lens = [MiB] * 96 + [3 * MiB + 17, 524288 + 65, 100]
+    offs, arena_len = pack_offsets(lens)
+    hosts = []
+    for a in range(2):
+        h = np.zeros(arena_len, dtype=np.uint8)
+        for i, (o, n) in enumerate(zip(offs, lens)):
+            h[int(o):int(o) + n] = oracle.stdrng_bytes(7000 + 1000 * a + i, n)
+        hosts.append(h)
+    devs = [torch.from_numpy(h).to("cuda:0") for h in hosts]
+    exp = [[oracle.chunk_cuts(h[int(o):int(o) + n]) for o, n in zip(offs, lens)] for h in hosts]
+    plan = DevicePlan(gpu_ctx, offs, lens, arena_len)
+    plan.set_pipeline(True)
+    for k in range(7):
+        plan.run(devs[k % 2].data_ptr())
+    got = plan.results()  # last run: arena 0
+    assert all(np.array_equal(g, e) for g, e in zip(got, exp[0]))
+    for k in range(3):
+        plan.run(devs[(k + 1) % 2].data_ptr())
+    plan.hash(devs[1].data_ptr())
+    got = plan.results()
+    assert all(np.array_equal(g, e) for g, e in zip(got, exp[1]))
+    digs = plan.digests()
+    h = hosts[1]
+    for i in (0, 96, 97):
+        o, prev = int(offs[i]), 0
+        for j, c in enumerate(got[i]):
+            assert bytes(digs[i][j]) == hashlib.sha256(h[o + prev:o + int(c)].tobytes()).digest()
+            prev = int(c)
+    plan.set_pipeline(False)
+    plan.run(devs[0].data_ptr())
+    assert all(np.array_equal(g, e) for g, e in zip(plan.results(), exp[0]))
+    plan.close()
