@@ -577,12 +577,13 @@ def sha_measure(torch, plan, ptr, sptr, dev, args, arena, offs, lens, cpu: bool)
             checked += 1
             prev = int(c)
     out = {
-        "kernel": "rcdc_sha256_plan_kernel",
+        "kernel": "rcdc_sha256_plan_split_kernel (+ count/order length buckets)",
         "chunks_per_launch": nchunks,
         "hash_ms_per_launch": round(hash_ms, 3),
         "hash_gibs": round(in_bytes / (hash_ms / 1e3) / GiB, 2),
         "fused_chunk_and_hash_gibs": round(in_bytes / fused_s / GiB, 2),
-        "bound": "valu (one lane per chunk; SHA-256 is a sequential chain per chunk)",
+        "bound": "per-chunk chain latency (SHA-256 is sequential within a chunk; one lane "
+                 "pair per chunk: schedule wave + rounds wave)",
         "spot_check": {"chunks": checked, "mismatches": mism, "checker": "hashlib"},
     }
     if cpu:

@@ -49,6 +49,7 @@ hipError_t launch_sha256_list(const uint8_t *arena, const ulonglong2 *refs, uint
                               uint32_t *digests, hipStream_t stream);
 hipError_t launch_sha256_plan(const uint8_t *arena, const StreamDesc *sds, uint32_t nstreams,
                               const uint64_t *cuts, const uint64_t *counts, uint64_t nslots,
+                              uint64_t max_len, uint32_t *bwork, uint32_t *order,
                               uint32_t *digests, hipStream_t stream);
 }  // namespace rcdc
 
@@ -174,6 +175,9 @@ struct rcdc_plan {
     // SHA-256 of every chunk (rcdc_plan_hash), slot-indexed like d_cuts
     uint32_t *d_dig = nullptr;
     uint64_t cap_dig = 0;
+    uint32_t *d_shaw = nullptr;   // length-bucket counters + total
+    uint32_t *d_order = nullptr;  // slots sorted by chunk length, longest first
+    uint64_t cap_shaw = 0, cap_order = 0;
     bool hashed = false;
     // optional per-run kernel timing
     bool timing = false;
@@ -713,6 +717,8 @@ void plan_release(rcdc_plan *pl) {
     (void)hipFree(pl->d_cuts);
     (void)hipFree(pl->d_counts);
     (void)hipFree(pl->d_dig);
+    (void)hipFree(pl->d_shaw);
+    (void)hipFree(pl->d_order);
     (void)hipFree(pl->d_units);
     (void)hipFree(pl->d_stitches);
     (void)hipFree(pl->d_piece_cuts);
@@ -1033,9 +1039,12 @@ rcdc_status rcdc_plan_hash(rcdc_plan *plan, const void *d_arena, void *hip_strea
     if (!st) st = plan->ctx->stream;
     rcdc_status rs;
     if ((rs = ensure_dev(&plan->d_dig, &plan->cap_dig, plan->ncuts * 8))) return rs;
+    if ((rs = ensure_dev(&plan->d_shaw, &plan->cap_shaw, 256))) return rs;
+    if ((rs = ensure_dev(&plan->d_order, &plan->cap_order, plan->ncuts))) return rs;
     if (st != plan->last_stream) HIP_TRY(hipStreamWaitEvent(st, plan->done, 0));
     HIP_TRY(launch_sha256_plan((const uint8_t *)d_arena, plan->d_sds, plan->n, plan->d_cuts,
-                               plan->d_counts, plan->ncuts, plan->d_dig, st));
+                               plan->d_counts, plan->ncuts, plan->ctx->max, plan->d_shaw,
+                               plan->d_order, plan->d_dig, st));
     HIP_TRY(hipEventRecord(plan->done, st));
     plan->hashed = true;
     return RCDC_OK;

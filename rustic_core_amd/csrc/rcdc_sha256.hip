@@ -17,6 +17,7 @@
 // throughput only with >= ~4 waves per SIMD of chunks in flight (C3/C4
 // scale), not on 1409 chunks (C2).
 #include <hip/hip_runtime.h>
+#include <stdlib.h>
 
 #include "rcdc_internal.h"
 
@@ -119,7 +120,52 @@ struct Sha {
         s[0] += a; s[1] += b; s[2] += c; s[3] += d;
         s[4] += e; s[5] += f; s[6] += g; s[7] += h;
     }
+    // rounds only: kw[t / 4][lane] holds K[t] + W[t] (schedule done elsewhere)
+    __device__ __forceinline__ void compress_kw(const uint4 (*kw)[64], uint32_t lane) {
+        uint32_t a = s[0], b = s[1], c = s[2], d = s[3], e = s[4], f = s[5], g = s[6], h = s[7];
+#pragma unroll
+        for (int t4 = 0; t4 < 16; t4++) {
+            const uint4 v = kw[t4][lane];
+            const uint32_t kwv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const uint32_t S1 = xor3(rotr(e, 6), rotr(e, 11), rotr(e, 25));
+                const uint32_t ch = (e & f) ^ (~e & g);
+                const uint32_t t1 = h + S1 + ch + kwv[u];
+                const uint32_t S0 = xor3(rotr(a, 2), rotr(a, 13), rotr(a, 22));
+                const uint32_t maj = (a & b) | (c & (a | b));
+                const uint32_t t2 = S0 + maj;
+                h = g; g = f; f = e; e = d + t1;
+                d = c; c = b; b = a; a = t1 + t2;
+            }
+        }
+        s[0] += a; s[1] += b; s[2] += c; s[3] += d;
+        s[4] += e; s[5] += f; s[6] += g; s[7] += h;
+    }
 };
+
+// K[t] + W[t] for t = 0..63 of one block (w: the 16 big-endian words),
+// written to kw[t / 4][lane].
+__device__ __forceinline__ void schedule_kw(uint32_t w[16], uint4 (*kw)[64], uint32_t lane) {
+    uint32_t o[4];
+#pragma unroll
+    for (int t = 0; t < 64; t++) {
+        uint32_t wt;
+        if (t < 16) {
+            wt = w[t];
+        } else {
+            const uint32_t w15 = w[(t - 15) & 15], w2 = w[(t - 2) & 15];
+            const uint32_t s0 = xor3(rotr(w15, 7), rotr(w15, 18), w15 >> 3);
+            const uint32_t s1 = xor3(rotr(w2, 17), rotr(w2, 19), w2 >> 10);
+            wt = w[t & 15] = w[t & 15] + s0 + w[(t - 7) & 15] + s1;
+        }
+        o[t & 3] = wt + kK[t];
+        if ((t & 3) == 3) kw[t >> 2][lane] = make_uint4(o[0], o[1], o[2], o[3]);
+    }
+}
+
+__device__ __forceinline__ void sha256_tail(Sha &sh, const uint32_t *q, uint32_t k, uint64_t len,
+                                            uint32_t *__restrict__ out);
 
 // SHA-256 of arena[p, p + len) into out[0..8) (digest words, big-endian
 // byte order when stored as bytes: out bytes = digest bytes).
@@ -156,7 +202,13 @@ __device__ __forceinline__ void sha256_range(const uint8_t *__restrict__ arena, 
         cur = nxt;
         q += 16;
     }
-    // tail: r < 64 data bytes, 0x80, zeros, 64-bit big-endian bit length
+    sha256_tail(sh, q, k, len, out);
+}
+
+// The last (len % 64) bytes at q (4-aligned-down, misalignment k) plus the
+// padding: 0x80, zeros, 64-bit big-endian bit length; then the digest.
+__device__ __forceinline__ void sha256_tail(Sha &sh, const uint32_t *q, uint32_t k, uint64_t len,
+                                            uint32_t *__restrict__ out) {
     const uint32_t r = (uint32_t)(len & 63);
     // last valid byte relative to q (aligned base): k + r - 1; dword j holds
     // a valid byte iff 4j <= k + r - 1
@@ -225,22 +277,205 @@ __global__ __launch_bounds__(64) void rcdc_sha256_plan_kernel(
     sha256_range(arena, sd.off + start, end - start, digests + 8ull * g);
 }
 
+// Two waves per 64 chunks.  Lane l of both waves owns the
+// same chunk.  Wave 0 loads block i + 1 (prefetched one ahead), realigns it
+// and expands the message schedule into LDS as K + W; wave 1 runs the 64
+// rounds of block i from LDS.  This takes the schedule (~1/3 of the VALU
+// ops) off the chain that bounds a chunk's latency.  The slots ping-pong
+// with one barrier per block; both waves loop to the wave-wide maximum block
+// count, so the barrier count is uniform.
+struct ChunkLoc {
+    uint64_t p, len;
+    bool valid;
+};
+
+__device__ __forceinline__ uint64_t wave_max_u64(uint64_t x) {
+#pragma unroll
+    for (int m = 1; m < 64; m <<= 1) {
+        const uint64_t y = __shfl_xor(x, m, 64);
+        x = y > x ? y : x;
+    }
+    return x;
+}
+
+__device__ __forceinline__ void sha256_split(const uint8_t *__restrict__ arena, ChunkLoc c,
+                                             uint32_t *__restrict__ out) {
+    __shared__ uint4 kw[2][16][64];  // [slot][t / 4][lane]: 32 KiB
+    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const uint32_t k = (uint32_t)(c.p & 3);
+    const uint32_t *q0 = (const uint32_t *)(arena + (c.p - k));
+    const uint64_t nfull = c.valid ? c.len >> 6 : 0;
+    const uint64_t nmax = wave_max_u64(nfull);
+    if (nmax == 0 && !c.valid) return;  // whole wave idle (both waves agree)
+    const uint32_t o16 = k ? 16u : 15u;
+    Sha sh;
+    sh.init();
+    Blk cur, nxt;
+    if (wv == 0 && nfull) {
+        issue_loads(q0, o16, cur);
+        wait_loads(cur);
+    }
+    for (uint64_t it = 0; it <= nmax; it++) {
+        if (wv == 0) {
+            if (it < nfull) {
+                const uint32_t *q = q0 + 16 * it;
+                const uint32_t *qn = (it + 1 < nfull) ? q + 16 : q;
+                issue_loads(qn, o16, nxt);
+                __builtin_amdgcn_sched_barrier(0);
+                uint32_t d[17];
+                unpack(cur, d);
+                uint32_t w[16];
+#pragma unroll
+                for (int i = 0; i < 16; i++)
+                    w[i] = bswap(__builtin_amdgcn_alignbyte(d[i + 1], d[i], k));
+                schedule_kw(w, kw[it & 1], lane);
+                wait_loads(nxt);
+                cur = nxt;
+            }
+        } else if (it >= 1 && it - 1 < nfull) {
+            sh.compress_kw(kw[(it - 1) & 1], lane);
+        }
+        __syncthreads();
+    }
+    if (wv == 1 && c.valid) sha256_tail(sh, q0 + 16 * nfull, k, c.len, out);
+}
+
+__global__ __launch_bounds__(128) void rcdc_sha256_list_split_kernel(
+    const uint8_t *__restrict__ arena, const ulonglong2 *__restrict__ refs, uint32_t n,
+    uint32_t *__restrict__ digests) {
+    const uint32_t ci = blockIdx.x * 64 + (threadIdx.x & 63);
+    ChunkLoc c{0, 0, false};
+    if (ci < n) {
+        const ulonglong2 ref = refs[ci];
+        c = {ref.x, ref.y, true};
+    }
+    sha256_split(arena, c, digests + 8ull * ci);
+}
+
+// Locate cut slot g of a plan: chunk [cuts[g-1], cuts[g]) of the stream
+// whose slot range holds g (binary search over cut_base).
+__device__ __forceinline__ ChunkLoc plan_chunk(const StreamDesc *__restrict__ sds,
+                                               uint32_t nstreams, const uint64_t *__restrict__ cuts,
+                                               const uint64_t *__restrict__ counts, uint64_t g) {
+    uint32_t lo = 0, hi = nstreams;
+    while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (sds[mid].cut_base <= g) lo = mid;
+        else hi = mid;
+    }
+    const uint64_t j = g - sds[lo].cut_base;
+    const uint64_t cnt = counts[lo];
+    if (cnt == ~0ull || j >= cnt) return {0, 0, false};
+    const uint64_t start = j ? cuts[g - 1] : 0;
+    return {sds[lo].off + start, cuts[g] - start, true};
+}
+
+// Length buckets, longest first: a wave's time is its longest chunk, so
+// chunks of similar length share a wave and the longest start first.
+constexpr uint32_t kShaBuckets = 64;
+__device__ __forceinline__ uint32_t len_bucket(uint64_t len, uint64_t max_len) {
+    const uint64_t l = len < max_len ? len : max_len;
+    const uint64_t b = (max_len - l) * kShaBuckets / (max_len + 1);
+    return (uint32_t)b;
+}
+
+__global__ __launch_bounds__(256) void rcdc_sha256_count_kernel(
+    const StreamDesc *__restrict__ sds, uint32_t nstreams, const uint64_t *__restrict__ cuts,
+    const uint64_t *__restrict__ counts, uint64_t nslots, uint64_t max_len,
+    uint32_t *__restrict__ bcount) {
+    const uint64_t g = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (g >= nslots) return;
+    const ChunkLoc c = plan_chunk(sds, nstreams, cuts, counts, g);
+    if (c.valid) atomicAdd(&bcount[len_bucket(c.len, max_len)], 1u);
+}
+
+// bcount[0..64) counts, bcount[64..128) cursors (zeroed), bcount[128] total
+__global__ __launch_bounds__(256) void rcdc_sha256_order_kernel(
+    const StreamDesc *__restrict__ sds, uint32_t nstreams, const uint64_t *__restrict__ cuts,
+    const uint64_t *__restrict__ counts, uint64_t nslots, uint64_t max_len,
+    uint32_t *__restrict__ bcount, uint32_t *__restrict__ order) {
+    __shared__ uint32_t boff[kShaBuckets];
+    if (threadIdx.x == 0) {
+        uint32_t acc = 0;
+        for (uint32_t b = 0; b < kShaBuckets; b++) {
+            boff[b] = acc;
+            acc += bcount[b];
+        }
+        if (blockIdx.x == 0) bcount[2 * kShaBuckets] = acc;
+    }
+    __syncthreads();
+    const uint64_t g = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (g >= nslots) return;
+    const ChunkLoc c = plan_chunk(sds, nstreams, cuts, counts, g);
+    if (!c.valid) return;
+    const uint32_t b = len_bucket(c.len, max_len);
+    order[boff[b] + atomicAdd(&bcount[kShaBuckets + b], 1u)] = (uint32_t)g;
+}
+
+__global__ __launch_bounds__(128) void rcdc_sha256_plan_split_kernel(
+    const uint8_t *__restrict__ arena, const StreamDesc *__restrict__ sds, uint32_t nstreams,
+    const uint64_t *__restrict__ cuts, const uint64_t *__restrict__ counts, uint64_t nslots,
+    const uint32_t *__restrict__ order, const uint32_t *__restrict__ total,
+    uint32_t *__restrict__ digests) {
+    const uint64_t i = (uint64_t)blockIdx.x * 64 + (threadIdx.x & 63);
+    ChunkLoc c{0, 0, false};
+    uint64_t g = i;
+    if (order) {
+        if (i < *total) {
+            g = order[i];
+            c = plan_chunk(sds, nstreams, cuts, counts, g);
+        }
+    } else if (i < nslots) {
+        c = plan_chunk(sds, nstreams, cuts, counts, g);
+    }
+    sha256_split(arena, c, digests + 8ull * g);
+}
+
 }  // namespace
+
+// RCDC_SHA_LANE=1 selects the one-wave kernels (one lane does schedule and
+// rounds) for A/B measurements.
+static bool lane_variant() {
+    static const bool v = getenv("RCDC_SHA_LANE") != nullptr;
+    return v;
+}
 
 hipError_t launch_sha256_list(const uint8_t *arena, const ulonglong2 *refs, uint32_t n,
                               uint32_t *digests, hipStream_t stream) {
     if (n == 0) return hipSuccess;
-    hipLaunchKernelGGL(rcdc_sha256_list_kernel, dim3((n + 63) / 64), dim3(64), 0, stream, arena,
-                       refs, n, digests);
+    if (lane_variant())
+        hipLaunchKernelGGL(rcdc_sha256_list_kernel, dim3((n + 63) / 64), dim3(64), 0, stream,
+                           arena, refs, n, digests);
+    else
+        hipLaunchKernelGGL(rcdc_sha256_list_split_kernel, dim3((n + 63) / 64), dim3(128), 0,
+                           stream, arena, refs, n, digests);
     return hipGetLastError();
 }
 
 hipError_t launch_sha256_plan(const uint8_t *arena, const StreamDesc *sds, uint32_t nstreams,
                               const uint64_t *cuts, const uint64_t *counts, uint64_t nslots,
+                              uint64_t max_len, uint32_t *bwork, uint32_t *order,
                               uint32_t *digests, hipStream_t stream) {
     if (nslots == 0 || nstreams == 0) return hipSuccess;
-    hipLaunchKernelGGL(rcdc_sha256_plan_kernel, dim3((uint32_t)((nslots + 63) / 64)), dim3(64), 0,
-                       stream, arena, sds, nstreams, cuts, counts, nslots, digests);
+    const dim3 grid((uint32_t)((nslots + 63) / 64));
+    if (lane_variant()) {
+        hipLaunchKernelGGL(rcdc_sha256_plan_kernel, grid, dim3(64), 0, stream, arena, sds,
+                           nstreams, cuts, counts, nslots, digests);
+        return hipGetLastError();
+    }
+    const bool sorted = order && bwork && nslots < (1ull << 32);
+    if (sorted) {
+        const dim3 g256((uint32_t)((nslots + 255) / 256));
+        hipError_t e = hipMemsetAsync(bwork, 0, (2 * kShaBuckets + 1) * sizeof(uint32_t), stream);
+        if (e != hipSuccess) return e;
+        hipLaunchKernelGGL(rcdc_sha256_count_kernel, g256, dim3(256), 0, stream, sds, nstreams,
+                           cuts, counts, nslots, max_len, bwork);
+        hipLaunchKernelGGL(rcdc_sha256_order_kernel, g256, dim3(256), 0, stream, sds, nstreams,
+                           cuts, counts, nslots, max_len, bwork, order);
+    }
+    hipLaunchKernelGGL(rcdc_sha256_plan_split_kernel, grid, dim3(128), 0, stream, arena, sds,
+                       nstreams, cuts, counts, nslots, sorted ? order : nullptr,
+                       sorted ? bwork + 2 * kShaBuckets : nullptr, digests);
     return hipGetLastError();
 }
 
