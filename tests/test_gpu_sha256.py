@@ -134,3 +134,43 @@ def test_plan_hash_batch(gpu_ctx, kind):
         exp = [hashlib.sha256(arena[s + int(a):s + int(b)].tobytes()).digest()
                for a, b in zip(starts, exp_cuts)]
         assert [bytes(d) for d in digs[i]] == exp, i
+
+
+@pytest.mark.parametrize("kind", ["random", "mixed"])
+def test_plan_hash_walk_path(gpu_ctx, kind, monkeypatch):
+    """Long streams take the walk path: the fused digests of
+    every chunk of 4 x 40 MiB streams (plus short ones on the scan path in
+    the same plan) == hashlib over the oracle's chunks; the plan is walked."""
+    import torch
+    from rustic_core_amd.device import DevicePlan, pack_offsets
+    monkeypatch.setenv("RCDC_WALK_MIN_PIECES", "4")  # small batch: walk anyway
+    lens = [40 * MiB + 13 * i for i in range(4)] + [MiB, 700000]
+    rng = np.random.default_rng(5)
+    bufs = []
+    for i, n in enumerate(lens):
+        b = oracle.stdrng_bytes(900 + i, n)
+        if kind == "mixed":
+            b = b.copy()
+            for _ in range(8):
+                z0 = int(rng.integers(0, n))
+                b[z0:z0 + int(rng.integers(4096, 3 * MiB))] = 0
+        bufs.append(b)
+    offs, arena_len = pack_offsets(lens)
+    arena = np.zeros(arena_len, dtype=np.uint8)
+    for o, b in zip(offs, bufs):
+        arena[int(o):int(o) + len(b)] = b
+    dev = torch.from_numpy(arena).to("cuda:0")
+    plan = DevicePlan(gpu_ctx, offs, lens, arena_len)
+    assert plan.info()["walk_pieces"] > 0
+    plan.run(dev.data_ptr())
+    plan.hash(dev.data_ptr())
+    digs = plan.digests()
+    cuts = plan.results()
+    plan.close()
+    for i, b in enumerate(bufs):
+        exp_cuts = oracle.chunk_cuts(b)
+        assert np.array_equal(cuts[i], exp_cuts), i
+        starts = np.concatenate([[0], exp_cuts[:-1]])
+        exp = [hashlib.sha256(b[int(a):int(e)].tobytes()).digest()
+               for a, e in zip(starts, exp_cuts)]
+        assert [bytes(d) for d in digs[i]] == exp, i
