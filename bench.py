@@ -72,6 +72,8 @@ def parse():
                     help="also measure the fused blob ids (rcdc_plan_hash, SURVEY 8(f) row 1), "
                          "reported as a separate object; the headline value is unchanged")
     ap.add_argument("--sha-steps", type=int, default=5)
+    ap.add_argument("--sha-depth", type=int, default=4,
+                    help="batches whose blob ids are in flight at once (pipelined ingest)")
     ap.add_argument("--pipeline", action="store_true",
                     help="overlap run k's resolve with run k+1's scan (rcdc_plan_set_pipeline; "
                          "measured slower on C2: the resolve waves starve behind the scan)")
@@ -533,6 +535,8 @@ def main():
 
 
 def sha_measure(torch, plan, ptr, sptr, dev, args, arena, offs, lens, cpu: bool) -> dict:
+    from rustic_core_amd.device import DevicePlan
+
     """Blob ids (SHA-256 per chunk, crypto/hasher.rs:17-19) on the device:
     hash-only kernel time over the plan's cut list (HIP events on the launch
     stream), the fused chunk + hash step rate, a hashlib spot check and a
@@ -586,6 +590,44 @@ def sha_measure(torch, plan, ptr, sptr, dev, args, arena, offs, lens, cpu: bool)
                  "pair per chunk: schedule wave + rounds wave)",
         "spot_check": {"chunks": checked, "mismatches": mism, "checker": "hashlib"},
     }
+    # ingest pipeline: D plans over the same (read-only) arena rotate; batch
+    # k's blob ids hash on a side stream while batches k + 1 .. k + D - 1 are
+    # chunked and hashed, so D hash launches share the longest-chunk
+    # latency floor
+    depth = max(args.sha_depth, 1)
+    plans = [plan] + [DevicePlan(plan.ctx, offs, lens, int(arena.numel()))
+                      for _ in range(depth - 1)]
+    sides = [torch.cuda.Stream(dev) for _ in range(depth)]
+    main = torch.cuda.Stream(dev)
+    done = [None] * depth
+    kp = max(2 * k, 2 * depth)
+
+    def ingest_step(j):
+        pl, sd = plans[j % depth], sides[j % depth]
+        if done[j % depth] is not None:
+            main.wait_event(done[j % depth])  # the plan's last hash has finished
+        pl.run(ptr, main.cuda_stream)
+        pl.hash(ptr, sd.cuda_stream)  # waits for the run (rcdc_plan_hash)
+        ev = torch.cuda.Event()
+        ev.record(sd)
+        done[j % depth] = ev
+
+    for j in range(depth):
+        ingest_step(j)
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for j in range(kp):
+        ingest_step(j)
+    torch.cuda.synchronize(dev)
+    out["pipelined_ingest_gibs"] = round(in_bytes * kp / (time.perf_counter() - t0) / GiB, 2)
+    out["pipelined_ingest_note"] = (f"{depth} plans rotate; batch k's SHA-256 overlaps the next "
+                                    f"{depth - 1} batches' chunk + SHA-256 ({kp} batches timed)")
+    last = plans[(kp - 1) % depth]
+    out["pipelined_ingest_consistent"] = bool(
+        all(np.array_equal(a, b) for a, b in zip(last.results(), cuts))
+        and all(np.array_equal(a, b) for a, b in zip(last.digests(), digs)))
+    for pl in plans[1:]:
+        pl.close()
     if cpu:
         sample = arena[int(offs[0]):int(offs[0]) + min(int(lens[0]), 256 << 20)].cpu().numpy()
         sample = sample.tobytes()
