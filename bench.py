@@ -590,39 +590,48 @@ def sha_measure(torch, plan, ptr, sptr, dev, args, arena, offs, lens, cpu: bool)
                  "pair per chunk: schedule wave + rounds wave)",
         "spot_check": {"chunks": checked, "mismatches": mism, "checker": "hashlib"},
     }
-    # ingest pipeline: D plans over the same (read-only) arena rotate; batch
-    # k's blob ids hash on a side stream while batches k + 1 .. k + D - 1 are
-    # chunked and hashed, so D hash launches share the longest-chunk
+    # ingest pipeline: 2 groups of D plans over the same (read-only) arena.
+    # A group's D batches are chunked on the main stream and their blob ids
+    # hashed in ONE launch (rcdc_plan_hash_many) on a side stream, while the
+    # other group's batches are chunked: D batches share the longest-chunk
     # latency floor
-    depth = max(args.sha_depth, 1)
+    from rustic_core_amd.device import hash_many
+    depth = min(max(args.sha_depth, 1), 8)
     plans = [plan] + [DevicePlan(plan.ctx, offs, lens, int(arena.numel()))
-                      for _ in range(depth - 1)]
-    sides = [torch.cuda.Stream(dev) for _ in range(depth)]
+                      for _ in range(2 * depth - 1)]
+    groups = [plans[:depth], plans[depth:]]
+    sides = [torch.cuda.Stream(dev), torch.cuda.Stream(dev)]
     main = torch.cuda.Stream(dev)
-    done = [None] * depth
-    kp = max(2 * k, 2 * depth)
+    done = [None, None]
+    ngroups = max(2, -(-2 * k // depth))
 
-    def ingest_step(j):
-        pl, sd = plans[j % depth], sides[j % depth]
-        if done[j % depth] is not None:
-            main.wait_event(done[j % depth])  # the plan's last hash has finished
-        pl.run(ptr, main.cuda_stream)
-        pl.hash(ptr, sd.cuda_stream)  # waits for the run (rcdc_plan_hash)
+    def ingest_group(j):
+        grp, sd = groups[j % 2], sides[j % 2]
+        if done[j % 2] is not None:
+            main.wait_event(done[j % 2])  # this group's last hash has finished
+        for pl in grp:
+            pl.run(ptr, main.cuda_stream)
+        ev_run = torch.cuda.Event()
+        ev_run.record(main)
+        sd.wait_event(ev_run)
+        hash_many(grp, [ptr] * len(grp), sd.cuda_stream)
         ev = torch.cuda.Event()
         ev.record(sd)
-        done[j % depth] = ev
+        done[j % 2] = ev
 
-    for j in range(depth):
-        ingest_step(j)
+    for j in range(2):
+        ingest_group(j)
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
-    for j in range(kp):
-        ingest_step(j)
+    for j in range(ngroups):
+        ingest_group(j)
     torch.cuda.synchronize(dev)
-    out["pipelined_ingest_gibs"] = round(in_bytes * kp / (time.perf_counter() - t0) / GiB, 2)
-    out["pipelined_ingest_note"] = (f"{depth} plans rotate; batch k's SHA-256 overlaps the next "
-                                    f"{depth - 1} batches' chunk + SHA-256 ({kp} batches timed)")
-    last = plans[(kp - 1) % depth]
+    nb = ngroups * depth
+    out["pipelined_ingest_gibs"] = round(in_bytes * nb / (time.perf_counter() - t0) / GiB, 2)
+    out["pipelined_ingest_note"] = (f"groups of {depth} batches: chunked on one stream, blob ids "
+                                    f"in one rcdc_plan_hash_many launch overlapping the next "
+                                    f"group ({nb} batches timed)")
+    last = groups[(ngroups - 1) % 2][-1]
     out["pipelined_ingest_consistent"] = bool(
         all(np.array_equal(a, b) for a, b in zip(last.results(), cuts))
         and all(np.array_equal(a, b) for a, b in zip(last.digests(), digs)))

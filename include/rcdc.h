@@ -193,6 +193,12 @@ rcdc_status rcdc_sha256_chunks(rcdc_ctx *ctx, const void *d_arena,
 rcdc_status rcdc_plan_hash(rcdc_plan *plan, const void *d_arena,
                            void *hip_stream);
 
+/* rcdc_plan_hash for up to 8 plans of one context in a single launch (plan
+ * j over d_arenas[j], its last run's arena), so their chunks share the
+ * longest-chunk latency floor instead of queueing per stream.            */
+rcdc_status rcdc_plan_hash_many(rcdc_plan *const *plans, uint32_t n,
+                                const void *const *d_arenas, void *hip_stream);
+
 /* Synchronise and copy the digests to the host: 32 bytes per chunk, in the
  * order of rcdc_plan_results' cuts (whose counts it also writes).          */
 rcdc_status rcdc_plan_digests(rcdc_plan *plan, uint8_t *digests,

@@ -23,7 +23,7 @@ EXPORTS = (
     "rcdc_plan_destroy", "rcdc_plan_run", "rcdc_plan_results", "rcdc_plan_device_results",
     "rcdc_plan_get_info", "rcdc_plan_set_timing", "rcdc_plan_kernel_times", "rcdc_fixed_cuts",
     "rcdc_sha256_chunks", "rcdc_plan_hash", "rcdc_plan_digests", "rcdc_plan_device_digests",
-    "rcdc_plan_set_pipeline",
+    "rcdc_plan_set_pipeline", "rcdc_plan_hash_many",
 )
 ABI_VERSION = 1
 
@@ -132,6 +132,8 @@ def lib() -> ctypes.CDLL:
     L.rcdc_plan_hash.argtypes = [vp, vp, vp]
     L.rcdc_plan_digests.restype = st
     L.rcdc_plan_digests.argtypes = [vp, vp, u64, vp]
+    L.rcdc_plan_hash_many.restype = st
+    L.rcdc_plan_hash_many.argtypes = [vp, u32, vp, vp]
     L.rcdc_plan_set_pipeline.restype = st
     L.rcdc_plan_set_pipeline.argtypes = [vp, ctypes.c_int]
     L.rcdc_plan_device_digests.restype = st

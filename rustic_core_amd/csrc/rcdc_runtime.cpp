@@ -51,6 +51,12 @@ hipError_t launch_sha256_plan(const uint8_t *arena, const StreamDesc *sds, uint3
                               const uint64_t *cuts, const uint64_t *counts, uint64_t nslots,
                               uint64_t max_len, uint32_t *bwork, uint32_t *order,
                               uint32_t *digests, hipStream_t stream);
+hipError_t launch_sha256_multi(uint32_t n, const uint8_t *const *arenas,
+                               const StreamDesc *const *sds, const uint32_t *nstreams,
+                               const uint64_t *const *cuts, const uint64_t *const *counts,
+                               const uint64_t *nslots, uint64_t max_len, uint32_t *const *bwork,
+                               uint32_t *const *order, uint32_t *const *digests,
+                               hipStream_t stream);
 }  // namespace rcdc
 
 using namespace rcdc;
@@ -1047,6 +1053,55 @@ rcdc_status rcdc_plan_hash(rcdc_plan *plan, const void *d_arena, void *hip_strea
                                plan->d_order, plan->d_dig, st));
     HIP_TRY(hipEventRecord(plan->done, st));
     plan->hashed = true;
+    return RCDC_OK;
+}
+
+rcdc_status rcdc_plan_hash_many(rcdc_plan *const *plans, uint32_t n,
+                                const void *const *d_arenas, void *hip_stream) {
+    if (n == 0) return RCDC_OK;
+    if (!plans || !d_arenas) return fail(RCDC_ERR_INVALID_INPUT, "null argument");
+    if (n > 8) return fail(RCDC_ERR_INVALID_INPUT, "at most 8 plans per call, got %u", n);
+    rcdc_ctx *ctx = plans[0] ? plans[0]->ctx : nullptr;
+    for (uint32_t j = 0; j < n; j++) {
+        rcdc_plan *pl = plans[j];
+        if (!pl || (!d_arenas[j] && pl->arena_len)) return fail(RCDC_ERR_INVALID_INPUT, "null argument");
+        if (!pl->ran) return fail(RCDC_ERR_INVALID_INPUT, "plan %u has not been run", j);
+        if (d_arenas[j] != pl->last_arena)
+            return fail(RCDC_ERR_INVALID_INPUT, "arena %u differs from its last rcdc_plan_run", j);
+        if (pl->ctx != ctx) return fail(RCDC_ERR_INVALID_INPUT, "plans of different contexts");
+        for (uint32_t i = 0; i < j; i++)
+            if (plans[i] == pl) return fail(RCDC_ERR_INVALID_INPUT, "plan %u repeated", j);
+    }
+    DeviceGuard g(ctx->device);
+    hipStream_t st = hip_stream ? (hipStream_t)hip_stream : ctx->stream;
+    const uint8_t *ar[8];
+    const StreamDesc *sd[8];
+    uint32_t ns[8];
+    const uint64_t *cu[8], *co[8];
+    uint64_t nsl[8];
+    uint32_t *bw[8], *od[8], *dg[8];
+    for (uint32_t j = 0; j < n; j++) {
+        rcdc_plan *pl = plans[j];
+        rcdc_status rs;
+        if ((rs = ensure_dev(&pl->d_dig, &pl->cap_dig, pl->ncuts * 8))) return rs;
+        if ((rs = ensure_dev(&pl->d_shaw, &pl->cap_shaw, 256))) return rs;
+        if ((rs = ensure_dev(&pl->d_order, &pl->cap_order, pl->ncuts))) return rs;
+        if (st != pl->last_stream) HIP_TRY(hipStreamWaitEvent(st, pl->done, 0));
+        ar[j] = (const uint8_t *)d_arenas[j];
+        sd[j] = pl->d_sds;
+        ns[j] = pl->n;
+        cu[j] = pl->d_cuts;
+        co[j] = pl->d_counts;
+        nsl[j] = pl->ncuts;
+        bw[j] = pl->d_shaw;
+        od[j] = pl->d_order;
+        dg[j] = pl->d_dig;
+    }
+    HIP_TRY(launch_sha256_multi(n, ar, sd, ns, cu, co, nsl, ctx->max, bw, od, dg, st));
+    for (uint32_t j = 0; j < n; j++) {
+        HIP_TRY(hipEventRecord(plans[j]->done, st));
+        plans[j]->hashed = true;
+    }
     return RCDC_OK;
 }
 

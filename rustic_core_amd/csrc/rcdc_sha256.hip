@@ -446,6 +446,37 @@ __global__ __launch_bounds__(128) void rcdc_sha256_plan_split_kernel(
     sha256_split(arena, c, digests + 8ull * g);
 }
 
+// Several plans in one launch (rcdc_plan_hash_many): blockIdx.y picks the
+// plan, so D batches share the longest-chunk floor without depending on
+// how many hardware queues the streams map to.
+constexpr uint32_t kShaMaxPlans = 8;
+struct ShaPlanDesc {
+    const uint8_t *arena;
+    const StreamDesc *sds;
+    const uint64_t *cuts;
+    const uint64_t *counts;
+    const uint32_t *order;
+    const uint32_t *total;
+    uint32_t *digests;
+    uint32_t nstreams;
+    uint32_t pad;
+};
+struct ShaMulti {
+    ShaPlanDesc p[kShaMaxPlans];
+};
+
+__global__ __launch_bounds__(128) void rcdc_sha256_multi_split_kernel(ShaMulti m) {
+    const ShaPlanDesc &d = m.p[blockIdx.y];
+    const uint64_t i = (uint64_t)blockIdx.x * 64 + (threadIdx.x & 63);
+    ChunkLoc c{0, 0, false};
+    uint64_t g = i;
+    if (i < *d.total) {
+        g = d.order[i];
+        c = plan_chunk(d.sds, d.nstreams, d.cuts, d.counts, g);
+    }
+    sha256_split(d.arena, c, d.digests + 8ull * g);
+}
+
 }  // namespace
 
 // RCDC_SHA_LANE=1 selects the one-wave kernels (one lane does schedule and
@@ -491,6 +522,38 @@ hipError_t launch_sha256_plan(const uint8_t *arena, const StreamDesc *sds, uint3
     hipLaunchKernelGGL(rcdc_sha256_plan_split_kernel, grid, dim3(128), 0, stream, arena, sds,
                        nstreams, cuts, counts, nslots, sorted ? order : nullptr,
                        sorted ? bwork + 2 * kShaBuckets : nullptr, digests);
+    return hipGetLastError();
+}
+
+hipError_t launch_sha256_multi(uint32_t n, const uint8_t *const *arenas,
+                               const StreamDesc *const *sds, const uint32_t *nstreams,
+                               const uint64_t *const *cuts, const uint64_t *const *counts,
+                               const uint64_t *nslots, uint64_t max_len, uint32_t *const *bwork,
+                               uint32_t *const *order, uint32_t *const *digests,
+                               hipStream_t stream) {
+    if (n == 0) return hipSuccess;
+    if (n > kShaMaxPlans) return hipErrorInvalidValue;
+    ShaMulti m{};
+    uint64_t maxslots = 0;
+    for (uint32_t j = 0; j < n; j++) {
+        if (nslots[j] >= (1ull << 32)) return hipErrorInvalidValue;
+        const dim3 g256((uint32_t)((nslots[j] + 255) / 256));
+        hipError_t e = hipMemsetAsync(bwork[j], 0, (2 * kShaBuckets + 1) * sizeof(uint32_t), stream);
+        if (e != hipSuccess) return e;
+        if (nslots[j] && nstreams[j]) {
+            hipLaunchKernelGGL(rcdc_sha256_count_kernel, g256, dim3(256), 0, stream, sds[j],
+                               nstreams[j], cuts[j], counts[j], nslots[j], max_len, bwork[j]);
+            hipLaunchKernelGGL(rcdc_sha256_order_kernel, g256, dim3(256), 0, stream, sds[j],
+                               nstreams[j], cuts[j], counts[j], nslots[j], max_len, bwork[j],
+                               order[j]);
+        }
+        m.p[j] = {arenas[j], sds[j], cuts[j], counts[j], order[j], bwork[j] + 2 * kShaBuckets,
+                  digests[j], nstreams[j], 0};
+        maxslots = nslots[j] > maxslots ? nslots[j] : maxslots;
+    }
+    if (maxslots == 0) return hipGetLastError();
+    hipLaunchKernelGGL(rcdc_sha256_multi_split_kernel, dim3((uint32_t)((maxslots + 63) / 64), n),
+                       dim3(128), 0, stream, m);
     return hipGetLastError();
 }
 

@@ -141,6 +141,18 @@ class DevicePlan:
             pass
 
 
+def hash_many(plans, d_arena_ptrs, hip_stream: Optional[int] = None) -> None:
+    """Blob ids of up to 8 plans' last runs in one launch (rcdc_plan_hash_many)."""
+    n = len(plans)
+    hs = (ctypes.c_void_p * max(n, 1))(*[p._h.value for p in plans])
+    ars = (ctypes.c_void_p * max(n, 1))(*[ctypes.c_void_p(a).value for a in d_arena_ptrs])
+    st = _lib.lib().rcdc_plan_hash_many(ctypes.cast(hs, ctypes.c_void_p), n,
+                                        ctypes.cast(ars, ctypes.c_void_p),
+                                        ctypes.c_void_p(hip_stream or 0))
+    if st:
+        raise status_error(st, _lib.last_error())
+
+
 def sha256_device(ctx: Context, arena_tensor, refs, out_tensor=None, stream=None):
     """SHA-256 of chunks ``refs`` (an ``(n, 2)`` int64 CUDA tensor of
     ``(offset, length)`` rows) of a device arena; returns an ``(n, 32)``

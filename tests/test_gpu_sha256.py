@@ -174,3 +174,37 @@ def test_plan_hash_walk_path(gpu_ctx, kind, monkeypatch):
         exp = [hashlib.sha256(b[int(a):int(e)].tobytes()).digest()
                for a, e in zip(starts, exp_cuts)]
         assert [bytes(d) for d in digs[i]] == exp, i
+
+
+def test_plan_hash_many(gpu_ctx):
+    """rcdc_plan_hash_many: 3 plans (different layouts and arenas) hashed in
+    one launch == each plan hashed alone == hashlib on a sample."""
+    import torch
+    from rustic_core_amd.device import DevicePlan, hash_many, pack_offsets
+    plans, devs, hosts, layouts = [], [], [], []
+    for a, lens in enumerate([[MiB] * 40, [3 * MiB + 5, 700001, 0, 2 * MiB], [524289] * 7]):
+        offs, alen = pack_offsets(lens)
+        h = np.zeros(alen, dtype=np.uint8)
+        for i, (o, n) in enumerate(zip(offs, lens)):
+            h[int(o):int(o) + n] = oracle.stdrng_bytes(3000 + 100 * a + i, n)
+        d = torch.from_numpy(h).to("cuda:0")
+        p = DevicePlan(gpu_ctx, offs, lens, alen)
+        p.run(d.data_ptr())
+        plans.append(p)
+        devs.append(d)
+        hosts.append(h)
+        layouts.append((offs, lens))
+    hash_many(plans, [d.data_ptr() for d in devs])
+    many = [p.digests() for p in plans]
+    for p, d in zip(plans, devs):
+        p.hash(d.data_ptr())
+    for p, m, h, (offs, lens) in zip(plans, many, hosts, layouts):
+        single = p.digests()
+        assert all(np.array_equal(x, y) for x, y in zip(m, single))
+        cuts = p.results()
+        for i in range(len(lens)):
+            o, prev = int(offs[i]), 0
+            for j, c in enumerate(cuts[i]):
+                assert bytes(m[i][j]) == hashlib.sha256(h[o + prev:o + int(c)].tobytes()).digest()
+                prev = int(c)
+        p.close()
