@@ -122,3 +122,25 @@ def test_product_does_not_import_oracle():
                 text = open(os.path.join(dirpath, f), errors="replace").read()
                 assert not re.search(r"^\s*(from|import)\s+oracle\b", text, flags=re.M), f
                 assert "cdc_ref" not in text, f
+
+
+def test_blob_id_entry_points_reject_null(rcdc_lib):
+    """rcdc_sha256_chunks / rcdc_plan_hash / rcdc_plan_hash_many /
+    rcdc_plan_digests / rcdc_plan_set_pipeline: invalid handles give
+    RCDC_ERR_INVALID_INPUT (2, ErrorKind::InvalidInput) before any HIP call;
+    more than 8 plans per rcdc_plan_hash_many is rejected the same way."""
+    from rustic_core_amd import _lib
+    L = _lib.lib()
+    assert L.rcdc_sha256_chunks(None, None, None, 1, None, None) == 2
+    assert L.rcdc_plan_hash(None, None, None) == 2
+    assert L.rcdc_plan_digests(None, None, 0, None) == 2
+    assert L.rcdc_plan_set_pipeline(None, 1) == 2
+    dd = ctypes.c_uint64(0)
+    assert L.rcdc_plan_device_digests(None, ctypes.byref(dd)) == 2
+    assert L.rcdc_plan_hash_many(None, 0, None, None) == 0  # nothing to do
+    assert L.rcdc_plan_hash_many(None, 1, None, None) == 2
+    hs = (ctypes.c_void_p * 9)()
+    ars = (ctypes.c_void_p * 9)()
+    assert L.rcdc_plan_hash_many(ctypes.cast(hs, ctypes.c_void_p), 9,
+                                 ctypes.cast(ars, ctypes.c_void_p), None) == 2
+    assert "8 plans" in _lib.last_error()
