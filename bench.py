@@ -601,18 +601,18 @@ def sha_measure(torch, plan, ptr, sptr, dev, args, arena, offs, lens, cpu: bool)
                       for _ in range(2 * depth - 1)]
     groups = [plans[:depth], plans[depth:]]
     sides = [torch.cuda.Stream(dev), torch.cuda.Stream(dev)]
-    main = torch.cuda.Stream(dev)
+    chunk_stream = torch.cuda.Stream(dev)
     done = [None, None]
     ngroups = max(2, -(-2 * k // depth))
 
     def ingest_group(j):
         grp, sd = groups[j % 2], sides[j % 2]
         if done[j % 2] is not None:
-            main.wait_event(done[j % 2])  # this group's last hash has finished
+            chunk_stream.wait_event(done[j % 2])  # this group's last hash has finished
         for pl in grp:
-            pl.run(ptr, main.cuda_stream)
+            pl.run(ptr, chunk_stream.cuda_stream)
         ev_run = torch.cuda.Event()
-        ev_run.record(main)
+        ev_run.record(chunk_stream)
         sd.wait_event(ev_run)
         hash_many(grp, [ptr] * len(grp), sd.cuda_stream)
         ev = torch.cuda.Event()
