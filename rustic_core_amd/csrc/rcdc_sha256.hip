@@ -29,6 +29,12 @@ __device__ __forceinline__ uint32_t rotr(uint32_t x, uint32_t n) {
     return __builtin_amdgcn_alignbit(x, x, n);
 }
 
+// Maj(x, y, z) in one v_bitop3_b32 (0xF0&0xCC | 0xF0&0xAA | 0xCC&0xAA);
+// the compiler's own lowering is v_xor + v_bfi
+__device__ __forceinline__ uint32_t maj3(uint32_t x, uint32_t y, uint32_t z) {
+    return __builtin_amdgcn_bitop3_b32(x, y, z, 0xE8);
+}
+
 // x ^ y ^ z in one v_bitop3_b32 (truth table 0xF0 ^ 0xCC ^ 0xAA)
 __device__ __forceinline__ uint32_t xor3(uint32_t x, uint32_t y, uint32_t z) {
     return __builtin_amdgcn_bitop3_b32(x, y, z, 0x96);
@@ -112,7 +118,7 @@ struct Sha {
             const uint32_t ch = (e & f) ^ (~e & g);
             const uint32_t t1 = h + S1 + ch + kK[t] + wt;
             const uint32_t S0 = xor3(rotr(a, 2), rotr(a, 13), rotr(a, 22));
-            const uint32_t maj = (a & b) | (c & (a | b));
+            const uint32_t maj = maj3(a, b, c);
             const uint32_t t2 = S0 + maj;
             h = g; g = f; f = e; e = d + t1;
             d = c; c = b; b = a; a = t1 + t2;
@@ -133,7 +139,7 @@ struct Sha {
                 const uint32_t ch = (e & f) ^ (~e & g);
                 const uint32_t t1 = h + S1 + ch + kwv[u];
                 const uint32_t S0 = xor3(rotr(a, 2), rotr(a, 13), rotr(a, 22));
-                const uint32_t maj = (a & b) | (c & (a | b));
+                const uint32_t maj = maj3(a, b, c);
                 const uint32_t t2 = S0 + maj;
                 h = g; g = f; f = e; e = d + t1;
                 d = c; c = b; b = a; a = t1 + t2;
