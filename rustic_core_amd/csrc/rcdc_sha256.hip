@@ -452,8 +452,8 @@ __global__ __launch_bounds__(128) void rcdc_sha256_plan_split_kernel(
     sha256_split(arena, c, digests + 8ull * g);
 }
 
-// Several plans in one launch (rcdc_plan_hash_many): blockIdx.y picks the
-// plan, so D batches share the longest-chunk floor without depending on
+// Several plans in one launch (rcdc_plan_hash_many): blockIdx.x % n picks
+// the plan, so D batches share the longest-chunk floor without depending on
 // how many hardware queues the streams map to.
 constexpr uint32_t kShaMaxPlans = 8;
 struct ShaPlanDesc {
@@ -471,9 +471,11 @@ struct ShaMulti {
     ShaPlanDesc p[kShaMaxPlans];
 };
 
-__global__ __launch_bounds__(128) void rcdc_sha256_multi_split_kernel(ShaMulti m) {
-    const ShaPlanDesc &d = m.p[blockIdx.y];
-    const uint64_t i = (uint64_t)blockIdx.x * 64 + (threadIdx.x & 63);
+__global__ __launch_bounds__(128) void rcdc_sha256_multi_split_kernel(ShaMulti m, uint32_t n) {
+    // plan-minor block order: every plan's longest chunks dispatch first
+    const uint32_t pj = blockIdx.x % n, xb = blockIdx.x / n;
+    const ShaPlanDesc &d = m.p[pj];
+    const uint64_t i = (uint64_t)xb * 64 + (threadIdx.x & 63);
     ChunkLoc c{0, 0, false};
     uint64_t g = i;
     if (i < *d.total) {
@@ -558,8 +560,10 @@ hipError_t launch_sha256_multi(uint32_t n, const uint8_t *const *arenas,
         maxslots = nslots[j] > maxslots ? nslots[j] : maxslots;
     }
     if (maxslots == 0) return hipGetLastError();
-    hipLaunchKernelGGL(rcdc_sha256_multi_split_kernel, dim3((uint32_t)((maxslots + 63) / 64), n),
-                       dim3(128), 0, stream, m);
+    const uint64_t blocks = (maxslots + 63) / 64 * n;
+    if (blocks >= (1ull << 31)) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(rcdc_sha256_multi_split_kernel, dim3((uint32_t)blocks), dim3(128), 0,
+                       stream, m, n);
     return hipGetLastError();
 }
 
