@@ -72,7 +72,7 @@ def parse():
                     help="also measure the fused blob ids (rcdc_plan_hash, SURVEY 8(f) row 1), "
                          "reported as a separate object; the headline value is unchanged")
     ap.add_argument("--sha-steps", type=int, default=5)
-    ap.add_argument("--sha-depth", type=int, default=4,
+    ap.add_argument("--sha-depth", type=int, default=8,
                     help="batches whose blob ids are in flight at once (pipelined ingest)")
     ap.add_argument("--pipeline", action="store_true",
                     help="overlap run k's resolve with run k+1's scan (rcdc_plan_set_pipeline; "
