@@ -56,8 +56,11 @@ typedef struct {
 
 /* check_rabin_params -- replaces crates/core/src/chunker/rabin.rs:17-42.
  * avg must be a power of two, min <= avg <= max.  Additionally rejected with
- * RCDC_ERR_UNSUPPORTED: min < 64 (the reference slices vec[len-64..],
- * rabin.rs:150) and max > 2^40.                                            */
+ * RCDC_ERR_UNSUPPORTED: min < 4096 and max > 2^40.  Below 4096 the
+ * reference's `min_size -= open_buf_len` (rabin.rs:124, up to 4095 bytes of
+ * its 4 KiB read buffer, rabin.rs:12) underflows -- a panic under debug
+ * assertions, a read-pattern-dependent wrap in release -- so no bit-exact
+ * cut list exists for such parameters.                                     */
 rcdc_status rcdc_check_params(uint64_t avg, uint64_t min, uint64_t max);
 
 /* ConfigFile::poly -- replaces crates/core/src/repofile/configfile.rs:165-175
@@ -165,6 +168,20 @@ rcdc_status rcdc_plan_set_timing(rcdc_plan *plan, int enable);
 rcdc_status rcdc_plan_kernel_times(rcdc_plan *plan, uint64_t *runs,
                                    double *scan_ms_total,
                                    double *resolve_ms_total);
+
+/* Work counters of the walk path (long streams) of the last run, after it
+ * completes: stats[0] 64-lane hashing rounds of rcdc_walk_kernel (64 x
+ * (S + 64) bytes hashed by lanes each, S = 2048), [1] its min-zone
+ * evaluations (64 windows of 64 bytes), [2] chunks it emitted, [3] 1024-lane
+ * rounds of the fixup kernel (1024 x (512 + 64) bytes each), [4] fixup zones,
+ * [5] cuts the fixups walked, [6..7] 0.  With the environment variable
+ * RCDC_WALK_TRACE=1 at plan creation, `trace` (if not NULL) receives 4
+ * words per walk piece: wall clock (100 MHz) at the piece's start and end,
+ * rounds, chunks -- at most trace_cap words.  All zero for plans without
+ * walked streams.                                                          */
+#define RCDC_WALK_STATS 8
+rcdc_status rcdc_plan_walk_stats(rcdc_plan *plan, uint64_t *stats, uint64_t *trace,
+                                 uint64_t trace_cap);
 
 /* ---- FixedSize chunker (crates/core/src/chunker/fixed_size.rs:41-70) ---- */
 /* Cuts every `size` bytes, last chunk short; returns the count.           */

@@ -149,23 +149,55 @@ typedef struct {
     uint8_t buf[4096]; /* BUF_SIZE, rabin.rs:12 */
     size_t buf_len, pos;
     int finished;
+    uint64_t short_reads; /* 0: Cursor (full reads); else xorshift state */
 } owned_iter;
 
-static size_t cursor_read(owned_iter *it, uint8_t *dst, size_t want) {
+/* One Read::read of at most `want` bytes.  A Cursor fills the request; with
+ * short_reads set every read returns a pseudo-random 1..want bytes (a pipe or
+ * stdin reader, commands/backup.rs:339-345), which also shrinks the 4 KiB
+ * buffer for good (`self.buf.truncate(size)`, rabin.rs:170). */
+static size_t reader_read(owned_iter *it, uint8_t *dst, size_t want) {
     size_t avail = it->src_len - it->src_pos;
     size_t k = want < avail ? want : avail;
+    if (it->short_reads && k > 1) {
+        uint64_t x = it->short_reads;
+        x ^= x << 13; x ^= x >> 7; x ^= x << 17;
+        it->short_reads = x;
+        k = 1 + (size_t)(x % k);
+    }
     memcpy(dst, it->src + it->src_pos, k);
     it->src_pos += k;
     return k;
 }
 
-/* returns chunk length, 0 at end; vec must hold max bytes */
+/* take(want).read_to_end(): loop reads until `want` bytes or EOF */
+static size_t cursor_read(owned_iter *it, uint8_t *dst, size_t want) {
+    size_t got = 0;
+    while (got < want) {
+        size_t k = reader_read(it, dst + got, want - got);
+        if (k == 0) break;
+        got += k;
+    }
+    return got;
+}
+
+/* returns chunk length, 0 at end, CDC_REF_UNDERFLOW where the reference's
+ * `min_size -= open_buf_len` (rabin.rs:124) would underflow: up to
+ * BUF_SIZE - 1 = 4095 read-ahead bytes (rabin.rs:12) exceed min.  The
+ * reference panics there under debug assertions (its test profile) and
+ * wraps in release (take(huge) then returns the whole remainder as one
+ * chunk, read-pattern dependent), so this mode stops instead of copying
+ * past `vec` (which holds max + 8 bytes).  librcdc rejects min < 4096. */
 static size_t owned_next(const cdc_ref_tables *t, owned_iter *it,
                          rabin_state *r, uint8_t *vec, uint64_t mask,
                          uint64_t min, uint64_t max) {
     if (it->finished) return 0;
     size_t min_size = min, len = 0;
     size_t open = it->buf_len - it->pos; /* rabin.rs:120-126 */
+    if (open > min_size) {
+        it->finished = 1;
+        return CDC_REF_UNDERFLOW;
+    }
     if (open > 0) {
         memcpy(vec, it->buf + it->pos, open);
         len = open;
@@ -183,7 +215,7 @@ static size_t owned_next(const cdc_ref_tables *t, owned_iter *it,
         if (len >= max) break;
         if ((r->hash & mask) == 0) break;
         if (it->buf_len == it->pos) {
-            size_t k = cursor_read(it, it->buf, it->buf_len); /* :163 */
+            size_t k = reader_read(it, it->buf, it->buf_len); /* :163 */
             if (k == 0) { it->finished = 1; break; }
             it->pos = 0;
             it->buf_len = k; /* buf.truncate(size) */
@@ -196,10 +228,12 @@ static size_t owned_next(const cdc_ref_tables *t, owned_iter *it,
     return len;
 }
 
-size_t cdc_ref_chunk_owned(const cdc_ref_tables *t, const uint8_t *data,
-                           size_t n, uint64_t min, uint64_t avg, uint64_t max,
-                           uint64_t *cuts, size_t cap) {
+size_t cdc_ref_chunk_owned_reads(const cdc_ref_tables *t, const uint8_t *data,
+                                 size_t n, uint64_t min, uint64_t avg,
+                                 uint64_t max, uint64_t read_seed,
+                                 uint64_t *cuts, size_t cap) {
     owned_iter *it = (owned_iter *)calloc(1, sizeof *it);
+    it->short_reads = read_seed;
     uint8_t *vec = (uint8_t *)malloc(max + 8);
     rabin_state r;
     memset(&r, 0, sizeof r);
@@ -211,6 +245,7 @@ size_t cdc_ref_chunk_owned(const cdc_ref_tables *t, const uint8_t *data,
     for (;;) {
         size_t len = owned_next(t, it, &r, vec, avg - 1, min, max);
         if (len == 0) break;
+        if (len == CDC_REF_UNDERFLOW) { nc = CDC_REF_UNDERFLOW; break; }
         off += len;
         if (nc < cap) cuts[nc] = off;
         nc++;
@@ -218,6 +253,12 @@ size_t cdc_ref_chunk_owned(const cdc_ref_tables *t, const uint8_t *data,
     free(vec);
     free(it);
     return nc;
+}
+
+size_t cdc_ref_chunk_owned(const cdc_ref_tables *t, const uint8_t *data,
+                           size_t n, uint64_t min, uint64_t avg, uint64_t max,
+                           uint64_t *cuts, size_t cap) {
+    return cdc_ref_chunk_owned_reads(t, data, n, min, avg, max, 0, cuts, cap);
 }
 
 typedef struct {
@@ -251,7 +292,11 @@ static void *many_worker(void *arg) {
         it->buf_len = sizeof it->buf;
         it->pos = sizeof it->buf;
         uint64_t k = 0;
-        while (owned_next(c->t, it, &r, vec, c->avg - 1, c->min, c->max)) k++;
+        for (;;) {
+            size_t len = owned_next(c->t, it, &r, vec, c->avg - 1, c->min, c->max);
+            if (len == 0 || len == CDC_REF_UNDERFLOW) break;
+            k++;
+        }
         if (c->counts) c->counts[f] = k;
         local += k;
     }

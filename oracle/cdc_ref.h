@@ -71,6 +71,16 @@ size_t cdc_ref_chunk(const cdc_ref_tables *t, const uint8_t *data, size_t n,
 size_t cdc_ref_chunk_owned(const cdc_ref_tables *t, const uint8_t *data,
                            size_t n, uint64_t min, uint64_t avg, uint64_t max,
                            uint64_t *cuts, size_t cap);
+/* Returned (instead of a count) where rabin.rs:124 `min_size -= open_buf_len`
+ * would underflow: min < the up-to-4095 read-ahead bytes (BUF_SIZE,
+ * rabin.rs:12).  Reachable only for min < 4096, which librcdc rejects. */
+#define CDC_REF_UNDERFLOW ((size_t)-1)
+/* Same, with a reader whose every read() returns a pseudo-random 1..want
+ * bytes (xorshift64 seeded by read_seed != 0; 0 = full Cursor reads). */
+size_t cdc_ref_chunk_owned_reads(const cdc_ref_tables *t, const uint8_t *data,
+                                 size_t n, uint64_t min, uint64_t avg,
+                                 uint64_t max, uint64_t read_seed,
+                                 uint64_t *cuts, size_t cap);
 
 /* Same as cdc_ref_chunk_owned over many independent files with nthreads
  * POSIX threads (per-file parallelism as in archiver.rs:195).  Each file i

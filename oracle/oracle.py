@@ -66,6 +66,9 @@ def lib():
         L.cdc_ref_chunk_owned.argtypes = [ctypes.POINTER(_Tables), p, sz, u64, u64,
                                           u64, p, sz]
         L.cdc_ref_chunk_owned.restype = sz
+        L.cdc_ref_chunk_owned_reads.argtypes = [ctypes.POINTER(_Tables), p, sz, u64, u64,
+                                                u64, u64, p, sz]
+        L.cdc_ref_chunk_owned_reads.restype = sz
         L.cdc_ref_chunk_many_owned.argtypes = [ctypes.POINTER(_Tables), p, p, p, sz,
                                                u64, u64, u64, ctypes.c_int, p]
         L.cdc_ref_chunk_many_owned.restype = u64
@@ -117,15 +120,29 @@ def chunk_cuts(data, poly=DEFAULT_POLY, min_size=DEFAULT_MIN, avg=DEFAULT_AVG,
     return cuts[:k].copy()
 
 
+class ReferenceUnderflow(ArithmeticError):
+    """rabin.rs:124 `min_size -= open_buf_len` would underflow (min below the
+    up-to-4095 read-ahead bytes of the 4 KiB buffer, rabin.rs:12): the
+    reference panics under debug assertions and wraps in release."""
+
+
+UNDERFLOW = (1 << 64) - 1  # CDC_REF_UNDERFLOW
+
+
 def chunk_cuts_owned(data, poly=DEFAULT_POLY, min_size=DEFAULT_MIN, avg=DEFAULT_AVG,
-                     max_size=DEFAULT_MAX) -> np.ndarray:
-    """Same cuts, reference-equivalent work (owned chunk buffers, 4 KiB reads)."""
+                     max_size=DEFAULT_MAX, read_seed: int = 0) -> np.ndarray:
+    """Same cuts, reference-equivalent work (owned chunk buffers, 4 KiB reads,
+    rabin.rs:110-191).  read_seed != 0: every reader read() returns a
+    pseudo-random 1..n bytes (a pipe-like reader) instead of filling the
+    request.  Raises ReferenceUnderflow where the reference would underflow."""
     a = _as_u8(data)
     n = a.size
     cap = n // max(min_size, 1) + 2
     cuts = np.zeros(cap, dtype=np.uint64)
-    k = lib().cdc_ref_chunk_owned(ctypes.byref(tables(poly)), _ptr(a), n, min_size,
-                                  avg, max_size, _ptr(cuts), cap)
+    k = lib().cdc_ref_chunk_owned_reads(ctypes.byref(tables(poly)), _ptr(a), n, min_size,
+                                        avg, max_size, read_seed, _ptr(cuts), cap)
+    if k == UNDERFLOW:
+        raise ReferenceUnderflow(f"rabin.rs:124 underflow at min={min_size}")
     return cuts[:k].copy()
 
 

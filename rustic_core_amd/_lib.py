@@ -23,7 +23,7 @@ EXPORTS = (
     "rcdc_plan_destroy", "rcdc_plan_run", "rcdc_plan_results", "rcdc_plan_device_results",
     "rcdc_plan_get_info", "rcdc_plan_set_timing", "rcdc_plan_kernel_times", "rcdc_fixed_cuts",
     "rcdc_sha256_chunks", "rcdc_plan_hash", "rcdc_plan_digests", "rcdc_plan_device_digests",
-    "rcdc_plan_set_pipeline", "rcdc_plan_hash_many",
+    "rcdc_plan_set_pipeline", "rcdc_plan_hash_many", "rcdc_plan_walk_stats",
 )
 ABI_VERSION = 1
 
@@ -49,7 +49,7 @@ class PlanInfo(ctypes.Structure):
 
 def build(verbose: bool = False) -> str:
     """Compile librcdc.so for gfx950 with hipcc (cross-compiles without a GPU)."""
-    out = subprocess.run(["make", "-s", "-C", CSRC], capture_output=not verbose, text=True)
+    out = subprocess.run(["make", "-s", "-j8", "-C", CSRC], capture_output=not verbose, text=True)
     if out.returncode != 0:
         raise RcdcLibraryError(f"building librcdc.so failed:\n{out.stdout}\n{out.stderr}")
     return LIB_PATH
@@ -136,6 +136,8 @@ def lib() -> ctypes.CDLL:
     L.rcdc_plan_hash_many.argtypes = [vp, u32, vp, vp]
     L.rcdc_plan_set_pipeline.restype = st
     L.rcdc_plan_set_pipeline.argtypes = [vp, ctypes.c_int]
+    L.rcdc_plan_walk_stats.restype = st
+    L.rcdc_plan_walk_stats.argtypes = [vp, vp, vp, u64]
     L.rcdc_plan_device_digests.restype = st
     L.rcdc_plan_device_digests.argtypes = [vp, P(u64)]
     _lib = L

@@ -15,6 +15,7 @@ namespace rcdc {
 
 constexpr uint32_t kNone = 0xFFFFFFFFu;
 constexpr int kWindow = 64;          // Rabin64::new_with_polynom(6, ..) -> 2^6
+constexpr uint64_t kRefBufSize = 4096;  // the reference's read buffer (rabin.rs:12): min >= it
 constexpr int kScanThreads = 1024;   // 16 waves; one workgroup per CU
 constexpr int kScanWaves = kScanThreads / 64;
 constexpr int kTableRepl = 32;       // per-lane table copies: bank = lane % 32
@@ -124,7 +125,22 @@ struct WalkParams {
     uint32_t fix_cap;      // fixup cut slots per boundary
     uint32_t fix_seg;      // S for the fixup walker (latency-bound: smaller rounds)
     uint32_t pad;
+    // kWalkStat* counters (always on: one atomic per piece / fixup boundary)
+    unsigned long long *stats;
+    // optional per-piece trace (nullptr = off): kTraceWords u64 per unit
+    unsigned long long *trace;
 };
+
+// WalkParams.stats slots
+constexpr int kWalkStatRounds = 0;     // walk kernel: 64-lane hashing rounds
+constexpr int kWalkStatZones = 1;      // walk kernel: zone evaluations (64 x 64 slides)
+constexpr int kWalkStatChunks = 2;     // walk kernel: chunks emitted (incl. zero-run ones)
+constexpr int kWalkStatFixRounds = 3;  // fixup kernel: 1024-lane rounds
+constexpr int kWalkStatFixZones = 4;   // fixup kernel: zone evaluations
+constexpr int kWalkStatFixCuts = 5;    // fixup kernel: cuts walked
+constexpr int kWalkStats = 8;
+// trace per unit: wall clock (100 MHz) at start and end, rounds, chunks
+constexpr int kTraceWords = 4;
 
 constexpr int kMaxHops = 13;  // chain steps the check kernel resolves itself
 

@@ -161,6 +161,9 @@ struct rcdc_plan {
     uint32_t *d_fixlist = nullptr;
     uint64_t *d_fixcuts = nullptr;
     FixRes *d_fixres = nullptr;
+    unsigned long long *d_wstats = nullptr;  // kWalkStats work counters of the last run
+    unsigned long long *d_wtrace = nullptr;  // per-unit trace (RCDC_WALK_TRACE=1)
+    uint64_t cap_wstats = 0, cap_wtrace = 0;
     uint64_t cap_wunits = 0, cap_wsu0 = 0, cap_wpiece = 0, cap_pstatus = 0, cap_bres = 0,
              cap_ctr = 0, cap_fixlist = 0, cap_fixcuts = 0, cap_fixres = 0;
     const void *last_arena = nullptr;  // of the last run (fallback re-runs)
@@ -502,6 +505,13 @@ rcdc_status plan_build(rcdc_ctx *ctx, rcdc_plan *pl, const uint64_t *offs, const
         if ((st = ensure_dev(&pl->d_fixlist, &pl->cap_fixlist, nw))) return st;
         if ((st = ensure_dev(&pl->d_fixcuts, &pl->cap_fixcuts, nw * pl->wprm.fix_cap))) return st;
         if ((st = ensure_dev(&pl->d_fixres, &pl->cap_fixres, nw))) return st;
+        if ((st = ensure_dev(&pl->d_wstats, &pl->cap_wstats, kWalkStats))) return st;
+        pl->wprm.stats = pl->d_wstats;
+        pl->wprm.trace = nullptr;
+        if (const char *e = getenv("RCDC_WALK_TRACE"); e && atoi(e) > 0) {
+            if ((st = ensure_dev(&pl->d_wtrace, &pl->cap_wtrace, nw * kTraceWords))) return st;
+            pl->wprm.trace = pl->d_wtrace;
+        }
         HIP_TRY(hipMemcpy(pl->d_wunits, pl->wunits.data(), nw * sizeof(WalkUnit),
                           hipMemcpyHostToDevice));
         HIP_TRY(hipMemcpy(pl->d_wsu0, pl->wstream_u0.data(),
@@ -709,6 +719,8 @@ void plan_release(rcdc_plan *pl) {
     (void)hipFree(pl->d_fixlist);
     (void)hipFree(pl->d_fixcuts);
     (void)hipFree(pl->d_fixres);
+    (void)hipFree(pl->d_wstats);
+    (void)hipFree(pl->d_wtrace);
     (void)hipFree(pl->d_items);
     (void)hipFree(pl->d_sds);
     (void)hipFree(pl->d_sums);
@@ -799,8 +811,19 @@ rcdc_status rcdc_check_params(uint64_t avg, uint64_t min, uint64_t max) {
     if (max < avg)
         return fail(RCDC_ERR_UNSUPPORTED,
                     "Chunk max size must be larger or equal than the chunk size.");
-    if (min < (uint64_t)kWindow)
-        return fail(RCDC_ERR_UNSUPPORTED, "Chunk min size must be at least 64 bytes (window).");
+    // The reference accepts any min, but its iterator is only well defined
+    // for min >= BUF_SIZE = 4096 (rabin.rs:12): a chunk that ends mid-buffer
+    // leaves up to 4095 read-ahead bytes, and the next chunk does
+    // `min_size -= open_buf_len` (rabin.rs:124).  Below 4096 that underflows:
+    // a panic under debug assertions (the reference's test profile), and in
+    // release a wrap that makes take(huge) return the whole remaining stream
+    // as one chunk -- dependent on how the reader splits its reads, not a
+    // function of the bytes.  No bit-exact cut list exists there, so such
+    // parameters are Unsupported (the same ErrorKind as rabin.rs:22-40).
+    if (min < (uint64_t)kRefBufSize)
+        return fail(RCDC_ERR_UNSUPPORTED,
+                    "Chunk min size must be at least 4096 bytes (the reference's read buffer, "
+                    "rabin.rs:12,124). chunk min size = %llu.", (unsigned long long)min);
     if (avg > (1ull << 32) || max > (1ull << 40))
         return fail(RCDC_ERR_UNSUPPORTED, "chunk size > 4 GiB or max size > 1 TiB");
     return RCDC_OK;
@@ -843,8 +866,10 @@ rcdc_status rcdc_ctx_create(uint64_t poly, uint64_t min, uint64_t avg_pow2, uint
     rcdc_status st = rcdc_check_params(avg_pow2, min, max);
     if (st) return st;
     const int deg = poly_degree(poly);
-    if (deg < 33 || deg > 56)
-        return fail(RCDC_ERR_UNSUPPORTED, "polynomial %#llx has degree %d; supported 33..56",
+    // deg <= 56: `h << 8` of the reference's slide must not overflow u64;
+    // deg >= 9: polynom_shift = deg - 8 must be positive
+    if (deg < 9 || deg > 56)
+        return fail(RCDC_ERR_UNSUPPORTED, "polynomial %#llx has degree %d; supported 9..56",
                     (unsigned long long)poly, deg);
     int ndev = 0;
     HIP_TRY(hipGetDeviceCount(&ndev));
@@ -972,6 +997,23 @@ rcdc_status rcdc_plan_get_info(const rcdc_plan *plan, rcdc_plan_info *info) {
     info->work_items = (uint32_t)plan->items.size();
     info->scan_blocks = plan->blocks;
     info->walk_pieces = (uint32_t)plan->wunits.size();
+    return RCDC_OK;
+}
+
+rcdc_status rcdc_plan_walk_stats(rcdc_plan *plan, uint64_t *stats, uint64_t *trace,
+                                 uint64_t trace_cap) {
+    if (!plan || !stats) return fail(RCDC_ERR_INVALID_INPUT, "null argument");
+    memset(stats, 0, RCDC_WALK_STATS * sizeof(uint64_t));
+    if (plan->wunits.empty()) return RCDC_OK;
+    if (!plan->ran) return fail(RCDC_ERR_INVALID_INPUT, "plan has not been run");
+    DeviceGuard g(plan->ctx->device);
+    HIP_TRY(hipEventSynchronize(plan->done));
+    static_assert(RCDC_WALK_STATS == kWalkStats, "stats slots");
+    HIP_TRY(hipMemcpy(stats, plan->d_wstats, kWalkStats * 8, hipMemcpyDeviceToHost));
+    const uint64_t nw = plan->wunits.size() * kTraceWords;
+    if (trace && trace_cap && plan->wprm.trace)
+        HIP_TRY(hipMemcpy(trace, plan->d_wtrace, std::min(trace_cap, nw) * 8,
+                          hipMemcpyDeviceToHost));
     return RCDC_OK;
 }
 

@@ -38,7 +38,7 @@ struct Consts {
     uint32_t lwo, lwm;  // lane's table-copy offset in OUT / MOD
     uint32_t kff00;     // 0xFF00 in a VGPR
     uint32_t mask;      // avg - 1 in a VGPR
-    uint32_t tsh;       // deg - 32 (generic-degree path only)
+    uint32_t tsh;       // deg - 8 (generic-degree path only)
 };
 
 // MOD table address of the top byte of h (h1 = hi32(h), a1 = hi32(h << 8)).
@@ -47,15 +47,18 @@ struct Consts {
 //   v_lshrrev, v_bitop3, ds_read_b64, v_bitop3);
 // 0 <= TSH < 100: compile-time deg - 40 from a1 (v_lshrrev by an inline
 //   constant + one v_bitop3 (x & 0xFF00) | lwm);
-// TSH < 0: any degree, runtime shift of a1.
+// TSH < 0: any degree 9..56, runtime 64-bit shift of h by deg - 8 (the
+//   top byte straddles h1:h0 for deg < 40; half-rate shift, off the deg-53
+//   fast path).
 template <int TSH>
-__device__ __forceinline__ uint32_t mod_addr(uint32_t h1, uint32_t a1, const Consts &k) {
+__device__ __forceinline__ uint32_t mod_addr(uint32_t h0, uint32_t h1, uint32_t a1,
+                                             const Consts &k) {
     if constexpr (TSH >= 100)
         return __builtin_amdgcn_bitop3_b32(h1 >> (TSH - 100), k.kff00, k.lwm, kAndOr);
     else if constexpr (TSH >= 0)
         return __builtin_amdgcn_bitop3_b32(a1 >> TSH, k.kff00, k.lwm, kAndOr);
     else
-        return ((a1 >> k.tsh) << 8) | k.lwm;
+        return (((uint32_t)(((uint64_t)h1 << 32 | h0) >> k.tsh) & 255u) << 8) | k.lwm;
 }
 
 // One slide: h ^= out[o]; i = top byte; h = ((h<<8)|n) ^ mod[i]
@@ -72,7 +75,7 @@ __device__ __forceinline__ void slide(uint32_t &h0, uint32_t &h1, uint32_t dnew,
                                       const uint8_t *tab, const Consts &k) {
     const uint2 o = lds_u2(tab, __builtin_amdgcn_perm(dold, k.lwo, 0x0C0C0000u | ((4u + K) << 8)));
     const uint32_t a1 = __builtin_amdgcn_alignbit(h1, h0, 24);
-    const uint2 m = lds_u2(tab, mod_addr<TSH>(h1, a1, k));
+    const uint2 m = lds_u2(tab, mod_addr<TSH>(h0, h1, a1, k));
     h0 = __builtin_amdgcn_bitop3_b32(__builtin_amdgcn_perm(h0, dnew, 0x06050400u | K), o.x, m.x, kXor3);
     h1 = __builtin_amdgcn_bitop3_b32(a1, o.y, m.y, kXor3);
 }
@@ -82,7 +85,7 @@ template <int K, int TSH>
 __device__ __forceinline__ void slide_in(uint32_t &h0, uint32_t &h1, uint32_t dnew,
                                          const uint8_t *tab, const Consts &k) {
     const uint32_t a1 = __builtin_amdgcn_alignbit(h1, h0, 24);
-    const uint2 m = lds_u2(tab, mod_addr<TSH>(h1, a1, k));
+    const uint2 m = lds_u2(tab, mod_addr<TSH>(h0, h1, a1, k));
     h0 = __builtin_amdgcn_perm(h0, dnew, 0x06050400u | K) ^ m.x;
     h1 = a1 ^ m.y;
 }
@@ -285,7 +288,8 @@ __device__ __forceinline__ Chain scan_segment(__amdgpu_buffer_rsrc_t rsrc, uint3
 // Kernel prologue: 32 lane-private copies of OM and MOD into LDS (entry e of
 // copy c at e * 256 + c * 8; MOD kTableBytes further).  OM[e] = OUT'[e]
 // reduced: the top byte of out << 8 sits at bits deg .. deg + 7 and MOD's
-// (i << deg) term cancels it.  Ends with a workgroup barrier.
+// (i << deg) term cancels it.  idx_shift = deg - 32 mod 2^32 (wraps for
+// deg < 32; idx_shift + 32 = deg either way).  Ends with a workgroup barrier.
 __device__ __forceinline__ void fill_tables(uint8_t *s_tab, const uint64_t *__restrict__ gtab,
                                             uint32_t idx_shift, uint32_t tid, uint32_t nthreads) {
     for (uint32_t i = tid; i < 256u * kTableRepl; i += nthreads) {
@@ -306,7 +310,7 @@ __device__ __forceinline__ Consts make_consts(uint32_t lane, uint32_t mask, uint
     k.lwm = k.lwo | kTableBytes;
     k.kff00 = in_vgpr(0xFF00u);
     k.mask = in_vgpr(mask);
-    k.tsh = idx_shift;
+    k.tsh = idx_shift + 24u;  // deg - 8
     return k;
 }
 

@@ -152,6 +152,8 @@ struct Walk {
     uint8_t *win;      // 128 B of LDS (the zone window)
     uint64_t *red;     // LDS: 16 reduction slots (workgroup walker)
     uint32_t lane, wave, tid;
+    // work counters of this walker (wave-uniform): hashing rounds, zones
+    uint32_t rounds, zones;
 };
 
 // First pure-window candidate p in [q, end) among the positions of one round
@@ -213,7 +215,7 @@ __device__ uint64_t round_first(const Walk &W, uint64_t A, uint64_t q, uint64_t 
 // cut was found below stop_scan (the search stopped there).  *kind: what the
 // walker verified (rcdc_internal.h kKind*); *zero: all-zero prefill cut.
 template <int LANES, int TSH, bool SMALL>
-__device__ uint64_t walk_next(const Walk &W, uint64_t pos, uint64_t stop_scan, uint64_t *kind,
+__device__ uint64_t walk_next(Walk &W, uint64_t pos, uint64_t stop_scan, uint64_t *kind,
                               bool *zero) {
     *zero = false;
     if (W.N - pos <= W.mn) {  // rabin.rs:141-147: the rest is the last chunk
@@ -225,6 +227,7 @@ __device__ uint64_t walk_next(const Walk &W, uint64_t pos, uint64_t stop_scan, u
     uint64_t zc;
     bool zz;
     const ModRepl mod{W.tab, W.k.lwm};
+    W.zones++;
     if constexpr (LANES == 64) {
         zc = zone_wave(W.arena + W.off, W.N, z, limit, W.mask, W.shift, mod, W.win, W.lane, &zz);
     } else {
@@ -254,6 +257,7 @@ __device__ uint64_t walk_next(const Walk &W, uint64_t pos, uint64_t stop_scan, u
     const uint64_t end = min(limit, stop_scan);
     uint64_t A = ((W.off + q - 1) & ~63ull) - W.off;  // A + 1 <= q: q is tested
     while (A < end) {
+        W.rounds++;
         const uint64_t p = round_first<LANES, TSH, SMALL>(W, A, q, end);
         if (p != kNoCut) {
             *kind = kKindHit;
@@ -325,6 +329,8 @@ __global__ __launch_bounds__(1024, 1) void rcdc_walk_kernel(
         if (lane == 0) u = atomicAdd(&ctr[0], 1u);
         u = __builtin_amdgcn_readfirstlane(u);
         if (u >= prm.nunits) break;
+        const uint64_t t0 = prm.trace ? (uint64_t)wall_clock64() : 0;
+        W.rounds = W.zones = 0;
         const WalkUnit U = units[u];
         const StreamDesc d = sds[U.stream];
         W.off = d.off;
@@ -360,9 +366,20 @@ __global__ __launch_bounds__(1024, 1) void rcdc_walk_kernel(
             }
             if (pos >= U.stop) break;
         }
-        if (lane == 0)
+        if (lane == 0) {
             pstatus[u] = min(n, (uint64_t)U.out_cap) | (open ? kOpenFlag : 0ull) |
                          (n > U.out_cap ? (kOpenFlag << 1) : 0ull);
+            atomicAdd(&prm.stats[kWalkStatRounds], (unsigned long long)W.rounds);
+            atomicAdd(&prm.stats[kWalkStatZones], (unsigned long long)W.zones);
+            atomicAdd(&prm.stats[kWalkStatChunks], (unsigned long long)n);
+            if (prm.trace) {
+                unsigned long long *tr = prm.trace + (uint64_t)u * kTraceWords;
+                tr[0] = t0;
+                tr[1] = (uint64_t)wall_clock64();
+                tr[2] = W.rounds;
+                tr[3] = n;
+            }
+        }
     }
 }
 
@@ -548,6 +565,7 @@ __global__ __launch_bounds__(1024, 1) void rcdc_walk_fixup_kernel(
         const uint8_t *s = arena + d.off;
         uint64_t *out = fix_cuts + (uint64_t)u * prm.fix_cap;
         uint64_t c = bres[u].fix_from, n = 0;
+        W.rounds = W.zones = 0;
         uint32_t munit = kNoUnit;
         int32_t midx = -1;
         while (c < d.n && n <= prm.fix_cap) {
@@ -610,6 +628,9 @@ __global__ __launch_bounds__(1024, 1) void rcdc_walk_fixup_kernel(
             if (merged) break;
         }
         if (threadIdx.x == 0) {
+            atomicAdd(&prm.stats[kWalkStatFixRounds], (unsigned long long)W.rounds);
+            atomicAdd(&prm.stats[kWalkStatFixZones], (unsigned long long)W.zones);
+            atomicAdd(&prm.stats[kWalkStatFixCuts], (unsigned long long)n);
             FixRes F;
             F.count = (uint32_t)min(n, (uint64_t)prm.fix_cap + 1);
             F.merge_unit = munit;
@@ -799,6 +820,8 @@ hipError_t launch_walk(const uint8_t *arena, const StreamDesc *sds, const WalkUn
                        uint64_t *pstatus, uint32_t *ctr, uint32_t blocks, hipStream_t stream) {
     if (prm.nunits == 0) return hipSuccess;
     hipError_t e = hipMemsetAsync(ctr, 0, 4 * sizeof(uint32_t), stream);
+    if (e == hipSuccess)
+        e = hipMemsetAsync(prm.stats, 0, kWalkStats * sizeof(unsigned long long), stream);
     if (e != hipSuccess) return e;
     const bool small = prm.mask < 0xFFFFu;
 #define RCDC_WALK_LAUNCH(TSH, SM)                                                                  \

@@ -129,6 +129,24 @@ class DevicePlan:
             raise status_error(st, _lib.last_error())
         return n.value, a.value, b.value
 
+    WALK_STAT_NAMES = ("rounds", "zones", "chunks", "fix_rounds", "fix_zones", "fix_cuts")
+
+    def walk_stats(self, trace: bool = False):
+        """Work counters of the last run's walk path (rcdc_plan_walk_stats):
+        a dict, plus the ``(pieces, 4)`` per-piece trace (t0, t1 in 100 MHz
+        ticks, rounds, chunks) when ``trace`` (plan built with
+        RCDC_WALK_TRACE=1)."""
+        stats = np.zeros(8, dtype=np.uint64)
+        pieces = self.info()["walk_pieces"]
+        tr = np.zeros((max(pieces, 1), 4), dtype=np.uint64) if trace else None
+        st = _lib.lib().rcdc_plan_walk_stats(self._h, stats.ctypes.data,
+                                             tr.ctypes.data if trace else None,
+                                             tr.size if trace else 0)
+        if st:
+            raise status_error(st, _lib.last_error())
+        d = {k: int(v) for k, v in zip(self.WALK_STAT_NAMES, stats)}
+        return (d, tr[:pieces]) if trace else d
+
     def close(self):
         if getattr(self, "_h", None):
             _lib.lib().rcdc_plan_destroy(self._h)

@@ -40,11 +40,35 @@ def test_abi_version(rcdc_lib):
     (1 << 20, (1 << 20) + 1, 1 << 23, 1),   # rabin.rs:29
     (1 << 20, 1 << 19, (1 << 20) - 1, 1),   # rabin.rs:35
     (1 << 20, 32, 1 << 23, 1),              # min < 64: rabin.rs:150 slices vec[len-64..]
+    (4096, 1024, 16384, 1),                 # min < 4096: rabin.rs:124 underflows
+    (4096, 4095, 4096, 1),
+    (4096, 4096, 4096, 0),
 ])
 def test_check_params(rcdc_lib, oracle_mod, avg, mn, mx, status):
     assert rcdc_lib.rcdc_check_params(avg, mn, mx) == status
-    if mn >= 64:
+    if mn >= 4096:
         assert oracle_mod.check_params(avg, mn, mx) == (status == 0)
+    if status == 1 and mn < 4096:
+        assert "4096" in __import__("rustic_core_amd")._lib.last_error()
+
+
+@pytest.mark.parametrize("poly,ok", [((1 << 8) | 0x1D, False), ((1 << 9) | 0x11, True),
+                                     ((1 << 20) | 0x9, True), ((1 << 56) | 0x95, True),
+                                     ((1 << 57) | 0x1, False)])
+def test_ctx_degree_range(rcdc_lib, poly, ok):
+    """deg(P) in 9..56 (polynom_shift = deg - 8 > 0, h << 8 fits
+    u64).  Out of range: Unsupported before any HIP call; in range the call
+    gets past the degree check (and on a GPU-less host fails at device
+    enumeration, never with Unsupported)."""
+    from rustic_core_amd import _lib
+    h = ctypes.c_void_p()
+    st = rcdc_lib.rcdc_ctx_create(poly, 4096, 8192, 65536, 0, ctypes.byref(h))
+    if ok:
+        assert st != 1, _lib.last_error()
+        if st == 0:
+            rcdc_lib.rcdc_ctx_destroy(h)
+    else:
+        assert st == 1 and "degree" in _lib.last_error()
 
 
 @pytest.mark.parametrize("text,value", [

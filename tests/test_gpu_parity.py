@@ -139,7 +139,7 @@ def _mixed(seed, n, zero_frac=0.5):
 
 @pytest.mark.parametrize("params", [(4096, 8192, 16384), (4096, 4096, 4096),
                                     (4096, 16384, 65536), (8192, 65536, 1 << 20),
-                                    (64, 256, 1024), (100, 128, 300)])
+                                    (4096, 4096, 1 << 16), (5000, 8192, 12000)])
 @pytest.mark.parametrize("kind", ["random", "zeros", "mixed", "lowent"])
 def test_small_params(params, kind):
     import torch
@@ -166,7 +166,11 @@ def test_other_polynomial():
     import torch
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
-    for poly in (0x3DA3358B4DC173 ^ (1 << 20), (1 << 40) | 0x1B, (1 << 56) | 0x95):
+    # deg 53 (other taps), 40, 56 and the low degrees 9..33 whose top byte
+    # straddles the two state words (generic runtime-shift instantiation)
+    for poly in (0x3DA3358B4DC173 ^ (1 << 20), (1 << 40) | 0x1B, (1 << 56) | 0x95,
+                 (1 << 9) | 0x11, (1 << 20) | 0x9, (1 << 31) | 0x9, (1 << 32) | 0x8D,
+                 (1 << 33) | 0x53):
         ctx = _ctx(4096, 8192, 65536, poly)
         b = oracle.stdrng_bytes(17, 2 * MiB)
         got = _device_cuts(ctx, [b])[0]

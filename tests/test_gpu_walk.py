@@ -134,7 +134,7 @@ def test_walk_unaligned_offsets_and_short_streams(walk_env):
 
 
 @pytest.mark.parametrize("poly", [(1 << 40) | 0x1B, 0x3DA3358B4DC173 ^ (1 << 20),
-                                  (1 << 56) | 0x95])
+                                  (1 << 56) | 0x95, (1 << 20) | 0x9, (1 << 9) | 0x11])
 def test_walk_other_degrees(walk_env, poly):
     walk_env(256 * KiB)
     _run(SMALL, [_rand(60, 4 * MiB), _mixed(61, 4 * MiB, 4 * KiB, 300 * KiB, 1 * KiB, 200 * KiB)],
@@ -144,7 +144,7 @@ def test_walk_other_degrees(walk_env, poly):
 def test_walk_small_mask(walk_env):
     """avg < 2^16: the masked (SMALL) prefilter instantiation."""
     walk_env(64 * KiB)
-    _run((1 * KiB, 4 * KiB, 16 * KiB), [_rand(70, 2 * MiB), _mixed(71, 2 * MiB, 1024, 64 * KiB,
+    _run((4 * KiB, 4 * KiB, 16 * KiB), [_rand(70, 2 * MiB), _mixed(71, 2 * MiB, 1024, 64 * KiB,
                                                                      256, 64 * KiB)])
 
 

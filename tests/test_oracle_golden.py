@@ -72,15 +72,18 @@ def test_stdrng_skip_consistent(oracle_mod):
         assert np.array_equal(part, full[skip:skip + 1000])
 
 
-@pytest.mark.parametrize("params", [(256, 64, 1024), (512, 128, 2048), (1024, 512, 1024)])
+@pytest.mark.parametrize("params", [(4096, 4096, 8192), (8192, 4096, 6000),
+                                    (4096, 4096, 4096)])
 def test_c_oracle_matches_pure_python(oracle_mod, params):
     """Two independent restatements of rabin.rs:107-191 agree: the C oracle
-    (literal ring-window Rabin64) and pyref (closed-form fp per window)."""
+    (literal ring-window Rabin64) and pyref (closed-form fp per window).
+    Small masks (avg 4096/8192) so that hits, max cuts and zone cuts occur
+    within a few chunks; min >= 4096, the domain librcdc accepts."""
     from oracle import pyref
     avg, mn, mx = params
-    rng = np.random.default_rng(avg)
-    parts = [rng.integers(0, 256, 3000, dtype=np.uint8), np.zeros(1500, np.uint8),
-             rng.integers(0, 4, 2500, dtype=np.uint8)]
+    rng = np.random.default_rng(avg + mx)
+    parts = [rng.integers(0, 256, 14000, dtype=np.uint8), np.zeros(9000, np.uint8),
+             rng.integers(0, 4, 9000, dtype=np.uint8)]
     data = np.concatenate(parts)
     c = oracle_mod.chunk_cuts(data, oracle_mod.DEFAULT_POLY, mn, avg, mx)
     p = pyref.chunk_cuts(data.tobytes(), oracle_mod.DEFAULT_POLY, mn, avg, mx)
@@ -108,3 +111,51 @@ def test_candidates_match_window_fp(oracle_mod):
 ])
 def test_check_params(oracle_mod, avg, mn, mx, ok):
     assert oracle_mod.check_params(avg, mn, mx) == ok
+
+
+# ----------------------------------------------------------------------------
+# The reference-equivalent mode (owned Vec per chunk fed from the 4 KiB read
+# buffer, rabin.rs:110-191) equals the ideal cut function on every parameter
+# set librcdc accepts, whatever the reader's read sizes.  Below min = 4096
+# rabin.rs:124 underflows -- the reason librcdc rejects those parameters.
+ACCEPTED = [(4096, 4096, 4096), (4096, 4096, 1 << 16), (4096, 8192, 16384),
+            (5000, 8192, 12000), (4096, 1 << 16, 1 << 20), (65536, 1 << 16, 1 << 16),
+            (1 << 19, 1 << 20, 1 << 23)]
+
+
+def _kinds(n, seed):
+    rng = np.random.default_rng(seed)
+    mixed = np.zeros(n, np.uint8)
+    p = 0
+    while p < n:
+        r = int(rng.integers(1, 20000))
+        mixed[p:p + r] = rng.integers(0, 256, len(mixed[p:p + r]), dtype=np.uint8)
+        p += r + int(rng.integers(1, 30000))
+    return {"random": rng.integers(0, 256, n, dtype=np.uint8), "zeros": np.zeros(n, np.uint8),
+            "mixed": mixed, "lowent": rng.integers(0, 2, n, dtype=np.uint8)}
+
+
+@pytest.mark.parametrize("params", ACCEPTED, ids=lambda p: "-".join(map(str, p)))
+def test_owned_mode_equals_ideal_on_accepted_params(oracle_mod, rcdc_lib, params):
+    mn, avg, mx = params
+    assert rcdc_lib.rcdc_check_params(avg, mn, mx) == 0
+    n = 3 * (1 << 20) + 4321 if mn >= (1 << 19) else 600_000 + 777
+    for kind, data in _kinds(n, mn + avg).items():
+        ideal = oracle_mod.chunk_cuts(data, oracle_mod.DEFAULT_POLY, mn, avg, mx)
+        for read_seed in (0, 12345):
+            owned = oracle_mod.chunk_cuts_owned(data, oracle_mod.DEFAULT_POLY, mn, avg, mx,
+                                                read_seed=read_seed)
+            assert np.array_equal(ideal, owned), (kind, read_seed)
+
+
+@pytest.mark.parametrize("mn", [64, 1024, 4000])
+def test_reference_underflows_below_4096(oracle_mod, rcdc_lib, mn):
+    """rabin.rs:124 on random bytes at min < 4096: a chunk ends mid-buffer
+    with more read-ahead bytes than min -> the reference's subtraction
+    underflows (the oracle reports it instead of wrapping), and librcdc
+    rejects the parameters as Unsupported."""
+    from oracle.oracle import ReferenceUnderflow
+    data = np.random.default_rng(mn).integers(0, 256, 400_000, dtype=np.uint8)
+    with pytest.raises(ReferenceUnderflow):
+        oracle_mod.chunk_cuts_owned(data, oracle_mod.DEFAULT_POLY, mn, 4096, 16384)
+    assert rcdc_lib.rcdc_check_params(4096, mn, 16384) == 1
