@@ -55,7 +55,9 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--workload", choices=["C2", "C3", "C4", "C5"], default="C2")
+    ap.add_argument("--workload", choices=["C1", "C2", "C3", "C4", "C5"], default="C3",
+                    help="default C3 (64 x 1 GiB mixed per GPU, BASELINE.json configs[2]): the "
+                         "largest single-GPU configuration")
     ap.add_argument("--c4-files", type=int, default=8192)
     ap.add_argument("--c4-batch", type=float, default=96.0, help="C4: GiB per resident batch")
     ap.add_argument("--streams", type=int, default=None, help="C2: 1024, C3: 64")
@@ -149,44 +151,66 @@ def build_workload(args, torch, dev, rank, world):
 
 
 # ------------------------------------------------------------- baselines etc.
-def cpu_baseline(host: np.ndarray, offs, lens, seconds: float) -> dict:
-    """Oracle (cdc_ref, reference-equivalent work: owned chunk buffers fed by
-    4 KiB reads, rabin.rs:110-191) over the workload's streams (a bounded
-    sample of at most 4 GiB), per-file threads as in archiver.rs:195.
-    Repeats whole passes until `seconds` elapsed."""
-    from oracle import oracle
+def cpu_threads():
+    """Host threads for the CPU baseline: the process's CPU affinity, capped by
+    OMP_NUM_THREADS when set (the GPU box gives one GPU's job a 16-CPU share
+    and sets OMP_NUM_THREADS=16; nproc shows the whole machine)."""
     try:
         ncpu = len(os.sched_getaffinity(0))
     except AttributeError:  # pragma: no cover
         ncpu = os.cpu_count() or 1
-    threads = max(1, min(16, ncpu))
+    omp = os.environ.get("OMP_NUM_THREADS")
+    if omp and omp.isdigit() and int(omp) > 0:
+        return min(ncpu, int(omp)), f"min(affinity {ncpu}, OMP_NUM_THREADS {omp})"
+    return ncpu, f"affinity {ncpu}"
+
+
+def cpu_baseline(arena, offs, lens, seconds: float, max_bytes: int = 16 << 30) -> dict:
+    """Oracle (cdc_ref, reference-equivalent work: owned chunk buffers fed by
+    4 KiB reads, rabin.rs:110-191) over a bounded sample of the workload's
+    streams (whole streams, at most max_bytes), per-file threads as in
+    archiver.rs:195.  Repeats whole passes until `seconds` elapsed.  `arena`
+    is the device tensor: only the sampled streams are copied to the host."""
+    from oracle import oracle
+    from rustic_core_amd.device import pack_offsets
+    threads, why = cpu_threads()
     k = len(lens)
-    while k > 1 and int(np.sum(lens[:k])) > 4 * (1 << 30):
+    while k > 1 and int(np.sum(lens[:k])) > max_bytes:
         k -= 1
-    offs, lens = offs[:k], lens[:k]
-    total = int(np.sum(lens))
-    oracle.chunk_many_owned(host, offs, lens, nthreads=threads)  # warm
+    slens = np.asarray(lens[:k], dtype=np.uint64)
+    soffs, alen = pack_offsets(slens)
+    host = np.empty(alen, dtype=np.uint8)
+    for i in range(k):
+        o, n = int(offs[i]), int(lens[i])
+        x = arena[o:o + n]
+        host[int(soffs[i]):int(soffs[i]) + n] = x.cpu().numpy() if hasattr(x, "cpu") else x
+    total = int(np.sum(slens))
+    oracle.chunk_many_owned(host, soffs, slens, nthreads=threads)  # warm
     t0 = time.perf_counter()
     passes = 0
     while True:
-        oracle.chunk_many_owned(host, offs, lens, nthreads=threads)
+        oracle.chunk_many_owned(host, soffs, slens, nthreads=threads)
         passes += 1
         el = time.perf_counter() - t0
         if el >= seconds or el >= 30.0:
             break
-    k1 = min(64, len(lens)) if int(lens[0]) < (64 << 20) else 1
+    # one thread: the first streams up to ~256 MiB
+    k1 = 1
+    while k1 < k and int(np.sum(slens[:k1 + 1])) <= (256 << 20):
+        k1 += 1
     t1 = time.perf_counter()
-    oracle.chunk_many_owned(host, offs[:k1], lens[:k1], nthreads=1)
+    oracle.chunk_many_owned(host, soffs[:k1], slens[:k1], nthreads=1)
     el1 = time.perf_counter() - t1
     return {
         "value": passes * total / el / GiB,
         "unit": "GiB/s",
         "cores": threads,
         "kind": "port",
-        "sample": (f"{passes} full passes over {len(lens)} streams of the workload "
+        "sample": (f"{passes} full passes over the first {k} streams of the workload "
                    f"({passes * total / GiB:.1f} GiB, {el:.1f} s), cdc_ref reference-equivalent "
                    f"mode, {threads} threads (per-file parallel, archiver.rs:195)"),
-        "single_thread_gibs": int(np.sum(lens[:k1])) / el1 / GiB,
+        "cores_note": why,
+        "single_thread_gibs": int(np.sum(slens[:k1])) / el1 / GiB,
         "cpu_model": _cpu_model(),
     }
 
@@ -201,17 +225,34 @@ def _cpu_model() -> str:
     return "unknown"
 
 
-def pmc_traffic():
-    """Per-launch HBM bytes of the scan kernel from the committed rocprofv3
-    PMC summary (profiles/pmc_scan.json: FETCH_SIZE + WRITE_SIZE converted
-    with the calibration for this access pattern, profiles/r01_pmc_hbm.txt);
-    (None, None) if absent.  Measured on C2."""
-    p = os.path.join(ROOT, "profiles", "pmc_scan.json")
+def pmc_traffic(workload: str, kernel: str):
+    """Per-launch HBM bytes of the dominant kernel from the committed rocprofv3
+    PMC summary of this workload (profiles/pmc_<workload>.json: FETCH_SIZE +
+    WRITE_SIZE in separate passes, converted with the calibration measured for
+    this access pattern, profiles/r01_pmc_hbm.txt); (None, None) if absent."""
+    p = os.path.join(ROOT, "profiles", f"pmc_{workload}.json")
     try:
         d = json.load(open(p))
-        return d.get("hbm_bytes_per_launch"), d
     except (OSError, ValueError):
         return None, None
+    if kernel not in d.get("kernel", ""):
+        return None, None
+    return d.get("hbm_bytes_per_launch"), d
+
+
+def ref_slide_bytes(cuts_list, mn: int) -> int:
+    """Bytes the reference slides over for these chunks (rabin.rs:127-188):
+    a chunk longer than min costs 63 prefill bytes (:149-151) plus one slide
+    per byte after s + min; the short final chunk (<= min) costs none."""
+    tot = 0
+    for c in cuts_list:
+        c = np.asarray(c, dtype=np.int64)
+        if c.size == 0:
+            continue
+        L = np.diff(np.concatenate([[0], c]))
+        full = L > mn
+        tot += int(np.sum(L[full] - mn)) + 63 * int(np.count_nonzero(full))
+    return tot
 
 
 def c4_files(n: int):
@@ -265,6 +306,7 @@ def run_c4(args, torch, dist, dev, rank, world, local):
     torch.cuda.synchronize(dev)
     el = 0.0
     sample_cuts = {}
+    ref_hashed = lane_hashed = walked_batches = 0
     rng = np.random.default_rng(4001)
     sample = set(int(x) for x in rng.choice(args.c4_files, size=min(64, args.c4_files),
                                              replace=False))
@@ -293,10 +335,18 @@ def run_c4(args, torch, dist, dev, rank, world, local):
             runs += r
             scan_ms += sm
             resolve_ms += rm
-            if step == 0 and not args.no_parity:
+            if step == 0:
                 got = plan.results()
+                ref_hashed += ref_slide_bytes(got, MIN)
+                inf = plan.info()
+                if inf["walk_pieces"]:
+                    wst = plan.walk_stats()
+                    lane_hashed += wst["rounds"] * 64 * (2048 + 64) + wst["zones"] * 4096
+                    walked_batches += 1
+                else:
+                    lane_hashed += inf["scanned_bytes"] + 64 * inf["segments"]
                 for i, f in enumerate(b):
-                    if f in sample:
+                    if f in sample and not args.no_parity:
                         o = int(offs[i])
                         sample_cuts[f] = (got[i], arena[o:o + sizes[f]].cpu().numpy())
     t = torch.tensor([el], dtype=torch.float64, device=dev)
@@ -305,6 +355,7 @@ def run_c4(args, torch, dist, dev, rank, world, local):
     el_max = float(t.item())
     total = sum(sizes) * args.steps
     share = sum(sizes[f] for f in mine)
+    hash_s = max(scan_ms / 1e3 / max(args.steps, 1), 1e-9)  # hashing kernels per pass
     bad = 0
     for f, (cuts, host) in sample_cuts.items():
         from oracle import oracle
@@ -325,15 +376,21 @@ def run_c4(args, torch, dist, dev, rank, world, local):
                        "batches_on_rank0": len(batches), "rank0_share_gib": round(share / GiB, 2),
                        "poly": hex(POLY), "min": MIN, "avg": AVG, "max": MAX,
                        "parallelism": f"per-file LPT sharding over {world} GPU(s), no collectives"},
-            "roofline": {"bound": "hbm", "kernel": "rcdc_scan_kernel",
-                         "achieved": round(share / (scan_ms / max(runs, 1) * len(layouts) / 1e3)
-                                           / 1e9, 1) if runs else None,
+            "roofline": {"bound": "hbm",
+                         "kernel": ("rcdc_walk_kernel" if walked_batches == len(layouts) else
+                                    f"rcdc_walk_kernel ({walked_batches} batches) + "
+                                    f"rcdc_scan_kernel ({len(layouts) - walked_batches})"),
+                         "achieved": round(share / hash_s / 1e9, 1) if runs else None,
                          "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(share / (scan_ms / max(runs, 1) * len(layouts) / 1e3) / 1e9
-                                       / HBM_PEAK_GBS, 4) if runs else None,
+                         "frac": round(share / hash_s / 1e9 / HBM_PEAK_GBS, 4) if runs else None,
+                         "basis": "input bytes of the rank's files per pass / hashing-kernel time",
                          "traffic": None,
-                         "scan_ms_per_pass": round(scan_ms / max(args.steps, 1), 3),
-                         "resolve_ms_per_pass": round(resolve_ms / max(args.steps, 1), 3)},
+                         "ref_hashed_bytes_per_pass": ref_hashed,
+                         "frac_ref_hashed": round(ref_hashed / hash_s / 1e9 / HBM_PEAK_GBS, 4),
+                         "lane_hashed_bytes_per_pass": lane_hashed,
+                         "frac_lane_hashed": round(lane_hashed / hash_s / 1e9 / HBM_PEAK_GBS, 4),
+                         "hash_ms_per_pass": round(scan_ms / max(args.steps, 1), 3),
+                         "chain_ms_per_pass": round(resolve_ms / max(args.steps, 1), 3)},
             "parity": {"files_checked": int(checked[0]), "mismatches": int(checked[1]),
                        "checker": "oracle/cdc_ref on a seeded sample of 64 files"},
         }
@@ -346,13 +403,39 @@ def run_c4(args, torch, dist, dev, rank, world, local):
                 buf[int(o):int(o) + len(h)] = h
             line["cpu_baseline"] = cpu_baseline(buf, offs, np.array([len(h) for h in hosts],
                                                                     np.uint64), args.cpu_seconds)
+            line["cpu_baseline"]["sample"] += " (the 64-file parity sample of C4)"
         print(json.dumps(line), flush=True)
     for _, _, p in layouts:
         p.close()
 
 
+def spawn_ranks(args) -> None:
+    """`bench.py --gpus N` without a launcher: start N ranks with torchrun as a
+    child process (before anything touches the GPU) and exit with its code.
+    Under a launcher, WORLD_SIZE must equal --gpus."""
+    ws = os.environ.get("WORLD_SIZE")
+    if ws is not None:
+        if int(ws) != args.gpus:
+            print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={ws}", file=sys.stderr)
+            sys.exit(2)
+        return
+    if args.gpus <= 1:
+        return
+    import socket
+    import subprocess
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={args.gpus}", "--master-addr", "127.0.0.1",
+           "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY=os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0"))
+    sys.exit(subprocess.run(cmd, env=env).returncode)
+
+
 def main():
     args = parse()
+    spawn_ranks(args)
     import torch
     import torch.distributed as dist
 
@@ -450,52 +533,83 @@ def main():
         total_bytes = int(lens.sum()) * args.steps * world
     value = total_bytes / el_max / GiB
 
-    # dominant kernel (scan), HIP events on its launch stream over the timed
-    # region.  Algorithmic bytes per launch:
-    # 1 byte read per INPUT byte -> achieved = input bytes / scan time.  The
-    # kernel physically reads only the bytes it must hash, sum(N - min) (the
-    # reference never hashes a chunk's first min bytes), plus 64 B of warm-up
-    # per segment: that rate and the PMC-measured HBM traffic are reported
-    # beside it.
+    # dominant kernel, HIP events on its launch stream over the timed region
+    # (rcdc_plan_set_timing: the first event pair brackets the hashing
+    # kernels -- rcdc_scan_kernel for short streams, rcdc_walk_kernel for
+    # long ones -- and the second the resolve / chain kernels).
+    # Algorithmic bytes per launch: 1 byte read per INPUT
+    # byte -> achieved = input bytes / hashing-kernel time.  Beside it:
+    #   ref_hashed: the bytes the reference itself slides over (rabin.rs:127-188:
+    #     per chunk 63 prefill bytes + (cut - (s + min)); from the cut lists);
+    #   lane_hashed: the bytes our lanes hashed (device work counters: walk
+    #     rounds x 64 x (S + 64) + zones x 64 x 64; the scan: every position
+    #     after the first min of a stream plus 64 B of warm-up per segment).
+    walked = info.get("walk_pieces", 0) > 0
     in_bytes = int(lens.sum())
-    hashed = int(sum(max(int(x) - MIN, 0) for x in lens))
     scan_s = scan_ms / max(runs, 1) / 1e3
     achieved = in_bytes / scan_s / 1e9
-    traffic, pmc = pmc_traffic() if args.workload == "C2" else (None, None)
-    # long streams take the walk path: the first event pair then
-    # brackets the hashing phase, rcdc_scan_kernel (short streams) followed by
-    # rcdc_walk_kernel, and the second one the chain (check/fixup/assemble)
-    walked = info.get("walk_pieces", 0) > 0
+    got_cuts = plan.results() if args.workload != "C5" else [np.asarray(plan.results()[0])]
+    ref_hashed = ref_slide_bytes(got_cuts, MIN)
+    if walked:
+        st = plan.walk_stats()
+        seg = int(os.environ.get("RCDC_WALK_SEG", "2048"))
+        lane_hashed = st["rounds"] * 64 * (seg + 64) + st["zones"] * 64 * 64
+        kernel = "rcdc_walk_kernel"
+    else:
+        st = None
+        lane_hashed = info["scanned_bytes"] + 64 * info["segments"]
+        kernel = "rcdc_scan_kernel"
+    traffic, pmc = pmc_traffic(args.workload, kernel)
     roofline = {
         "bound": "hbm",
-        "kernel": "rcdc_scan_kernel+rcdc_walk_kernel" if walked else "rcdc_scan_kernel",
+        "kernel": kernel,
         "achieved": round(achieved, 1),
         "peak": HBM_PEAK_GBS,
         "unit": "GB/s",
         "frac": round(achieved / HBM_PEAK_GBS, 4),
         "traffic": traffic,
         "algorithmic_bytes_per_launch": in_bytes,
-        "scan_us_per_launch": round(scan_s * 1e6, 2),
+        "basis": "input bytes per launch (SURVEY.md 8(d)); the kernel skips what the reference "
+                 "skips, so hashed-byte rates are reported beside it",
+        "kernel_us_per_launch": round(scan_s * 1e6, 2),
         "timed_launches": runs,
         ("chain_us_per_launch" if walked else "resolve_us_per_launch"):
             round(resolve_ms / max(runs, 1) * 1e3, 2),
-        "hashed_bytes_per_launch": hashed,
-        "achieved_hashed_gbs": round(hashed / scan_s / 1e9, 1),
-        "frac_hashed": round(hashed / scan_s / 1e9 / HBM_PEAK_GBS, 4),
-        "segment_bytes": info["segment_bytes"],
-        "bytes_read_by_lanes": info["scanned_bytes"] + 64 * info["segments"],
-        "limiter": "VALU issue (DESIGN.md 3: ~95% of the measured compute ceiling)",
+        "ref_hashed_bytes_per_launch": ref_hashed,
+        "achieved_ref_hashed_gbs": round(ref_hashed / scan_s / 1e9, 1),
+        "frac_ref_hashed": round(ref_hashed / scan_s / 1e9 / HBM_PEAK_GBS, 4),
+        "lane_hashed_bytes_per_launch": lane_hashed,
+        "achieved_lane_hashed_gbs": round(lane_hashed / scan_s / 1e9, 1),
+        "frac_lane_hashed": round(lane_hashed / scan_s / 1e9 / HBM_PEAK_GBS, 4),
+        "segment_bytes": int(os.environ.get("RCDC_WALK_SEG", "2048")) if walked
+        else info["segment_bytes"],
+        "limiter": "VALU issue (~7 VALU + 2 LDS reads per hashed byte; DESIGN.md 3)",
         "pipelined": pipelined,
     }
+    if st is not None:
+        roofline["walk_work"] = st
     if pmc:
         roofline["traffic_source"] = pmc.get("source")
+    if args.workload == "C5":
+        # zeros: every chunk is decided by its all-zero prefill window; the
+        # kernel reads ~64 B per chunk, so an input-basis "fraction of HBM"
+        # is meaningless (it exceeds 1): report the bytes actually read
+        read = lane_hashed + 64 * int(sum(len(c) for c in got_cuts))
+        roofline.update({
+            "achieved": round(read / scan_s / 1e9, 1),
+            "frac": round(read / scan_s / 1e9 / HBM_PEAK_GBS, 6),
+            "algorithmic_bytes_per_launch": read,
+            "basis": "bytes the walk reads (zone windows + 64-B zero-run prefill windows); "
+                     "input-basis rate beside it",
+            "input_basis_gbs": round(achieved, 1),
+            "limiter": "latency of the zero-run hops (64 chunks per wave step), not bandwidth",
+        })
 
     out_extra = {}
     if rank == 0 and not args.no_parity:
         out_extra["parity"] = parity_check(args, arena, offs, lens, plan, last, desc)
     if rank == 0 and not args.no_cpu_baseline and world == 1:
-        out_extra["cpu_baseline"] = cpu_baseline(arena.cpu().numpy(), offs, lens,
-                                                 args.cpu_seconds)
+        out_extra["cpu_baseline"] = cpu_baseline(arena, offs, lens, args.cpu_seconds)
     if args.sha256:
         out_extra["sha256"] = sha_measure(torch, plan, ptr, sptr, dev, args, arena, offs, lens,
                                           rank == 0 and world == 1 and not args.no_cpu_baseline)

@@ -174,7 +174,9 @@ rcdc_status rcdc_plan_kernel_times(rcdc_plan *plan, uint64_t *runs,
  * (S + 64) bytes hashed by lanes each, S = 2048), [1] its min-zone
  * evaluations (64 windows of 64 bytes), [2] chunks it emitted, [3] 1024-lane
  * rounds of the fixup kernel (1024 x (512 + 64) bytes each), [4] fixup zones,
- * [5] cuts the fixups walked, [6..7] 0.  With the environment variable
+ * [5] cuts the fixups walked, [6] 64-lane rounds of the boundary check
+ * kernel over bytes no walker searched (64 x (S + 64) bytes each), [7] its
+ * zone evaluations.  With the environment variable
  * RCDC_WALK_TRACE=1 at plan creation, `trace` (if not NULL) receives 4
  * words per walk piece: wall clock (100 MHz) at the piece's start and end,
  * rounds, chunks -- at most trace_cap words.  All zero for plans without

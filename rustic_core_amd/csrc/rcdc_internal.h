@@ -138,6 +138,8 @@ constexpr int kWalkStatChunks = 2;     // walk kernel: chunks emitted (incl. zer
 constexpr int kWalkStatFixRounds = 3;  // fixup kernel: 1024-lane rounds
 constexpr int kWalkStatFixZones = 4;   // fixup kernel: zone evaluations
 constexpr int kWalkStatFixCuts = 5;    // fixup kernel: cuts walked
+constexpr int kWalkStatChkRounds = 6;  // check kernel: 64-lane rounds over unsearched gaps
+constexpr int kWalkStatChkZones = 7;   // check kernel: zone evaluations
 constexpr int kWalkStats = 8;
 // trace per unit: wall clock (100 MHz) at start and end, rounds, chunks
 constexpr int kTraceWords = 4;

@@ -654,7 +654,8 @@ rcdc_status plan_results(rcdc_plan *pl, uint64_t *cuts, uint64_t cap, uint64_t *
                 fprintf(stderr, "\n   bound kind %u nhops %u merge %u/%d fix_from %llu hops:", B.kind,
                         B.nhops, B.merge_unit, B.merge_idx, (unsigned long long)B.fix_from);
                 for (uint32_t i = 0; i < B.nhops && i < (uint32_t)kMaxHops; i++)
-                    fprintf(stderr, " %llu", (unsigned long long)B.hops[i]);
+                    fprintf(stderr, " %llu%s", (unsigned long long)(B.hops[i] & kCutVal),
+                            (B.hops[i] >> 62) ? "r" : "");
                 if (B.kind == kBoundFixup) {
                     fprintf(stderr, "\n   fix count %u merge %u/%d:", fr[u].count, fr[u].merge_unit,
                             fr[u].merge_idx);

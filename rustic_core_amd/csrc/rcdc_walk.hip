@@ -35,6 +35,7 @@
 // moves work between the walk and the (rare) fixups.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdio>
 #include <cstdlib>
 
@@ -384,140 +385,363 @@ __global__ __launch_bounds__(1024, 1) void rcdc_walk_kernel(
 }
 
 // ---------------------------------------------------------------------------
-// Check: one wave per unit with piece >= 1 (the boundary at its start).
-__global__ __launch_bounds__(64) void rcdc_walk_check_kernel(
+// Check: one wave per boundary (piece j >= 1 starts at a_j), boundaries pulled
+// from ctr[2]; 16 waves per workgroup share the LDS tables.
+//
+// From the exact chain state at the end of piece j - 1 the wave steps the
+// true chain (rabin.rs:110-191) until one of its cuts lies on a later
+// piece's chain (a piece start or a cut of its list: from there both chains
+// are the same function of the position).  A step needs, for the chunk from
+// c, its zone (zone_wave) and the first pure-window hit >= c + min + 64.
+// What the walkers verified answers most of that: every walked chunk t of
+// any piece searched [prev_t + min + 64, cut_t) hit-free, ending at a hit
+// (kind Hit), at prev_t + max (Max) or at N (Eof), and an open piece
+// searched [c_last + min + 64, stop + min + 64).  These are facts about
+// positions, whichever chain produced them.  Positions nobody hashed (the
+// skipped min-prefix of a piece's own chunks: the true chain is out of phase
+// there) are hashed here, at most min + 64 bytes per gap, with the walk's
+// 64-lane rounds.  Inside a zero run (all-zero prefill: every chunk exactly
+// min) the chain advances 64 chunks per step and records them as one run.
+// A boundary that needs more than kMaxHops entries or kCheckBudget hashed
+// bytes goes on the fixup list.
+constexpr uint64_t kHopRun = 1;  // hop entry kind: cuts prev + min, prev + 2 min, ..., value
+
+struct PieceView {
+    const uint64_t *L;
+    uint64_t n, start, stop;
+    bool open, full;  // full: the list holds every cut the walker found
+};
+
+__device__ __forceinline__ PieceView piece_view(const WalkUnit *units, const uint64_t *pstatus,
+                                                const uint64_t *piece_cuts, uint32_t uk) {
+    const WalkUnit Uk = units[uk];
+    const uint64_t st = pstatus[uk];
+    PieceView V;
+    V.L = piece_cuts + Uk.out_base;
+    V.n = st & 0xFFFFFFFFu;
+    V.start = Uk.start;
+    V.stop = Uk.stop;
+    V.open = (st & kOpenFlag) != 0;
+    V.full = (st & (kOpenFlag << 1)) == 0;
+    return V;
+}
+
+// First index t with cut value >= p (n if none); uniform binary search.
+__device__ __forceinline__ uint64_t lower_cut(const uint64_t *L, uint64_t n, uint64_t p) {
+    uint64_t lo = 0, hi = n;
+    while (lo < hi) {
+        const uint64_t mid = (lo + hi) >> 1;
+        if ((L[mid] & kCutVal) < p) lo = mid + 1;
+        else hi = mid;
+    }
+    return lo;
+}
+
+// What piece V knows about position p: returns true if a searched interval
+// holds p -- [p, *vend) is hit-free, and *vkind says what *vend is (kKindHit:
+// a hit; kKindMax / kOpen: nothing known at *vend; kKindEof: p .. N hit-free);
+// otherwise *next = the start of V's next searched interval after p (~0 if
+// none known).
+__device__ bool cover(const PieceView &V, uint64_t p, uint64_t mn, uint64_t *vend, uint64_t *vkind,
+                      uint64_t *next) {
+    *next = ~0ull;
+    if (!V.full) return false;
+    const uint64_t t = lower_cut(V.L, V.n, p);
+    if (t < V.n) {
+        const uint64_t prev = t ? (V.L[t - 1] & kCutVal) : V.start;
+        const uint64_t base = prev + mn + 64;
+        const uint64_t kd = V.L[t] >> 62, v = V.L[t] & kCutVal;
+        // chunk t searched [base, v) hit-free; v is a hit (Hit), untested
+        // (Max: the reference stops before testing prev + max) or N (Eof)
+        if (kd != kKindZone && base <= p && (p < v || kd == kKindHit)) {
+            *vend = v;
+            *vkind = kd;
+            return true;
+        }
+        // otherwise the next searched interval: chunk t's own (p before it),
+        // or chunk t + 1's, which starts at v (Zone cuts search nothing;
+        // p == v: the untested end of a Max chunk)
+        *next = (kd != kKindZone && p < base) ? base : v + mn + 64;
+        return false;
+    }
+    if (V.open) {
+        const uint64_t base = (V.n ? (V.L[V.n - 1] & kCutVal) : V.start) + mn + 64;
+        const uint64_t oend = V.stop + mn + 64;
+        if (base <= p && p < oend) {
+            *vend = oend;
+            *vkind = kOpen;
+            return true;
+        }
+        if (p < base) *next = base;
+    }
+    return false;
+}
+
+struct CheckCtx {
+    const WalkUnit *units;
+    const uint64_t *pstatus, *piece_cuts;
+    WalkUnit U;   // the boundary's unit (piece j)
+    uint32_t u;   // its index
+    uint64_t N, Lp, mn, mx;
+    uint64_t budget;  // bytes this boundary may still hash
+};
+
+constexpr uint64_t kCheckBudgetMax = 4;  // x max bytes of gap hashing per boundary
+
+// Piece index (within the stream) holding position p.
+__device__ __forceinline__ uint32_t piece_of(const CheckCtx &C, uint64_t p) {
+    return (uint32_t)min(p / C.Lp, (uint64_t)C.U.npieces - 1);
+}
+
+// First pure-window hit in [lo, lim) of the stream, or lim if none;
+// kNoCut if the hashing budget ran out.
+template <int TSH, bool SMALL>
+__device__ uint64_t check_first_hit(Walk &W, CheckCtx &C, uint64_t lo, uint64_t lim) {
+    uint64_t p = lo;
+    // every iteration passes one searched interval or one gap: at most ~2 per
+    // min bytes of [lo, lim); the cap only guarantees termination
+    const uint64_t max_iter = 2 * ((lim - lo) / C.mn) + 16;
+    for (uint64_t it = 0; p < lim; it++) {
+        if (it > max_iter) return kNoCut;  // (never) -> fixup list
+        const uint32_t k = piece_of(C, p);
+        bool known = false;
+        uint64_t gap_end = lim;
+        for (int back = 0; back < 2 && !known; back++) {
+            if (back == 1 && k == 0) break;
+            const PieceView V = piece_view(C.units, C.pstatus, C.piece_cuts, C.U.unit0 + k - back);
+            uint64_t vend, vkind, nxt;
+            if (cover(V, p, C.mn, &vend, &vkind, &nxt)) {
+                if (vkind == kKindHit) return min(vend, lim);
+                if (vkind == kKindEof || lim <= vend) return lim;
+                p = vend;  // Max / open: hit-free below vend, vend itself unknown
+                known = true;
+            } else {
+                gap_end = min(gap_end, nxt);
+            }
+        }
+        if (known) continue;
+        gap_end = max(gap_end, p + 1);
+        // hash [p, gap_end): nobody searched it
+        if (gap_end - p > C.budget) return kNoCut;
+        C.budget -= gap_end - p;
+        uint64_t A = ((W.off + p - 1) & ~63ull) - W.off;
+        while (A < gap_end) {
+            W.rounds++;
+            const uint64_t h = round_first<64, TSH, SMALL>(W, A, p, gap_end);
+            if (h != kNoCut) return h;
+            A += 64ull * W.S;
+        }
+        p = gap_end;
+    }
+    return lim;
+}
+
+// The true chain has a cut at c: does a later piece's chain (unit >= C.u)
+// have one there too?  *mu / *idx: the unit and list index (-1 = its start).
+__device__ __forceinline__ bool merged_at(const CheckCtx &C, uint64_t c, uint32_t *mu, int32_t *idx) {
+    const uint32_t k = piece_of(C, c);
+    for (int back = 0; back < 2; back++) {
+        if (back == 1 && k == 0) break;
+        const uint32_t uk = C.U.unit0 + k - back;
+        if (uk < C.u) break;
+        const PieceView V = piece_view(C.units, C.pstatus, C.piece_cuts, uk);
+        if (back == 0 && c == V.start) {
+            *mu = uk;
+            *idx = -1;
+            return true;
+        }
+        if (!V.full) continue;
+        const uint64_t t = lower_cut(V.L, V.n, c);
+        if (t < V.n && (V.L[t] & kCutVal) == c) {
+            *mu = uk;
+            *idx = (int32_t)t;
+            return true;
+        }
+    }
+    return false;
+}
+
+template <int TSH, bool SMALL>
+__global__ __launch_bounds__(1024, 1) void rcdc_walk_check_kernel(
     const uint8_t *__restrict__ arena, const StreamDesc *__restrict__ sds,
     const WalkUnit *__restrict__ units, WalkParams prm, const uint64_t *__restrict__ gtab,
     const uint64_t *__restrict__ piece_cuts, const uint64_t *__restrict__ pstatus,
     BoundRes *__restrict__ bres, uint32_t *ctr, uint32_t *__restrict__ fixlist) {
-    __shared__ uint64_t s_mod[256];
-    __shared__ uint8_t s_win[128];
-    const uint32_t lane = threadIdx.x;
-    for (uint32_t i = lane; i < 256; i += 64) s_mod[i] = gtab[256 + i];
-    __syncthreads();
-    const uint32_t u = blockIdx.x;
-    if (u >= prm.nunits) return;
-    const WalkUnit U = units[u];
-    if (U.piece == 0) return;
-    const WalkUnit Up = units[u - 1];
-    const StreamDesc d = sds[U.stream];
-    const uint8_t *s = arena + d.off;
-    const uint64_t N = d.n, mn = prm.min_size, mx = prm.max_size;
-    const ModPlain mod{s_mod};
-    BoundRes R;
-    R.kind = kBoundNone;
-    R.nhops = 0;
-    R.merge_unit = u;
-    R.merge_idx = -1;
-    R.fix_from = 0;
-
-    const uint64_t sp = pstatus[u - 1];
-    const uint64_t np = sp & 0xFFFFFFFFu;
-    const bool open_prev = (sp & kOpenFlag) != 0;
-    const uint64_t *Lprev = piece_cuts + Up.out_base;
-    const uint64_t sj = pstatus[u];
-    const uint64_t nj = sj & 0xFFFFFFFFu;
-    const bool open_j = (sj & kOpenFlag) != 0;
-    const uint64_t *L = piece_cuts + U.out_base;
-    const uint64_t aj = U.start;
-    const uint64_t open_end = U.stop + mn + 64;  // open_j: searched hit-free below this
-
-    // Exact state at the previous piece's end (exact if that piece is):
-    // closed at c, or open at c with [c+min+64, aj+min+64) hit-free and no
-    // zone cut in c's zone.
-    uint64_t c;
-    bool pending = false;
-    if (open_prev) {
-        c = np ? (Lprev[np - 1] & kCutVal) : Up.start;
-        pending = true;
-    } else {
-        c = np ? (Lprev[np - 1] & kCutVal) : N;
-    }
-    if (!pending && c >= N) {
-        if (lane == 0) bres[u] = R;  // the stream ended before this piece
-        return;
-    }
-    // region lookup in L: first pure hit >= lo below lim as far as the walker
-    // verified it; kNoCut = unknown.
-    auto region = [&](uint64_t lo, uint64_t lim) -> uint64_t {
-        uint64_t res = kNoCut;
-        bool found = false;
-        for (uint64_t t0 = 0; t0 < nj && !found; t0 += 64) {
-            const uint64_t t = t0 + lane;
-            bool mine = false;
-            uint64_t r = kNoCut;
-            if (t < nj) {
-                const uint64_t prev = t == 0 ? aj : (L[t - 1] & kCutVal);
-                const uint64_t v = L[t] & kCutVal, kd = L[t] >> 62;
-                const uint64_t base = prev + mn + 64;
-                if (kd != kKindZone && base <= lo && lo <= v) {
-                    mine = true;
-                    if (kd == kKindHit) r = min(v, lim);
-                    else if (kd == kKindMax) r = lim <= v ? lim : kNoCut;
-                    else r = lim;  // EOF: hit-free to N >= lim
-                }
-            }
-            const uint64_t b = __builtin_amdgcn_ballot_w64(mine);
-            if (b) {
-                found = true;
-                res = readlane64(r, (uint32_t)__builtin_ctzll(b));
-            }
-        }
-        if (!found && open_j) {
-            const uint64_t base = (nj ? (L[nj - 1] & kCutVal) : aj) + mn + 64;
-            if (base <= lo && lo < open_end && lim <= open_end) res = lim;
-        }
-        return res;
-    };
-
-    for (int step = 0; step <= kMaxHops; step++) {
-        if (!pending) {
-            if (c == aj) {
-                R.kind = kBoundMerged;
-                R.merge_idx = -1;
-                break;
-            }
-            const int64_t at = find_cut(L, nj, c, lane);
-            if (at >= 0) {
-                R.kind = kBoundMerged;
-                R.merge_idx = (int32_t)at;
-                break;
-            }
-            if (step == kMaxHops) {
-                R.kind = kBoundFixup;
-                R.fix_from = c;
-                break;
-            }
-        }
-        uint64_t nxt;
-        if (pending) {
-            pending = false;
-            nxt = region(aj + mn + 64, min(c + mx, N));
-        } else if (N - c <= mn) {
-            nxt = N;
+    __shared__ __attribute__((aligned(16))) uint8_t s_tab[kLdsBytes];
+    __shared__ __attribute__((aligned(16))) uint8_t s_win[16][128];
+    __shared__ uint64_t s_hops[16][kMaxHops];  // the wave's hop entries (uniform values)
+    fill_tables(s_tab, gtab, prm.idx_shift, threadIdx.x, 1024);
+    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+    Walk W;
+    W.arena = arena;
+    W.arena_len = prm.arena_len;
+    W.mn = prm.min_size;
+    W.mx = prm.max_size;
+    W.S = prm.seg_bytes;
+    W.mask = prm.mask;
+    W.shift = prm.shift;
+    W.tab = s_tab;
+    W.k = make_consts(lane, prm.mask, prm.idx_shift);
+    W.win = s_win[wave];
+    W.red = nullptr;
+    W.lane = lane;
+    W.wave = 0;
+    W.tid = lane;
+    const ModRepl mod{s_tab, W.k.lwm};
+    const uint64_t mn = prm.min_size, mx = prm.max_size;
+    for (;;) {
+        uint32_t u = 0;
+        if (lane == 0) u = atomicAdd(&ctr[2], 1u);
+        u = __builtin_amdgcn_readfirstlane(u);
+        if (u >= prm.nunits) break;
+        const WalkUnit U = units[u];
+        if (U.piece == 0) continue;
+        W.rounds = W.zones = 0;
+        const StreamDesc d = sds[U.stream];
+        W.off = d.off;
+        W.N = d.n;
+        const uint8_t *s = arena + d.off;
+        const uint64_t N = d.n;
+        CheckCtx C;
+        C.units = units;
+        C.pstatus = pstatus;
+        C.piece_cuts = piece_cuts;
+        C.U = U;
+        C.u = u;
+        C.N = N;
+        C.Lp = prm.piece_bytes;
+        C.mn = mn;
+        C.mx = mx;
+        C.budget = kCheckBudgetMax * mx;
+        // result (wave-uniform scalars; the hop entries in LDS, not in a
+        // dynamically indexed register array, which would go to scratch)
+        struct {
+            uint32_t kind, nhops, merge_unit;
+            int32_t merge_idx;
+            uint64_t fix_from;
+        } R = {kBoundNone, 0, u, -1, 0};
+        uint64_t *hops = s_hops[wave];
+        // exact state at the previous piece's end: closed at c, or open from c
+        // ([c+min+64, a_j+min+64) hit-free, no zone cut in c's zone)
+        const PieceView Vp = piece_view(units, pstatus, piece_cuts, u - 1);
+        uint64_t c;
+        bool pending = false;
+        if (Vp.open) {
+            c = Vp.n ? (Vp.L[Vp.n - 1] & kCutVal) : Vp.start;
+            pending = true;
         } else {
-            const uint64_t z = c + mn, lim = min(c + mx, N);
-            bool zz;
-            const uint64_t zc = zone_wave(s, N, z, lim, prm.mask, prm.shift, mod, s_win, lane, &zz);
-            if (zc != kNoCut) nxt = zc;
-            else if (lim <= z + 64) nxt = lim;
-            else nxt = region(z + 64, lim);
+            c = Vp.n ? (Vp.L[Vp.n - 1] & kCutVal) : N;
         }
-        if (nxt == kNoCut) {
-            R.kind = kBoundFixup;
+        if (!Vp.full) {
+            R.kind = kBoundFixup;  // (never: lists are sized for every cut)
             R.fix_from = c;
-            break;
+        } else if (!pending && c >= N) {
+            // the stream ended before this piece: kBoundNone
+        } else {
+            for (;;) {
+                if (!pending) {
+                    uint32_t mu;
+                    int32_t mi;
+                    if (merged_at(C, c, &mu, &mi)) {
+                        R.kind = kBoundMerged;
+                        R.merge_unit = mu;
+                        R.merge_idx = mi;
+                        break;
+                    }
+                    if (R.nhops >= (uint32_t)kMaxHops) {
+                        R.kind = kBoundFixup;
+                        R.fix_from = c;
+                        break;
+                    }
+                }
+                uint64_t nxt = kNoCut, lo = 0;
+                const uint64_t lim = min(c + mx, N);
+                bool zz = false;
+                if (pending) {
+                    pending = false;
+                    lo = U.start + mn + 64;
+                } else if (N - c <= mn) {
+                    nxt = N;
+                } else {
+                    const uint64_t z = c + mn;
+                    W.zones++;
+                    const uint64_t zc = zone_wave(s, N, z, lim, prm.mask, prm.shift, mod, W.win,
+                                                  lane, &zz);
+                    if (zc != kNoCut) nxt = zc;
+                    else if (lim <= z + 64) nxt = lim;
+                    else lo = z + 64;
+                }
+                if (lo) nxt = check_first_hit<TSH, SMALL>(W, C, lo, lim);
+                if (nxt == kNoCut) {
+                    R.kind = kBoundFixup;
+                    R.fix_from = c;
+                    break;
+                }
+                hops[R.nhops++] = nxt;
+                c = nxt;
+                if (c >= N) {
+                    R.kind = kBoundEnd;
+                    break;
+                }
+                // inside a zero run: 64 min-sized chunks per step, the first
+                // one on a later piece's chain ends the boundary
+                bool done = false;
+                while (zz && c < N) {
+                    uint32_t mu0;
+                    int32_t mi0;
+                    if (merged_at(C, c, &mu0, &mi0)) break;  // the loop top merges
+                    const uint32_t m = zero_run(s, N, mn, mx, c, lane);
+                    if (m == 0) break;
+                    const uint64_t cut = c + (uint64_t)(lane + 1) * mn;
+                    uint32_t mu = kNoUnit;
+                    int32_t mi = -1;
+                    const bool on = lane < m && merged_at(C, cut, &mu, &mi);
+                    const uint64_t hit = __builtin_amdgcn_ballot_w64(on);
+                    const uint32_t f = hit ? (uint32_t)__builtin_ctzll(hit) : m - 1;
+                    const uint64_t end = c + (uint64_t)(f + 1) * mn;
+                    // record c+min .. end as one run entry (extending a run
+                    // just before it)
+                    if (R.nhops > 0 && (hops[R.nhops - 1] >> 62) == kHopRun) {
+                        hops[R.nhops - 1] = end | (kHopRun << 62);
+                    } else if (R.nhops < (uint32_t)kMaxHops) {
+                        hops[R.nhops++] = end | (kHopRun << 62);
+                    } else {
+                        R.kind = kBoundFixup;
+                        R.fix_from = c;
+                        done = true;
+                        break;
+                    }
+                    c = end;
+                    if (hit) {
+                        R.kind = kBoundMerged;
+                        R.merge_unit = (uint32_t)__builtin_amdgcn_readlane(mu, f);
+                        R.merge_idx = (int32_t)__builtin_amdgcn_readlane((uint32_t)mi, f);
+                        done = true;
+                        break;
+                    }
+                    if (c >= N) {
+                        R.kind = kBoundEnd;
+                        done = true;
+                        break;
+                    }
+                    if (m < 64) break;
+                }
+                if (done) break;
+            }
         }
-        R.hops[R.nhops++] = nxt;
-        c = nxt;
-        if (c >= N) {
-            R.kind = kBoundEnd;
-            break;
+        wave_sync();
+        BoundRes *B = bres + u;
+        if (lane < R.nhops) B->hops[lane] = hops[lane];
+        if (lane == 0) {
+            B->kind = R.kind;
+            B->nhops = R.nhops;
+            B->merge_unit = R.merge_unit;
+            B->merge_idx = R.merge_idx;
+            B->fix_from = R.fix_from;
+            if (R.kind == kBoundFixup) fixlist[atomicAdd(&ctr[1], 1u)] = u;
+            atomicAdd(&prm.stats[kWalkStatChkRounds], (unsigned long long)W.rounds);
+            atomicAdd(&prm.stats[kWalkStatChkZones], (unsigned long long)W.zones);
         }
-    }
-    if (lane == 0) {
-        bres[u] = R;
-        if (R.kind == kBoundFixup) fixlist[atomicAdd(&ctr[1], 1u)] = u;
     }
 }
 
@@ -719,7 +943,17 @@ __global__ __launch_bounds__(kAsmB) void rcdc_walk_assemble_kernel(
                 }
             }
         }
-        const uint64_t len = nbad ? 0 : nh + fc + (tail_hi - tail_lo);
+        // hop entries: single cuts, or runs of min-sized chunks (kHopRun)
+        uint64_t nhc = 0;
+        if (valid) {
+            uint64_t pv = 0;
+            for (uint32_t i = 0; i < nh; i++) {
+                const uint64_t e = bres[u].hops[i], v = e & kCutVal;
+                nhc += (e >> 62) == kHopRun ? (v - pv) / prm.min_size : 1;
+                pv = v;
+            }
+        }
+        const uint64_t len = nbad ? 0 : nhc + fc + (tail_hi - tail_lo);
         s_next[tid] = nxt;
         s_term[tid] = term;
         const uint64_t ns = __builtin_amdgcn_ballot_w64(!(valid && !term && nxt == j + 1));
@@ -791,8 +1025,18 @@ __global__ __launch_bounds__(kAsmB) void rcdc_walk_assemble_kernel(
         }
         if (on) {
             uint64_t o = nc + base + v - len;
-            for (uint32_t i = 0; i < nh; i++, o++)
-                if (o < cap) out[o] = bres[u].hops[i];
+            uint64_t pv = 0;
+            for (uint32_t i = 0; i < nh; i++) {
+                const uint64_t e = bres[u].hops[i], v = e & kCutVal;
+                if ((e >> 62) == kHopRun) {
+                    for (uint64_t x = pv + prm.min_size; x <= v; x += prm.min_size, o++)
+                        if (o < cap) out[o] = x;
+                } else {
+                    if (o < cap) out[o] = v;
+                    o++;
+                }
+                pv = v;
+            }
             const uint64_t *fsrc = fix_cuts + (uint64_t)u * prm.fix_cap;
             for (uint32_t i = 0; i < fc; i++, o++)
                 if (o < cap) out[o] = fsrc[i];
@@ -844,15 +1088,21 @@ hipError_t launch_walk_chain(const uint8_t *arena, const StreamDesc *sds, const 
                              uint32_t fix_blocks, hipStream_t stream) {
     if (prm.nunits == 0) return hipSuccess;
     static const bool dbg = getenv("RCDC_DEBUG_SYNC") != nullptr;
-    hipLaunchKernelGGL(rcdc_walk_check_kernel, dim3(prm.nunits), dim3(64), 0, stream, arena, sds,
-                       units, prm, gtab, piece_cuts, pstatus, bres, ctr, fixlist);
+    const bool small = prm.mask < 0xFFFFu;
+    const uint32_t chk_blocks = std::min<uint32_t>(fix_blocks, (prm.nunits + 15) / 16);
+#define RCDC_CHK_LAUNCH(TSH, SM)                                                                   \
+    hipLaunchKernelGGL((rcdc_walk_check_kernel<TSH, SM>), dim3(chk_blocks), dim3(1024), 0, stream, \
+                       arena, sds, units, prm, gtab, piece_cuts, pstatus, bres, ctr, fixlist)
+    if (prm.idx_shift == 21 && !small) RCDC_CHK_LAUNCH(105, false);
+    else if (small) RCDC_CHK_LAUNCH(-1, true);
+    else RCDC_CHK_LAUNCH(-1, false);
+#undef RCDC_CHK_LAUNCH
     if (dbg) {
         (void)hipStreamSynchronize(stream);
         uint32_t h[4];
         (void)hipMemcpy(h, ctr, 16, hipMemcpyDeviceToHost);
         fprintf(stderr, "rcdc: check done, %u fixups\n", h[1]);
     }
-    const bool small = prm.mask < 0xFFFFu;
 #define RCDC_FIX_LAUNCH(TSH, SM)                                                                   \
     hipLaunchKernelGGL((rcdc_walk_fixup_kernel<TSH, SM>), dim3(fix_blocks), dim3(1024), 0, stream, \
                        arena, sds, units, prm, gtab, piece_cuts, pstatus, bres, ctr, fixlist,      \

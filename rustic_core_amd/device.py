@@ -129,7 +129,8 @@ class DevicePlan:
             raise status_error(st, _lib.last_error())
         return n.value, a.value, b.value
 
-    WALK_STAT_NAMES = ("rounds", "zones", "chunks", "fix_rounds", "fix_zones", "fix_cuts")
+    WALK_STAT_NAMES = ("rounds", "zones", "chunks", "fix_rounds", "fix_zones", "fix_cuts",
+                       "chk_rounds", "chk_zones")
 
     def walk_stats(self, trace: bool = False):
         """Work counters of the last run's walk path (rcdc_plan_walk_stats):
