@@ -116,7 +116,7 @@ static_assert(sizeof(WalkUnit) == 48, "WalkUnit is 48 B");
 struct WalkParams {
     uint64_t min_size, max_size;
     uint64_t arena_len;
-    uint64_t piece_bytes;  // Lp: piece j starts at j * Lp
+    uint64_t piece_bytes;  // Lp: the (big) piece size; the last ones of a stream are smaller
     uint32_t seg_bytes;    // S: bytes per lane per round
     uint32_t mask;         // avg - 1
     uint32_t idx_shift;    // deg - 32
@@ -129,6 +129,8 @@ struct WalkParams {
     unsigned long long *stats;
     // optional per-piece trace (nullptr = off): kTraceWords u64 per unit
     unsigned long long *trace;
+    // queue order of the walk kernel: the q-th piece handed out is order[q]
+    const uint32_t *order;
 };
 
 // WalkParams.stats slots

@@ -149,11 +149,13 @@ struct rcdc_plan {
     bool no_walk = false;             // force the scan path (fallback re-runs)
     std::vector<WalkUnit> wunits;
     std::vector<uint32_t> wstream_u0;  // unit0 of every walked stream
+    std::vector<uint32_t> worder;      // walk queue order (big pieces first)
     std::vector<uint8_t> walked;       // per stream: on the walk path
     uint64_t nwpiece_cuts = 0;
     WalkParams wprm{};
     WalkUnit *d_wunits = nullptr;
     uint32_t *d_wsu0 = nullptr;
+    uint32_t *d_worder = nullptr;
     uint64_t *d_wpiece = nullptr;
     uint64_t *d_pstatus = nullptr;
     BoundRes *d_bres = nullptr;
@@ -164,6 +166,7 @@ struct rcdc_plan {
     unsigned long long *d_wstats = nullptr;  // kWalkStats work counters of the last run
     unsigned long long *d_wtrace = nullptr;  // per-unit trace (RCDC_WALK_TRACE=1)
     uint64_t cap_wstats = 0, cap_wtrace = 0;
+    uint64_t cap_worder = 0;
     uint64_t cap_wunits = 0, cap_wsu0 = 0, cap_wpiece = 0, cap_pstatus = 0, cap_bres = 0,
              cap_ctr = 0, cap_fixlist = 0, cap_fixcuts = 0, cap_fixres = 0;
     const void *last_arena = nullptr;  // of the last run (fallback re-runs)
@@ -434,31 +437,56 @@ rcdc_status plan_build(rcdc_ctx *ctx, rcdc_plan *pl, const uint64_t *offs, const
     pl->nseg = nseg;
     pl->ncuts = ncut;
     build_resolve_units(pl, ctx->min);
-    // walk units: pieces [j Lp, (j+1) Lp) of every walked stream, the last
-    // one to N (between Lp and 2 Lp)
+    // walk units: pieces of Lp bytes of every walked stream (the last one to
+    // N), except that the last RCDC_WALK_SPLIT % (default 20) of a stream's
+    // pieces are cut into pieces of Ls = Lp / 4 (a multiple of min).  Units
+    // stay in stream order (the chain kernels need that); the walk kernel's
+    // queue hands out all big pieces first and the small ones last, so the
+    // last pieces the waves take are short and the grid drains evenly.
     pl->wunits.clear();
     pl->wstream_u0.clear();
+    pl->worder.clear();
     pl->nwpiece_cuts = 0;
-    for (uint32_t i = 0; i < n && Lp; i++) {
-        if (!pl->walked[i]) continue;
-        const uint64_t N = lens[i];
-        const uint32_t P = (uint32_t)std::max<uint64_t>(N / Lp, 1);
-        const uint32_t u0 = (uint32_t)pl->wunits.size();
-        pl->wstream_u0.push_back(u0);
-        for (uint32_t j = 0; j < P; j++) {
-            WalkUnit u{};
-            u.start = (uint64_t)j * Lp;
-            u.stop = j + 1 < P ? (uint64_t)(j + 1) * Lp : N;
-            u.out_base = pl->nwpiece_cuts;
-            // cuts in [start, first cut >= stop]: >= min apart, plus the crossing and EOF cuts
-            u.out_cap = (uint32_t)((u.stop - u.start) / ctx->min + ctx->max / ctx->min + 4);
-            u.stream = i;
-            u.piece = j;
-            u.unit0 = u0;
-            u.npieces = P;
-            pl->nwpiece_cuts += u.out_cap;
-            pl->wunits.push_back(u);
+    {
+        uint64_t split_pct = 20;
+        if (const char *e = getenv("RCDC_WALK_SPLIT")) split_pct = std::min<uint64_t>(atoll(e), 100);
+        const uint64_t Ls = Lp ? std::max<uint64_t>(Lp / 4 / ctx->min, 1) * ctx->min : 0;
+        std::vector<uint32_t> small;
+        for (uint32_t i = 0; i < n && Lp; i++) {
+            if (!pl->walked[i]) continue;
+            const uint64_t N = lens[i];
+            const uint64_t P = std::max<uint64_t>(N / Lp, 1);
+            const uint64_t nsplit = Ls < Lp ? (P * split_pct + 50) / 100 : 0;
+            const uint32_t u0 = (uint32_t)pl->wunits.size();
+            pl->wstream_u0.push_back(u0);
+            uint32_t j = 0;
+            auto add = [&](uint64_t a, uint64_t e, bool is_small) {
+                WalkUnit u{};
+                u.start = a;
+                u.stop = e;
+                u.out_base = pl->nwpiece_cuts;
+                // cuts in [start, first cut >= stop]: >= min apart, plus the crossing and EOF cuts
+                u.out_cap = (uint32_t)((e - a) / ctx->min + ctx->max / ctx->min + 4);
+                u.stream = i;
+                u.piece = j++;
+                u.unit0 = u0;
+                pl->nwpiece_cuts += u.out_cap;
+                (is_small ? small : pl->worder).push_back((uint32_t)pl->wunits.size());
+                pl->wunits.push_back(u);
+            };
+            for (uint64_t b = 0; b < P; b++) {
+                const uint64_t a = b * Lp, e = b + 1 < P ? (b + 1) * Lp : N;
+                if (b + nsplit < P) {
+                    add(a, e, false);
+                } else {
+                    const uint64_t q = std::max<uint64_t>((e - a) / Ls, 1);
+                    for (uint64_t k = 0; k < q; k++)
+                        add(a + k * Ls, k + 1 < q ? a + (k + 1) * Ls : e, true);
+                }
+            }
+            for (uint32_t k = u0; k < (uint32_t)pl->wunits.size(); k++) pl->wunits[k].npieces = j;
         }
+        pl->worder.insert(pl->worder.end(), small.begin(), small.end());
     }
     WalkParams &wp = pl->wprm;
     wp = WalkParams{};
@@ -498,6 +526,10 @@ rcdc_status plan_build(rcdc_ctx *ctx, rcdc_plan *pl, const uint64_t *offs, const
     if (nw) {
         if ((st = ensure_dev(&pl->d_wunits, &pl->cap_wunits, nw))) return st;
         if ((st = ensure_dev(&pl->d_wsu0, &pl->cap_wsu0, pl->wstream_u0.size()))) return st;
+        if ((st = ensure_dev(&pl->d_worder, &pl->cap_worder, nw))) return st;
+        pl->wprm.order = pl->d_worder;
+        HIP_TRY(hipMemcpy(pl->d_worder, pl->worder.data(), nw * sizeof(uint32_t),
+                          hipMemcpyHostToDevice));
         if ((st = ensure_dev(&pl->d_wpiece, &pl->cap_wpiece, pl->nwpiece_cuts))) return st;
         if ((st = ensure_dev(&pl->d_pstatus, &pl->cap_pstatus, nw))) return st;
         if ((st = ensure_dev(&pl->d_bres, &pl->cap_bres, nw))) return st;
@@ -575,7 +607,9 @@ rcdc_status plan_run(rcdc_plan *pl, const void *d_arena, hipStream_t stream) {
                         (uint32_t)std::min<uint64_t>(cus, (pl->wunits.size() + 15) / 16), stream));
     if (dbg) {
         HIP_TRY(hipStreamSynchronize(stream));
-        fprintf(stderr, "rcdc: walk done (%zu units)\n", pl->wunits.size());
+        uint32_t h[4] = {0, 0, 0, 0};
+        if (!pl->wunits.empty()) HIP_TRY(hipMemcpy(h, pl->d_ctr, 16, hipMemcpyDeviceToHost));
+        fprintf(stderr, "rcdc: walk done (%zu units; queue %u)\n", pl->wunits.size(), h[0]);
     }
     if (ev) HIP_TRY(hipEventRecord(ev[1], stream));
     const hipStream_t scan_stream = stream;
@@ -713,6 +747,7 @@ void plan_release(rcdc_plan *pl) {
     DeviceGuard g(pl->ctx ? pl->ctx->device : 0);
     (void)hipFree(pl->d_wunits);
     (void)hipFree(pl->d_wsu0);
+    (void)hipFree(pl->d_worder);
     (void)hipFree(pl->d_wpiece);
     (void)hipFree(pl->d_pstatus);
     (void)hipFree(pl->d_bres);

@@ -326,10 +326,11 @@ __global__ __launch_bounds__(1024, 1) void rcdc_walk_kernel(
     W.wave = 0;  // a wave walker: lane t of the round is t
     W.tid = lane;
     for (;;) {
-        uint32_t u = 0;
-        if (lane == 0) u = atomicAdd(&ctr[0], 1u);
-        u = __builtin_amdgcn_readfirstlane(u);
-        if (u >= prm.nunits) break;
+        uint32_t q = 0;
+        if (lane == 0) q = atomicAdd(&ctr[0], 1u);
+        q = __builtin_amdgcn_readfirstlane(q);
+        if (q >= prm.nunits) break;
+        const uint32_t u = __builtin_amdgcn_readfirstlane(prm.order[q]);
         const uint64_t t0 = prm.trace ? (uint64_t)wall_clock64() : 0;
         W.rounds = W.zones = 0;
         const WalkUnit U = units[u];
@@ -482,15 +483,27 @@ struct CheckCtx {
     const uint64_t *pstatus, *piece_cuts;
     WalkUnit U;   // the boundary's unit (piece j)
     uint32_t u;   // its index
-    uint64_t N, Lp, mn, mx;
+    uint64_t N, mn, mx;
     uint64_t budget;  // bytes this boundary may still hash
 };
 
 constexpr uint64_t kCheckBudgetMax = 4;  // x max bytes of gap hashing per boundary
 
-// Piece index (within the stream) holding position p.
+// Piece index k (within the stream of unit0, npieces pieces) holding
+// position p: the last piece with start <= p (pieces differ in size).
+__device__ __forceinline__ uint32_t piece_at(const WalkUnit *units, uint32_t unit0,
+                                             uint32_t npieces, uint64_t p) {
+    uint32_t lo = 0, hi = npieces - 1;
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi + 1) >> 1;
+        if (units[unit0 + mid].start <= p) lo = mid;
+        else hi = mid - 1;
+    }
+    return lo;
+}
+
 __device__ __forceinline__ uint32_t piece_of(const CheckCtx &C, uint64_t p) {
-    return (uint32_t)min(p / C.Lp, (uint64_t)C.U.npieces - 1);
+    return piece_at(C.units, C.U.unit0, C.U.npieces, p);
 }
 
 // First pure-window hit in [lo, lim) of the stream, or lim if none;
@@ -561,16 +574,18 @@ __device__ __forceinline__ bool merged_at(const CheckCtx &C, uint64_t c, uint32_
     return false;
 }
 
+constexpr int kChkThreads = 512;  // 8 waves: 256 VGPRs per lane, the gap search spill-free
+
 template <int TSH, bool SMALL>
-__global__ __launch_bounds__(1024, 1) void rcdc_walk_check_kernel(
+__global__ __launch_bounds__(kChkThreads, 1) void rcdc_walk_check_kernel(
     const uint8_t *__restrict__ arena, const StreamDesc *__restrict__ sds,
     const WalkUnit *__restrict__ units, WalkParams prm, const uint64_t *__restrict__ gtab,
     const uint64_t *__restrict__ piece_cuts, const uint64_t *__restrict__ pstatus,
     BoundRes *__restrict__ bres, uint32_t *ctr, uint32_t *__restrict__ fixlist) {
     __shared__ __attribute__((aligned(16))) uint8_t s_tab[kLdsBytes];
-    __shared__ __attribute__((aligned(16))) uint8_t s_win[16][128];
-    __shared__ uint64_t s_hops[16][kMaxHops];  // the wave's hop entries (uniform values)
-    fill_tables(s_tab, gtab, prm.idx_shift, threadIdx.x, 1024);
+    __shared__ __attribute__((aligned(16))) uint8_t s_win[kChkThreads / 64][128];
+    __shared__ uint64_t s_hops[kChkThreads / 64][kMaxHops];  // the wave's hop entries
+    fill_tables(s_tab, gtab, prm.idx_shift, threadIdx.x, kChkThreads);
     const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
     Walk W;
     W.arena = arena;
@@ -609,7 +624,6 @@ __global__ __launch_bounds__(1024, 1) void rcdc_walk_check_kernel(
         C.U = U;
         C.u = u;
         C.N = N;
-        C.Lp = prm.piece_bytes;
         C.mn = mn;
         C.mx = mx;
         C.budget = kCheckBudgetMax * mx;
@@ -811,7 +825,7 @@ __global__ __launch_bounds__(1024, 1) void rcdc_walk_fixup_kernel(
                     if (cut >= d.n) {
                         stop = true;
                     } else {
-                        const uint64_t k = min(cut / prm.piece_bytes, (uint64_t)U.npieces - 1);
+                        const uint64_t k = piece_at(units, U.unit0, U.npieces, cut);
                         for (int back = 0; back < 2 && mu == kNoUnit; back++) {
                             if (back == 1 && k == 0) break;
                             const uint32_t uk = U.unit0 + (uint32_t)(k - back);
@@ -919,7 +933,7 @@ __global__ __launch_bounds__(kAsmB) void rcdc_walk_assemble_kernel(
         if (valid) {
             const uint32_t kind = bres[u].kind;
             if (kind != kBoundNone) {
-                nh = bres[u].nhops;
+                nh = min(bres[u].nhops, (uint32_t)kMaxHops);
                 if (kind == kBoundMerged || kind == kBoundFixup) {
                     int32_t mi = bres[u].merge_idx;
                     mu = bres[u].merge_unit;
@@ -1029,8 +1043,8 @@ __global__ __launch_bounds__(kAsmB) void rcdc_walk_assemble_kernel(
             for (uint32_t i = 0; i < nh; i++) {
                 const uint64_t e = bres[u].hops[i], v = e & kCutVal;
                 if ((e >> 62) == kHopRun) {
-                    for (uint64_t x = pv + prm.min_size; x <= v; x += prm.min_size, o++)
-                        if (o < cap) out[o] = x;
+                    for (uint64_t x = pv + prm.min_size; x <= v && o < cap; x += prm.min_size, o++)
+                        out[o] = x;
                 } else {
                     if (o < cap) out[o] = v;
                     o++;
@@ -1089,9 +1103,10 @@ hipError_t launch_walk_chain(const uint8_t *arena, const StreamDesc *sds, const 
     if (prm.nunits == 0) return hipSuccess;
     static const bool dbg = getenv("RCDC_DEBUG_SYNC") != nullptr;
     const bool small = prm.mask < 0xFFFFu;
-    const uint32_t chk_blocks = std::min<uint32_t>(fix_blocks, (prm.nunits + 15) / 16);
+    const uint32_t chk_blocks = std::min<uint32_t>(fix_blocks, (prm.nunits + 7) / 8);
 #define RCDC_CHK_LAUNCH(TSH, SM)                                                                   \
-    hipLaunchKernelGGL((rcdc_walk_check_kernel<TSH, SM>), dim3(chk_blocks), dim3(1024), 0, stream, \
+    hipLaunchKernelGGL((rcdc_walk_check_kernel<TSH, SM>), dim3(chk_blocks), dim3(kChkThreads), 0,  \
+                       stream,                                                                     \
                        arena, sds, units, prm, gtab, piece_cuts, pstatus, bres, ctr, fixlist)
     if (prm.idx_shift == 21 && !small) RCDC_CHK_LAUNCH(105, false);
     else if (small) RCDC_CHK_LAUNCH(-1, true);

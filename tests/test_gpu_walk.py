@@ -169,7 +169,8 @@ def test_walk_selected_by_default_for_large_batches():
     g.manual_seed(90)
     arena = torch.randint(0, 256, (alen,), dtype=torch.uint8, device="cuda:0", generator=g)
     plan = DevicePlan(ctx, offs, lens, alen)
-    assert plan.info()["walk_pieces"] == 1024
+    # 16 pieces of 4 MiB per stream; the last 20 % (3) cut into 4 each
+    assert plan.info()["walk_pieces"] == 64 * (13 + 3 * 4)
     plan.run(arena.data_ptr())
     got = plan.results()
     plan.close()
