@@ -81,6 +81,11 @@ def parse():
                          "measured slower on C2: the resolve waves starve behind the scan)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-parity", action="store_true")
+    ap.add_argument("--abi-e2e", action="store_true",
+                    help="also measure the drop-in C ABI path (rcdc_stream_feed from pageable host "
+                         "memory, --abi-threads workers) on the workload's first --abi-files streams")
+    ap.add_argument("--abi-threads", type=int, default=16)
+    ap.add_argument("--abi-files", type=int, default=16)
     ap.add_argument("--e2e", action="store_true",
                     help="also measure the PCIe-inclusive rate (pinned H2D + chunk + D2H cuts)")
     return ap.parse_args()
@@ -89,19 +94,28 @@ def parse():
 # ----------------------------------------------------------------- workloads
 def make_mixed(torch, arena, off, length, rng, dev):
     """C3 stream: random runs 64 KiB-16 MiB and zero runs 4 KiB-16 MiB
-    (log-uniform lengths), each kind with probability 1/2."""
-    pos = 0
+    (log-uniform lengths), each kind with probability 1/2.  The run layout is
+    drawn on the host; the bytes come from one randint and one masked fill
+    (a handful of launches per stream, so profilers see few foreign kernels)."""
     g = torch.Generator(device=dev)
     g.manual_seed(int(rng.integers(1 << 62)))
+    pos, zero, lens = 0, [], []
     while pos < length:
         if rng.random() < 0.5:
             L = min(int(np.exp(rng.uniform(np.log(64 << 10), np.log(16 << 20)))), length - pos)
-            arena[off + pos:off + pos + L] = torch.randint(0, 256, (L,), dtype=torch.uint8,
-                                                           device=dev, generator=g)
+            zero.append(False)
         else:
             L = min(int(np.exp(rng.uniform(np.log(4 << 10), np.log(16 << 20)))), length - pos)
-            arena[off + pos:off + pos + L] = 0
+            zero.append(True)
+        lens.append(L)
         pos += L
+    view = arena[off:off + length]
+    torch.randint(0, 256, (length,), dtype=torch.uint8, device=dev, generator=g, out=view)
+    mask = torch.repeat_interleave(torch.tensor(zero, device=dev),
+                                   torch.tensor(lens, dtype=torch.int64, device=dev),
+                                   output_size=length)
+    view.masked_fill_(mask, 0)
+    del mask
 
 
 def build_workload(args, torch, dev, rank, world):
@@ -148,6 +162,105 @@ def build_workload(args, torch, dev, rank, world):
                 "stream_bytes_total": total, "slice": [a, b, e],
                 "data": "synthetic: zeros on device"}
     return arena, offs, lens, desc
+
+
+# ------------------------------------------------------------------ StdRng
+def stdrng_numpy(seed: int, n: int) -> np.ndarray:
+    """rand 0.10 StdRng::seed_from_u64(seed).fill_bytes(n) (SURVEY.md
+    Appendix B: PCG32 seed expansion, ChaCha12 keystream), vectorised over
+    64-byte blocks.  Input generator for C1 (the reference's own test data
+    recipe, rabin.rs:343-347); tests/test_bench_host.py pins it to the oracle."""
+    def rotl(x, k):
+        return ((x << np.uint32(k)) | (x >> np.uint32(32 - k))).astype(np.uint32)
+    MUL, INC = 6364136223846793005, 11634580027462260723
+    state, key = seed & (2**64 - 1), []
+    for _ in range(8):
+        state = (state * MUL + INC) & (2**64 - 1)
+        xs = ((((state >> 18) ^ state) >> 27) & 0xFFFFFFFF)
+        rot = state >> 59
+        key.append(((xs >> rot) | (xs << ((32 - rot) & 31))) & 0xFFFFFFFF)
+    nb = (n + 63) // 64
+    ctr = np.arange(nb, dtype=np.uint64)
+    x0 = [np.full(nb, c, np.uint32) for c in (0x61707865, 0x3320646E, 0x79622D32, 0x6B206574)]
+    x0 += [np.full(nb, k, np.uint32) for k in key]
+    x0 += [(ctr & 0xFFFFFFFF).astype(np.uint32), (ctr >> np.uint64(32)).astype(np.uint32),
+           np.zeros(nb, np.uint32), np.zeros(nb, np.uint32)]
+    x = [v.copy() for v in x0]
+
+    def qr(a, b, c, d):
+        x[a] += x[b]; x[d] = rotl(x[d] ^ x[a], 16)
+        x[c] += x[d]; x[b] = rotl(x[b] ^ x[c], 12)
+        x[a] += x[b]; x[d] = rotl(x[d] ^ x[a], 8)
+        x[c] += x[d]; x[b] = rotl(x[b] ^ x[c], 7)
+    for _ in range(6):
+        qr(0, 4, 8, 12); qr(1, 5, 9, 13); qr(2, 6, 10, 14); qr(3, 7, 11, 15)
+        qr(0, 5, 10, 15); qr(1, 6, 11, 12); qr(2, 7, 8, 13); qr(3, 4, 9, 14)
+    out = np.stack([x[i] + x0[i] for i in range(16)], axis=1).astype("<u4")
+    return out.view(np.uint8).reshape(-1)[:n]
+
+
+def pcie_rates(torch, dev, nbytes: int = 1 << 30) -> dict:
+    """Host->device copy rates on this box: pinned and pageable sources."""
+    d = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+    out = {}
+    for kind in ("pinned", "pageable"):
+        h = torch.empty(nbytes, dtype=torch.uint8, pin_memory=(kind == "pinned"))
+        h.fill_(1)
+        d.copy_(h, non_blocking=True)
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for _ in range(3):
+            d.copy_(h, non_blocking=True)
+        torch.cuda.synchronize(dev)
+        out[f"h2d_{kind}_gibs"] = round(3 * nbytes / (time.perf_counter() - t0) / GiB, 2)
+        del h
+    return out
+
+
+def abi_e2e(files, threads: int, read_bytes: int = 16 << 20) -> dict:
+    """The drop-in path under the caller's load: `threads` workers, one file
+    each at a time (archiver.rs:195), each fed to rcdc_stream_feed in
+    `read_bytes` reads from pageable host memory (ChunkIter's plumbing,
+    chunker.rs:22-47 over a Read).  Returns the aggregate GiB/s and the cut
+    lists (for the parity check)."""
+    import threading
+    from rustic_core_amd.chunker import Context, _Stream
+    ctx = Context.get(POLY, MIN, AVG, MAX)
+    nxt = [0]
+    lock = threading.Lock()
+    cuts = [None] * len(files)
+
+    def work():
+        while True:
+            with lock:
+                i = nxt[0]
+                nxt[0] += 1
+            if i >= len(files):
+                return
+            f = files[i]
+            st = _Stream(ctx)
+            out = []
+            for o in range(0, max(f.size, 1), read_bytes):
+                piece = f[o:o + read_bytes]
+                out.append(st.feed(piece, o + read_bytes >= f.size))
+            st.close()
+            cuts[i] = np.concatenate(out) if out else np.zeros(0, np.uint64)
+
+    work_warm = _Stream(ctx)  # lanes and plans warm up outside the timed span
+    work_warm.feed(files[0][:64 << 20], True)
+    work_warm.close()
+    t0 = time.perf_counter()
+    th = [threading.Thread(target=work) for _ in range(threads)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    el = time.perf_counter() - t0
+    total = sum(int(f.size) for f in files)
+    return {"value": round(total / el / GiB, 2), "unit": "GiB/s", "threads": threads,
+            "files": len(files), "bytes": total, "read_bytes": read_bytes,
+            "path": "rcdc_stream_feed (C ABI) from pageable host memory, one stream per file, "
+                    "files on worker threads sharing one rcdc_ctx"}, cuts
 
 
 # ------------------------------------------------------------- baselines etc.
@@ -242,15 +355,16 @@ def pmc_traffic(workload: str, kernel: str):
 
 def ref_slide_bytes(cuts_list, mn: int) -> int:
     """Bytes the reference slides over for these chunks (rabin.rs:127-188):
-    a chunk longer than min costs 63 prefill bytes (:149-151) plus one slide
-    per byte after s + min; the short final chunk (<= min) costs none."""
+    a chunk of at least min bytes costs 63 prefill bytes (:149-151) plus one
+    slide per byte after s + min; a final chunk shorter than min costs none
+    (:141-147)."""
     tot = 0
     for c in cuts_list:
         c = np.asarray(c, dtype=np.int64)
         if c.size == 0:
             continue
         L = np.diff(np.concatenate([[0], c]))
-        full = L > mn
+        full = L >= mn
         tot += int(np.sum(L[full] - mn)) + 63 * int(np.count_nonzero(full))
     return tot
 
@@ -349,7 +463,7 @@ def run_c4(args, torch, dist, dev, rank, world, local):
                     if f in sample and not args.no_parity:
                         o = int(offs[i])
                         sample_cuts[f] = (got[i], arena[o:o + sizes[f]].cpu().numpy())
-    t = torch.tensor([el], dtype=torch.float64, device=dev)
+    t = torch.tensor([el], dtype=torch.float64, device=coll_device(dev))
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     el_max = float(t.item())
@@ -360,7 +474,7 @@ def run_c4(args, torch, dist, dev, rank, world, local):
     for f, (cuts, host) in sample_cuts.items():
         from oracle import oracle
         bad += not np.array_equal(cuts, oracle.chunk_cuts(host, POLY, MIN, AVG, MAX))
-    checked = torch.tensor([len(sample_cuts), bad], dtype=torch.int64, device=dev)
+    checked = torch.tensor([len(sample_cuts), bad], dtype=torch.int64, device=coll_device(dev))
     if world > 1:
         dist.all_reduce(checked)
     if rank == 0:
@@ -409,6 +523,112 @@ def run_c4(args, torch, dist, dev, rank, world, local):
         p.close()
 
 
+def run_c1(args, torch, dev, rank, world):
+    """C1 (BASELINE.json configs[0]): one 256 MiB file through the chunker,
+    examples/backup/examples/backup.rs:14-36 plumbing restated: a file on
+    disk, opened and read by ChunkIter.from_config (chunker.rs:22-47) as
+    FileArchiver::backup_reader does (archiver/file_archiver.rs:144-160).
+    The bytes are StdRng::seed_from_u64(0x256) (SURVEY.md 8(d)).
+    value: the drop-in path (file reads + rcdc_stream_feed: H2D, device
+    chunking, cuts D2H), GiB/s; beside it the device-resident rate of the
+    same bytes and the reference-equivalent CPU chunker on 1 thread (the
+    configuration's own measurement: one file is one iterator, one thread)."""
+    import tempfile
+    from rustic_core_amd import ChunkIter, ConfigFile
+    from rustic_core_amd.chunker import Context
+    from rustic_core_amd.device import DevicePlan, pack_offsets
+    n = args.stream_bytes or (256 << 20)
+    data = stdrng_numpy(0x256, n)
+    fd, path = tempfile.mkstemp(prefix="rcdc_c1_", dir=os.environ.get("TMPDIR", "/tmp"))
+    with os.fdopen(fd, "wb") as f:
+        f.write(data.tobytes())
+    cfg = ConfigFile.new(2, POLY)
+    try:
+        def one_pass():
+            out = []
+            with open(path, "rb") as f:
+                for c in ChunkIter.from_config(cfg, f, n):
+                    out.append(len(c))
+            return out
+        lens = one_pass()  # warm: context, lanes, plans, page cache
+        for _ in range(max(args.warmup - 1, 0)):
+            one_pass()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            lens = one_pass()
+        el = time.perf_counter() - t0
+    finally:
+        os.unlink(path)
+    cuts = np.cumsum(np.array(lens, dtype=np.uint64))
+    # the same bytes device-resident
+    ctx = Context.get(POLY, MIN, AVG, MAX, device=dev.index)
+    offs, alen = pack_offsets([n])
+    arena = torch.zeros(alen, dtype=torch.uint8, device=dev)
+    arena[:n] = torch.from_numpy(data).to(dev)
+    plan = DevicePlan(ctx, offs, [n], alen)
+    sptr = torch.cuda.current_stream(dev).cuda_stream
+    for _ in range(20):
+        plan.run(arena.data_ptr(), sptr)
+    torch.cuda.synchronize(dev)
+    plan.set_timing(True, 1)
+    t1 = time.perf_counter()
+    for _ in range(50):
+        plan.run(arena.data_ptr(), sptr)
+    torch.cuda.synchronize(dev)
+    el_dev = (time.perf_counter() - t1) / 50
+    plan.set_timing(False)
+    runs, scan_ms, res_ms = plan.kernel_times()
+    dev_cuts = plan.results()[0]
+    inf = plan.info()
+    plan.close()
+    from oracle import oracle  # checker + CPU baseline
+    want = oracle.chunk_cuts(data)
+    t2 = time.perf_counter()
+    reps = 0
+    while time.perf_counter() - t2 < args.cpu_seconds:
+        oracle.chunk_many_owned(data, np.zeros(1, np.uint64), np.array([n], np.uint64),
+                                nthreads=1)
+        reps += 1
+    el_cpu = (time.perf_counter() - t2) / reps
+    scan_s = scan_ms / max(runs, 1) / 1e3
+    line = {
+        "metric": METRIC, "value": round(n * args.steps / el / GiB, 3), "unit": "GiB/s",
+        "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(el / args.steps * 1e3, 3), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "u8",
+        "data": "StdRng::seed_from_u64(0x256) bytes (ChaCha12, SURVEY.md 8(d)) in a file",
+        "config": {"workload": f"C1: one {n >> 20} MiB file through ChunkIter.from_config "
+                               "(file reads + C ABI stream: H2D, device chunking, cuts D2H; "
+                               "BASELINE.json configs[0])",
+                   "poly": hex(POLY), "min": MIN, "avg": AVG, "max": MAX,
+                   "parallelism": "one file = one iterator (the reference runs it on one thread)"},
+        "device_resident": {"gibs": round(n / el_dev / GiB, 1), "kernel_us": round(scan_s * 1e6, 1),
+                            "chain_or_resolve_us": round(res_ms / max(runs, 1) * 1e3, 1),
+                            "walk_pieces": inf["walk_pieces"]},
+        "roofline": {"bound": "hbm", "kernel": "rcdc_scan_kernel" if not inf["walk_pieces"]
+                     else "rcdc_walk_kernel", "achieved": round(n / scan_s / 1e9, 1),
+                     "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(n / scan_s / 1e9 / HBM_PEAK_GBS, 4), "traffic": None,
+                     "basis": "input bytes / hashing-kernel time (one 256 MiB stream: "
+                              "latency-bound, far too small to fill the chip)"},
+        "parity": {"chunks": int(len(cuts)),
+                   "mismatches": int(not np.array_equal(cuts, want)) +
+                   int(not np.array_equal(dev_cuts, want)),
+                   "checker": "oracle/cdc_ref on the same bytes (drop-in path and device plan)"},
+        "cpu_baseline": {"value": round(n / el_cpu / GiB, 3), "unit": "GiB/s", "cores": 1,
+                         "kind": "port", "sample": f"the whole {n >> 20} MiB file, {reps} passes, "
+                         "cdc_ref reference-equivalent mode (owned chunks, 4 KiB reads)",
+                         "cpu_model": _cpu_model()},
+    }
+    print(json.dumps(line), flush=True)
+
+
+def coll_device(dev):
+    """Device of the timing collectives' tensors: the GPU under RCCL, the host
+    under the gloo rehearsal backend."""
+    return "cpu" if os.environ.get("RCDC_BENCH_BACKEND") == "gloo" else dev
+
+
 def spawn_ranks(args) -> None:
     """`bench.py --gpus N` without a launcher: start N ranks with torchrun as a
     child process (before anything touches the GPU) and exit with its code.
@@ -442,14 +662,26 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # RCDC_BENCH_BACKEND=gloo: rehearse N ranks on fewer GPUs (ranks share
+    # devices round-robin; timing collectives over gloo).  Default: RCCL,
+    # one GPU per rank.
+    backend = os.environ.get("RCDC_BENCH_BACKEND", "nccl")
+    if backend == "gloo":
+        local = local % max(torch.cuda.device_count(), 1)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "gloo":
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
 
     from rustic_core_amd.chunker import Context
     from rustic_core_amd.device import DevicePlan
 
+    if args.workload == "C1":
+        run_c1(args, torch, dev, rank, world)
+        return
     if args.workload == "C4":
         run_c4(args, torch, dist, dev, rank, world, local)
         if world > 1:
@@ -522,7 +754,7 @@ def main():
         dist.barrier()
     plan.set_timing(False)
     runs, scan_ms, resolve_ms = plan.kernel_times()
-    t = torch.tensor([el], dtype=torch.float64, device=dev)
+    t = torch.tensor([el], dtype=torch.float64, device=coll_device(dev))
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     el_max = float(t.item())
@@ -615,6 +847,16 @@ def main():
                                           rank == 0 and world == 1 and not args.no_cpu_baseline)
     if args.e2e and rank == 0:
         out_extra["e2e"] = e2e_rate(torch, arena, offs, lens, plan, args.workload)
+    if args.abi_e2e and rank == 0 and args.workload in ("C2", "C3"):
+        k = min(len(lens), args.abi_files)
+        files = [arena[int(offs[i]):int(offs[i]) + int(lens[i])].cpu().numpy() for i in range(k)]
+        res, cuts = abi_e2e(files, args.abi_threads)
+        from oracle import oracle
+        res["mismatches"] = int(sum(not np.array_equal(c, oracle.chunk_cuts(f))
+                                    for c, f in zip(cuts[:4], files[:4])))
+        res["parity_files"] = min(4, k)
+        res.update(pcie_rates(torch, dev))
+        out_extra["abi_e2e"] = res
 
     if rank == 0:
         parallel = (f"per-stream sharding over {world} GPU(s), no collectives"

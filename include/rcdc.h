@@ -19,7 +19,9 @@
  * Plain C types only (pointers + sizes); no HIP or torch types appear in a
  * signature.  Device pointers are passed as `const void *` / `uint64_t`.
  * All entry points are thread-safe for distinct contexts/streams/plans; one
- * context may be shared by threads (internal lock around its HIP stream).
+ * context may be shared by any number of threads (a pool of per-call lanes,
+ * see the host-stream section).  A stream or plan is used by one thread at
+ * a time.
  */
 #ifndef RCDC_H
 #define RCDC_H
@@ -85,12 +87,21 @@ uint64_t rcdc_max_cuts(const rcdc_ctx *ctx, uint64_t n);
 
 /* ---- independent host streams (per-file parallel path, archiver.rs:195) - */
 
-/* Chunk n independent host buffers.  Their bytes are copied H2D through
- * pinned staging buffers on the context's stream, scanned on the device and
- * only the cut offsets are copied back.  Cuts of stream i are written
- * consecutively to cuts[] in stream order; cut_counts[i] receives the count.
- * If the total exceeds cuts_cap, RCDC_ERR_CAPACITY is returned with every
- * cut_counts[i] valid and cuts[] untouched.                                 */
+/* Host-buffer calls (rcdc_chunk_batch, rcdc_stream_feed) may come from many
+ * threads at once on one context, as the reference runs one ChunkIter per
+ * file on pariter workers (archiver.rs:195).  Each call takes one of the
+ * context's lanes -- a HIP stream, two pinned staging slots and a device
+ * arena of its own -- for its duration, so concurrent calls overlap instead
+ * of serialising; at most RCDC_LANES (environment, default 16) lanes exist,
+ * further callers wait for a free one.  The caller's pageable bytes go
+ * through the staging slots in 16 MiB blocks, the copy of block k + 1
+ * overlapping the DMA of block k.                                          */
+
+/* Chunk n independent host buffers; only the cut offsets come back.  Cuts of
+ * stream i are written consecutively to cuts[] in stream order;
+ * cut_counts[i] receives the count.  If the total exceeds cuts_cap,
+ * RCDC_ERR_CAPACITY is returned with every cut_counts[i] valid and cuts[]
+ * untouched (call again with a larger buffer).                            */
 rcdc_status rcdc_chunk_batch(rcdc_ctx *ctx, const rcdc_buf *bufs, uint32_t n,
                              uint64_t *cuts, uint64_t cuts_cap,
                              uint64_t *cut_counts);
@@ -99,15 +110,27 @@ rcdc_status rcdc_chunk_batch(rcdc_ctx *ctx, const rcdc_buf *bufs, uint32_t n,
 
 /* Replaces the read loop of rabin.rs:110-191: the caller feeds the file in
  * arbitrary pieces (any split gives the same cuts, like the reference's
- * read()-independence).  After each feed, *n_cuts cut offsets (absolute,
- * from the start of the file) that are now final are written to cuts[].
- * is_final = 1 marks EOF (the reference's Ok(0)); then the last cut is the
- * file length.  Bytes are retained internally only until they can no longer
- * influence a cut (at most max + 128 bytes).                               */
+ * read()-independence).  Cut offsets (absolute, from the start of the file)
+ * become final as enough bytes arrive; each call hands out up to `cap` of
+ * them (*n_cuts) and keeps the rest queued for the next call -- a call with
+ * len = 0 only drains the queue, and rcdc_stream_queued() tells how many
+ * wait.  A feed never fails for lack of cut space and never consumes input
+ * twice.  is_final = 1 marks EOF (the reference's Ok(0)); the last cut is
+ * then the file length.
+ * Retention: the stream buffers bytes until rcdc_stream_batch_bytes(ctx)
+ * (64 MiB, at least 2 max + 256; environment RCDC_STREAM_BATCH) are
+ * pending, then runs one device pass; afterwards it keeps only the tail
+ * after the last final cut (< max bytes).  So at most batch + max + the
+ * last piece fed are held -- more than the reference's 4 KiB + one chunk,
+ * for one device pass per 64 MiB instead of one per chunk.
+ * On an HIP failure the bytes stay buffered and the status is returned;
+ * the feed may be retried with len = 0 (same is_final).                    */
 rcdc_status rcdc_stream_open(rcdc_ctx *ctx, rcdc_stream **out);
 rcdc_status rcdc_stream_feed(rcdc_stream *st, const uint8_t *data,
                              uint64_t len, int is_final, uint64_t *cuts,
                              uint64_t cap, uint64_t *n_cuts);
+uint64_t rcdc_stream_queued(const rcdc_stream *st);
+uint64_t rcdc_stream_batch_bytes(const rcdc_ctx *ctx);
 void rcdc_stream_close(rcdc_stream *st);
 
 /* ---- device-resident batches (the measured hot path) ------------------- */
@@ -127,13 +150,24 @@ void rcdc_plan_destroy(rcdc_plan *plan);
 rcdc_status rcdc_plan_run(rcdc_plan *plan, const void *d_arena,
                           void *hip_stream);
 
-/* Synchronise with the last run and copy the results to the host: same
- * layout and capacity rule as rcdc_chunk_batch.                           */
+/* Complete the last run on the host side: wait for it and, for any long
+ * stream whose walk-path fixup overflowed its slots (never seen outside
+ * forced tests), re-chunk it on the scan path and write its cuts -- and, if
+ * the run was hashed, its digests -- back into the device buffers.  Until
+ * this returns the device arena of the run must stay unchanged; after it,
+ * the device views below are complete.  rcdc_plan_results and
+ * rcdc_plan_digests call it.                                                */
+rcdc_status rcdc_plan_finish(rcdc_plan *plan);
+
+/* Finish the last run and copy the results to the host: same layout and
+ * capacity rule as rcdc_chunk_batch.                                      */
 rcdc_status rcdc_plan_results(rcdc_plan *plan, uint64_t *cuts,
                               uint64_t cuts_cap, uint64_t *cut_counts);
 
-/* Device-side view of the results (valid after the run completes):
- * stream i's cuts are d_cuts[cut_base[i] .. cut_base[i] + d_counts[i]).   */
+/* Device-side view of the results: stream i's cuts are
+ * d_cuts[cut_base[i] .. cut_base[i] + d_counts[i]).  Complete after
+ * rcdc_plan_finish; before it, a stream whose walk needs host completion
+ * reads d_counts[i] == UINT64_MAX (and its digests are not written).        */
 rcdc_status rcdc_plan_device_results(rcdc_plan *plan, uint64_t *d_cuts,
                                      uint64_t *d_counts,
                                      const uint64_t **cut_base);

@@ -24,6 +24,7 @@ EXPORTS = (
     "rcdc_plan_get_info", "rcdc_plan_set_timing", "rcdc_plan_kernel_times", "rcdc_fixed_cuts",
     "rcdc_sha256_chunks", "rcdc_plan_hash", "rcdc_plan_digests", "rcdc_plan_device_digests",
     "rcdc_plan_set_pipeline", "rcdc_plan_hash_many", "rcdc_plan_walk_stats",
+    "rcdc_plan_finish", "rcdc_stream_queued", "rcdc_stream_batch_bytes",
 )
 ABI_VERSION = 1
 
@@ -106,6 +107,12 @@ def lib() -> ctypes.CDLL:
     L.rcdc_stream_open.argtypes = [vp, P(vp)]
     L.rcdc_stream_feed.restype = st
     L.rcdc_stream_feed.argtypes = [vp, vp, u64, ctypes.c_int, vp, u64, P(u64)]
+    L.rcdc_stream_queued.restype = u64
+    L.rcdc_stream_queued.argtypes = [vp]
+    L.rcdc_stream_batch_bytes.restype = u64
+    L.rcdc_stream_batch_bytes.argtypes = [vp]
+    L.rcdc_plan_finish.restype = st
+    L.rcdc_plan_finish.argtypes = [vp]
     L.rcdc_stream_close.restype = None
     L.rcdc_stream_close.argtypes = [vp]
     L.rcdc_plan_create.restype = st

@@ -16,6 +16,7 @@ constructor raises.
 """
 from __future__ import annotations
 
+import collections
 import ctypes
 import enum
 import io
@@ -190,18 +191,29 @@ class _Stream:
             raise status_error(st, _lib.last_error())
         self._h = h
 
-    def feed(self, data: bytes, is_final: bool) -> np.ndarray:
+    def feed(self, data, is_final: bool) -> np.ndarray:
+        """Feed one piece; returns every cut that became final (the C ABI
+        hands out at most `cap` per call and queues the rest: drained here)."""
         L = _lib.lib()
         a = np.frombuffer(data, dtype=np.uint8) if len(data) else np.zeros(0, np.uint8)
-        # bound: cuts come from at most the buffered bytes + this piece
-        cap = self._ctx.max_cuts(len(data) + 2 * self._ctx.max_size + (96 << 20)) + 1
-        cuts = np.zeros(cap, dtype=np.uint64)
+        cap = self._ctx.max_cuts(len(a)) + 1
+        out = []
         n = ctypes.c_uint64(0)
-        st = L.rcdc_stream_feed(self._h, a.ctypes.data if a.size else None, a.size,
-                                int(is_final), cuts.ctypes.data, cap, ctypes.byref(n))
-        if st:
-            raise status_error(st, _lib.last_error())
-        return cuts[:n.value]
+        first = True
+        while True:
+            cuts = np.zeros(cap, dtype=np.uint64)
+            st = L.rcdc_stream_feed(self._h, a.ctypes.data if (first and a.size) else None,
+                                    a.size if first else 0, int(is_final), cuts.ctypes.data,
+                                    cap, ctypes.byref(n))
+            if st:
+                raise status_error(st, _lib.last_error())
+            first = False
+            out.append(cuts[:n.value])
+            q = int(L.rcdc_stream_queued(self._h))
+            if q == 0:
+                break
+            cap = q
+        return out[0] if len(out) == 1 else np.concatenate(out)
 
     def close(self):
         if self._h:
@@ -237,9 +249,10 @@ class RabinChunkIter:
         self._reader = reader
         self.size_hint = size_hint  # capacity hint only; never affects cuts
         self._stream = _Stream(ctx)
-        self._buf = bytearray()      # bytes not yet yielded
-        self._base = 0               # absolute offset of _buf[0]
-        self._cuts: list = []
+        self._buf = bytearray()      # bytes read, not yet compacted away
+        self._off = 0                # _buf[_off:] not yet yielded
+        self._base = 0               # absolute offset of _buf[_off]
+        self._cuts = collections.deque()
         self._eof = False
         self._finished = False
 
@@ -251,6 +264,11 @@ class RabinChunkIter:
             data = _read(self._reader, READ_SIZE)
             if not data:
                 self._eof = True
+            # compact what was yielded once it dominates the buffer (amortised
+            # O(1) per byte instead of a memmove per chunk)
+            if self._off and self._off >= len(self._buf) // 2:
+                del self._buf[:self._off]
+                self._off = 0
             self._buf += data
             self._cuts.extend(int(c) for c in self._stream.feed(data, self._eof))
 
@@ -261,15 +279,16 @@ class RabinChunkIter:
             self._fill()
         except RusticError:
             self._finished = True
+            self._stream.close()
             raise
         if not self._cuts:
             self._finished = True
             self._stream.close()
             raise StopIteration
-        end = self._cuts.pop(0)
+        end = self._cuts.popleft()
         k = end - self._base
-        chunk = bytes(self._buf[:k])
-        del self._buf[:k]
+        chunk = bytes(memoryview(self._buf)[self._off:self._off + k])
+        self._off += k
         self._base = end
         self.size_hint = max(self.size_hint - len(chunk), 0)
         return chunk

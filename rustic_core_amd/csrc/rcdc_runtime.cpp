@@ -17,6 +17,8 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <condition_variable>
+#include <deque>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -191,12 +193,31 @@ struct rcdc_plan {
     uint32_t *d_order = nullptr;  // slots sorted by chunk length, longest first
     uint64_t cap_shaw = 0, cap_order = 0;
     bool hashed = false;
+    bool finished = false;           // rcdc_plan_finish done for the last run
+    std::vector<uint64_t> fin_counts;  // per-stream counts after the finish
     // optional per-run kernel timing
     bool timing = false;
     uint32_t tperiod = 1;         // record every tperiod-th run (rcdc_plan_set_timing)
     uint64_t tcalls = 0;          // runs since timing was enabled
     std::vector<hipEvent_t> tev;  // 3 per timed run: before scan, after scan, after resolve
     uint64_t truns = 0;
+};
+
+// One host-buffer worker of a context ("lane"): a HIP stream of its own, two
+// pinned staging slots (the caller's pageable bytes are copied into one while
+// the other's DMA runs), a device arena and a cached plan.  Calling threads
+// take a free lane for the duration of a call, so concurrent files
+// (archiver.rs:195) run on separate streams without a context-wide lock.
+struct Lane {
+    hipStream_t stream = nullptr;
+    hipEvent_t ev[2] = {nullptr, nullptr};
+    uint8_t *pinned[2] = {nullptr, nullptr};
+    uint64_t stage = 0;  // bytes per staging slot
+    uint8_t *d_arena = nullptr;
+    uint64_t arena_cap = 0;
+    rcdc_plan *plan = nullptr;
+    std::vector<uint64_t> lay_offs, lay_lens;  // layout of the cached plan
+    uint64_t lay_arena = 0;
 };
 
 struct rcdc_ctx {
@@ -207,21 +228,20 @@ struct rcdc_ctx {
     int variant = kDefaultScanCode;  // scan-kernel configuration (RCDC_SCAN_VARIANT)
     hipStream_t stream = nullptr;
     uint64_t *d_tables = nullptr;
-    std::mutex mu;
-    // host-buffer batch path
-    uint8_t *pinned = nullptr;
-    uint64_t pinned_cap = 0;
-    uint8_t *d_arena = nullptr;
-    uint64_t arena_cap = 0;
-    rcdc_plan *batch_plan = nullptr;
+    // host-buffer path: a pool of lanes (RCDC_LANES, default 16)
+    std::mutex pool_mu;
+    std::condition_variable pool_cv;
+    std::vector<Lane *> lanes, free_lanes;
+    uint32_t max_lanes = 16;
 };
 
 struct rcdc_stream {
     rcdc_ctx *ctx = nullptr;
     std::vector<uint8_t> pending;  // bytes from the current chunk start
     uint64_t base = 0;             // absolute offset of pending[0]
+    uint64_t batch = 0;            // bytes buffered before a device pass
     bool done = false;
-    rcdc_plan *plan = nullptr;
+    std::deque<uint64_t> out;      // final cuts not yet handed to the caller
 };
 
 namespace {
@@ -649,16 +669,52 @@ rcdc_status plan_run(rcdc_plan *pl, const void *d_arena, hipStream_t stream) {
     HIP_TRY(hipEventRecord(pl->done, stream));
     pl->ran = true;
     pl->hashed = false;
+    pl->finished = false;
     return RCDC_OK;
 }
 
 void plan_release(rcdc_plan *pl);
 
-rcdc_status plan_results(rcdc_plan *pl, uint64_t *cuts, uint64_t cap, uint64_t *counts) {
+// SHA-256 of (offset, length) refs of the plan's last arena into the plan's
+// digest slots (a stream the walk path handed back to the scan path).
+rcdc_status launch_list_hash(rcdc_plan *pl, const std::vector<ulonglong2> &refs,
+                             const std::vector<uint64_t> &slots) {
+    DeviceGuard g(pl->ctx->device);
+    ulonglong2 *d_refs = nullptr;
+    uint32_t *d_out = nullptr;
+    std::vector<uint8_t> out(refs.size() * 32);
+    hipStream_t st = pl->ctx->stream;
+    hipError_t e = hipMalloc((void **)&d_refs, refs.size() * sizeof(ulonglong2));
+    if (e == hipSuccess) e = hipMalloc((void **)&d_out, out.size());
+    if (e == hipSuccess)
+        e = hipMemcpy(d_refs, refs.data(), refs.size() * sizeof(ulonglong2), hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipStreamWaitEvent(st, pl->done, 0);  // after the plan's hash
+    if (e == hipSuccess)
+        e = launch_sha256_list((const uint8_t *)pl->last_arena, d_refs, (uint32_t)refs.size(),
+                               d_out, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    if (e == hipSuccess) e = hipMemcpy(out.data(), d_out, out.size(), hipMemcpyDeviceToHost);
+    for (size_t r = 0; r < refs.size() && e == hipSuccess; r++)
+        e = hipMemcpy((uint8_t *)pl->d_dig + slots[r] * 32, out.data() + r * 32, 32,
+                      hipMemcpyHostToDevice);
+    (void)hipFree(d_refs);
+    (void)hipFree(d_out);
+    HIP_TRY(e);
+    return RCDC_OK;
+}
+
+
+// Completes the last run: waits for it, redoes on the scan path any walked
+// stream whose fixup overflowed (device count ~0; never seen outside forced
+// tests) and writes those cuts -- and, if the run was hashed, their digests
+// -- back into the device buffers, so the device views are complete.
+rcdc_status plan_finish(rcdc_plan *pl) {
     if (!pl->ran) return fail(RCDC_ERR_INVALID_INPUT, "plan has not been run");
+    if (pl->finished) return RCDC_OK;
     DeviceGuard g(pl->ctx->device);
     HIP_TRY(hipEventSynchronize(pl->done));
-    std::vector<uint64_t> cnt(pl->n);
+    std::vector<uint64_t> &cnt = pl->fin_counts;
+    cnt.assign(pl->n, 0);
     if (pl->n)
         HIP_TRY(hipMemcpy(cnt.data(), pl->d_counts, pl->n * 8, hipMemcpyDeviceToHost));
     if (const char *e = getenv("RCDC_WALK_DUMP"); e && !pl->wunits.empty()) {  // debugging aid
@@ -700,9 +756,8 @@ rcdc_status plan_results(rcdc_plan *pl, uint64_t *cuts, uint64_t cap, uint64_t *
             fprintf(stderr, "\n");
         }
     }
-    // a walked stream whose fixup overflowed (count ~0): redo it on the scan
-    // path over the same device bytes
-    std::vector<std::vector<uint64_t>> redo(pl->n);
+    std::vector<ulonglong2> refs;
+    std::vector<uint64_t> slots;
     for (uint32_t i = 0; i < pl->n; i++) {
         if (cnt[i] != ~0ull) continue;
         rcdc_plan tmp;
@@ -710,17 +765,44 @@ rcdc_status plan_results(rcdc_plan *pl, uint64_t *cuts, uint64_t cap, uint64_t *
         const uint64_t off = pl->sds[i].off, len = pl->sds[i].n;
         rcdc_status st = plan_build(pl->ctx, &tmp, &off, &len, 1, pl->arena_len);
         if (!st) st = plan_run(&tmp, pl->last_arena, pl->last_stream);
-        if (!st) HIP_TRY(hipEventSynchronize(tmp.done));
+        if (!st) st = tmp.done ? (hipEventSynchronize(tmp.done) == hipSuccess ? RCDC_OK
+                                  : fail(RCDC_ERR_INTERNAL, "redo sync")) : RCDC_OK;
         uint64_t c1 = 0;
-        if (!st) HIP_TRY(hipMemcpy(&c1, tmp.d_counts, 8, hipMemcpyDeviceToHost));
+        std::vector<uint64_t> redo;
+        if (!st && hipMemcpy(&c1, tmp.d_counts, 8, hipMemcpyDeviceToHost) != hipSuccess)
+            st = fail(RCDC_ERR_INTERNAL, "redo counts");
+        if (!st && c1 > pl->sds[i].cut_cap)
+            st = fail(RCDC_ERR_INTERNAL, "stream %u: %llu cuts > bound", i, (unsigned long long)c1);
         if (!st) {
-            redo[i].resize(c1);
-            if (c1) HIP_TRY(hipMemcpy(redo[i].data(), tmp.d_cuts, c1 * 8, hipMemcpyDeviceToHost));
+            redo.resize(c1);
+            if (c1 && hipMemcpy(redo.data(), tmp.d_cuts, c1 * 8, hipMemcpyDeviceToHost) != hipSuccess)
+                st = fail(RCDC_ERR_INTERNAL, "redo cuts");
         }
         plan_release(&tmp);
         if (st) return st;
+        if (c1) HIP_TRY(hipMemcpy(pl->d_cuts + pl->cut_base[i], redo.data(), c1 * 8,
+                                  hipMemcpyHostToDevice));
+        HIP_TRY(hipMemcpy(pl->d_counts + i, &c1, 8, hipMemcpyHostToDevice));
         cnt[i] = c1;
+        uint64_t prev = 0;
+        for (uint64_t j = 0; j < c1; j++) {
+            refs.push_back({pl->sds[i].off + prev, redo[j] - prev});
+            slots.push_back(pl->cut_base[i] + j);
+            prev = redo[j];
+        }
     }
+    if (pl->hashed && !refs.empty()) {
+        rcdc_status st = launch_list_hash(pl, refs, slots);
+        if (st) return st;
+    }
+    pl->finished = true;
+    return RCDC_OK;
+}
+
+rcdc_status plan_results(rcdc_plan *pl, uint64_t *cuts, uint64_t cap, uint64_t *counts) {
+    rcdc_status st = plan_finish(pl);
+    if (st) return st;
+    const std::vector<uint64_t> &cnt = pl->fin_counts;
     uint64_t total = 0;
     for (uint32_t i = 0; i < pl->n; i++) {
         if (cnt[i] > pl->sds[i].cut_cap)
@@ -731,13 +813,13 @@ rcdc_status plan_results(rcdc_plan *pl, uint64_t *cuts, uint64_t cap, uint64_t *
     }
     if (total > cap) return fail(RCDC_ERR_CAPACITY, "need %llu cut slots, have %llu",
                                  (unsigned long long)total, (unsigned long long)cap);
+    DeviceGuard g(pl->ctx->device);
     std::vector<uint64_t> all(pl->ncuts);
     if (pl->ncuts)
         HIP_TRY(hipMemcpy(all.data(), pl->d_cuts, pl->ncuts * 8, hipMemcpyDeviceToHost));
     uint64_t o = 0;
     for (uint32_t i = 0; i < pl->n; i++) {
-        memcpy(cuts + o, redo[i].empty() ? all.data() + pl->cut_base[i] : redo[i].data(),
-               cnt[i] * 8);
+        memcpy(cuts + o, all.data() + pl->cut_base[i], cnt[i] * 8);
         o += cnt[i];
     }
     return RCDC_OK;
@@ -787,39 +869,108 @@ void plan_free(rcdc_plan *pl) {
     delete pl;
 }
 
-// Host bytes -> (pinned staging) -> device arena -> plan -> cuts.
-rcdc_status run_host_batch(rcdc_ctx *ctx, rcdc_plan **cache, const rcdc_buf *bufs, uint32_t n,
+void lane_free(rcdc_ctx *ctx, Lane *L) {
+    if (!L) return;
+    DeviceGuard g(ctx->device);
+    if (L->stream) (void)hipStreamSynchronize(L->stream);
+    plan_free(L->plan);
+    for (int k = 0; k < 2; k++) {
+        if (L->ev[k]) (void)hipEventDestroy(L->ev[k]);
+        if (L->pinned[k]) (void)hipHostFree(L->pinned[k]);
+    }
+    (void)hipFree(L->d_arena);
+    if (L->stream) (void)hipStreamDestroy(L->stream);
+    delete L;
+}
+
+// Take a free lane (creating one while fewer than max_lanes exist, else
+// waiting for one); give it back with lane_release.
+rcdc_status lane_acquire(rcdc_ctx *ctx, Lane **out) {
+    std::unique_lock<std::mutex> lk(ctx->pool_mu);
+    while (ctx->free_lanes.empty() && ctx->lanes.size() >= ctx->max_lanes) ctx->pool_cv.wait(lk);
+    if (!ctx->free_lanes.empty()) {
+        *out = ctx->free_lanes.back();
+        ctx->free_lanes.pop_back();
+        return RCDC_OK;
+    }
+    Lane *L = new Lane();
+    ctx->lanes.push_back(L);  // counted now; its HIP objects are made below
+    lk.unlock();
+    DeviceGuard g(ctx->device);
+    hipError_t e = hipStreamCreateWithFlags(&L->stream, hipStreamNonBlocking);
+    for (int k = 0; k < 2 && e == hipSuccess; k++)
+        e = hipEventCreateWithFlags(&L->ev[k], hipEventDisableTiming);
+    if (e != hipSuccess) {
+        std::lock_guard<std::mutex> lk2(ctx->pool_mu);
+        ctx->lanes.erase(std::find(ctx->lanes.begin(), ctx->lanes.end(), L));
+        lane_free(ctx, L);
+        ctx->pool_cv.notify_one();
+        return fail(RCDC_ERR_INTERNAL, "lane setup: %s", hipGetErrorString(e));
+    }
+    *out = L;
+    return RCDC_OK;
+}
+
+void lane_release(rcdc_ctx *ctx, Lane *L) {
+    std::lock_guard<std::mutex> lk(ctx->pool_mu);
+    ctx->free_lanes.push_back(L);
+    ctx->pool_cv.notify_one();
+}
+
+constexpr uint64_t kStageBytes = 16ull << 20;  // per pinned staging slot
+
+// Host bytes -> pinned staging (two slots, copy k + 1 overlapping the DMA of
+// copy k) -> the lane's device arena -> plan -> cuts, all on the lane's
+// stream.  The plan is rebuilt only when the batch layout changes.
+rcdc_status run_host_batch(rcdc_ctx *ctx, Lane *L, const rcdc_buf *bufs, uint32_t n,
                            uint64_t *cuts, uint64_t cap, uint64_t *counts) {
     std::vector<uint64_t> offs(n), lens(n);
     uint64_t total = 0;
     for (uint32_t i = 0; i < n; i++) {
+        if (bufs[i].len && !bufs[i].data)
+            return fail(RCDC_ERR_INVALID_INPUT, "buffer %u is NULL with length %llu", i,
+                        (unsigned long long)bufs[i].len);
         offs[i] = total;
         lens[i] = bufs[i].len;
         total = round_up(total + bufs[i].len, 256);
     }
     const uint64_t arena_len = total + 256;
     DeviceGuard g(ctx->device);
-    if (arena_len > ctx->pinned_cap) {
-        if (ctx->pinned) HIP_TRY(hipHostFree(ctx->pinned));
-        ctx->pinned = nullptr;
-        ctx->pinned_cap = 0;
-        HIP_TRY(hipHostMalloc((void **)&ctx->pinned, arena_len, hipHostMallocDefault));
-        ctx->pinned_cap = arena_len;
-    }
     rcdc_status st;
-    if ((st = ensure_dev(&ctx->d_arena, &ctx->arena_cap, arena_len))) return st;
-    for (uint32_t i = 0; i < n; i++) {
-        if (bufs[i].len && !bufs[i].data)
-            return fail(RCDC_ERR_INVALID_INPUT, "buffer %u is NULL with length %llu", i,
-                        (unsigned long long)bufs[i].len);
-        if (bufs[i].len) memcpy(ctx->pinned + offs[i], bufs[i].data, bufs[i].len);
+    if ((st = ensure_dev(&L->d_arena, &L->arena_cap, arena_len))) return st;
+    if (!L->pinned[0]) {
+        L->stage = kStageBytes;
+        for (int k = 0; k < 2; k++)
+            HIP_TRY(hipHostMalloc((void **)&L->pinned[k], L->stage, hipHostMallocDefault));
     }
-    HIP_TRY(hipMemcpyAsync(ctx->d_arena, ctx->pinned, arena_len, hipMemcpyHostToDevice,
-                           ctx->stream));
-    if (!*cache) *cache = new rcdc_plan();
-    if ((st = plan_build(ctx, *cache, offs.data(), lens.data(), n, arena_len))) return st;
-    if ((st = plan_run(*cache, ctx->d_arena, ctx->stream))) return st;
-    return plan_results(*cache, cuts, cap, counts);
+    // staged copies: block k of the arena goes through slot k & 1
+    uint32_t bi = 0;  // first buffer that may overlap the block
+    uint64_t k = 0;
+    for (uint64_t p = 0; p < total; p += L->stage, k++) {
+        const uint64_t e = std::min(p + L->stage, total);
+        const int slot = (int)(k & 1);
+        if (k >= 2) HIP_TRY(hipEventSynchronize(L->ev[slot]));  // its previous DMA is done
+        uint8_t *dst = L->pinned[slot];
+        while (bi < n && offs[bi] + lens[bi] <= p) bi++;
+        for (uint32_t i = bi; i < n && offs[i] < e; i++) {
+            const uint64_t a = std::max(offs[i], p), b = std::min(offs[i] + lens[i], e);
+            if (a < b) memcpy(dst + (a - p), bufs[i].data + (a - offs[i]), b - a);
+        }
+        HIP_TRY(hipMemcpyAsync(L->d_arena + p, dst, e - p, hipMemcpyHostToDevice, L->stream));
+        HIP_TRY(hipEventRecord(L->ev[slot], L->stream));
+    }
+    if (!L->plan || L->lay_offs != offs || L->lay_lens != lens || L->lay_arena != arena_len) {
+        if (!L->plan) L->plan = new rcdc_plan();
+        if ((st = plan_build(ctx, L->plan, offs.data(), lens.data(), n, arena_len))) {
+            L->lay_offs.clear();
+            return st;
+        }
+        L->lay_offs = offs;
+        L->lay_lens = lens;
+        L->lay_arena = arena_len;
+    }
+    if ((st = plan_run(L->plan, L->d_arena, L->stream))) return st;
+    return plan_results(L->plan, cuts, cap, counts);
 }
 
 bool valid_ctx(const rcdc_ctx *c) { return c != nullptr; }
@@ -927,6 +1078,7 @@ rcdc_status rcdc_ctx_create(uint64_t poly, uint64_t min, uint64_t avg_pow2, uint
     }
     c->num_cus = prop.multiProcessorCount;
     if (const char *v = getenv("RCDC_SCAN_VARIANT")) c->variant = atoi(v);
+    if (const char *v = getenv("RCDC_LANES")) c->max_lanes = (uint32_t)std::max(atoi(v), 1);
     uint64_t img[512];
     build_tables(poly, img);
     if ((e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking)) != hipSuccess ||
@@ -944,10 +1096,8 @@ void rcdc_ctx_destroy(rcdc_ctx *c) {
     {
         DeviceGuard g(c->device);
         if (c->stream) (void)hipStreamSynchronize(c->stream);
-        plan_free(c->batch_plan);
+        for (Lane *L : c->lanes) lane_free(c, L);
         (void)hipFree(c->d_tables);
-        (void)hipFree(c->d_arena);
-        if (c->pinned) (void)hipHostFree(c->pinned);
         if (c->stream) (void)hipStreamDestroy(c->stream);
     }
     delete c;
@@ -959,8 +1109,12 @@ rcdc_status rcdc_chunk_batch(rcdc_ctx *ctx, const rcdc_buf *bufs, uint32_t n, ui
                              uint64_t cuts_cap, uint64_t *cut_counts) {
     if (!valid_ctx(ctx)) return fail(RCDC_ERR_INVALID_INPUT, "ctx is NULL");
     if (n && (!bufs || !cut_counts)) return fail(RCDC_ERR_INVALID_INPUT, "null argument");
-    std::lock_guard<std::mutex> lk(ctx->mu);
-    return run_host_batch(ctx, &ctx->batch_plan, bufs, n, cuts, cuts_cap, cut_counts);
+    Lane *L = nullptr;
+    rcdc_status st = lane_acquire(ctx, &L);
+    if (st) return st;
+    st = run_host_batch(ctx, L, bufs, n, cuts, cuts_cap, cut_counts);
+    lane_release(ctx, L);
+    return st;
 }
 
 rcdc_status rcdc_plan_create(rcdc_ctx *ctx, const uint64_t *offs, const uint64_t *lens,
@@ -1183,65 +1337,35 @@ rcdc_status rcdc_plan_hash_many(rcdc_plan *const *plans, uint32_t n,
     return RCDC_OK;
 }
 
+rcdc_status rcdc_plan_finish(rcdc_plan *plan) {
+    if (!plan) return fail(RCDC_ERR_INVALID_INPUT, "null argument");
+    return plan_finish(plan);
+}
+
 rcdc_status rcdc_plan_digests(rcdc_plan *plan, uint8_t *digests, uint64_t cap_chunks,
                               uint64_t *cut_counts) {
     if (!plan || (plan->n && !cut_counts)) return fail(RCDC_ERR_INVALID_INPUT, "null argument");
     if (!plan->hashed) return fail(RCDC_ERR_INVALID_INPUT, "rcdc_plan_hash has not been run");
-    DeviceGuard g(plan->ctx->device);
-    std::vector<uint64_t> dcnt(plan->n);
-    HIP_TRY(hipEventSynchronize(plan->done));
-    if (plan->n)
-        HIP_TRY(hipMemcpy(dcnt.data(), plan->d_counts, plan->n * 8, hipMemcpyDeviceToHost));
-    uint64_t total_cap = 0;
-    for (uint32_t i = 0; i < plan->n; i++) total_cap += plan->sds[i].cut_cap;
-    std::vector<uint64_t> cuts(total_cap);
-    rcdc_status rs = plan_results(plan, cuts.data(), total_cap, cut_counts);
+    rcdc_status rs = plan_finish(plan);
     if (rs) return rs;
+    DeviceGuard g(plan->ctx->device);
+    HIP_TRY(hipEventSynchronize(plan->done));  // the hash may follow the finish
+    const std::vector<uint64_t> &cnt = plan->fin_counts;
     uint64_t total = 0;
-    for (uint32_t i = 0; i < plan->n; i++) total += cut_counts[i];
+    for (uint32_t i = 0; i < plan->n; i++) {
+        cut_counts[i] = cnt[i];
+        total += cnt[i];
+    }
     if (total > cap_chunks)
         return fail(RCDC_ERR_CAPACITY, "need %llu digest slots, have %llu",
                     (unsigned long long)total, (unsigned long long)cap_chunks);
     std::vector<uint8_t> all(plan->ncuts * 32);
     if (plan->ncuts)
         HIP_TRY(hipMemcpy(all.data(), plan->d_dig, all.size(), hipMemcpyDeviceToHost));
-    // streams the walk path handed back to the scan path (device count ~0):
-    // their cuts came from the host-side redo, so hash them from that list
-    std::vector<ulonglong2> refs;
-    std::vector<uint64_t> ref_slot;
     uint64_t o = 0;
     for (uint32_t i = 0; i < plan->n; i++) {
-        if (dcnt[i] == ~0ull) {
-            uint64_t prev = 0;
-            for (uint64_t j = 0; j < cut_counts[i]; j++) {
-                refs.push_back({plan->sds[i].off + prev, cuts[o + j] - prev});
-                ref_slot.push_back(o + j);
-                prev = cuts[o + j];
-            }
-        } else if (cut_counts[i]) {
-            memcpy(digests + o * 32, all.data() + plan->cut_base[i] * 32, cut_counts[i] * 32);
-        }
-        o += cut_counts[i];
-    }
-    if (!refs.empty()) {
-        ulonglong2 *d_refs = nullptr;
-        uint32_t *d_out = nullptr;
-        std::vector<uint8_t> out(refs.size() * 32);
-        hipError_t e = hipMalloc((void **)&d_refs, refs.size() * sizeof(ulonglong2));
-        if (e == hipSuccess) e = hipMalloc((void **)&d_out, out.size());
-        if (e == hipSuccess)
-            e = hipMemcpy(d_refs, refs.data(), refs.size() * sizeof(ulonglong2),
-                          hipMemcpyHostToDevice);
-        if (e == hipSuccess)
-            e = launch_sha256_list((const uint8_t *)plan->last_arena, d_refs,
-                                   (uint32_t)refs.size(), d_out, plan->ctx->stream);
-        if (e == hipSuccess) e = hipStreamSynchronize(plan->ctx->stream);
-        if (e == hipSuccess) e = hipMemcpy(out.data(), d_out, out.size(), hipMemcpyDeviceToHost);
-        (void)hipFree(d_refs);
-        (void)hipFree(d_out);
-        HIP_TRY(e);
-        for (size_t r = 0; r < refs.size(); r++)
-            memcpy(digests + ref_slot[r] * 32, out.data() + r * 32, 32);
+        memcpy(digests + o * 32, all.data() + plan->cut_base[i] * 32, cnt[i] * 32);
+        o += cnt[i];
     }
     return RCDC_OK;
 }
@@ -1259,60 +1383,78 @@ rcdc_status rcdc_stream_open(rcdc_ctx *ctx, rcdc_stream **out) {
     if (!valid_ctx(ctx) || !out) return fail(RCDC_ERR_INVALID_INPUT, "null argument");
     rcdc_stream *s = new rcdc_stream();
     s->ctx = ctx;
+    s->batch = rcdc_stream_batch_bytes(ctx);
     *out = s;
     return RCDC_OK;
 }
 
-void rcdc_stream_close(rcdc_stream *st) {
-    if (!st) return;
-    plan_free(st->plan);
-    delete st;
+void rcdc_stream_close(rcdc_stream *st) { delete st; }
+
+uint64_t rcdc_stream_batch_bytes(const rcdc_ctx *ctx) {
+    if (!ctx) return 0;
+    uint64_t b = 64ull << 20;
+    if (const char *e = getenv("RCDC_STREAM_BATCH")) b = (uint64_t)atoll(e);
+    return std::max<uint64_t>(b, 2 * ctx->max + 256);
+}
+
+uint64_t rcdc_stream_queued(const rcdc_stream *st) { return st ? st->out.size() : 0; }
+
+// One device pass over the buffered bytes: every cut except the one at the
+// end of the buffer depends only on bytes before it, so it is final; the
+// end-of-buffer cut is final only at EOF.  The unfinished tail (< max bytes
+// from the last final cut) stays buffered and is re-chunked with more data.
+static rcdc_status stream_pass(rcdc_stream *st, bool is_final) {
+    rcdc_ctx *ctx = st->ctx;
+    const uint64_t N = st->pending.size();
+    if (!N) return RCDC_OK;
+    std::vector<uint64_t> tmp(rcdc_max_cuts(ctx, N));
+    rcdc_buf b{st->pending.data(), N};
+    uint64_t cnt = 0;
+    Lane *L = nullptr;
+    rcdc_status s2 = lane_acquire(ctx, &L);
+    if (s2) return s2;
+    s2 = run_host_batch(ctx, L, &b, 1, tmp.data(), tmp.size(), &cnt);
+    lane_release(ctx, L);
+    if (s2) return s2;
+    uint64_t keep = cnt;
+    if (!is_final && cnt && tmp[cnt - 1] == N) keep = cnt - 1;
+    for (uint64_t i = 0; i < keep; i++) st->out.push_back(st->base + tmp[i]);
+    const uint64_t consumed = keep ? tmp[keep - 1] : 0;
+    st->pending.erase(st->pending.begin(), st->pending.begin() + (long)consumed);
+    st->base += consumed;
+    return RCDC_OK;
 }
 
 rcdc_status rcdc_stream_feed(rcdc_stream *st, const uint8_t *data, uint64_t len, int is_final,
                              uint64_t *cuts, uint64_t cap, uint64_t *n_cuts) {
-    if (!st || !n_cuts || (len && !data)) return fail(RCDC_ERR_INVALID_INPUT, "null argument");
+    if (!st || !n_cuts || (len && !data) || (cap && !cuts))
+        return fail(RCDC_ERR_INVALID_INPUT, "null argument");
     *n_cuts = 0;
-    if (st->done) {
-        if (len) return fail(RCDC_ERR_INVALID_INPUT, "stream already finished");
-        return RCDC_OK;
+    if (st->done && len) return fail(RCDC_ERR_INVALID_INPUT, "stream already finished");
+    if (!st->done) {
+        st->pending.insert(st->pending.end(), data, data + len);
+        // a device pass once enough bytes are buffered that cuts are certain
+        // (every chunk ends by chunk start + max), or at EOF
+        if (is_final || st->pending.size() >= st->batch) {
+            rcdc_status s2 = stream_pass(st, is_final != 0);
+            if (s2) {
+                // the bytes stay buffered: the caller may retry the feed with
+                // len = 0, or close the stream
+                return s2;
+            }
+            if (is_final) {
+                st->pending.clear();
+                st->done = true;
+            }
+        }
     }
-    rcdc_ctx *ctx = st->ctx;
-    st->pending.insert(st->pending.end(), data, data + len);
-    // Process once enough bytes are buffered that a cut is guaranteed
-    // (every chunk ends by chunk start + max), or at EOF.
-    const uint64_t batch = std::max<uint64_t>(64ull << 20, 2 * ctx->max + 256);
-    if (!is_final && st->pending.size() < batch) return RCDC_OK;
-
-    std::lock_guard<std::mutex> lk(ctx->mu);
-    // One device pass over everything buffered: every cut except the one at
-    // the end of the buffer depends only on bytes before it, so it is final;
-    // the end-of-buffer cut is final only at EOF.  The unfinished tail
-    // (< max bytes, from the last final cut) is re-chunked with more data.
-    uint64_t produced = 0;
-    const uint64_t N = st->pending.size();
-    if (N) {
-        std::vector<uint64_t> tmp(rcdc_max_cuts(ctx, N));
-        rcdc_buf b{st->pending.data(), N};
-        uint64_t cnt = 0;
-        rcdc_status s2 = run_host_batch(ctx, &st->plan, &b, 1, tmp.data(), tmp.size(), &cnt);
-        if (s2) return s2;
-        uint64_t keep = cnt;
-        if (!is_final && cnt && tmp[cnt - 1] == N) keep = cnt - 1;
-        if (keep > cap)
-            return fail(RCDC_ERR_CAPACITY, "need %llu cut slots, have %llu",
-                        (unsigned long long)keep, (unsigned long long)cap);
-        for (uint64_t i = 0; i < keep; i++) cuts[i] = st->base + tmp[i];
-        produced = keep;
-        const uint64_t consumed = keep ? tmp[keep - 1] : 0;
-        st->pending.erase(st->pending.begin(), st->pending.begin() + (long)consumed);
-        st->base += consumed;
+    // hand out what fits; the rest stays queued for the next call
+    uint64_t k = 0;
+    while (k < cap && !st->out.empty()) {
+        cuts[k++] = st->out.front();
+        st->out.pop_front();
     }
-    if (is_final) {
-        st->pending.clear();
-        st->done = true;
-    }
-    *n_cuts = produced;
+    *n_cuts = k;
     return RCDC_OK;
 }
 

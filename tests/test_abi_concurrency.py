@@ -1,0 +1,217 @@
+"""The drop-in boundary under the caller's real load:
+one ChunkIter per file on many worker threads at once (archiver.rs:195),
+each file fed in arbitrary read sizes (rabin.rs:162-182), and the reader
+error semantics of rabin.rs:131-138,173-180 (InputOutput, Interrupted
+retried).  GPU tests go through the C ABI (rcdc_stream_feed /
+rcdc_chunk_batch); the oracle is the checker."""
+import io
+import threading
+
+import numpy as np
+import pytest
+
+from oracle import oracle
+
+MiB = 1 << 20
+
+
+# ---------------------------------------------------------------- CPU: _read
+class _Flaky(io.RawIOBase):
+    """A reader whose read() raises `exc` on the listed calls."""
+
+    def __init__(self, data: bytes, fail_at=(), exc=InterruptedError, chunk=None):
+        self._b = io.BytesIO(data)
+        self._calls = 0
+        self._fail_at = set(fail_at)
+        self._exc = exc
+        self._chunk = chunk
+
+    def readable(self):
+        return True
+
+    def read(self, n=-1):
+        self._calls += 1
+        if self._calls in self._fail_at:
+            raise self._exc("injected")
+        if self._chunk:
+            n = min(n, self._chunk) if n and n > 0 else self._chunk
+        return self._b.read(n)
+
+
+def test_read_retries_interrupted_and_maps_io_errors():
+    """rabin.rs:173 retries ErrorKind::Interrupted; any other read error is
+    ErrorKind::InputOutput (rabin.rs:131-138, 174-180)."""
+    from rustic_core_amd.chunker import _read
+    from rustic_core_amd.errors import ErrorKind, RusticError
+    r = _Flaky(b"abcdef", fail_at=(1, 2))
+    assert _read(r, 4) == b"abcd"
+    r = _Flaky(b"abcdef", fail_at=(1,), exc=OSError)
+    with pytest.raises(RusticError) as e:
+        _read(r, 4)
+    assert e.value.kind == ErrorKind.InputOutput
+
+
+def test_stream_abi_symbols_reject_null(rcdc_lib):
+    assert rcdc_lib.rcdc_stream_queued(None) == 0
+    assert rcdc_lib.rcdc_stream_batch_bytes(None) == 0
+    assert rcdc_lib.rcdc_plan_finish(None) == 2
+
+
+# ---------------------------------------------------------------- GPU
+def _mixed(seed, n):
+    rng = np.random.default_rng(seed)
+    out = np.zeros(n, np.uint8)
+    p = 0
+    while p < n:
+        r = int(rng.integers(1, 3 * MiB))
+        out[p:p + r] = rng.integers(0, 256, len(out[p:p + r]), dtype=np.uint8)
+        p += r + int(rng.integers(1, 4 * MiB))
+    return out
+
+
+@pytest.mark.gpu
+def test_sixteen_threads_one_context(gpu_ctx):
+    """16 threads share one rcdc_ctx, each streams its own file in random
+    read sizes through rcdc_stream_feed; every cut list equals the oracle."""
+    from rustic_core_amd.chunker import _Stream
+    files = [_mixed(100 + t, (20 + 7 * t) * MiB + 13 * t) for t in range(16)]
+    want = [oracle.chunk_cuts(f) for f in files]
+    got = [None] * 16
+    errs = []
+
+    def work(t):
+        try:
+            rng = np.random.default_rng(t)
+            st = _Stream(gpu_ctx)
+            cuts, i, b = [], 0, files[t]
+            while i < b.size:
+                k = int(rng.integers(1, 9 * MiB))
+                piece = b[i:i + k]
+                i += piece.size
+                cuts.extend(st.feed(piece.tobytes(), i >= b.size).tolist())
+            st.close()
+            got[t] = np.array(cuts, np.uint64)
+        except Exception as e:  # pragma: no cover - reported below
+            errs.append((t, repr(e)))
+
+    th = [threading.Thread(target=work, args=(t,)) for t in range(16)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join()
+    assert not errs, errs
+    for t in range(16):
+        assert np.array_equal(got[t], want[t]), t
+
+
+@pytest.mark.gpu
+def test_threads_chunk_batch_one_context(gpu_ctx):
+    """rcdc_chunk_batch from 8 threads at once (lanes), 40 files each."""
+    bufs = [[oracle.stdrng_bytes(5000 + 40 * t + i, (i % 5 + 1) * MiB + 17 * i)
+             for i in range(40)] for t in range(8)]
+    got = [None] * 8
+
+    def work(t):
+        got[t] = gpu_ctx.chunk_batch(bufs[t])
+
+    th = [threading.Thread(target=work, args=(t,)) for t in range(8)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join()
+    for t in range(8):
+        for i, b in enumerate(bufs[t]):
+            assert np.array_equal(got[t][i], oracle.chunk_cuts(b)), (t, i)
+
+
+@pytest.mark.gpu
+def test_stream_queue_small_cap(gpu_ctx):
+    """A feed with too little cut space keeps the rest queued (no error, no
+    input consumed twice); len = 0 feeds drain it in order."""
+    import ctypes
+    from rustic_core_amd import _lib
+    L = _lib.lib()
+    data = np.zeros(40 * MiB, np.uint8)  # 80 chunks of min
+    h = ctypes.c_void_p()
+    assert L.rcdc_stream_open(gpu_ctx.handle, ctypes.byref(h)) == 0
+    cuts = np.zeros(3, np.uint64)
+    n = ctypes.c_uint64(0)
+    assert L.rcdc_stream_feed(h, data.ctypes.data, data.size, 1, cuts.ctypes.data, 3,
+                              ctypes.byref(n)) == 0
+    out = list(cuts[:n.value])
+    assert n.value == 3 and L.rcdc_stream_queued(h) == 77
+    while L.rcdc_stream_queued(h):
+        assert L.rcdc_stream_feed(h, None, 0, 1, cuts.ctypes.data, 3, ctypes.byref(n)) == 0
+        out += list(cuts[:n.value])
+    L.rcdc_stream_close(h)
+    assert np.array_equal(np.array(out, np.uint64), oracle.chunk_cuts(data))
+
+
+@pytest.mark.gpu
+def test_chunkiter_reader_errors(gpu_ctx):
+    """Interrupted reads are retried (same chunks); another read error ends
+    the iterator with ErrorKind::InputOutput (rabin.rs:131-138,173-180)."""
+    from rustic_core_amd import ChunkIter, ConfigFile
+    from rustic_core_amd.errors import ErrorKind, RusticError
+    cfg = ConfigFile.new(2, oracle.DEFAULT_POLY)
+    data = _mixed(7, 30 * MiB).tobytes()
+    want = oracle.chunk_cuts(np.frombuffer(data, np.uint8))
+    lens = [len(c) for c in ChunkIter.from_config(cfg, _Flaky(data, fail_at=(1, 3, 4),
+                                                               chunk=3 * MiB + 1), len(data))]
+    assert np.array_equal(np.cumsum(lens, dtype=np.uint64), want)
+    it = ChunkIter.from_config(cfg, _Flaky(data, fail_at=(2,), exc=OSError), len(data))
+    with pytest.raises(RusticError) as e:
+        list(it)
+    assert e.value.kind == ErrorKind.InputOutput
+    assert list(it) == []  # finished after the error
+
+
+@pytest.mark.gpu
+def test_plan_finish_device_views_after_fallback(monkeypatch, gpu_ctx):
+    """A walked stream forced onto the host redo (fixup capacity 1): after
+    rcdc_plan_finish the DEVICE views hold its cuts and blob ids, even when
+    the arena is overwritten right after the finish."""
+    import hashlib
+    import torch
+    from rustic_core_amd.chunker import Context
+    from rustic_core_amd.device import DevicePlan, pack_offsets
+    monkeypatch.setenv("RCDC_WALK_PIECE", str(128 << 10))
+    monkeypatch.setenv("RCDC_WALK_MIN_PIECES", "1")
+    monkeypatch.setenv("RCDC_WALK_FIXCAP", "1")
+    mn, avg, mx = 8 << 10, 16 << 10, 64 << 10
+    ctx = Context.get(oracle.DEFAULT_POLY, mn, avg, mx, device=0)
+    rng = np.random.default_rng(3)
+    a = np.concatenate([rng.integers(0, 256, 999, dtype=np.uint8), np.zeros(3 * MiB, np.uint8),
+                        rng.integers(0, 256, MiB, dtype=np.uint8)])
+    offs, alen = pack_offsets([a.size])
+    host = np.zeros(alen, np.uint8)
+    host[:a.size] = a
+    dev = torch.from_numpy(host).to("cuda:0")
+    plan = DevicePlan(ctx, offs, [a.size], alen)
+    plan.run(dev.data_ptr())
+    plan.hash(dev.data_ptr())
+    from rustic_core_amd import _lib
+    assert _lib.lib().rcdc_plan_finish(plan._h) == 0
+    dev.zero_()  # the arena is no longer needed
+    torch.cuda.synchronize()
+    want = oracle.chunk_cuts(a, oracle.DEFAULT_POLY, mn, avg, mx)
+    # the device views themselves: counts and cuts read straight from HBM
+    d_cuts, d_counts, base = plan.device_results()
+
+    class _View:  # a raw device pointer as a torch tensor (no copy)
+        def __init__(self, ptr, n):
+            self.__cuda_array_interface__ = {"shape": (n,), "typestr": "<u8",
+                                             "data": (ptr, False), "version": 2}
+
+    cnt = torch.as_tensor(_View(d_counts, 1), device="cuda:0").cpu().numpy()
+    assert int(cnt[0]) == len(want)
+    dc = torch.as_tensor(_View(d_cuts + 8 * int(base[0]), len(want)), device="cuda:0")
+    assert np.array_equal(dc.cpu().numpy().astype(np.uint64), want)
+    got = plan.results()[0]
+    assert np.array_equal(got, want)
+    digs = plan.digests()[0]
+    prev = 0
+    for j, c in enumerate(got):
+        assert bytes(digs[j]) == hashlib.sha256(a[prev:int(c)].tobytes()).digest(), j
+        prev = int(c)
+    plan.close()

@@ -1,0 +1,16 @@
+#!/bin/bash
+# Round-2 measurement pass: bench lines (C3 default, C2), rocprofv3 kernel
+# stats of the default bench command, and PMC passes (one counter per
+# rocprofv3 run) for HBM traffic.  Output under gpurun_out/$1.
+set -o pipefail
+OUT=gpurun_out/$1
+mkdir -p $OUT
+cd /tmp && export TMPDIR=/tmp && cd ${GRAFT_REPO_ROOT:-$(pwd)}
+python -c "import torch" || exit 1
+timeout -k 10 300 python bench.py --steps 20 --warmup 5 > $OUT/c3.json 2> $OUT/c3.err || exit 1
+timeout -k 10 200 python bench.py --workload C2 --steps 50 --warmup 5 > $OUT/c2.json 2> $OUT/c2.err || exit 1
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/stats -o run --output-format csv -- python bench.py --steps 20 --warmup 5 --no-cpu-baseline > $OUT/stats.log 2>&1 || exit 1
+for c in FETCH_SIZE WRITE_SIZE; do
+  timeout -s KILL 300 rocprofv3 --pmc $c -d $OUT/pmc_$c -o run --output-format csv -- python bench.py --steps 4 --warmup 1 --prewarm 0 --no-cpu-baseline --no-parity > $OUT/pmc_$c.log 2>&1 || exit 1
+done
+echo done

@@ -60,7 +60,7 @@ def run(kind, nstreams, sgib):
     for c in cuts:
         prev = np.concatenate([[0], c[:-1]]).astype(np.int64)
         L = c.astype(np.int64) - prev
-        full = L > oracle.DEFAULT_MIN
+        full = L >= oracle.DEFAULT_MIN
         ref += int(np.sum(L[full] - oracle.DEFAULT_MIN)) + 63 * int(np.count_nonzero(full))
     t0 = tr[:, 0].astype(np.int64)
     t1 = tr[:, 1].astype(np.int64)
