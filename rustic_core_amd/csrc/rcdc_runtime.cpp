@@ -11,6 +11,8 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
+#include <chrono>
 #include <cmath>
 #include <cerrno>
 #include <cstdarg>
@@ -919,20 +921,42 @@ void lane_release(rcdc_ctx *ctx, Lane *L) {
 
 constexpr uint64_t kStageBytes = 16ull << 20;  // per pinned staging slot
 
+// Host-path phase timing (RCDC_HOST_PROFILE=1: summary on stderr when the
+// context is destroyed): staging copies, waits for a staging slot, plan
+// (re)builds, device run + result copy.
+struct HostProfile {
+    std::atomic<uint64_t> ns[4] = {{0}, {0}, {0}, {0}};
+    std::atomic<uint64_t> passes{0}, bytes{0}, builds{0};
+};
+HostProfile g_hprof;
+const bool g_hprof_on = getenv("RCDC_HOST_PROFILE") != nullptr;
+
+inline uint64_t now_ns() {
+    return (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
+               std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+// One piece of host memory at an arena offset.
+struct HostPiece {
+    uint64_t off;
+    const uint8_t *p;
+    uint64_t n;
+};
+
 // Host bytes -> pinned staging (two slots, copy k + 1 overlapping the DMA of
 // copy k) -> the lane's device arena -> plan -> cuts, all on the lane's
-// stream.  The plan is rebuilt only when the batch layout changes.
-rcdc_status run_host_batch(rcdc_ctx *ctx, Lane *L, const rcdc_buf *bufs, uint32_t n,
-                           uint64_t *cuts, uint64_t cap, uint64_t *counts) {
-    std::vector<uint64_t> offs(n), lens(n);
+// stream.  Stream i of the batch is the concatenation of its pieces (a
+// streaming caller's buffered tail and its new read need no intermediate
+// copy).  The plan is rebuilt only when the batch layout changes.
+rcdc_status run_host_pieces(rcdc_ctx *ctx, Lane *L, const std::vector<uint64_t> &lens,
+                            const std::vector<HostPiece> &pieces, uint64_t *cuts, uint64_t cap,
+                            uint64_t *counts) {
+    const uint32_t n = (uint32_t)lens.size();
+    std::vector<uint64_t> offs(n);
     uint64_t total = 0;
     for (uint32_t i = 0; i < n; i++) {
-        if (bufs[i].len && !bufs[i].data)
-            return fail(RCDC_ERR_INVALID_INPUT, "buffer %u is NULL with length %llu", i,
-                        (unsigned long long)bufs[i].len);
         offs[i] = total;
-        lens[i] = bufs[i].len;
-        total = round_up(total + bufs[i].len, 256);
+        total = round_up(total + lens[i], 256);
     }
     const uint64_t arena_len = total + 256;
     DeviceGuard g(ctx->device);
@@ -943,22 +967,30 @@ rcdc_status run_host_batch(rcdc_ctx *ctx, Lane *L, const rcdc_buf *bufs, uint32_
         for (int k = 0; k < 2; k++)
             HIP_TRY(hipHostMalloc((void **)&L->pinned[k], L->stage, hipHostMallocDefault));
     }
+    uint64_t t_copy = 0, t_wait = 0, t0 = g_hprof_on ? now_ns() : 0;
     // staged copies: block k of the arena goes through slot k & 1
-    uint32_t bi = 0;  // first buffer that may overlap the block
+    size_t pi = 0;  // first piece that may overlap the block
     uint64_t k = 0;
     for (uint64_t p = 0; p < total; p += L->stage, k++) {
         const uint64_t e = std::min(p + L->stage, total);
         const int slot = (int)(k & 1);
-        if (k >= 2) HIP_TRY(hipEventSynchronize(L->ev[slot]));  // its previous DMA is done
-        uint8_t *dst = L->pinned[slot];
-        while (bi < n && offs[bi] + lens[bi] <= p) bi++;
-        for (uint32_t i = bi; i < n && offs[i] < e; i++) {
-            const uint64_t a = std::max(offs[i], p), b = std::min(offs[i] + lens[i], e);
-            if (a < b) memcpy(dst + (a - p), bufs[i].data + (a - offs[i]), b - a);
+        if (k >= 2) {
+            const uint64_t w0 = g_hprof_on ? now_ns() : 0;
+            HIP_TRY(hipEventSynchronize(L->ev[slot]));  // its previous DMA is done
+            if (g_hprof_on) t_wait += now_ns() - w0;
         }
+        const uint64_t c0 = g_hprof_on ? now_ns() : 0;
+        uint8_t *dst = L->pinned[slot];
+        while (pi < pieces.size() && pieces[pi].off + pieces[pi].n <= p) pi++;
+        for (size_t j = pi; j < pieces.size() && pieces[j].off < e; j++) {
+            const uint64_t a = std::max(pieces[j].off, p), b = std::min(pieces[j].off + pieces[j].n, e);
+            if (a < b) memcpy(dst + (a - p), pieces[j].p + (a - pieces[j].off), b - a);
+        }
+        if (g_hprof_on) t_copy += now_ns() - c0;
         HIP_TRY(hipMemcpyAsync(L->d_arena + p, dst, e - p, hipMemcpyHostToDevice, L->stream));
         HIP_TRY(hipEventRecord(L->ev[slot], L->stream));
     }
+    const uint64_t b0 = g_hprof_on ? now_ns() : 0;
     if (!L->plan || L->lay_offs != offs || L->lay_lens != lens || L->lay_arena != arena_len) {
         if (!L->plan) L->plan = new rcdc_plan();
         if ((st = plan_build(ctx, L->plan, offs.data(), lens.data(), n, arena_len))) {
@@ -968,9 +1000,39 @@ rcdc_status run_host_batch(rcdc_ctx *ctx, Lane *L, const rcdc_buf *bufs, uint32_
         L->lay_offs = offs;
         L->lay_lens = lens;
         L->lay_arena = arena_len;
+        if (g_hprof_on) g_hprof.builds++;
     }
+    const uint64_t r0 = g_hprof_on ? now_ns() : 0;
     if ((st = plan_run(L->plan, L->d_arena, L->stream))) return st;
-    return plan_results(L->plan, cuts, cap, counts);
+    st = plan_results(L->plan, cuts, cap, counts);
+    if (g_hprof_on) {
+        const uint64_t t1 = now_ns();
+        g_hprof.ns[0] += t_copy;
+        g_hprof.ns[1] += t_wait;
+        g_hprof.ns[2] += r0 - b0;
+        g_hprof.ns[3] += t1 - r0;
+        g_hprof.passes++;
+        g_hprof.bytes += total;
+        (void)t0;
+    }
+    return st;
+}
+
+rcdc_status run_host_batch(rcdc_ctx *ctx, Lane *L, const rcdc_buf *bufs, uint32_t n,
+                           uint64_t *cuts, uint64_t cap, uint64_t *counts) {
+    std::vector<uint64_t> lens(n);
+    std::vector<HostPiece> pieces;
+    pieces.reserve(n);
+    uint64_t off = 0;
+    for (uint32_t i = 0; i < n; i++) {
+        if (bufs[i].len && !bufs[i].data)
+            return fail(RCDC_ERR_INVALID_INPUT, "buffer %u is NULL with length %llu", i,
+                        (unsigned long long)bufs[i].len);
+        lens[i] = bufs[i].len;
+        if (bufs[i].len) pieces.push_back({off, bufs[i].data, bufs[i].len});
+        off = round_up(off + bufs[i].len, 256);
+    }
+    return run_host_pieces(ctx, L, lens, pieces, cuts, cap, counts);
 }
 
 bool valid_ctx(const rcdc_ctx *c) { return c != nullptr; }
@@ -1093,6 +1155,13 @@ rcdc_status rcdc_ctx_create(uint64_t poly, uint64_t min, uint64_t avg_pow2, uint
 
 void rcdc_ctx_destroy(rcdc_ctx *c) {
     if (!c) return;
+    if (g_hprof_on && g_hprof.passes)
+        fprintf(stderr,
+                "rcdc host path: %llu passes, %.1f MiB, %llu plan builds; thread-summed ms: "
+                "staging copy %.1f, slot waits %.1f, plan build %.1f, run+results %.1f\n",
+                (unsigned long long)g_hprof.passes.load(), g_hprof.bytes.load() / 1048576.0,
+                (unsigned long long)g_hprof.builds.load(), g_hprof.ns[0] / 1e6,
+                g_hprof.ns[1] / 1e6, g_hprof.ns[2] / 1e6, g_hprof.ns[3] / 1e6);
     {
         DeviceGuard g(c->device);
         if (c->stream) (void)hipStreamSynchronize(c->stream);
@@ -1403,24 +1472,34 @@ uint64_t rcdc_stream_queued(const rcdc_stream *st) { return st ? st->out.size() 
 // end of the buffer depends only on bytes before it, so it is final; the
 // end-of-buffer cut is final only at EOF.  The unfinished tail (< max bytes
 // from the last final cut) stays buffered and is re-chunked with more data.
-static rcdc_status stream_pass(rcdc_stream *st, bool is_final) {
+static rcdc_status stream_pass(rcdc_stream *st, const uint8_t *data, uint64_t len,
+                               bool is_final) {
     rcdc_ctx *ctx = st->ctx;
-    const uint64_t N = st->pending.size();
+    const uint64_t P = st->pending.size(), N = P + len;
     if (!N) return RCDC_OK;
     std::vector<uint64_t> tmp(rcdc_max_cuts(ctx, N));
-    rcdc_buf b{st->pending.data(), N};
+    std::vector<uint64_t> lens{N};
+    std::vector<HostPiece> pieces;
+    if (P) pieces.push_back({0, st->pending.data(), P});
+    if (len) pieces.push_back({P, data, len});
     uint64_t cnt = 0;
     Lane *L = nullptr;
     rcdc_status s2 = lane_acquire(ctx, &L);
     if (s2) return s2;
-    s2 = run_host_batch(ctx, L, &b, 1, tmp.data(), tmp.size(), &cnt);
+    s2 = run_host_pieces(ctx, L, lens, pieces, tmp.data(), tmp.size(), &cnt);
     lane_release(ctx, L);
     if (s2) return s2;
     uint64_t keep = cnt;
     if (!is_final && cnt && tmp[cnt - 1] == N) keep = cnt - 1;
     for (uint64_t i = 0; i < keep; i++) st->out.push_back(st->base + tmp[i]);
     const uint64_t consumed = keep ? tmp[keep - 1] : 0;
-    st->pending.erase(st->pending.begin(), st->pending.begin() + (long)consumed);
+    // the unfinished tail [consumed, N) becomes the new pending bytes
+    std::vector<uint8_t> tail;
+    tail.reserve(N - consumed);
+    if (consumed < P) tail.insert(tail.end(), st->pending.begin() + (long)consumed, st->pending.end());
+    const uint64_t d0 = consumed > P ? consumed - P : 0;
+    if (len > d0) tail.insert(tail.end(), data + d0, data + len);
+    st->pending.swap(tail);
     st->base += consumed;
     return RCDC_OK;
 }
@@ -1432,20 +1511,23 @@ rcdc_status rcdc_stream_feed(rcdc_stream *st, const uint8_t *data, uint64_t len,
     *n_cuts = 0;
     if (st->done && len) return fail(RCDC_ERR_INVALID_INPUT, "stream already finished");
     if (!st->done) {
-        st->pending.insert(st->pending.end(), data, data + len);
         // a device pass once enough bytes are buffered that cuts are certain
-        // (every chunk ends by chunk start + max), or at EOF
-        if (is_final || st->pending.size() >= st->batch) {
-            rcdc_status s2 = stream_pass(st, is_final != 0);
+        // (every chunk ends by chunk start + max), or at EOF; the new bytes
+        // go straight from the caller's buffer to the staging slots
+        if (is_final || st->pending.size() + len >= st->batch) {
+            rcdc_status s2 = stream_pass(st, data, len, is_final != 0);
             if (s2) {
-                // the bytes stay buffered: the caller may retry the feed with
+                // keep the bytes buffered: the caller may retry the feed with
                 // len = 0, or close the stream
+                st->pending.insert(st->pending.end(), data, data + len);
                 return s2;
             }
             if (is_final) {
                 st->pending.clear();
                 st->done = true;
             }
+        } else {
+            st->pending.insert(st->pending.end(), data, data + len);
         }
     }
     // hand out what fits; the rest stays queued for the next call
