@@ -847,6 +847,18 @@ def main():
                                           rank == 0 and world == 1 and not args.no_cpu_baseline)
     if args.e2e and rank == 0:
         out_extra["e2e"] = e2e_rate(torch, arena, offs, lens, plan, args.workload)
+    if args.abi_e2e and rank == 0 and os.path.exists(os.path.join(ROOT, "tools", "abi_e2e")):
+        # the native driver of the C ABI (tools/abi_e2e.cpp): 16 threads,
+        # 64 files x 256 MiB in pageable host memory, 16 MiB reads through
+        # rcdc_stream_feed, and rcdc_chunk_batch over the same files; the
+        # box's H2D copy rates beside them (the bound of this path)
+        import subprocess
+        r = subprocess.run([os.path.join(ROOT, "tools", "abi_e2e"), "--threads",
+                            str(args.abi_threads), "--files", "64", "--file-mib", "256",
+                            "--batch"] + (["--mixed"] if args.workload == "C3" else []),
+                           capture_output=True, text=True, timeout=300)
+        if r.returncode == 0:
+            out_extra["abi_e2e_native"] = json.loads(r.stdout.strip().splitlines()[-1])
     if args.abi_e2e and rank == 0 and args.workload in ("C2", "C3"):
         k = min(len(lens), args.abi_files)
         files = [arena[int(offs[i]):int(offs[i]) + int(lens[i])].cpu().numpy() for i in range(k)]

@@ -118,11 +118,12 @@ rcdc_status rcdc_chunk_batch(rcdc_ctx *ctx, const rcdc_buf *bufs, uint32_t n,
  * twice.  is_final = 1 marks EOF (the reference's Ok(0)); the last cut is
  * then the file length.
  * Retention: the stream buffers bytes until rcdc_stream_batch_bytes(ctx)
- * (64 MiB, at least 2 max + 256; environment RCDC_STREAM_BATCH) are
- * pending, then runs one device pass; afterwards it keeps only the tail
- * after the last final cut (< max bytes).  So at most batch + max + the
- * last piece fed are held -- more than the reference's 4 KiB + one chunk,
- * for one device pass per 64 MiB instead of one per chunk.
+ * (16 MiB, at least 2 max + 256; environment RCDC_STREAM_BATCH) would be
+ * pending, then runs one device pass over the buffered tail plus the new
+ * piece, straight from the caller's buffer; afterwards it keeps only the
+ * tail after the last final cut (< max bytes).  So at most batch + max
+ * bytes are held -- more than the reference's 4 KiB + one chunk, for one
+ * device pass per 16 MiB instead of a byte loop per chunk.
  * On an HIP failure the bytes stay buffered and the status is returned;
  * the feed may be retried with len = 0 (same is_final).                    */
 rcdc_status rcdc_stream_open(rcdc_ctx *ctx, rcdc_stream **out);

@@ -257,13 +257,17 @@ struct DeviceGuard {
     ~DeviceGuard() { (void)hipSetDevice(prev); }
 };
 
+// Device buffer of at least `need` elements.  Grows with 25 % headroom: a
+// reallocation's hipFree synchronises the whole device (every lane of every
+// thread), so slowly varying sizes (stream passes of batch + tail bytes)
+// must not reallocate each time.
 template <typename T>
 rcdc_status ensure_dev(T **p, uint64_t *cap, uint64_t need) {
     if (need <= *cap && *p) return RCDC_OK;
     if (*p) HIP_TRY(hipFree(*p));
     *p = nullptr;
     *cap = 0;
-    const uint64_t n = std::max<uint64_t>(need, 1);
+    const uint64_t n = std::max<uint64_t>(need + need / 4, 1);
     HIP_TRY(hipMalloc((void **)p, n * sizeof(T)));
     *cap = n;
     return RCDC_OK;
@@ -393,8 +397,11 @@ static uint64_t walk_piece_bytes(const uint64_t *lens, uint32_t n, uint64_t mn, 
     return lp;
 }
 
+// up: the stream the work lists are uploaded on (nullptr: synchronous copies).
+// Uploads from the plan's own host vectors, which stay unchanged until the
+// next build of this plan (after its previous run has been waited for).
 rcdc_status plan_build(rcdc_ctx *ctx, rcdc_plan *pl, const uint64_t *offs, const uint64_t *lens,
-                       uint32_t n, uint64_t arena_len) {
+                       uint32_t n, uint64_t arena_len, hipStream_t up = nullptr) {
     const uint64_t pos_lo = ctx->min + kWindow;  // first pure-window test position
     pl->ctx = ctx;
     pl->n = n;
@@ -533,6 +540,10 @@ rcdc_status plan_build(rcdc_ctx *ctx, rcdc_plan *pl, const uint64_t *offs, const
     pl->blocks = (uint32_t)std::min<uint64_t>(waves_needed, (uint64_t)std::max(ctx->num_cus, 1));
 
     DeviceGuard g(ctx->device);
+    auto upload = [up](void *dst, const void *src, size_t bytes) {
+        return up ? hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, up)
+                  : hipMemcpy(dst, src, bytes, hipMemcpyHostToDevice);
+    };
     rcdc_status st;
     if ((st = ensure_dev(&pl->d_items, &pl->cap_items, pl->items.size()))) return st;
     if ((st = ensure_dev(&pl->d_sds, &pl->cap_sds, n))) return st;
@@ -550,8 +561,7 @@ rcdc_status plan_build(rcdc_ctx *ctx, rcdc_plan *pl, const uint64_t *offs, const
         if ((st = ensure_dev(&pl->d_wsu0, &pl->cap_wsu0, pl->wstream_u0.size()))) return st;
         if ((st = ensure_dev(&pl->d_worder, &pl->cap_worder, nw))) return st;
         pl->wprm.order = pl->d_worder;
-        HIP_TRY(hipMemcpy(pl->d_worder, pl->worder.data(), nw * sizeof(uint32_t),
-                          hipMemcpyHostToDevice));
+        HIP_TRY(upload(pl->d_worder, pl->worder.data(), nw * sizeof(uint32_t)));
         if ((st = ensure_dev(&pl->d_wpiece, &pl->cap_wpiece, pl->nwpiece_cuts))) return st;
         if ((st = ensure_dev(&pl->d_pstatus, &pl->cap_pstatus, nw))) return st;
         if ((st = ensure_dev(&pl->d_bres, &pl->cap_bres, nw))) return st;
@@ -566,23 +576,19 @@ rcdc_status plan_build(rcdc_ctx *ctx, rcdc_plan *pl, const uint64_t *offs, const
             if ((st = ensure_dev(&pl->d_wtrace, &pl->cap_wtrace, nw * kTraceWords))) return st;
             pl->wprm.trace = pl->d_wtrace;
         }
-        HIP_TRY(hipMemcpy(pl->d_wunits, pl->wunits.data(), nw * sizeof(WalkUnit),
-                          hipMemcpyHostToDevice));
-        HIP_TRY(hipMemcpy(pl->d_wsu0, pl->wstream_u0.data(),
-                          pl->wstream_u0.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+        HIP_TRY(upload(pl->d_wunits, pl->wunits.data(), nw * sizeof(WalkUnit)));
+        HIP_TRY(upload(pl->d_wsu0, pl->wstream_u0.data(),
+                          pl->wstream_u0.size() * sizeof(uint32_t)));
     }
     if (!pl->units.empty())
-        HIP_TRY(hipMemcpy(pl->d_units, pl->units.data(), pl->units.size() * sizeof(ResolveUnit),
-                          hipMemcpyHostToDevice));
+        HIP_TRY(upload(pl->d_units, pl->units.data(), pl->units.size() * sizeof(ResolveUnit)));
     if (!pl->stitches.empty())
-        HIP_TRY(hipMemcpy(pl->d_stitches, pl->stitches.data(),
-                          pl->stitches.size() * sizeof(StitchDesc), hipMemcpyHostToDevice));
+        HIP_TRY(upload(pl->d_stitches, pl->stitches.data(),
+                          pl->stitches.size() * sizeof(StitchDesc)));
     if (!pl->items.empty())
-        HIP_TRY(hipMemcpy(pl->d_items, pl->items.data(), pl->items.size() * sizeof(ScanItem),
-                          hipMemcpyHostToDevice));
+        HIP_TRY(upload(pl->d_items, pl->items.data(), pl->items.size() * sizeof(ScanItem)));
     if (n)
-        HIP_TRY(hipMemcpy(pl->d_sds, pl->sds.data(), n * sizeof(StreamDesc),
-                          hipMemcpyHostToDevice));
+        HIP_TRY(upload(pl->d_sds, pl->sds.data(), n * sizeof(StreamDesc)));
     if (!pl->done) HIP_TRY(hipEventCreateWithFlags(&pl->done, hipEventDisableTiming));
     pl->ran = false;
     return RCDC_OK;
@@ -993,7 +999,7 @@ rcdc_status run_host_pieces(rcdc_ctx *ctx, Lane *L, const std::vector<uint64_t> 
     const uint64_t b0 = g_hprof_on ? now_ns() : 0;
     if (!L->plan || L->lay_offs != offs || L->lay_lens != lens || L->lay_arena != arena_len) {
         if (!L->plan) L->plan = new rcdc_plan();
-        if ((st = plan_build(ctx, L->plan, offs.data(), lens.data(), n, arena_len))) {
+        if ((st = plan_build(ctx, L->plan, offs.data(), lens.data(), n, arena_len, L->stream))) {
             L->lay_offs.clear();
             return st;
         }
@@ -1453,6 +1459,7 @@ rcdc_status rcdc_stream_open(rcdc_ctx *ctx, rcdc_stream **out) {
     rcdc_stream *s = new rcdc_stream();
     s->ctx = ctx;
     s->batch = rcdc_stream_batch_bytes(ctx);
+    s->pending.reserve(s->batch + ctx->max);
     *out = s;
     return RCDC_OK;
 }
@@ -1461,7 +1468,10 @@ void rcdc_stream_close(rcdc_stream *st) { delete st; }
 
 uint64_t rcdc_stream_batch_bytes(const rcdc_ctx *ctx) {
     if (!ctx) return 0;
-    uint64_t b = 64ull << 20;
+    // a pass per 16 MiB: large enough that a pass's fixed cost (plan, launch,
+    // result copy) is small, small enough that a typical read size triggers a
+    // pass straight from the caller's buffer (no intermediate copy)
+    uint64_t b = 16ull << 20;
     if (const char *e = getenv("RCDC_STREAM_BATCH")) b = (uint64_t)atoll(e);
     return std::max<uint64_t>(b, 2 * ctx->max + 256);
 }
@@ -1493,13 +1503,15 @@ static rcdc_status stream_pass(rcdc_stream *st, const uint8_t *data, uint64_t le
     if (!is_final && cnt && tmp[cnt - 1] == N) keep = cnt - 1;
     for (uint64_t i = 0; i < keep; i++) st->out.push_back(st->base + tmp[i]);
     const uint64_t consumed = keep ? tmp[keep - 1] : 0;
-    // the unfinished tail [consumed, N) becomes the new pending bytes
-    std::vector<uint8_t> tail;
-    tail.reserve(N - consumed);
-    if (consumed < P) tail.insert(tail.end(), st->pending.begin() + (long)consumed, st->pending.end());
-    const uint64_t d0 = consumed > P ? consumed - P : 0;
-    if (len > d0) tail.insert(tail.end(), data + d0, data + len);
-    st->pending.swap(tail);
+    // the unfinished tail [consumed, N) becomes the new pending bytes (in
+    // place: the buffer keeps its capacity)
+    if (consumed < P) {
+        st->pending.erase(st->pending.begin(), st->pending.begin() + (long)consumed);
+        st->pending.insert(st->pending.end(), data, data + len);
+    } else {
+        const uint64_t d0 = consumed - P;
+        st->pending.assign(data + d0, data + len);
+    }
     st->base += consumed;
     return RCDC_OK;
 }
