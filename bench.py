@@ -706,20 +706,9 @@ def main():
         a, b, e = desc["slice"]
         total_c5 = desc["stream_bytes_total"]
 
-        def chunk_from(s):
-            # the chain from s on this rank's bytes (s > a only after a failed
-            # merge: a fresh plan over the sub-stream), cut after the crossing
-            if s == a:
-                cuts = plan.results()[0] + a
-            else:
-                p2 = DevicePlan(ctx, np.array([s - a], np.uint64), np.array([e - s], np.uint64),
-                                int(arena.numel()))
-                p2.run(ptr, sptr)
-                cuts = p2.results()[0] + s
-                p2.close()
-            if e < total_c5:
-                cuts = cuts[:int(np.searchsorted(cuts, b)) + 1]
-            return cuts
+        from rustic_core_amd.shard import device_chunk_from
+        chunk_from = device_chunk_from(ctx, arena, a, b, e, total_c5, first_plan=plan,
+                                       stream=sptr)
 
         def step():  # noqa: F811
             plan.run(ptr, sptr)

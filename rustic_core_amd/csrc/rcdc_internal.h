@@ -109,14 +109,15 @@ struct WalkUnit {
     uint32_t piece;        // index within the stream
     uint32_t unit0;        // unit index of the stream's piece 0
     uint32_t npieces;
-    uint32_t pad;
+    uint32_t nbig;         // the stream's first nbig pieces are Lp long, the rest Ls
 };
 static_assert(sizeof(WalkUnit) == 48, "WalkUnit is 48 B");
 
 struct WalkParams {
     uint64_t min_size, max_size;
     uint64_t arena_len;
-    uint64_t piece_bytes;  // Lp: the (big) piece size; the last ones of a stream are smaller
+    uint64_t piece_bytes;  // Lp: the (big) piece size
+    uint64_t small_bytes;  // Ls: the size of a stream's last (split) pieces
     uint32_t seg_bytes;    // S: bytes per lane per round
     uint32_t mask;         // avg - 1
     uint32_t idx_shift;    // deg - 32

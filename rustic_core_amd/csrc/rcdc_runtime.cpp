@@ -154,6 +154,7 @@ struct rcdc_plan {
     std::vector<WalkUnit> wunits;
     std::vector<uint32_t> wstream_u0;  // unit0 of every walked stream
     std::vector<uint32_t> worder;      // walk queue order (big pieces first)
+    uint64_t walk_small = 0;           // Ls of the split pieces
     std::vector<uint8_t> walked;       // per stream: on the walk path
     uint64_t nwpiece_cuts = 0;
     WalkParams wprm{};
@@ -477,9 +478,17 @@ rcdc_status plan_build(rcdc_ctx *ctx, rcdc_plan *pl, const uint64_t *offs, const
     pl->worder.clear();
     pl->nwpiece_cuts = 0;
     {
-        uint64_t split_pct = 20;
+        // splitting pays only when a wave takes several pieces (the tail is
+        // then the last pieces' length); with about one piece per wave slot
+        // (C5: 3200 pieces, 4096 slots) it only adds boundaries
+        uint64_t big_total = 0;
+        for (uint32_t i = 0; i < n && Lp; i++)
+            if (pl->walked[i]) big_total += std::max<uint64_t>(lens[i] / Lp, 1);
+        const uint64_t slots = (uint64_t)std::max(ctx->num_cus, 1) * 16;
+        uint64_t split_pct = big_total >= 2 * slots ? 20 : 0;
         if (const char *e = getenv("RCDC_WALK_SPLIT")) split_pct = std::min<uint64_t>(atoll(e), 100);
         const uint64_t Ls = Lp ? std::max<uint64_t>(Lp / 4 / ctx->min, 1) * ctx->min : 0;
+        pl->walk_small = Ls;
         std::vector<uint32_t> small;
         for (uint32_t i = 0; i < n && Lp; i++) {
             if (!pl->walked[i]) continue;
@@ -513,7 +522,10 @@ rcdc_status plan_build(rcdc_ctx *ctx, rcdc_plan *pl, const uint64_t *offs, const
                         add(a + k * Ls, k + 1 < q ? a + (k + 1) * Ls : e, true);
                 }
             }
-            for (uint32_t k = u0; k < (uint32_t)pl->wunits.size(); k++) pl->wunits[k].npieces = j;
+            for (uint32_t k = u0; k < (uint32_t)pl->wunits.size(); k++) {
+                pl->wunits[k].npieces = j;
+                pl->wunits[k].nbig = (uint32_t)(P - nsplit);
+            }
         }
         pl->worder.insert(pl->worder.end(), small.begin(), small.end());
     }
@@ -523,6 +535,7 @@ rcdc_status plan_build(rcdc_ctx *ctx, rcdc_plan *pl, const uint64_t *offs, const
     wp.max_size = ctx->max;
     wp.arena_len = arena_len;
     wp.piece_bytes = Lp ? Lp : 1;
+    wp.small_bytes = pl->walk_small ? pl->walk_small : wp.piece_bytes;
     wp.seg_bytes = 2048;
     if (const char *e = getenv("RCDC_WALK_SEG")) wp.seg_bytes = (uint32_t)std::max(atoi(e) / 128 * 128, 128);
     wp.mask = (uint32_t)(ctx->avg - 1);

@@ -142,6 +142,27 @@ __device__ uint32_t zero_run(const uint8_t *s, uint64_t N, uint64_t mn, uint64_t
     return bad ? (uint32_t)__builtin_ctzll(bad) : 64u;
 }
 
+// Work counters (WalkParams.stats): per-workgroup sums in LDS and one global
+// atomic per counter and workgroup at the end -- the same few global
+// addresses hit once per piece serialise at the L2 (C5: 5120 pieces, 15 k
+// atomics on one line cost more than the walk itself).
+struct BlockStats {
+    unsigned long long v[kWalkStats];
+};
+
+__device__ __forceinline__ void stats_init(BlockStats &S) {
+    if (threadIdx.x < kWalkStats) S.v[threadIdx.x] = 0;  // (a barrier follows)
+}
+
+__device__ __forceinline__ void stats_add(BlockStats &S, int i, uint64_t x) {
+    if (x) atomicAdd(&S.v[i], (unsigned long long)x);
+}
+
+__device__ __forceinline__ void stats_flush(BlockStats &S, unsigned long long *g) {
+    __syncthreads();
+    if (threadIdx.x < kWalkStats && S.v[threadIdx.x]) atomicAdd(&g[threadIdx.x], S.v[threadIdx.x]);
+}
+
 // A walker over one stream: one wave (LANES = 64) or one workgroup of 1024.
 struct Walk {
     const uint8_t *arena;
@@ -308,6 +329,8 @@ __global__ __launch_bounds__(1024, 1) void rcdc_walk_kernel(
     uint64_t *__restrict__ piece_cuts, uint64_t *__restrict__ pstatus, uint32_t *ctr) {
     __shared__ __attribute__((aligned(16))) uint8_t s_tab[kLdsBytes];
     __shared__ __attribute__((aligned(16))) uint8_t s_win[16][128];
+    __shared__ BlockStats s_st;
+    stats_init(s_st);
     fill_tables(s_tab, gtab, prm.idx_shift, threadIdx.x, 1024);
     const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
     Walk W;
@@ -371,9 +394,9 @@ __global__ __launch_bounds__(1024, 1) void rcdc_walk_kernel(
         if (lane == 0) {
             pstatus[u] = min(n, (uint64_t)U.out_cap) | (open ? kOpenFlag : 0ull) |
                          (n > U.out_cap ? (kOpenFlag << 1) : 0ull);
-            atomicAdd(&prm.stats[kWalkStatRounds], (unsigned long long)W.rounds);
-            atomicAdd(&prm.stats[kWalkStatZones], (unsigned long long)W.zones);
-            atomicAdd(&prm.stats[kWalkStatChunks], (unsigned long long)n);
+            stats_add(s_st, kWalkStatRounds, W.rounds);
+            stats_add(s_st, kWalkStatZones, W.zones);
+            stats_add(s_st, kWalkStatChunks, n);
             if (prm.trace) {
                 unsigned long long *tr = prm.trace + (uint64_t)u * kTraceWords;
                 tr[0] = t0;
@@ -383,6 +406,7 @@ __global__ __launch_bounds__(1024, 1) void rcdc_walk_kernel(
             }
         }
     }
+    stats_flush(s_st, prm.stats);
 }
 
 // ---------------------------------------------------------------------------
@@ -438,6 +462,20 @@ __device__ __forceinline__ uint64_t lower_cut(const uint64_t *L, uint64_t n, uin
     return lo;
 }
 
+// lower_cut for a wave-uniform query: piece lists are short (<= Lp / min +
+// max / min + 4 entries), so a wave reads 64 of them per round trip instead
+// of a chain of dependent loads.
+__device__ __forceinline__ uint64_t lower_cut_wave(const uint64_t *L, uint64_t n, uint64_t p) {
+    const uint32_t lane = __lane_id();
+    for (uint64_t i0 = 0; i0 < n; i0 += 64) {
+        const uint64_t i = i0 + lane;
+        const uint64_t v = i < n ? (L[i] & kCutVal) : ~0ull;
+        const uint64_t ge = __builtin_amdgcn_ballot_w64(v >= p);
+        if (ge) return i0 + (uint64_t)__builtin_ctzll(ge);
+    }
+    return n;
+}
+
 // What piece V knows about position p: returns true if a searched interval
 // holds p -- [p, *vend) is hit-free, and *vkind says what *vend is (kKindHit:
 // a hit; kKindMax / kOpen: nothing known at *vend; kKindEof: p .. N hit-free);
@@ -447,7 +485,7 @@ __device__ bool cover(const PieceView &V, uint64_t p, uint64_t mn, uint64_t *ven
                       uint64_t *next) {
     *next = ~0ull;
     if (!V.full) return false;
-    const uint64_t t = lower_cut(V.L, V.n, p);
+    const uint64_t t = lower_cut_wave(V.L, V.n, p);
     if (t < V.n) {
         const uint64_t prev = t ? (V.L[t - 1] & kCutVal) : V.start;
         const uint64_t base = prev + mn + 64;
@@ -484,6 +522,7 @@ struct CheckCtx {
     WalkUnit U;   // the boundary's unit (piece j)
     uint32_t u;   // its index
     uint64_t N, mn, mx;
+    uint64_t Lp, Ls;  // piece sizes (piece_at)
     uint64_t budget;  // bytes this boundary may still hash
 };
 
@@ -502,8 +541,17 @@ __device__ __forceinline__ uint32_t piece_at(const WalkUnit *units, uint32_t uni
     return lo;
 }
 
+// The same in closed form: nbig pieces of Lp, then pieces of Ls, the last
+// one running to N.
+__device__ __forceinline__ uint32_t piece_at(const WalkUnit &U, uint64_t Lp, uint64_t Ls,
+                                             uint64_t p) {
+    const uint64_t B = (uint64_t)U.nbig * Lp;
+    const uint64_t k = p < B ? p / Lp : (uint64_t)U.nbig + (p - B) / Ls;
+    return (uint32_t)min(k, (uint64_t)U.npieces - 1);
+}
+
 __device__ __forceinline__ uint32_t piece_of(const CheckCtx &C, uint64_t p) {
-    return piece_at(C.units, C.U.unit0, C.U.npieces, p);
+    return piece_at(C.U, C.Lp, C.Ls, p);
 }
 
 // First pure-window hit in [lo, lim) of the stream, or lim if none;
@@ -585,6 +633,8 @@ __global__ __launch_bounds__(kChkThreads, 1) void rcdc_walk_check_kernel(
     __shared__ __attribute__((aligned(16))) uint8_t s_tab[kLdsBytes];
     __shared__ __attribute__((aligned(16))) uint8_t s_win[kChkThreads / 64][128];
     __shared__ uint64_t s_hops[kChkThreads / 64][kMaxHops];  // the wave's hop entries
+    __shared__ BlockStats s_st;
+    stats_init(s_st);
     fill_tables(s_tab, gtab, prm.idx_shift, threadIdx.x, kChkThreads);
     const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
     Walk W;
@@ -626,6 +676,8 @@ __global__ __launch_bounds__(kChkThreads, 1) void rcdc_walk_check_kernel(
         C.N = N;
         C.mn = mn;
         C.mx = mx;
+        C.Lp = prm.piece_bytes;
+        C.Ls = prm.small_bytes;
         C.budget = kCheckBudgetMax * mx;
         // result (wave-uniform scalars; the hop entries in LDS, not in a
         // dynamically indexed register array, which would go to scratch)
@@ -753,10 +805,11 @@ __global__ __launch_bounds__(kChkThreads, 1) void rcdc_walk_check_kernel(
             B->merge_idx = R.merge_idx;
             B->fix_from = R.fix_from;
             if (R.kind == kBoundFixup) fixlist[atomicAdd(&ctr[1], 1u)] = u;
-            atomicAdd(&prm.stats[kWalkStatChkRounds], (unsigned long long)W.rounds);
-            atomicAdd(&prm.stats[kWalkStatChkZones], (unsigned long long)W.zones);
+            stats_add(s_st, kWalkStatChkRounds, W.rounds);
+            stats_add(s_st, kWalkStatChkZones, W.zones);
         }
     }
+    stats_flush(s_st, prm.stats);
 }
 
 // ---------------------------------------------------------------------------
@@ -825,7 +878,7 @@ __global__ __launch_bounds__(1024, 1) void rcdc_walk_fixup_kernel(
                     if (cut >= d.n) {
                         stop = true;
                     } else {
-                        const uint64_t k = piece_at(units, U.unit0, U.npieces, cut);
+                        const uint64_t k = piece_at(U, prm.piece_bytes, prm.small_bytes, cut);
                         for (int back = 0; back < 2 && mu == kNoUnit; back++) {
                             if (back == 1 && k == 0) break;
                             const uint32_t uk = U.unit0 + (uint32_t)(k - back);

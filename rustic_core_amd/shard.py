@@ -173,3 +173,32 @@ def chunk_long_stream_sharded(total: int, rank: int, world: int, min_size: int,
         if r == rank:
             entry = x
             mine = np.asarray(chunk_from(x), dtype=np.uint64)
+
+
+def device_chunk_from(ctx, arena, a: int, b: int, e: int, total: int, first_plan=None,
+                      stream: Optional[int] = None) -> Callable[[int], np.ndarray]:
+    """The device `chunk_from` of chunk_long_stream_sharded for rank slice
+    [a, b) with readable extent [a, e): `arena` (a CUDA uint8 tensor) holds
+    stream bytes [a, e) at offset 0.  The chain from s is a fresh plan over
+    arena[s - a, e - a) as an independent stream (a stream starting at s is
+    exactly the chain with a cut at s), or `first_plan`'s last run for
+    s == a; cuts are truncated after the first one >= b (beyond it the halo's
+    end looks like EOF)."""
+    from .device import DevicePlan
+
+    def chunk_from(s: int) -> np.ndarray:
+        if s == a and first_plan is not None:
+            cuts = first_plan.results()[0] + np.uint64(a)
+        else:
+            p = DevicePlan(ctx, np.array([s - a], np.uint64), np.array([e - s], np.uint64),
+                           int(arena.numel()))
+            try:
+                p.run(arena.data_ptr(), stream)
+                cuts = p.results()[0] + np.uint64(s)
+            finally:
+                p.close()
+        if e < total:
+            cuts = cuts[:int(np.searchsorted(cuts, b)) + 1]
+        return cuts
+
+    return chunk_from

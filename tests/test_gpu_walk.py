@@ -169,8 +169,9 @@ def test_walk_selected_by_default_for_large_batches():
     g.manual_seed(90)
     arena = torch.randint(0, 256, (alen,), dtype=torch.uint8, device="cuda:0", generator=g)
     plan = DevicePlan(ctx, offs, lens, alen)
-    # 16 pieces of 4 MiB per stream; the last 20 % (3) cut into 4 each
-    assert plan.info()["walk_pieces"] == 64 * (13 + 3 * 4)
+    # 16 pieces of 4 MiB per stream; 1024 pieces are fewer than two per wave
+    # slot (256 CUs x 16 waves), so none is split (RCDC_WALK_SPLIT forces it)
+    assert plan.info()["walk_pieces"] == 1024
     plan.run(arena.data_ptr())
     got = plan.results()
     plan.close()
@@ -178,6 +179,16 @@ def test_walk_selected_by_default_for_large_batches():
         o = int(offs[i])
         host = arena[o:o + lens[i]].cpu().numpy()
         assert np.array_equal(got[i], oracle.chunk_cuts(host, oracle.DEFAULT_POLY, mn, avg, mx))
+
+
+def test_walk_split_pieces(walk_env, monkeypatch):
+    """The split tail pieces (RCDC_WALK_SPLIT: the last share of a stream's
+    pieces cut in four, handed out last) on every data kind."""
+    walk_env(256 * KiB)
+    monkeypatch.setenv("RCDC_WALK_SPLIT", "50")
+    _run(SMALL, [_rand(95, 6 * MiB + 5), np.zeros(5 * MiB, np.uint8),
+                 _mixed(96, 8 * MiB, 4 * KiB, 512 * KiB, 1 * KiB, 600 * KiB),
+                 np.concatenate([_rand(97, 999), np.zeros(3 * MiB, np.uint8), _rand(98, MiB)])])
 
 
 def test_walk_many_pieces_per_stream(walk_env):

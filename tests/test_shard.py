@@ -177,3 +177,73 @@ def test_long_stream_single_rank_no_process_group():
         len(data), 0, 1, LPARAMS["min_size"], LPARAMS["max_size"],
         lambda s: oracle.chunk_cuts(data[s:], oracle.DEFAULT_POLY, **LPARAMS) + s)
     assert np.array_equal(cuts, oracle.chunk_cuts(data, oracle.DEFAULT_POLY, **LPARAMS))
+
+
+# ------------------------------------- the device path over ranks (GPU, gloo)
+def _device_long_worker(rank, world, port, errfile, kind, params):
+    """Rank r holds only its slice + halo on cuda:0 and chunks it with the real
+    device plan (shard.device_chunk_from); the cross-rank stitch runs over
+    gloo (several ranks share the one GPU of the test box)."""
+    import torch
+    import torch.distributed as dist
+    from oracle import oracle
+    from rustic_core_amd.chunker import Context
+    from rustic_core_amd.shard import chunk_long_stream_sharded, device_chunk_from, slice_bounds
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        mn, avg, mx = params
+        data = _long_data(kind) if mn < 65536 else _long_data_big(kind)
+        total = len(data)
+        a, b, e = slice_bounds(total, world, mn, mx)[rank]
+        torch.cuda.set_device(0)
+        arena = torch.zeros(e - a + 256, dtype=torch.uint8, device="cuda:0")
+        arena[:e - a] = torch.from_numpy(np.ascontiguousarray(data[a:e])).to("cuda:0")
+        ctx = Context.get(oracle.DEFAULT_POLY, mn, avg, mx, device=0)
+        mine = chunk_long_stream_sharded(total, rank, world, mn, mx,
+                                         device_chunk_from(ctx, arena, a, b, e, total))
+        parts = [None] * world
+        dist.all_gather_object(parts, mine)
+        got = np.concatenate([np.asarray(p, np.uint64) for p in parts])
+        want = oracle.chunk_cuts(data, oracle.DEFAULT_POLY, mn, avg, mx)
+        assert np.array_equal(got, want), (kind, len(got), len(want))
+        dist.barrier()
+    except Exception as ex:  # pragma: no cover
+        with open(errfile, "a") as f:
+            f.write(f"rank {rank}: {ex!r}\n")
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+def _long_data_big(kind):
+    """40 MiB + 3 for the default parameters (min 512 KiB)."""
+    rng = np.random.default_rng(22)
+    n = 40 * (1 << 20) + 3
+    if kind == "zeros":
+        return np.zeros(n, np.uint8)
+    if kind == "phase_zeros":
+        a = np.zeros(n, np.uint8)
+        a[:123457] = rng.integers(0, 256, 123457, dtype=np.uint8)
+        return a
+    if kind == "random":
+        return rng.integers(0, 256, n, dtype=np.uint8)
+    out = np.zeros(n, np.uint8)
+    i = 0
+    while i < n:
+        k = int(rng.integers(64 << 10, 4 << 20))
+        if rng.random() < 0.5:
+            out[i:i + k] = rng.integers(0, 256, len(out[i:i + k]), dtype=np.uint8)
+        i += k
+    return out
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind", ["zeros", "phase_zeros", "random", "mixed"])
+@pytest.mark.parametrize("params", [(4096, 16384, 65536), (512 << 10, 1 << 20, 8 << 20)],
+                         ids=["small", "default"])
+def test_long_stream_sharded_device_gloo(tmp_path, kind, params):
+    import torch.multiprocessing as mp
+    err = str(tmp_path / "err.txt")
+    mp.spawn(_device_long_worker, args=(2, _free_port(), err, kind, params), nprocs=2, join=True)
+    assert not os.path.exists(err)
