@@ -49,9 +49,9 @@ _lib = None
 def lib():
     global _lib
     if _lib is None:
-        src = os.path.join(_HERE, "cdc_ref.c")
-        if not os.path.exists(_SO) or (
-            os.path.exists(src) and os.path.getmtime(src) > os.path.getmtime(_SO)
+        srcs = [os.path.join(_HERE, f) for f in ("cdc_ref.c", "crypto_ref.c")]
+        if not os.path.exists(_SO) or any(
+            os.path.exists(src) and os.path.getmtime(src) > os.path.getmtime(_SO) for src in srcs
         ):
             build()
         L = ctypes.CDLL(_SO)
@@ -80,6 +80,16 @@ def lib():
         L.cdc_ref_stdrng_fill.restype = None
         L.cdc_ref_stdrng_fill_at.argtypes = [u64, u64, p, sz]
         L.cdc_ref_stdrng_fill_at.restype = None
+        L.crypto_ref_seal.argtypes = [p, p, p, sz, p]
+        L.crypto_ref_seal.restype = None
+        L.crypto_ref_open.argtypes = [p, p, sz, p]
+        L.crypto_ref_open.restype = ctypes.c_int
+        L.crypto_ref_aes_expand.argtypes = [p, ctypes.c_int, p]
+        L.crypto_ref_aes_expand.restype = ctypes.c_int
+        L.crypto_ref_aes_encrypt.argtypes = [p, ctypes.c_int, p, p]
+        L.crypto_ref_aes_encrypt.restype = None
+        L.crypto_ref_poly1305.argtypes = [p, p, p, sz, p]
+        L.crypto_ref_poly1305.restype = None
         _lib = L
     return _lib
 
@@ -193,3 +203,52 @@ def table_arrays(poly: int = DEFAULT_POLY):
     t = tables(poly)
     return (np.array(t.out_table[:], dtype=np.uint64),
             np.array(t.mod_table[:], dtype=np.uint64), t.degree, t.shift)
+
+
+# ------------------------------------------------------------ blob encryption
+# rustic Key::encrypt_data / decrypt_data (crates/core/src/crypto/aespoly1305.rs:88-135)
+# restated in oracle/crypto_ref.c (aes256ctr_poly1305aes 0.2.1 = the restic format).
+def _buf(b) -> np.ndarray:
+    return np.frombuffer(bytes(b), dtype=np.uint8) if not isinstance(b, np.ndarray) else \
+        np.ascontiguousarray(b, dtype=np.uint8).reshape(-1)
+
+
+def aes_encrypt_block(key: bytes, block: bytes) -> bytes:
+    """One AES-128/256 block encryption (FIPS-197)."""
+    rk = np.zeros(60, np.uint32)
+    k = _buf(key)
+    nr = lib().crypto_ref_aes_expand(_ptr(k), len(key) // 4, _ptr(rk))
+    out = np.zeros(16, np.uint8)
+    lib().crypto_ref_aes_encrypt(_ptr(rk), nr, _ptr(_buf(block)), _ptr(out))
+    return out.tobytes()
+
+
+def poly1305(r: bytes, s: bytes, msg: bytes) -> bytes:
+    out = np.zeros(16, np.uint8)
+    m = _buf(msg) if len(msg) else np.zeros(1, np.uint8)
+    lib().crypto_ref_poly1305(_ptr(_buf(r)), _ptr(_buf(s)), _ptr(m), len(msg), _ptr(out))
+    return out.tobytes()
+
+
+def seal(key: bytes, nonce: bytes, data) -> bytes:
+    """nonce || AES-256-CTR ciphertext || Poly1305-AES tag."""
+    d = _buf(data) if len(data) else np.zeros(1, np.uint8)
+    n = len(data)
+    out = np.zeros(n + 32, np.uint8)
+    lib().crypto_ref_seal(_ptr(_buf(key)), _ptr(_buf(nonce)), _ptr(d), n, _ptr(out))
+    return out.tobytes()
+
+
+class MacMismatch(ValueError):
+    """decrypt_data: MAC check failed (ErrorKind::Cryptography, aespoly1305.rs:97-108)."""
+
+
+def open_(key: bytes, data) -> bytes:
+    d = _buf(data)
+    out = np.zeros(max(d.size - 32, 1), np.uint8)
+    st = lib().crypto_ref_open(_ptr(_buf(key)), _ptr(d), d.size, _ptr(out))
+    if st == 2:
+        raise ValueError("data too short")
+    if st == 1:
+        raise MacMismatch("MAC check failed")
+    return out[:d.size - 32].tobytes()
