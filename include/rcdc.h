@@ -261,6 +261,39 @@ rcdc_status rcdc_plan_digests(rcdc_plan *plan, uint8_t *digests,
 /* Device view: slot-indexed like rcdc_plan_device_results' d_cuts. */
 rcdc_status rcdc_plan_device_digests(rcdc_plan *plan, uint64_t *d_digests);
 
+/* ---- blob encryption: crypto/aespoly1305.rs:88-135 `Key::encrypt_data` /
+ * `decrypt_data` (aes256ctr_poly1305aes 0.2.1, the restic format), applied
+ * by the packer to every new blob (blob/packer.rs:268-270,
+ * backend/decrypt.rs:566-572) -- here to chunks already in HBM. ---------- */
+
+/* One blob.  seal: data [in_off, in_off + len) of d_in becomes
+ * nonce || AES-256-CTR ciphertext || Poly1305-AES tag (len + 32 bytes) at
+ * out_off of d_out.  open: the sealed blob [in_off, in_off + len) (len >= 32)
+ * becomes its len - 32 plaintext bytes at out_off.  out_off must be 16-byte
+ * aligned; in_off may have any alignment (allow 4 readable bytes after the
+ * data).  The nonce is the caller's (rustic draws it at random, :117). */
+typedef struct {
+    uint64_t in_off;
+    uint64_t len;
+    uint64_t out_off;
+    uint8_t nonce[16]; /* seal only; open reads it from the blob */
+} rcdc_aead_ref;
+
+/* key: 64 bytes, AES-256 key || Poly1305-AES k || r (aespoly1305.rs:15-24).
+ * refs is a HOST array.  Asynchronous on hip_stream (0: the context's
+ * stream); calls on one context take turns (the second waits for the
+ * first's kernels).                                                         */
+rcdc_status rcdc_aead_seal(rcdc_ctx *ctx, const uint8_t *key, const void *d_in,
+                           const rcdc_aead_ref *refs, uint32_t n, void *d_out,
+                           void *hip_stream);
+/* status[i] (host array): 0 = MAC ok, 1 = MAC mismatch or shorter than
+ * nonce + tag (ErrorKind::Cryptography, aespoly1305.rs:97-108; the plaintext
+ * written is then not to be used), 2 = shorter than 16 bytes (:89-94).
+ * Synchronous.                                                              */
+rcdc_status rcdc_aead_open(rcdc_ctx *ctx, const uint8_t *key, const void *d_in,
+                           const rcdc_aead_ref *refs, uint32_t n, void *d_out,
+                           uint32_t *status, void *hip_stream);
+
 /* ABI version of the loaded library (== RCDC_ABI_VERSION). */
 uint32_t rcdc_abi_version(void);
 

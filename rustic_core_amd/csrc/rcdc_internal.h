@@ -169,4 +169,29 @@ struct FixRes {
     uint32_t pad;
 };
 
+// ---- blob encryption (rcdc_aead.hip) ---------------------------------------
+constexpr uint32_t kAeadUnitBlocks = 4096;  // 16-byte blocks per wave work unit (64 KiB)
+
+struct AeadKeyDev {
+    uint32_t rk256[60];    // AES-256 round keys (big-endian column words)
+    uint32_t rk128[44];    // AES-128 round keys of Poly1305-AES's k
+    uint32_t rpow[65][5];  // r^0 .. r^64, 26-bit limbs (r clamped)
+    uint32_t r2j[32][5];   // r^(2^j)
+    uint32_t te[256];      // T-table: (2S, S, S, 3S) as a big-endian word
+};
+
+struct AeadBlob {  // 40 B
+    uint64_t in_off;   // seal: plaintext; open: nonce || ct || tag
+    uint64_t len;      // plaintext / ciphertext bytes
+    uint64_t out_off;  // seal: nonce || ct || tag; open: plaintext (16-B aligned)
+    uint32_t nonce[4]; // the nonce's bytes as 4 little-endian words
+};
+static_assert(sizeof(AeadBlob) == 40, "AeadBlob is 40 B");
+
+struct AeadUnit {  // 16 B
+    uint32_t blob;
+    uint32_t b0, b1;   // block range [b0, b1) of the blob
+    uint32_t pad;
+};
+
 }  // namespace rcdc

@@ -61,6 +61,10 @@ hipError_t launch_sha256_multi(uint32_t n, const uint8_t *const *arenas,
                                const uint64_t *nslots, uint64_t max_len, uint32_t *const *bwork,
                                uint32_t *const *order, uint32_t *const *digests,
                                hipStream_t stream);
+hipError_t launch_aead(bool open, const uint8_t *in, uint8_t *out, const AeadBlob *blobs,
+                       uint32_t nblobs, const AeadUnit *units, uint32_t nunits,
+                       const uint32_t *unit0, const AeadKeyDev *key, uint32_t *partials,
+                       uint32_t *status, uint32_t cus, hipStream_t stream);
 }  // namespace rcdc
 
 using namespace rcdc;
@@ -236,6 +240,17 @@ struct rcdc_ctx {
     std::condition_variable pool_cv;
     std::vector<Lane *> lanes, free_lanes;
     uint32_t max_lanes = 16;
+    // blob encryption (rcdc_aead_*): calls on one context take turns
+    std::mutex aead_mu;
+    uint8_t aead_key[64] = {0};
+    bool aead_key_set = false;
+    AeadKeyDev *d_aead_key = nullptr;
+    AeadBlob *d_aead_blobs = nullptr;
+    AeadUnit *d_aead_units = nullptr;
+    uint32_t *d_aead_unit0 = nullptr, *d_aead_partials = nullptr, *d_aead_status = nullptr;
+    uint64_t cap_aead_key = 0, cap_aead_blobs = 0, cap_aead_units = 0, cap_aead_unit0 = 0,
+             cap_aead_partials = 0, cap_aead_status = 0;
+    hipEvent_t aead_done = nullptr;
 };
 
 struct rcdc_stream {
@@ -1186,6 +1201,13 @@ void rcdc_ctx_destroy(rcdc_ctx *c) {
         if (c->stream) (void)hipStreamSynchronize(c->stream);
         for (Lane *L : c->lanes) lane_free(c, L);
         (void)hipFree(c->d_tables);
+        (void)hipFree(c->d_aead_key);
+        (void)hipFree(c->d_aead_blobs);
+        (void)hipFree(c->d_aead_units);
+        (void)hipFree(c->d_aead_unit0);
+        (void)hipFree(c->d_aead_partials);
+        (void)hipFree(c->d_aead_status);
+        if (c->aead_done) (void)hipEventDestroy(c->aead_done);
         if (c->stream) (void)hipStreamDestroy(c->stream);
     }
     delete c;
@@ -1463,6 +1485,196 @@ rcdc_status rcdc_plan_device_digests(rcdc_plan *plan, uint64_t *d_digests) {
     if (!plan->hashed) return fail(RCDC_ERR_INVALID_INPUT, "rcdc_plan_hash has not been run");
     *d_digests = (uint64_t)(uintptr_t)plan->d_dig;
     return RCDC_OK;
+}
+
+// ---- blob encryption (crypto/aespoly1305.rs:88-135 over HBM) ---------------
+
+}  // extern "C"
+
+namespace {
+
+// AES S-box from its definition (multiplicative inverse in GF(2^8), then the
+// affine map; FIPS-197 5.1.1), and the T-table / key schedules on the host.
+void aes_sbox(uint8_t sb[256]) {
+    uint8_t p = 1, q = 1;
+    do {
+        p = (uint8_t)(p ^ (p << 1) ^ ((p & 0x80) ? 0x1b : 0));  // p * 3
+        q ^= (uint8_t)(q << 1);                                  // q / 3
+        q ^= (uint8_t)(q << 2);
+        q ^= (uint8_t)(q << 4);
+        if (q & 0x80) q ^= 0x09;
+        const uint8_t x = (uint8_t)(q ^ (uint8_t)((q << 1) | (q >> 7)) ^
+                                    (uint8_t)((q << 2) | (q >> 6)) ^
+                                    (uint8_t)((q << 3) | (q >> 5)) ^ (uint8_t)((q << 4) | (q >> 4)));
+        sb[p] = x ^ 0x63;
+    } while (p != 1);
+    sb[0] = 0x63;
+}
+
+void aes_expand_host(const uint8_t *key, int nk, const uint8_t sb[256], uint32_t *rk) {
+    const int nr = nk + 6;
+    uint8_t rcon = 1;
+    for (int i = 0; i < nk; i++)
+        rk[i] = (uint32_t)key[4 * i] << 24 | (uint32_t)key[4 * i + 1] << 16 |
+                (uint32_t)key[4 * i + 2] << 8 | key[4 * i + 3];
+    auto sub = [&](uint32_t t) {
+        return (uint32_t)sb[t >> 24] << 24 | (uint32_t)sb[(t >> 16) & 255] << 16 |
+               (uint32_t)sb[(t >> 8) & 255] << 8 | sb[t & 255];
+    };
+    for (int i = nk; i < 4 * (nr + 1); i++) {
+        uint32_t t = rk[i - 1];
+        if (i % nk == 0) {
+            t = sub((t << 8) | (t >> 24)) ^ (uint32_t)rcon << 24;
+            rcon = (uint8_t)((rcon << 1) ^ ((rcon & 0x80) ? 0x1b : 0));
+        } else if (nk > 6 && i % nk == 4) {
+            t = sub(t);
+        }
+        rk[i] = rk[i - nk] ^ t;
+    }
+}
+
+// 2^130 - 5 arithmetic in 26-bit limbs (the device pmul, on the host)
+void p26_mul(const uint32_t a[5], const uint32_t b[5], uint32_t r[5]) {
+    const uint64_t b0 = b[0], b1 = b[1], b2 = b[2], b3 = b[3], b4 = b[4];
+    const uint64_t s1 = b1 * 5, s2 = b2 * 5, s3 = b3 * 5, s4 = b4 * 5;
+    const uint64_t a0 = a[0], a1 = a[1], a2 = a[2], a3 = a[3], a4 = a[4];
+    uint64_t d0 = a0 * b0 + a1 * s4 + a2 * s3 + a3 * s2 + a4 * s1;
+    uint64_t d1 = a0 * b1 + a1 * b0 + a2 * s4 + a3 * s3 + a4 * s2;
+    uint64_t d2 = a0 * b2 + a1 * b1 + a2 * b0 + a3 * s4 + a4 * s3;
+    uint64_t d3 = a0 * b3 + a1 * b2 + a2 * b1 + a3 * b0 + a4 * s4;
+    uint64_t d4 = a0 * b4 + a1 * b3 + a2 * b2 + a3 * b1 + a4 * b0;
+    d1 += d0 >> 26; d2 += d1 >> 26; d3 += d2 >> 26; d4 += d3 >> 26;
+    uint64_t h0 = (d0 & 0x3ffffff) + (d4 >> 26) * 5;
+    r[1] = (uint32_t)((d1 & 0x3ffffff) + (h0 >> 26));
+    r[0] = (uint32_t)(h0 & 0x3ffffff);
+    r[2] = (uint32_t)(d2 & 0x3ffffff);
+    r[3] = (uint32_t)(d3 & 0x3ffffff);
+    r[4] = (uint32_t)(d4 & 0x3ffffff);
+    // fully normalise (r[1] may carry)
+    const uint32_t c = r[1] >> 26;
+    r[1] &= 0x3ffffff;
+    r[2] += c;
+}
+
+void aead_key_material(const uint8_t key[64], AeadKeyDev *K) {
+    uint8_t sb[256];
+    aes_sbox(sb);
+    for (int x = 0; x < 256; x++) {
+        const uint8_t s1 = sb[x], s2 = (uint8_t)((s1 << 1) ^ ((s1 & 0x80) ? 0x1b : 0));
+        const uint8_t s3 = s2 ^ s1;
+        K->te[x] = (uint32_t)s2 << 24 | (uint32_t)s1 << 16 | (uint32_t)s1 << 8 | s3;
+    }
+    aes_expand_host(key, 8, sb, K->rk256);
+    aes_expand_host(key + 32, 4, sb, K->rk128);
+    uint8_t rb[16];
+    memcpy(rb, key + 48, 16);
+    rb[3] &= 15; rb[7] &= 15; rb[11] &= 15; rb[15] &= 15;
+    rb[4] &= 252; rb[8] &= 252; rb[12] &= 252;
+    uint64_t t0 = 0, t1 = 0;
+    for (int i = 7; i >= 0; i--) {
+        t0 = t0 << 8 | rb[i];
+        t1 = t1 << 8 | rb[8 + i];
+    }
+    const uint32_t r[5] = {(uint32_t)(t0 & 0x3ffffff), (uint32_t)((t0 >> 26) & 0x3ffffff),
+                           (uint32_t)(((t0 >> 52) | (t1 << 12)) & 0x3ffffff),
+                           (uint32_t)((t1 >> 14) & 0x3ffffff), (uint32_t)((t1 >> 40) & 0x3ffffff)};
+    const uint32_t one[5] = {1, 0, 0, 0, 0};
+    memcpy(K->rpow[0], one, sizeof one);
+    for (int i = 1; i <= 64; i++) p26_mul(K->rpow[i - 1], r, K->rpow[i]);
+    memcpy(K->r2j[0], r, sizeof r);
+    for (int j = 1; j < 32; j++) p26_mul(K->r2j[j - 1], K->r2j[j - 1], K->r2j[j]);
+}
+
+rcdc_status aead_run(rcdc_ctx *ctx, bool open, const uint8_t key[64], const void *d_in,
+                     const rcdc_aead_ref *refs, uint32_t n, void *d_out, uint32_t *status,
+                     void *hip_stream) {
+    if (!valid_ctx(ctx) || !key || (n && (!refs || !d_in || !d_out)) || (open && n && !status))
+        return fail(RCDC_ERR_INVALID_INPUT, "null argument");
+    std::vector<AeadBlob> blobs;
+    std::vector<AeadUnit> units;
+    std::vector<uint32_t> unit0, which;  // which: device blob -> caller index
+    blobs.reserve(n);
+    for (uint32_t i = 0; i < n; i++) {
+        const rcdc_aead_ref &r = refs[i];
+        if (r.out_off & 15)
+            return fail(RCDC_ERR_INVALID_INPUT, "blob %u: out_off must be 16-byte aligned", i);
+        if (open && r.len < 32) {
+            // no room for nonce + tag: aespoly1305.rs:89-94 (< 16 bytes) and
+            // the AEAD's own length check (16..31) both fail before any MAC
+            status[i] = r.len < 16 ? 2u : 1u;
+            continue;
+        }
+        which.push_back(i);
+        unit0.push_back((uint32_t)units.size());
+        blobs.emplace_back();
+        AeadBlob &b = blobs.back();
+        const uint32_t bi = (uint32_t)blobs.size() - 1;
+        b.in_off = r.in_off;
+        b.len = open ? r.len - 32 : r.len;
+        b.out_off = r.out_off;
+        uint8_t nonce[16];
+        memcpy(nonce, r.nonce, 16);
+        memcpy(b.nonce, nonce, 16);  // little-endian words of the nonce bytes
+        const uint64_t nb = (b.len + 15) / 16;
+        if (nb >= (1ull << 32)) return fail(RCDC_ERR_UNSUPPORTED, "blob %u too large", i);
+        for (uint64_t b0 = 0; b0 < nb; b0 += kAeadUnitBlocks)
+            units.push_back({bi, (uint32_t)b0, (uint32_t)std::min<uint64_t>(nb, b0 + kAeadUnitBlocks), 0});
+    }
+    const uint32_t m = (uint32_t)blobs.size();
+    unit0.push_back((uint32_t)units.size());
+    std::lock_guard<std::mutex> lk(ctx->aead_mu);
+    DeviceGuard g(ctx->device);
+    hipStream_t st = hip_stream ? (hipStream_t)hip_stream : ctx->stream;
+    if (ctx->aead_done) HIP_TRY(hipEventSynchronize(ctx->aead_done));  // the scratch is free
+    else HIP_TRY(hipEventCreateWithFlags(&ctx->aead_done, hipEventDisableTiming));
+    rcdc_status rs;
+    if ((rs = ensure_dev(&ctx->d_aead_key, &ctx->cap_aead_key, 1))) return rs;
+    if (!ctx->aead_key_set || memcmp(ctx->aead_key, key, 64) != 0) {
+        AeadKeyDev K;
+        aead_key_material(key, &K);
+        HIP_TRY(hipMemcpy(ctx->d_aead_key, &K, sizeof K, hipMemcpyHostToDevice));
+        memcpy(ctx->aead_key, key, 64);
+        ctx->aead_key_set = true;
+    }
+    if ((rs = ensure_dev(&ctx->d_aead_blobs, &ctx->cap_aead_blobs, m))) return rs;
+    if ((rs = ensure_dev(&ctx->d_aead_units, &ctx->cap_aead_units, units.size()))) return rs;
+    if ((rs = ensure_dev(&ctx->d_aead_unit0, &ctx->cap_aead_unit0, m + 1))) return rs;
+    if ((rs = ensure_dev(&ctx->d_aead_partials, &ctx->cap_aead_partials, units.size() * 5))) return rs;
+    if ((rs = ensure_dev(&ctx->d_aead_status, &ctx->cap_aead_status, m))) return rs;
+    if (m) {
+        HIP_TRY(hipMemcpy(ctx->d_aead_blobs, blobs.data(), m * sizeof(AeadBlob), hipMemcpyHostToDevice));
+        HIP_TRY(hipMemcpy(ctx->d_aead_unit0, unit0.data(), (m + 1) * 4, hipMemcpyHostToDevice));
+    }
+    if (!units.empty())
+        HIP_TRY(hipMemcpy(ctx->d_aead_units, units.data(), units.size() * sizeof(AeadUnit),
+                          hipMemcpyHostToDevice));
+    HIP_TRY(launch_aead(open, (const uint8_t *)d_in, (uint8_t *)d_out, ctx->d_aead_blobs, m,
+                        ctx->d_aead_units, (uint32_t)units.size(), ctx->d_aead_unit0,
+                        ctx->d_aead_key, ctx->d_aead_partials, ctx->d_aead_status,
+                        (uint32_t)std::max(ctx->num_cus, 1), st));
+    HIP_TRY(hipEventRecord(ctx->aead_done, st));
+    if (open) {
+        HIP_TRY(hipEventSynchronize(ctx->aead_done));
+        std::vector<uint32_t> ds(m);
+        if (m) HIP_TRY(hipMemcpy(ds.data(), ctx->d_aead_status, m * 4, hipMemcpyDeviceToHost));
+        for (uint32_t j = 0; j < m; j++) status[which[j]] = ds[j];
+    }
+    return RCDC_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+rcdc_status rcdc_aead_seal(rcdc_ctx *ctx, const uint8_t *key, const void *d_in,
+                           const rcdc_aead_ref *refs, uint32_t n, void *d_out, void *hip_stream) {
+    return aead_run(ctx, false, key, d_in, refs, n, d_out, nullptr, hip_stream);
+}
+
+rcdc_status rcdc_aead_open(rcdc_ctx *ctx, const uint8_t *key, const void *d_in,
+                           const rcdc_aead_ref *refs, uint32_t n, void *d_out, uint32_t *status,
+                           void *hip_stream) {
+    return aead_run(ctx, true, key, d_in, refs, n, d_out, status, hip_stream);
 }
 
 // ---- streaming: one file fed in pieces -------------------------------------

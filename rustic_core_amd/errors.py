@@ -14,6 +14,7 @@ class ErrorKind(enum.Enum):
     InvalidInput = "InvalidInput"    # configfile.rs:166-171 (poly hex)
     Internal = "Internal"            # device / runtime failure
     InputOutput = "InputOutput"      # rabin.rs:131-138,174-180 (reader errors)
+    Cryptography = "Cryptography"    # crypto/aespoly1305.rs:89-108 (MAC check)
 
 
 class RusticError(Exception):
