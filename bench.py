@@ -79,6 +79,10 @@ def parse():
     ap.add_argument("--pipeline", action="store_true",
                     help="overlap run k's resolve with run k+1's scan (rcdc_plan_set_pipeline; "
                          "measured slower on C2: the resolve waves starve behind the scan)")
+    ap.add_argument("--aead", action="store_true",
+                    help="also seal + open the chunks as blobs on the device (rcdc_aead_*)")
+    ap.add_argument("--aead-streams", type=int, default=16,
+                    help="--aead: blobs = the chunks of the first N streams")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-parity", action="store_true")
     ap.add_argument("--abi-e2e", action="store_true",
@@ -834,6 +838,9 @@ def main():
     if args.sha256:
         out_extra["sha256"] = sha_measure(torch, plan, ptr, sptr, dev, args, arena, offs, lens,
                                           rank == 0 and world == 1 and not args.no_cpu_baseline)
+    if args.aead and rank == 0:
+        out_extra["aead"] = aead_measure(torch, plan, arena, offs, lens, dev, args,
+                                         world == 1 and not args.no_cpu_baseline)
     if args.e2e and rank == 0:
         out_extra["e2e"] = e2e_rate(torch, arena, offs, lens, plan, args.workload)
     if args.abi_e2e and rank == 0 and os.path.exists(os.path.join(ROOT, "tools", "abi_e2e")):
@@ -1002,6 +1009,97 @@ def sha_measure(torch, plan, ptr, sptr, dev, args, arena, offs, lens, cpu: bool)
             hashlib.sha256(sample).digest()
             n += len(sample)
         out["cpu_hashlib_gibs_1thread"] = round(n / (time.perf_counter() - t0) / GiB, 3)
+    return out
+
+
+def aead_measure(torch, plan, arena, offs, lens, dev, args, cpu: bool) -> dict:
+    """Blob encryption of the chunks just cut: every
+    chunk of the first --aead-streams streams becomes one blob, sealed
+    (crypto/aespoly1305.rs:119-135, per blob as blob/packer.rs:268-270 does)
+    into a packed output arena and opened back (:88-108).  Kernel time by
+    HIP events on the launch stream; spot checks against the oracle; the
+    oracle's 1-thread C AES-CTR + Poly1305 as the CPU rate."""
+    from rustic_core_amd.crypto import Key, make_refs, sealed_layout
+    ns = min(len(lens), max(args.aead_streams, 1))
+    cuts = plan.results()[:ns]
+    in_offs, blens = [], []
+    for i in range(ns):
+        prev = 0
+        for c in cuts[i]:
+            in_offs.append(int(offs[i]) + prev)
+            blens.append(int(c) - prev)
+            prev = int(c)
+    nb = len(blens)
+    tot = int(sum(blens))
+    rng = np.random.default_rng(0x5EA1)
+    key = Key(rng.integers(0, 256, 64, dtype=np.uint8).tobytes())
+    nonces = rng.integers(0, 256, (nb, 16), dtype=np.uint8)
+    oo, olen = sealed_layout(blens)
+    seal_refs = make_refs(in_offs, blens, oo, nonces)
+    sealed = torch.empty(olen + 64, dtype=torch.uint8, device=dev)
+    po, p = [], 0
+    for n in blens:
+        po.append(p)
+        p = (p + n + 15) // 16 * 16
+    open_refs = make_refs(oo, [n + 32 for n in blens], po)
+    plain = torch.empty(p + 64, dtype=torch.uint8, device=dev)
+    side = torch.cuda.Stream(dev)
+    sp = side.cuda_stream
+    a, s_ptr, pl = arena.data_ptr(), sealed.data_ptr(), plain.data_ptr()
+    key.seal_blobs(a, seal_refs, s_ptr, sp)
+    st = key.open_blobs(s_ptr, open_refs, pl, sp)
+    torch.cuda.synchronize(dev)
+    k = 5
+    e = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+    e[0].record(side)
+    for _ in range(k):
+        key.seal_blobs(a, seal_refs, s_ptr, sp)
+    e[1].record(side)
+    torch.cuda.synchronize(dev)
+    seal_ms = e[0].elapsed_time(e[1]) / k
+    # open is synchronous (status to the host): time the launches the same way
+    e[2].record(side)
+    for _ in range(k):
+        st = key.open_blobs(s_ptr, open_refs, pl, sp)
+    e[3].record(side)
+    torch.cuda.synchronize(dev)
+    open_ms = e[2].elapsed_time(e[3]) / k
+    from oracle import oracle
+    checked = mism = 0
+    idx = sorted(set([0, 1, nb - 1] + [int(x) for x in rng.integers(0, nb, 5)]))
+    for i in idx:
+        d = arena[in_offs[i]:in_offs[i] + blens[i]].cpu().numpy().tobytes()
+        want = oracle.seal(key._key, nonces[i].tobytes(), d)
+        got = sealed[int(oo[i]):int(oo[i]) + blens[i] + 32].cpu().numpy().tobytes()
+        back = plain[po[i]:po[i] + blens[i]].cpu().numpy().tobytes()
+        mism += (got != want) + (back != d)
+        checked += 1
+    out = {
+        "kernel": "rcdc_aead_unit_kernel (+ rcdc_aead_finish_kernel)",
+        "blobs": nb,
+        "bytes": tot,
+        "seal_ms_per_launch": round(seal_ms, 3),
+        "seal_gibs": round(tot / (seal_ms / 1e3) / GiB, 2),
+        "open_ms_per_launch": round(open_ms, 3),
+        "open_gibs": round(tot / (open_ms / 1e3) / GiB, 2),
+        "hbm_frac_seal": round(2 * tot / (seal_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
+        "bound": "VALU/LDS issue: AES-256 = 14 rounds x 16 T-table LDS lookups + ~40 VALU per "
+                 "16-byte block, Poly1305 ~30 VALU per block (DESIGN.md 3d)",
+        "mac_failures": int(np.count_nonzero(st)),
+        "spot_check": {"blobs": checked, "mismatches": int(mism),
+                       "checker": "oracle/crypto_ref (seal) + round trip (open)"},
+    }
+    if cpu:
+        sample = arena[in_offs[0]:in_offs[0] + min(tot, 64 << 20)].cpu().numpy().tobytes()
+        t0, n = time.perf_counter(), 0
+        while time.perf_counter() - t0 < 3.0:
+            oracle.seal(key._key, nonces[0].tobytes(), sample)
+            n += len(sample)
+        out["cpu_baseline"] = {"value": round(n / (time.perf_counter() - t0) / GiB, 3),
+                               "unit": "GiB/s", "cores": 1, "kind": "port",
+                               "sample": f"oracle seal of {len(sample) >> 20} MiB, repeated 3 s"}
+    del sealed, plain
+    torch.cuda.empty_cache()
     return out
 
 

@@ -7,17 +7,25 @@
 //   sealed blob = nonce (16) || AES-256-CTR_{K_enc, IV = nonce}(data) || tag (16)
 //   tag         = (poly1305_r(ciphertext) + AES-128_{K_k}(nonce)) mod 2^128
 //
-// Work: a blob is cut into units of kUnitBlocks 16-byte blocks; one wave per
-// unit.  Lane l takes blocks l, l + 64, ... of the unit: counter block =
-// nonce + block index (128-bit big-endian), AES-256 with one T-table
-// replicated per lane in LDS (64 copies: every ds_read_b32 of a wave hits 64
-// distinct banks), keystream XOR data, and the ciphertext block goes into the
-// lane's Poly1305 accumulator by Horner with R = r^64 (26-bit limbs).  The
-// lanes combine with r^(unit end - lane's last block) and a wave reduction;
-// the unit's partial is positioned with r^(blocks after the unit) (binary
-// powers of r).  rcdc_aead_finish_kernel sums a blob's partials mod
-// 2^130 - 5, adds AES-128_k(nonce) and writes (seal) or checks (open) the
-// tag.  Poly1305 is linear in the message blocks, so this split is exact.
+// Work: a blob is cut into units of kAeadUnitBlocks 16-byte blocks; one wave
+// per unit.  Lane l takes blocks l, l + 64, ... of the unit, two per step (two
+// independent AES chains; the next step's data already loading): counter
+// block = nonce + block index (128-bit big-endian), AES-256 by T-tables in
+// LDS, keystream XOR data, and the ciphertext block goes into the lane's
+// Poly1305 accumulator by Horner with R = r^64 (26-bit limbs).  The lanes
+// combine with r^(unit end - lane's last block) and a wave reduction; the
+// unit's partial is positioned with r^(blocks after the unit) (binary powers
+// of r).  rcdc_aead_finish_kernel sums a blob's partials mod 2^130 - 5, adds
+// AES-128_k(nonce) and writes (seal) or checks (open) the tag.  Poly1305 is
+// linear in the message blocks, so this split is exact.
+//
+// Tables: T and its 3 byte rotations (no v_alignbit per lookup), 32 copies
+// each (copy = lane & 31: ds_read_b32 banks are (a/4) mod 32 per 32-lane
+// half, so every lookup is conflict-free), 128 KiB: one 1024-thread
+// workgroup per CU.  A lookup address is ONE v_perm_b32 (tlu); a round is
+// 16 v_perm + 16 ds_read_b32 + 8 v_bitop3 (3-input XOR, round key from an
+// SGPR).  Measured (tools/aead_prof.py): ~725 GiB/s seal on
+// 8 GiB of 0.5-8 MiB blobs; VALU and LDS each ~2/3 busy.
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
@@ -27,7 +35,11 @@
 using namespace rcdc;
 
 namespace rcdc {
-constexpr int kAeadThreads = 512;  // 8 waves; 2 workgroups per CU (64 KiB LDS each)
+// 16 waves, one workgroup per CU (the 128 KiB of tables): 4 waves per SIMD,
+// up to 128 VGPRs
+constexpr int kAeadThreads = 1024;
+constexpr int kAeadBlocksPerCU = 1;
+constexpr uint32_t kAeadTableWords = 2u * 256u * 64u;
 }  // namespace rcdc
 
 namespace {
@@ -101,43 +113,67 @@ __device__ __forceinline__ P26 pblock(const uint32_t w[4], uint32_t k) {
     return m;
 }
 
-// AES encryption of one block held as 4 big-endian column words; T-table
-// entry e of copy c at LDS word e * 64 + c (c = lane), rk in LDS (uniform).
+// a ^ b ^ c in one VALU op (gfx950 v_bitop3_b32, truth table 0x96)
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+    uint32_t r;
+    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+
+// a ^ b ^ k, k a wave-uniform value held in an SGPR (the round key)
+__device__ __forceinline__ uint32_t xor3k(uint32_t a, uint32_t b, uint32_t k) {
+    uint32_t r;
+    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(r) : "v"(a), "v"(b), "s"(k));
+    return r;
+}
+
+// Lookup of byte K of s in table j: LDS byte address
+//   (j >> 1) << 16 | e << 8 | (j & 1) << 7 | c * 4      (e = the byte, c = lane & 31)
+// i.e. byte 1 of the address is e and bytes 0, 2 come from the lane's
+// constant Lj = the rest: ONE v_perm_b32 builds it.
+template <int K>
+__device__ __forceinline__ uint32_t tlu(const uint8_t *__restrict__ tt, uint32_t s, uint32_t Lj) {
+    constexpr uint32_t sel = 0x0c020000u | ((4u + K) << 8);
+    const uint32_t a = __builtin_amdgcn_perm(s, Lj, sel);
+    return *reinterpret_cast<const uint32_t *>(tt + a);
+}
+
+// AES encryption of one block held as 4 big-endian column words; round keys
+// uniform (rk: global, scalar loads), tables in LDS (see tlu; lane4 = L0).
 template <int NR>
 __device__ __forceinline__ void aes_block(uint32_t &s0, uint32_t &s1, uint32_t &s2, uint32_t &s3,
-                                          const uint32_t *__restrict__ tt, uint32_t lane,
+                                          const uint8_t *__restrict__ tt, uint32_t lane4,
                                           const uint32_t *__restrict__ rk) {
     s0 ^= rk[0]; s1 ^= rk[1]; s2 ^= rk[2]; s3 ^= rk[3];
-#define TE(x) tt[((x) << 6) | lane]
+    // table j = T rotated right by 8 j (no v_alignbit per lookup)
+    const uint32_t L1 = lane4 + 128u, L2 = lane4 | 0x10000u, L3 = (lane4 + 128u) | 0x10000u;
 #pragma unroll
     for (int r = 1; r < NR; r++) {
-        const uint4 k = *reinterpret_cast<const uint4 *>(rk + 4 * r);
-        const uint32_t t0 = TE(s0 >> 24) ^ ror32(TE((s1 >> 16) & 255), 8) ^
-                            ror32(TE((s2 >> 8) & 255), 16) ^ ror32(TE(s3 & 255), 24) ^ k.x;
-        const uint32_t t1 = TE(s1 >> 24) ^ ror32(TE((s2 >> 16) & 255), 8) ^
-                            ror32(TE((s3 >> 8) & 255), 16) ^ ror32(TE(s0 & 255), 24) ^ k.y;
-        const uint32_t t2 = TE(s2 >> 24) ^ ror32(TE((s3 >> 16) & 255), 8) ^
-                            ror32(TE((s0 >> 8) & 255), 16) ^ ror32(TE(s1 & 255), 24) ^ k.z;
-        const uint32_t t3 = TE(s3 >> 24) ^ ror32(TE((s0 >> 16) & 255), 8) ^
-                            ror32(TE((s1 >> 8) & 255), 16) ^ ror32(TE(s2 & 255), 24) ^ k.w;
+        const uint32_t t0 = xor3k(xor3(tlu<3>(tt, s0, lane4), tlu<2>(tt, s1, L1), tlu<1>(tt, s2, L2)),
+                                  tlu<0>(tt, s3, L3), rk[4 * r]);
+        const uint32_t t1 = xor3k(xor3(tlu<3>(tt, s1, lane4), tlu<2>(tt, s2, L1), tlu<1>(tt, s3, L2)),
+                                  tlu<0>(tt, s0, L3), rk[4 * r + 1]);
+        const uint32_t t2 = xor3k(xor3(tlu<3>(tt, s2, lane4), tlu<2>(tt, s3, L1), tlu<1>(tt, s0, L2)),
+                                  tlu<0>(tt, s1, L3), rk[4 * r + 2]);
+        const uint32_t t3 = xor3k(xor3(tlu<3>(tt, s3, lane4), tlu<2>(tt, s0, L1), tlu<1>(tt, s1, L2)),
+                                  tlu<0>(tt, s2, L3), rk[4 * r + 3]);
         s0 = t0; s1 = t1; s2 = t2; s3 = t3;
     }
-    // final round: SubBytes (S[x] = byte 2 of T[x]) + ShiftRows + AddRoundKey
-    const uint4 k = *reinterpret_cast<const uint4 *>(rk + 4 * NR);
-#define SB3(x) ((TE(x) << 8) & 0xff000000u)
-#define SB2(x) (TE(x) & 0x00ff0000u)
-#define SB1(x) ((TE(x) >> 8) & 0x0000ff00u)
-#define SB0(x) ((TE(x) >> 16) & 0x000000ffu)
-    const uint32_t t0 = SB3(s0 >> 24) | SB2((s1 >> 16) & 255) | SB1((s2 >> 8) & 255) | SB0(s3 & 255);
-    const uint32_t t1 = SB3(s1 >> 24) | SB2((s2 >> 16) & 255) | SB1((s3 >> 8) & 255) | SB0(s0 & 255);
-    const uint32_t t2 = SB3(s2 >> 24) | SB2((s3 >> 16) & 255) | SB1((s0 >> 8) & 255) | SB0(s1 & 255);
-    const uint32_t t3 = SB3(s3 >> 24) | SB2((s0 >> 16) & 255) | SB1((s1 >> 8) & 255) | SB0(s2 & 255);
-#undef SB0
-#undef SB1
-#undef SB2
-#undef SB3
-#undef TE
-    s0 = t0 ^ k.x; s1 = t1 ^ k.y; s2 = t2 ^ k.z; s3 = t3 ^ k.w;
+    // final round: SubBytes (S[x] = byte 2 of T[x]) + ShiftRows + AddRoundKey;
+    // v_perm gathers byte 2 of four lookups into one word
+    const uint32_t *k = rk + 4 * NR;
+#define SBW(a, b, c, d)                                                                    \
+    __builtin_amdgcn_perm(__builtin_amdgcn_perm(tlu<3>(tt, a, lane4), tlu<2>(tt, b, lane4), \
+                                                0x0c0c0602u),                              \
+                          __builtin_amdgcn_perm(tlu<1>(tt, c, lane4), tlu<0>(tt, d, lane4), \
+                                                0x0c0c0602u),                              \
+                          0x05040100u)
+    const uint32_t t0 = SBW(s0, s1, s2, s3);
+    const uint32_t t1 = SBW(s1, s2, s3, s0);
+    const uint32_t t2 = SBW(s2, s3, s0, s1);
+    const uint32_t t3 = SBW(s3, s0, s1, s2);
+#undef SBW
+    s0 = t0 ^ k[0]; s1 = t1 ^ k[1]; s2 = t2 ^ k[2]; s3 = t3 ^ k[3];
 }
 
 // Unaligned 16-byte load at byte address p (4 dwords + 1 from the 4-aligned
@@ -204,10 +240,15 @@ __device__ __forceinline__ void pfull(P26 &a) {
     }
 }
 
-__device__ __forceinline__ void fill_aead_lds(uint32_t *s_tt, uint32_t *s_rk, uint32_t *s_rp,
+__device__ __forceinline__ void fill_aead_lds(uint32_t *s_tt, uint32_t *s_rp,
                                               const AeadKeyDev *__restrict__ K) {
-    for (uint32_t i = threadIdx.x; i < 256u * 64u; i += blockDim.x) s_tt[i] = K->te[i >> 6];
-    for (uint32_t i = threadIdx.x; i < 60u; i += blockDim.x) s_rk[i] = K->rk256[i];
+    // [pair p: 64 KiB][entry e: 256 B][half h: 128 B][copy c = lane & 31];
+    // table 2p + h = T rotated right by 8 (2p + h)
+    for (uint32_t i = threadIdx.x; i < kAeadTableWords; i += blockDim.x) {
+        const uint32_t j = 2u * (i >> 14) + ((i >> 5) & 1u);
+        const uint32_t t = K->te[(i >> 6) & 255u];
+        s_tt[i] = j ? ror32(t, 8 * j) : t;
+    }
     for (uint32_t i = threadIdx.x; i < 65u * 5u; i += blockDim.x) s_rp[i] = (&K->rpow[0][0])[i];
     __syncthreads();
 }
@@ -219,15 +260,15 @@ __device__ __forceinline__ void fill_aead_lds(uint32_t *s_tt, uint32_t *s_rk, ui
 // nonce || ct || tag, the MAC runs over the input ciphertext; SEAL: the MAC
 // runs over the ciphertext this lane produced.
 template <bool OPEN>
-__global__ __launch_bounds__(kAeadThreads, 2) void rcdc_aead_unit_kernel(
+__global__ __launch_bounds__(kAeadThreads, kAeadBlocksPerCU) void rcdc_aead_unit_kernel(
     const uint8_t *__restrict__ in, uint8_t *__restrict__ out, const AeadBlob *__restrict__ blobs,
     const AeadUnit *__restrict__ units, uint32_t nunits, const AeadKeyDev *__restrict__ K,
     uint32_t *__restrict__ partials) {
-    __shared__ uint32_t s_tt[256 * 64];
-    __shared__ __attribute__((aligned(16))) uint32_t s_rk[60];
+    __shared__ uint32_t s_tt[kAeadTableWords];
     __shared__ uint32_t s_rp[65 * 5];
-    fill_aead_lds(s_tt, s_rk, s_rp, K);
-    const uint32_t lane = threadIdx.x & 63u;
+    fill_aead_lds(s_tt, s_rp, K);
+    const uint8_t *tt = reinterpret_cast<const uint8_t *>(s_tt);
+    const uint32_t lane = threadIdx.x & 63u, lane4 = (lane & 31u) * 4u;
     const uint32_t wpb = blockDim.x / 64u;
     for (uint32_t u = blockIdx.x * wpb + (threadIdx.x >> 6); u < nunits; u += gridDim.x * wpb) {
         const AeadUnit U = units[u];
@@ -238,17 +279,37 @@ __global__ __launch_bounds__(kAeadThreads, 2) void rcdc_aead_unit_kernel(
         blob_nonce<OPEN>(in, B, nonce);
         const uint8_t *src = in + B.in_off + (OPEN ? 16 : 0);
         uint8_t *dst = out + B.out_off + (OPEN ? 0 : 16);
+        // full blocks: 4 dwords (+ 1 when src is not 4-aligned; the shift is
+        // wave-uniform) from the 4-aligned base, loaded one step ahead
+        const uintptr_t sa = reinterpret_cast<uintptr_t>(src);
+        const uint32_t sh = (uint32_t)(sa & 3u) * 8u;
+        const uint32_t *q0 = reinterpret_cast<const uint32_t *>(src - (sa & 3u));
+        const uint64_t nfull = len / 16;
+        const uint64_t b1 = U.b1;
+        auto fetch = [&](uint64_t bb, uint32_t x[5]) {
+            if (bb < b1 && bb < nfull) {
+                const uint32_t *q = q0 + bb * 4;
+                x[0] = q[0]; x[1] = q[1]; x[2] = q[2]; x[3] = q[3];
+                if (sh) x[4] = q[4];
+            }
+        };
         P26 acc = {{0, 0, 0, 0, 0}};
         uint64_t last = ~0ull;
-        for (uint64_t b = (uint64_t)U.b0 + lane; b < U.b1; b += 64) {
-            const uint64_t o = b * 16;
-            const uint32_t k = len - o < 16 ? (uint32_t)(len - o) : 16u;
+        // one block: keystream (s0..s3, big-endian words) XOR data, store,
+        // Horner step acc = acc * r^64 + m (the MAC runs over the ciphertext)
+        auto finish_block = [&](uint64_t bb, const uint32_t x[5], uint32_t s0, uint32_t s1,
+                                uint32_t s2, uint32_t s3) {
+            const uint64_t o = bb * 16;
+            const uint32_t k = bb < nfull ? 16u : (uint32_t)(len - o);
             uint32_t w[4];
-            if (k == 16) load16(src + o, w);
-            else load_partial(src + o, k, w);
-            uint32_t s0, s1, s2, s3;
-            ctr_block(nonce, b, s0, s1, s2, s3);
-            aes_block<14>(s0, s1, s2, s3, s_tt, lane, s_rk);
+            if (k == 16) {
+                w[0] = __builtin_amdgcn_alignbit(x[1], x[0], sh);
+                w[1] = __builtin_amdgcn_alignbit(x[2], x[1], sh);
+                w[2] = __builtin_amdgcn_alignbit(x[3], x[2], sh);
+                w[3] = __builtin_amdgcn_alignbit(x[4], x[3], sh);
+            } else {
+                load_partial(src + o, k, w);
+            }
             uint32_t c[4] = {w[0] ^ bswap32(s0), w[1] ^ bswap32(s1), w[2] ^ bswap32(s2),
                              w[3] ^ bswap32(s3)};
             if (k == 16) {
@@ -256,11 +317,28 @@ __global__ __launch_bounds__(kAeadThreads, 2) void rcdc_aead_unit_kernel(
             } else {
                 for (uint32_t i = 0; i < k; i++) dst[o + i] = (uint8_t)(c[i >> 2] >> (8 * (i & 3)));
             }
-            // Horner: acc = acc * r^64 + m (the MAC runs over the ciphertext)
             const P26 m = pblock(OPEN ? w : c, k);
-            if (last != ~0ull) acc = pmul(acc, s_rp + 64 * 5);
+            acc = pmul(acc, K->rpow[64]);  // acc = 0 before the first block
             for (int i = 0; i < 5; i++) acc.h[i] += m.h[i];
-            last = b;
+            last = bb;
+        };
+        // two blocks per step (b, b + 64): two independent AES chains
+        uint32_t xa[5] = {0, 0, 0, 0, 0}, xb[5] = {0, 0, 0, 0, 0};
+        uint64_t b = (uint64_t)U.b0 + lane;
+        fetch(b, xa);
+        fetch(b + 64, xb);
+        for (; b < b1; b += 128) {
+            const uint32_t ca[5] = {xa[0], xa[1], xa[2], xa[3], xa[4]};
+            const uint32_t cb[5] = {xb[0], xb[1], xb[2], xb[3], xb[4]};
+            fetch(b + 128, xa);
+            fetch(b + 192, xb);
+            uint32_t a0, a1, a2, a3, e0, e1, e2, e3;
+            ctr_block(nonce, b, a0, a1, a2, a3);
+            ctr_block(nonce, b + 64, e0, e1, e2, e3);
+            aes_block<14>(a0, a1, a2, a3, tt, lane4, K->rk256);
+            aes_block<14>(e0, e1, e2, e3, tt, lane4, K->rk256);
+            finish_block(b, ca, a0, a1, a2, a3);
+            if (b + 64 < b1) finish_block(b + 64, cb, e0, e1, e2, e3);
         }
         // lane -> unit partial: acc * r^(b1 - last), then the wave's sum
         if (last != ~0ull) {
@@ -375,7 +453,7 @@ hipError_t launch_aead(bool open, const uint8_t *in, uint8_t *out, const AeadBlo
                        uint32_t *status, uint32_t cus, hipStream_t stream) {
     if (nblobs == 0) return hipSuccess;
     const uint32_t wpb = kAeadThreads / 64;
-    const uint64_t want = (nunits + wpb - 1) / wpb, cap = 2ull * cus * 4;
+    const uint64_t want = (nunits + wpb - 1) / wpb, cap = (uint64_t)kAeadBlocksPerCU * cus;
     const uint32_t blocks = (uint32_t)(want < cap ? want : cap);
     if (nunits) {
         if (open)
