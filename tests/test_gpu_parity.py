@@ -72,6 +72,24 @@ def test_chunk_empty(gpu_ctx):
     assert list(ChunkIter.from_config(cfg, b"", 100)) == []
 
 
+def test_c1_stdrng_256mib_file(gpu_ctx, tmp_path):
+    """C1 (BASELINE.json configs[0]): one 256 MiB file of
+    StdRng::seed_from_u64(0x256) bytes, read by ChunkIter.from_config as
+    FileArchiver::backup_reader does (file_archiver.rs:144-160) -- through
+    rcdc_stream_feed -- vs the oracle on the same bytes."""
+    from rustic_core_amd import ChunkIter, ConfigFile
+    n = 256 * MiB
+    data = oracle.stdrng_bytes(0x256, n)
+    path = tmp_path / "c1.bin"
+    path.write_bytes(data.tobytes())
+    cfg = ConfigFile.new(2, oracle.DEFAULT_POLY)
+    with open(path, "rb") as f:
+        lens = [len(c) for c in ChunkIter.from_config(cfg, f, n)]
+    exp = oracle.chunk_cuts(data)
+    assert np.array_equal(np.cumsum(lens, dtype=np.uint64), exp)
+    assert sum(lens) == n
+
+
 def test_chunk_zeros(gpu_ctx):
     """rabin.rs:378-385: zeros -> first chunk is exactly MIN_SIZE."""
     from rustic_core_amd import ChunkIter, ConfigFile
