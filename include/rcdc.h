@@ -269,9 +269,10 @@ rcdc_status rcdc_plan_device_digests(rcdc_plan *plan, uint64_t *d_digests);
 /* One blob.  seal: data [in_off, in_off + len) of d_in becomes
  * nonce || AES-256-CTR ciphertext || Poly1305-AES tag (len + 32 bytes) at
  * out_off of d_out.  open: the sealed blob [in_off, in_off + len) (len >= 32)
- * becomes its len - 32 plaintext bytes at out_off.  out_off must be 16-byte
- * aligned; in_off may have any alignment (allow 4 readable bytes after the
- * data).  The nonce is the caller's (rustic draws it at random, :117). */
+ * becomes its len - 32 plaintext bytes at out_off.  Offsets may have any
+ * alignment (16-byte aligned outputs store fastest; allow 4 readable bytes
+ * after each input).  The nonce is the caller's (rustic draws it at random,
+ * :120-121). */
 typedef struct {
     uint64_t in_off;
     uint64_t len;
@@ -293,6 +294,43 @@ rcdc_status rcdc_aead_seal(rcdc_ctx *ctx, const uint8_t *key, const void *d_in,
 rcdc_status rcdc_aead_open(rcdc_ctx *ctx, const uint8_t *key, const void *d_in,
                            const rcdc_aead_ref *refs, uint32_t n, void *d_out,
                            uint32_t *status, void *hip_stream);
+
+/* ---- pack files: blob/packer.rs:615-655 (add_raw), :693-735 (save,
+ * write_header) and repofile/packfile.rs (HeaderEntry, PackHeaderRef) -- the
+ * packer's byte work for blobs in HBM: each pack is its blobs sealed back to
+ * back, then the sealed pack header, then its length (u32 LE). ---------- */
+
+typedef struct {
+    uint64_t in_off;           /* the blob's bytes in d_in (as stored: the raw blob, or the
+                                  zstd frame of a compressed one)                         */
+    uint32_t len;              /* bytes at in_off                                          */
+    uint32_t uncompressed_len; /* 0: stored as is (HeaderEntry Data / Tree); else the raw
+                                  length of a compressed blob (CompData / CompTree)       */
+    uint32_t type;             /* BlobType: 0 data, 1 tree                                 */
+    uint32_t pad;
+    uint8_t id[32];            /* blob id                                                  */
+    uint8_t nonce[16];
+} rcdc_pack_blob;              /* 72 B */
+
+typedef struct {
+    uint64_t out_off;          /* where the pack file starts in d_out                      */
+    uint32_t blob0, nblobs;    /* its blobs, in pack order: blobs[blob0 .. blob0 + nblobs) */
+    uint8_t header_nonce[16];
+    uint64_t size;             /* out: pack file bytes                                     */
+    uint32_t header_len;       /* out: sealed header bytes (the trailing u32)              */
+    uint32_t pad;
+} rcdc_pack;                   /* 48 B */
+
+/* Build npacks pack files in d_out (out_len bytes).  blobs and packs are HOST
+ * arrays; blob_offsets (optional, host, nblobs) receives each blob's offset
+ * in its pack (IndexBlob location.offset; its length is len + 32).  Grouping
+ * blobs into packs (PackSizer, packer.rs:65-200) and the pack id (SHA-256
+ * of the file, packer.rs:833) stay with the caller.  Asynchronous on
+ * hip_stream; the outputs of `packs` are set on return.                     */
+rcdc_status rcdc_pack_build(rcdc_ctx *ctx, const uint8_t *key, const void *d_in,
+                            const rcdc_pack_blob *blobs, uint32_t nblobs, rcdc_pack *packs,
+                            uint32_t npacks, void *d_out, uint64_t out_len,
+                            uint32_t *blob_offsets, void *hip_stream);
 
 /* ABI version of the loaded library (== RCDC_ABI_VERSION). */
 uint32_t rcdc_abi_version(void);

@@ -252,3 +252,51 @@ def open_(key: bytes, data) -> bytes:
     if st == 1:
         raise MacMismatch("MAC check failed")
     return out[:d.size - 32].tobytes()
+
+
+# ---- pack files (test checker): blob/packer.rs:615-655 (add_raw),
+# :693-735 (save / write_header), repofile/packfile.rs:88-124 (HeaderEntry),
+# :355-372 (PackHeaderRef::size / pack_size) ---------------------------------
+
+def pack_header_entry(tpe: int, sealed_len: int, blob_id: bytes,
+                      uncompressed_len: int = 0) -> bytes:
+    """HeaderEntry, little-endian: magic 0 Data / 1 Tree (+ u32 length + id),
+    2 CompData / 3 CompTree (+ u32 length + u32 raw length + id)."""
+    out = bytes([tpe + (2 if uncompressed_len else 0)]) + sealed_len.to_bytes(4, "little")
+    if uncompressed_len:
+        out += uncompressed_len.to_bytes(4, "little")
+    return out + bytes(blob_id)
+
+
+def pack_file(key: bytes, blobs, header_nonce: bytes):
+    """blobs: (type, data, id, nonce, uncompressed_len) in pack order.
+    Returns (pack bytes, [(offset, length)] per blob): the blobs sealed back
+    to back, the sealed header, then its length as u32 LE."""
+    body, index, off, header = [], [], 0, b""
+    for tpe, data, bid, nonce, ulen in blobs:
+        sealed = seal(key, nonce, data)
+        body.append(sealed)
+        index.append((off, len(sealed)))
+        header += pack_header_entry(tpe, len(sealed), bid, ulen)
+        off += len(sealed)
+    sh = seal(key, header_nonce, header)
+    return b"".join(body) + sh + len(sh).to_bytes(4, "little"), index
+
+
+def parse_pack(key: bytes, pack: bytes):
+    """PackHeader::from_binary over the decrypted header
+    (packfile.rs:207-220): [(type, offset, length, uncompressed_len, id)]."""
+    hlen = int.from_bytes(pack[-4:], "little")
+    header = open_(key, pack[-4 - hlen:-4])
+    out, pos, off = [], 0, 0
+    while pos < len(header):
+        t = header[pos]
+        length = int.from_bytes(header[pos + 1:pos + 5], "little")
+        if t in (0, 1):
+            ulen, bid, pos = 0, header[pos + 5:pos + 37], pos + 37
+        else:
+            ulen = int.from_bytes(header[pos + 5:pos + 9], "little")
+            bid, pos = header[pos + 9:pos + 41], pos + 41
+        out.append((t & 1, off, length, ulen, bid))
+        off += length
+    return out

@@ -25,7 +25,7 @@ EXPORTS = (
     "rcdc_sha256_chunks", "rcdc_plan_hash", "rcdc_plan_digests", "rcdc_plan_device_digests",
     "rcdc_plan_set_pipeline", "rcdc_plan_hash_many", "rcdc_plan_walk_stats",
     "rcdc_plan_finish", "rcdc_stream_queued", "rcdc_stream_batch_bytes",
-    "rcdc_aead_seal", "rcdc_aead_open",
+    "rcdc_aead_seal", "rcdc_aead_open", "rcdc_pack_build",
 )
 ABI_VERSION = 1
 
@@ -150,6 +150,8 @@ def lib() -> ctypes.CDLL:
     L.rcdc_aead_seal.argtypes = [vp, vp, vp, vp, u32, vp, vp]
     L.rcdc_aead_open.restype = st
     L.rcdc_aead_open.argtypes = [vp, vp, vp, vp, u32, vp, vp, vp]
+    L.rcdc_pack_build.restype = st
+    L.rcdc_pack_build.argtypes = [vp, vp, vp, vp, u32, vp, u32, vp, u64, vp, vp]
     L.rcdc_plan_device_digests.restype = st
     L.rcdc_plan_device_digests.argtypes = [vp, P(u64)]
     _lib = L

@@ -56,6 +56,15 @@ class ConfigFile:
     chunk_size_: Optional[int] = None
     chunk_min_size_: Optional[int] = None
     chunk_max_size_: Optional[int] = None
+    # pack sizing (configfile.rs:60-100), used by rustic_core_amd.pack
+    treepack_size: Optional[int] = None
+    treepack_growfactor: Optional[int] = None
+    treepack_size_limit: Optional[int] = None
+    datapack_size: Optional[int] = None
+    datapack_growfactor: Optional[int] = None
+    datapack_size_limit: Optional[int] = None
+    min_packsize_tolerate_percent: Optional[int] = None
+    max_packsize_tolerate_percent: Optional[int] = None
 
     @classmethod
     def new(cls, version: int, poly: int) -> "ConfigFile":
@@ -69,6 +78,25 @@ class ConfigFile:
         if st:
             raise status_error(st, _lib.last_error())
         return out.value
+
+    def packsize(self, blob_type: int):
+        """configfile.rs:211-231: (size, grow factor, limit) for BlobType
+        0 = data, 1 = tree."""
+        MB = 1 << 20
+        if blob_type == 1:
+            return (4 * MB if self.treepack_size is None else self.treepack_size,
+                    32 if self.treepack_growfactor is None else self.treepack_growfactor,
+                    0xFFFFFFFF if self.treepack_size_limit is None else self.treepack_size_limit)
+        return (32 * MB if self.datapack_size is None else self.datapack_size,
+                32 if self.datapack_growfactor is None else self.datapack_growfactor,
+                0xFFFFFFFF if self.datapack_size_limit is None else self.datapack_size_limit)
+
+    def packsize_ok_percents(self):
+        """configfile.rs:236-245."""
+        mx = self.max_packsize_tolerate_percent
+        return (30 if self.min_packsize_tolerate_percent is None
+                else self.min_packsize_tolerate_percent,
+                0xFFFFFFFF if not mx else mx)
 
     def get_chunker(self) -> Chunker:
         return self.chunker or Chunker.Rabin

@@ -194,6 +194,33 @@ __device__ __forceinline__ void load16(const uint8_t *p, uint32_t w[4]) {
     }
 }
 
+// 16 bytes (4 little-endian words) to any address: one dwordx4 when 16-B
+// aligned, else the 3 whole dwords the block covers plus byte stores for the
+// two partial ones (pack layouts put blobs at any offset).
+__device__ __forceinline__ void store16(uint8_t *p, const uint32_t c[4]) {
+    const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+    if ((a & 15u) == 0) {
+        *reinterpret_cast<uint4 *>(p) = make_uint4(c[0], c[1], c[2], c[3]);
+        return;
+    }
+    const uint32_t m = (uint32_t)(a & 3u);
+    if (m == 0) {
+        uint32_t *q = reinterpret_cast<uint32_t *>(p);
+        q[0] = c[0]; q[1] = c[1]; q[2] = c[2]; q[3] = c[3];
+        return;
+    }
+    // bytes [m, m + 16) of the 5 dwords from the aligned base: dwords 1..3
+    // whole (d_i = c[i-1] >> 8(4-m) | c[i] << 8m), dword 0 bytes m..3 and
+    // dword 4 bytes 0..m-1 partial
+    uint32_t *q = reinterpret_cast<uint32_t *>(p - m);
+    const uint32_t sh = 8u * (4u - m);
+    q[1] = __builtin_amdgcn_alignbit(c[1], c[0], sh);
+    q[2] = __builtin_amdgcn_alignbit(c[2], c[1], sh);
+    q[3] = __builtin_amdgcn_alignbit(c[3], c[2], sh);
+    for (uint32_t i = 0; i < 4u - m; i++) p[i] = (uint8_t)(c[0] >> (8 * i));
+    for (uint32_t i = 0; i < m; i++) p[12 + (4 - m) + i] = (uint8_t)(c[3] >> (8 * (4 - m + i)));
+}
+
 // Bytes [0, k) of a block of k < 16 bytes (no read past the data's end).
 __device__ __forceinline__ void load_partial(const uint8_t *p, uint32_t k, uint32_t w[4]) {
     w[0] = w[1] = w[2] = w[3] = 0;
@@ -313,7 +340,7 @@ __global__ __launch_bounds__(kAeadThreads, kAeadBlocksPerCU) void rcdc_aead_unit
             uint32_t c[4] = {w[0] ^ bswap32(s0), w[1] ^ bswap32(s1), w[2] ^ bswap32(s2),
                              w[3] ^ bswap32(s3)};
             if (k == 16) {
-                *reinterpret_cast<uint4 *>(dst + o) = make_uint4(c[0], c[1], c[2], c[3]);
+                store16(dst + o, c);
             } else {
                 for (uint32_t i = 0; i < k; i++) dst[o + i] = (uint8_t)(c[i >> 2] >> (8 * (i & 3)));
             }
@@ -440,8 +467,12 @@ __global__ __launch_bounds__(256) void rcdc_aead_finish_kernel(
         status[i] = d ? 1u : 0u;
     } else {
         uint8_t *o = out + B.out_off;
-        *reinterpret_cast<uint4 *>(o) = make_uint4(B.nonce[0], B.nonce[1], B.nonce[2], B.nonce[3]);
+        store16(o, B.nonce);
         for (int j = 0; j < 16; j++) o[16 + B.len + j] = tag[j];
+        if (B.flags & kAeadAppendLen) {  // packer.rs:713-725: the header length, unencrypted
+            const uint32_t hl = (uint32_t)B.len + 32u;
+            for (int j = 0; j < 4; j++) o[32 + B.len + j] = (uint8_t)(hl >> (8 * j));
+        }
     }
 }
 

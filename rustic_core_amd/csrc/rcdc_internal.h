@@ -180,13 +180,17 @@ struct AeadKeyDev {
     uint32_t te[256];      // T-table: (2S, S, S, 3S) as a big-endian word
 };
 
-struct AeadBlob {  // 40 B
+constexpr uint32_t kAeadAppendLen = 1;  // seal: write u32 LE (len + 32) after the tag
+
+struct AeadBlob {  // 48 B
     uint64_t in_off;   // seal: plaintext; open: nonce || ct || tag
     uint64_t len;      // plaintext / ciphertext bytes
-    uint64_t out_off;  // seal: nonce || ct || tag; open: plaintext (16-B aligned)
+    uint64_t out_off;  // seal: nonce || ct || tag; open: plaintext (any alignment)
     uint32_t nonce[4]; // the nonce's bytes as 4 little-endian words
+    uint32_t flags;    // kAeadAppendLen: a pack header (packfile.rs PackHeaderLength)
+    uint32_t pad;
 };
-static_assert(sizeof(AeadBlob) == 40, "AeadBlob is 40 B");
+static_assert(sizeof(AeadBlob) == 48, "AeadBlob is 48 B");
 
 struct AeadUnit {  // 16 B
     uint32_t blob;

@@ -248,8 +248,9 @@ struct rcdc_ctx {
     AeadBlob *d_aead_blobs = nullptr;
     AeadUnit *d_aead_units = nullptr;
     uint32_t *d_aead_unit0 = nullptr, *d_aead_partials = nullptr, *d_aead_status = nullptr;
+    uint8_t *d_aead_stage = nullptr;  // pack headers
     uint64_t cap_aead_key = 0, cap_aead_blobs = 0, cap_aead_units = 0, cap_aead_unit0 = 0,
-             cap_aead_partials = 0, cap_aead_status = 0;
+             cap_aead_partials = 0, cap_aead_status = 0, cap_aead_stage = 0;
     hipEvent_t aead_done = nullptr;
 };
 
@@ -1207,6 +1208,7 @@ void rcdc_ctx_destroy(rcdc_ctx *c) {
         (void)hipFree(c->d_aead_unit0);
         (void)hipFree(c->d_aead_partials);
         (void)hipFree(c->d_aead_status);
+        (void)hipFree(c->d_aead_stage);
         if (c->aead_done) (void)hipEventDestroy(c->aead_done);
         if (c->stream) (void)hipStreamDestroy(c->stream);
     }
@@ -1585,46 +1587,34 @@ void aead_key_material(const uint8_t key[64], AeadKeyDev *K) {
     for (int j = 1; j < 32; j++) p26_mul(K->r2j[j - 1], K->r2j[j - 1], K->r2j[j]);
 }
 
-rcdc_status aead_run(rcdc_ctx *ctx, bool open, const uint8_t key[64], const void *d_in,
-                     const rcdc_aead_ref *refs, uint32_t n, void *d_out, uint32_t *status,
-                     void *hip_stream) {
-    if (!valid_ctx(ctx) || !key || (n && (!refs || !d_in || !d_out)) || (open && n && !status))
-        return fail(RCDC_ERR_INVALID_INPUT, "null argument");
+// A list of blobs over one input base, cut into units of kAeadUnitBlocks.
+struct AeadBatch {
+    const uint8_t *in = nullptr;
     std::vector<AeadBlob> blobs;
     std::vector<AeadUnit> units;
-    std::vector<uint32_t> unit0, which;  // which: device blob -> caller index
-    blobs.reserve(n);
-    for (uint32_t i = 0; i < n; i++) {
-        const rcdc_aead_ref &r = refs[i];
-        if (r.out_off & 15)
-            return fail(RCDC_ERR_INVALID_INPUT, "blob %u: out_off must be 16-byte aligned", i);
-        if (open && r.len < 32) {
-            // no room for nonce + tag: aespoly1305.rs:89-94 (< 16 bytes) and
-            // the AEAD's own length check (16..31) both fail before any MAC
-            status[i] = r.len < 16 ? 2u : 1u;
-            continue;
-        }
-        which.push_back(i);
-        unit0.push_back((uint32_t)units.size());
-        blobs.emplace_back();
-        AeadBlob &b = blobs.back();
-        const uint32_t bi = (uint32_t)blobs.size() - 1;
-        b.in_off = r.in_off;
-        b.len = open ? r.len - 32 : r.len;
-        b.out_off = r.out_off;
-        uint8_t nonce[16];
-        memcpy(nonce, r.nonce, 16);
-        memcpy(b.nonce, nonce, 16);  // little-endian words of the nonce bytes
-        const uint64_t nb = (b.len + 15) / 16;
-        if (nb >= (1ull << 32)) return fail(RCDC_ERR_UNSUPPORTED, "blob %u too large", i);
-        for (uint64_t b0 = 0; b0 < nb; b0 += kAeadUnitBlocks)
-            units.push_back({bi, (uint32_t)b0, (uint32_t)std::min<uint64_t>(nb, b0 + kAeadUnitBlocks), 0});
-    }
-    const uint32_t m = (uint32_t)blobs.size();
-    unit0.push_back((uint32_t)units.size());
+    std::vector<uint32_t> unit0;  // per blob + 1 (closed by aead_launch)
+};
+
+rcdc_status aead_add(AeadBatch &B, const AeadBlob &b, uint32_t caller_index) {
+    const uint64_t nb = (b.len + 15) / 16;
+    if (nb >= (1ull << 32)) return fail(RCDC_ERR_UNSUPPORTED, "blob %u too large", caller_index);
+    const uint32_t bi = (uint32_t)B.blobs.size();
+    B.unit0.push_back((uint32_t)B.units.size());
+    B.blobs.push_back(b);
+    for (uint64_t b0 = 0; b0 < nb; b0 += kAeadUnitBlocks)
+        B.units.push_back({bi, (uint32_t)b0, (uint32_t)std::min<uint64_t>(nb, b0 + kAeadUnitBlocks), 0});
+    return RCDC_OK;
+}
+
+// Launch the batches (each its own input base) on one context scratch.
+// `staging` (optional) is copied to the scratch input buffer first and a
+// batch whose `in` is nullptr reads from it.  open: status per blob of the
+// batches in order (synchronous).  Calls on one context take turns.
+rcdc_status aead_launch(rcdc_ctx *ctx, bool open, const uint8_t key[64], std::vector<AeadBatch> &bt,
+                        uint8_t *out, hipStream_t st, const std::vector<uint8_t> *staging,
+                        std::vector<uint32_t> *status) {
     std::lock_guard<std::mutex> lk(ctx->aead_mu);
     DeviceGuard g(ctx->device);
-    hipStream_t st = hip_stream ? (hipStream_t)hip_stream : ctx->stream;
     if (ctx->aead_done) HIP_TRY(hipEventSynchronize(ctx->aead_done));  // the scratch is free
     else HIP_TRY(hipEventCreateWithFlags(&ctx->aead_done, hipEventDisableTiming));
     rcdc_status rs;
@@ -1636,30 +1626,151 @@ rcdc_status aead_run(rcdc_ctx *ctx, bool open, const uint8_t key[64], const void
         memcpy(ctx->aead_key, key, 64);
         ctx->aead_key_set = true;
     }
-    if ((rs = ensure_dev(&ctx->d_aead_blobs, &ctx->cap_aead_blobs, m))) return rs;
-    if ((rs = ensure_dev(&ctx->d_aead_units, &ctx->cap_aead_units, units.size()))) return rs;
-    if ((rs = ensure_dev(&ctx->d_aead_unit0, &ctx->cap_aead_unit0, m + 1))) return rs;
-    if ((rs = ensure_dev(&ctx->d_aead_partials, &ctx->cap_aead_partials, units.size() * 5))) return rs;
-    if ((rs = ensure_dev(&ctx->d_aead_status, &ctx->cap_aead_status, m))) return rs;
-    if (m) {
-        HIP_TRY(hipMemcpy(ctx->d_aead_blobs, blobs.data(), m * sizeof(AeadBlob), hipMemcpyHostToDevice));
-        HIP_TRY(hipMemcpy(ctx->d_aead_unit0, unit0.data(), (m + 1) * 4, hipMemcpyHostToDevice));
+    uint64_t nb = 0, nu = 0;
+    for (AeadBatch &B : bt) {
+        B.unit0.push_back((uint32_t)B.units.size());
+        nb += B.blobs.size();
+        nu += B.units.size();
     }
-    if (!units.empty())
-        HIP_TRY(hipMemcpy(ctx->d_aead_units, units.data(), units.size() * sizeof(AeadUnit),
+    if ((rs = ensure_dev(&ctx->d_aead_blobs, &ctx->cap_aead_blobs, nb))) return rs;
+    if ((rs = ensure_dev(&ctx->d_aead_units, &ctx->cap_aead_units, nu))) return rs;
+    if ((rs = ensure_dev(&ctx->d_aead_unit0, &ctx->cap_aead_unit0, nb + bt.size()))) return rs;
+    if ((rs = ensure_dev(&ctx->d_aead_partials, &ctx->cap_aead_partials, nu * 5))) return rs;
+    if ((rs = ensure_dev(&ctx->d_aead_status, &ctx->cap_aead_status, nb))) return rs;
+    if (staging && !staging->empty()) {
+        if ((rs = ensure_dev(&ctx->d_aead_stage, &ctx->cap_aead_stage, staging->size() + 16)))
+            return rs;
+        HIP_TRY(hipMemcpy(ctx->d_aead_stage, staging->data(), staging->size(),
                           hipMemcpyHostToDevice));
-    HIP_TRY(launch_aead(open, (const uint8_t *)d_in, (uint8_t *)d_out, ctx->d_aead_blobs, m,
-                        ctx->d_aead_units, (uint32_t)units.size(), ctx->d_aead_unit0,
-                        ctx->d_aead_key, ctx->d_aead_partials, ctx->d_aead_status,
-                        (uint32_t)std::max(ctx->num_cus, 1), st));
+    }
+    uint64_t ob = 0, ou = 0, o0 = 0;
+    for (AeadBatch &B : bt) {
+        const uint32_t m = (uint32_t)B.blobs.size(), u = (uint32_t)B.units.size();
+        if (m) {
+            HIP_TRY(hipMemcpy(ctx->d_aead_blobs + ob, B.blobs.data(), m * sizeof(AeadBlob),
+                              hipMemcpyHostToDevice));
+            HIP_TRY(hipMemcpy(ctx->d_aead_unit0 + o0, B.unit0.data(), (m + 1) * 4,
+                              hipMemcpyHostToDevice));
+        }
+        if (u)
+            HIP_TRY(hipMemcpy(ctx->d_aead_units + ou, B.units.data(), u * sizeof(AeadUnit),
+                              hipMemcpyHostToDevice));
+        const uint8_t *in = B.in ? B.in : ctx->d_aead_stage;
+        HIP_TRY(launch_aead(open, in, out, ctx->d_aead_blobs + ob, m, ctx->d_aead_units + ou, u,
+                            ctx->d_aead_unit0 + o0, ctx->d_aead_key, ctx->d_aead_partials + ou * 5,
+                            ctx->d_aead_status + ob, (uint32_t)std::max(ctx->num_cus, 1), st));
+        ob += m;
+        ou += u;
+        o0 += m + 1;
+    }
     HIP_TRY(hipEventRecord(ctx->aead_done, st));
-    if (open) {
+    if (open && status) {
         HIP_TRY(hipEventSynchronize(ctx->aead_done));
-        std::vector<uint32_t> ds(m);
-        if (m) HIP_TRY(hipMemcpy(ds.data(), ctx->d_aead_status, m * 4, hipMemcpyDeviceToHost));
-        for (uint32_t j = 0; j < m; j++) status[which[j]] = ds[j];
+        status->assign(nb, 0);
+        if (nb) HIP_TRY(hipMemcpy(status->data(), ctx->d_aead_status, nb * 4, hipMemcpyDeviceToHost));
     }
     return RCDC_OK;
+}
+
+rcdc_status aead_run(rcdc_ctx *ctx, bool open, const uint8_t key[64], const void *d_in,
+                     const rcdc_aead_ref *refs, uint32_t n, void *d_out, uint32_t *status,
+                     void *hip_stream) {
+    if (!valid_ctx(ctx) || !key || (n && (!refs || !d_in || !d_out)) || (open && n && !status))
+        return fail(RCDC_ERR_INVALID_INPUT, "null argument");
+    std::vector<AeadBatch> bt(1);
+    bt[0].in = (const uint8_t *)d_in;
+    std::vector<uint32_t> which;  // device blob -> caller index
+    rcdc_status rs;
+    for (uint32_t i = 0; i < n; i++) {
+        const rcdc_aead_ref &r = refs[i];
+        if (open && r.len < 32) {
+            // no room for nonce + tag: aespoly1305.rs:89-94 (< 16 bytes) and
+            // the AEAD's own length check (16..31) both fail before any MAC
+            status[i] = r.len < 16 ? 2u : 1u;
+            continue;
+        }
+        AeadBlob b{};
+        b.in_off = r.in_off;
+        b.len = open ? r.len - 32 : r.len;
+        b.out_off = r.out_off;
+        memcpy(b.nonce, r.nonce, 16);  // little-endian words of the nonce bytes
+        if ((rs = aead_add(bt[0], b, i))) return rs;
+        which.push_back(i);
+    }
+    std::vector<uint32_t> ds;
+    hipStream_t st = hip_stream ? (hipStream_t)hip_stream : ctx->stream;
+    if ((rs = aead_launch(ctx, open, key, bt, (uint8_t *)d_out, st, nullptr, open ? &ds : nullptr)))
+        return rs;
+    if (open)
+        for (size_t j = 0; j < which.size(); j++) status[which[j]] = ds[j];
+    return RCDC_OK;
+}
+
+static_assert(sizeof(rcdc_pack_blob) == 72, "rcdc_pack_blob is 72 B");
+static_assert(sizeof(rcdc_pack) == 48, "rcdc_pack is 48 B");
+
+// Pack files (blob/packer.rs:615-655, 693-735; repofile/packfile.rs): blobs
+// sealed back to back, then the sealed header (one HeaderEntry per blob:
+// type, u32 length, [u32 raw length], id) and its u32 length.
+rcdc_status pack_build(rcdc_ctx *ctx, const uint8_t key[64], const void *d_in,
+                       const rcdc_pack_blob *blobs, uint32_t nblobs, rcdc_pack *packs,
+                       uint32_t npacks, void *d_out, uint64_t out_len, uint32_t *blob_offsets,
+                       void *hip_stream) {
+    if (!valid_ctx(ctx) || !key || (npacks && (!packs || !d_out)) || (nblobs && (!blobs || !d_in)))
+        return fail(RCDC_ERR_INVALID_INPUT, "null argument");
+    std::vector<AeadBatch> bt(2);
+    bt[0].in = (const uint8_t *)d_in;
+    bt[1].in = nullptr;  // headers: from the staging buffer
+    std::vector<uint8_t> hdr;
+    rcdc_status rs;
+    for (uint32_t p = 0; p < npacks; p++) {
+        rcdc_pack &P = packs[p];
+        if (P.nblobs == 0 || (uint64_t)P.blob0 + P.nblobs > nblobs)
+            return fail(RCDC_ERR_INVALID_INPUT, "pack %u: blobs [%u, +%u) of %u", p, P.blob0,
+                        P.nblobs, nblobs);
+        uint64_t off = 0;
+        const size_t h0 = hdr.size();
+        for (uint32_t i = P.blob0; i < P.blob0 + P.nblobs; i++) {
+            const rcdc_pack_blob &b = blobs[i];
+            if (b.type > 1) return fail(RCDC_ERR_INVALID_INPUT, "blob %u: type %u", i, b.type);
+            const uint32_t sealed = b.len + 32u;
+            if (b.len > 0xFFFFFFFFu - 32u)
+                return fail(RCDC_ERR_UNSUPPORTED, "blob %u: %u bytes", i, b.len);
+            if (blob_offsets) blob_offsets[i] = (uint32_t)off;
+            AeadBlob a{};
+            a.in_off = b.in_off;
+            a.len = b.len;
+            a.out_off = P.out_off + off;
+            memcpy(a.nonce, b.nonce, 16);
+            if ((rs = aead_add(bt[0], a, i))) return rs;
+            // HeaderEntry (packfile.rs:88-124, little-endian)
+            hdr.push_back((uint8_t)(b.type + (b.uncompressed_len ? 2u : 0u)));
+            for (int j = 0; j < 4; j++) hdr.push_back((uint8_t)(sealed >> (8 * j)));
+            if (b.uncompressed_len)
+                for (int j = 0; j < 4; j++) hdr.push_back((uint8_t)(b.uncompressed_len >> (8 * j)));
+            hdr.insert(hdr.end(), b.id, b.id + 32);
+            off += sealed;
+        }
+        const uint64_t hlen = hdr.size() - h0;
+        P.header_len = (uint32_t)(hlen + 32);
+        P.size = off + hlen + 32 + 4;
+        if (P.size > 0xFFFFFFFFull)  // packer.rs:58 MAX_SIZE; offsets are u32
+            return fail(RCDC_ERR_UNSUPPORTED, "pack %u: %llu bytes", p, (unsigned long long)P.size);
+        if (P.out_off + P.size > out_len)
+            return fail(RCDC_ERR_INVALID_INPUT, "pack %u does not fit the output (%llu + %llu > %llu)",
+                        p, (unsigned long long)P.out_off, (unsigned long long)P.size,
+                        (unsigned long long)out_len);
+        AeadBlob h{};
+        h.in_off = h0;
+        h.len = hlen;
+        h.out_off = P.out_off + off;
+        memcpy(h.nonce, P.header_nonce, 16);
+        h.flags = kAeadAppendLen;
+        if ((rs = aead_add(bt[1], h, p))) return rs;
+    }
+    hdr.resize(hdr.size() + 4, 0);  // the kernel may read 3 bytes past a blob
+    hipStream_t st = hip_stream ? (hipStream_t)hip_stream : ctx->stream;
+    return aead_launch(ctx, false, key, bt, (uint8_t *)d_out, st, &hdr, nullptr);
 }
 
 }  // namespace
@@ -1675,6 +1786,14 @@ rcdc_status rcdc_aead_open(rcdc_ctx *ctx, const uint8_t *key, const void *d_in,
                            const rcdc_aead_ref *refs, uint32_t n, void *d_out, uint32_t *status,
                            void *hip_stream) {
     return aead_run(ctx, true, key, d_in, refs, n, d_out, status, hip_stream);
+}
+
+rcdc_status rcdc_pack_build(rcdc_ctx *ctx, const uint8_t *key, const void *d_in,
+                            const rcdc_pack_blob *blobs, uint32_t nblobs, rcdc_pack *packs,
+                            uint32_t npacks, void *d_out, uint64_t out_len,
+                            uint32_t *blob_offsets, void *hip_stream) {
+    return pack_build(ctx, key, d_in, blobs, nblobs, packs, npacks, d_out, out_len, blob_offsets,
+                      hip_stream);
 }
 
 // ---- streaming: one file fed in pieces -------------------------------------
