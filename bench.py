@@ -83,6 +83,8 @@ def parse():
                     help="also seal + open the chunks as blobs on the device (rcdc_aead_*)")
     ap.add_argument("--aead-streams", type=int, default=16,
                     help="--aead: blobs = the chunks of the first N streams")
+    ap.add_argument("--pack", action="store_true",
+                    help="also build pack files of the chunks on the device (rcdc_pack_build)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-parity", action="store_true")
     ap.add_argument("--abi-e2e", action="store_true",
@@ -841,6 +843,8 @@ def main():
     if args.aead and rank == 0:
         out_extra["aead"] = aead_measure(torch, plan, arena, offs, lens, dev, args,
                                          world == 1 and not args.no_cpu_baseline)
+    if args.pack and rank == 0:
+        out_extra["pack"] = pack_measure(torch, plan, arena, offs, lens, dev, args)
     if args.e2e and rank == 0:
         out_extra["e2e"] = e2e_rate(torch, arena, offs, lens, plan, args.workload)
     if args.abi_e2e and rank == 0 and os.path.exists(os.path.join(ROOT, "tools", "abi_e2e")):
@@ -1101,6 +1105,89 @@ def aead_measure(torch, plan, arena, offs, lens, dev, args, cpu: bool) -> dict:
     del sealed, plain
     torch.cuda.empty_cache()
     return out
+
+
+def pack_measure(torch, plan, arena, offs, lens, dev, args) -> dict:
+    """The packer's byte work on the chunks just cut:
+    blob ids on the device (rcdc_plan_hash), dedup by id (the indexer's
+    has(), packer.rs:304-315), grouping by PackSizer (32 MiB data packs,
+    packer.rs:65-200), then ONE rcdc_pack_build over all packs: every unique
+    chunk sealed into its pack, headers sealed and appended.  Kernel time by
+    HIP events on the launch stream; one pack checked with the oracle."""
+    from rustic_core_amd.chunker import ConfigFile
+    from rustic_core_amd.pack import PackSizer, build_packs, group_blobs, make_blobs, pack_layout
+    ns = min(len(lens), max(args.aead_streams, 1))
+    side = torch.cuda.Stream(dev)
+    sp = side.cuda_stream
+    ptr = arena.data_ptr()
+    plan.run(ptr, sp)
+    e = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    e[0].record(side)
+    plan.hash(ptr, sp)
+    e[1].record(side)
+    torch.cuda.synchronize(dev)
+    hash_ms = e[0].elapsed_time(e[1])
+    cuts, digs = plan.results()[:ns], plan.digests()[:ns]
+    seen, in_offs, blens, ids = set(), [], [], []
+    nchunks = 0
+    for i in range(ns):
+        prev = 0
+        for c, d in zip(cuts[i], digs[i]):
+            nchunks += 1
+            k = d.tobytes()
+            if k not in seen:
+                seen.add(k)
+                in_offs.append(int(offs[i]) + prev)
+                blens.append(int(c) - prev)
+                ids.append(d)
+            prev = int(c)
+    rng = np.random.default_rng(0x9AC)
+    nb = len(blens)
+    blobs = make_blobs(in_offs, blens, ids, rng.integers(0, 256, (nb, 16), dtype=np.uint8))
+    groups = group_blobs(blens, PackSizer.from_config(ConfigFile.new(2, POLY), 0, 0))
+    packs, total = pack_layout(blobs, groups,
+                               rng.integers(0, 256, (len(groups), 16), dtype=np.uint8))
+    out = torch.empty(total + 64, dtype=torch.uint8, device=dev)
+    key = rng.integers(0, 256, 64, dtype=np.uint8).tobytes()
+    ctx = plan.ctx
+    build_packs(ctx, key, ptr, blobs, packs, out.data_ptr(), total, sp)
+    torch.cuda.synchronize(dev)
+    k = 5
+    e[0].record(side)
+    for _ in range(k):
+        offsets = build_packs(ctx, key, ptr, blobs, packs, out.data_ptr(), total, sp)
+    e[1].record(side)
+    torch.cuda.synchronize(dev)
+    pack_ms = e[0].elapsed_time(e[1]) / k
+    uniq = int(sum(blens))
+    from oracle import oracle
+    j = len(groups) // 2
+    p = packs[j]
+    f = out[int(p["out_off"]):int(p["out_off"]) + int(p["size"])].cpu().numpy().tobytes()
+    parsed = oracle.parse_pack(key, f)
+    b0 = int(p["blob0"])
+    ok = [bytes(bid) for _, _, _, _, bid in parsed] == \
+        [blobs[i]["id"].tobytes() for i in range(b0, b0 + int(p["nblobs"]))]
+    o0, l0 = parsed[0][1], parsed[0][2]
+    ok &= oracle.open_(key, f[o0:o0 + l0]) == \
+        arena[in_offs[b0]:in_offs[b0] + blens[b0]].cpu().numpy().tobytes()
+    ok &= [int(x) for x in offsets[b0:b0 + int(p["nblobs"])]] == [o for _, o, _, _, _ in parsed]
+    del out
+    torch.cuda.empty_cache()
+    return {
+        "kernels": "rcdc_sha256 plan kernels (ids) + rcdc_aead_unit/finish_kernel (blobs, headers)",
+        "chunks": nchunks, "unique_blobs": nb, "packs": len(groups),
+        "input_bytes": int(sum(int(x) for x in lens[:ns])), "unique_bytes": uniq,
+        "pack_bytes": int(total),
+        "hash_ms": round(hash_ms, 3), "pack_build_ms": round(pack_ms, 3),
+        "pack_build_gibs_unique": round(uniq / (pack_ms / 1e3) / GiB, 2),
+        "hash_plus_pack_gibs_input": round(int(sum(int(x) for x in lens[:ns])) /
+                                           ((hash_ms + pack_ms) / 1e3) / GiB, 2),
+        "check": {"pack": j, "ok": bool(ok),
+                  "checker": "oracle.parse_pack (header ids, offsets) + oracle.open_ of its "
+                             "first blob vs the source chunk"},
+        "note": "pack ids (SHA-256 of each pack file, packer.rs:833) are left to the writer",
+    }
 
 
 def parity_check(args, arena, offs, lens, plan, last, desc) -> dict:
