@@ -132,6 +132,12 @@ struct WalkParams {
     unsigned long long *trace;
     // queue order of the walk kernel: the q-th piece handed out is order[q]
     const uint32_t *order;
+    // cost ordering (nullptr = off): the plan's static order (big pieces,
+    // then small ones) and the buffer the per-run sort writes `order` into
+    const uint32_t *order_in;
+    uint32_t *order_out;
+    uint32_t nbig_units;   // order_in[0, nbig_units) are big pieces
+    uint32_t pad2;
 };
 
 // WalkParams.stats slots

@@ -158,6 +158,7 @@ struct rcdc_plan {
     std::vector<WalkUnit> wunits;
     std::vector<uint32_t> wstream_u0;  // unit0 of every walked stream
     std::vector<uint32_t> worder;      // walk queue order (big pieces first)
+    uint32_t nsmall_units = 0;         // the split pieces at worder's end
     uint64_t walk_small = 0;           // Ls of the split pieces
     std::vector<uint8_t> walked;       // per stream: on the walk path
     uint64_t nwpiece_cuts = 0;
@@ -544,6 +545,7 @@ rcdc_status plan_build(rcdc_ctx *ctx, rcdc_plan *pl, const uint64_t *offs, const
             }
         }
         pl->worder.insert(pl->worder.end(), small.begin(), small.end());
+        pl->nsmall_units = (uint32_t)small.size();
     }
     WalkParams &wp = pl->wprm;
     wp = WalkParams{};
@@ -588,8 +590,15 @@ rcdc_status plan_build(rcdc_ctx *ctx, rcdc_plan *pl, const uint64_t *offs, const
     if (nw) {
         if ((st = ensure_dev(&pl->d_wunits, &pl->cap_wunits, nw))) return st;
         if ((st = ensure_dev(&pl->d_wsu0, &pl->cap_wsu0, pl->wstream_u0.size()))) return st;
-        if ((st = ensure_dev(&pl->d_worder, &pl->cap_worder, nw))) return st;
-        pl->wprm.order = pl->d_worder;
+        // d_worder: the static order, then (cost ordering) the per-run
+        // sorted order and one key byte per piece
+        const bool cost = !getenv("RCDC_WALK_COSTSORT") || atoi(getenv("RCDC_WALK_COSTSORT")) != 0;
+        if ((st = ensure_dev(&pl->d_worder, &pl->cap_worder, cost ? 2 * nw + (nw + 3) / 4 : nw)))
+            return st;
+        pl->wprm.order = cost ? pl->d_worder + nw : pl->d_worder;
+        pl->wprm.order_in = cost ? pl->d_worder : nullptr;
+        pl->wprm.order_out = cost ? pl->d_worder + nw : nullptr;
+        pl->wprm.nbig_units = (uint32_t)(nw - pl->nsmall_units);
         HIP_TRY(upload(pl->d_worder, pl->worder.data(), nw * sizeof(uint32_t)));
         if ((st = ensure_dev(&pl->d_wpiece, &pl->cap_wpiece, pl->nwpiece_cuts))) return st;
         if ((st = ensure_dev(&pl->d_pstatus, &pl->cap_pstatus, nw))) return st;

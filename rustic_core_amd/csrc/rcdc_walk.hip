@@ -1123,9 +1123,57 @@ __global__ __launch_bounds__(kAsmB) void rcdc_walk_assemble_kernel(
 }
 
 // ---------------------------------------------------------------------------
+// Cost-ordered queue.  A piece's walk time is its hashed bytes, and on
+// mixed data most of the variation is how much of it is a zero run (64 B per
+// chunk) rather than random bytes.  One wave per piece samples 64 aligned
+// 8-byte words spread over the piece and counts the non-zero ones (0..64);
+// one workgroup then counting-sorts the queue by that class, big pieces
+// before small ones and heavier before lighter (longest-processing-time
+// first): the last pieces the waves take are the cheap ones.  Only the
+// schedule changes, never the cuts.
+constexpr int kCostKeys = 2 * 65;
+
+__global__ __launch_bounds__(256) void rcdc_walk_cost_kernel(
+    const uint8_t *__restrict__ arena, const StreamDesc *__restrict__ sds,
+    const WalkUnit *__restrict__ units, WalkParams prm, uint8_t *__restrict__ key) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wpb = blockDim.x / 64u;
+    for (uint32_t q = blockIdx.x * wpb + (threadIdx.x >> 6); q < prm.nunits; q += gridDim.x * wpb) {
+        const uint32_t u = prm.order_in[q];
+        const WalkUnit U = units[u];
+        const StreamDesc d = sds[U.stream];
+        const uint64_t len = U.stop - U.start;
+        const uint64_t a = (d.off + U.start + (len * lane) / 64u) & ~7ull;
+        const uint64_t w = a + 8 <= d.off + d.n ? *reinterpret_cast<const uint64_t *>(arena + a) : 0;
+        const uint32_t cls = (uint32_t)__builtin_popcountll(__ballot(w != 0));
+        if (lane == 0) key[q] = (uint8_t)((q < prm.nbig_units ? 65u : 0u) + cls);
+    }
+}
+
+// One workgroup: counting sort of the queue by key, descending.
+__global__ __launch_bounds__(1024) void rcdc_walk_sort_kernel(WalkParams prm,
+                                                              const uint8_t *__restrict__ key) {
+    __shared__ uint32_t s_cnt[kCostKeys];
+    for (uint32_t i = threadIdx.x; i < (uint32_t)kCostKeys; i += blockDim.x) s_cnt[i] = 0;
+    __syncthreads();
+    for (uint32_t q = threadIdx.x; q < prm.nunits; q += blockDim.x) atomicAdd(&s_cnt[key[q]], 1u);
+    __syncthreads();
+    if (threadIdx.x == 0) {  // exclusive prefix, highest key first
+        uint32_t acc = 0;
+        for (int k = kCostKeys - 1; k >= 0; k--) {
+            const uint32_t c = s_cnt[k];
+            s_cnt[k] = acc;
+            acc += c;
+        }
+    }
+    __syncthreads();
+    for (uint32_t q = threadIdx.x; q < prm.nunits; q += blockDim.x)
+        prm.order_out[atomicAdd(&s_cnt[key[q]], 1u)] = prm.order_in[q];
+}
+
 namespace rcdc {
 
-// The hashing part: counters reset + the walk kernel.
+// The hashing part: counters reset, the queue's cost order, the walk kernel.
 hipError_t launch_walk(const uint8_t *arena, const StreamDesc *sds, const WalkUnit *units,
                        const WalkParams &prm, const uint64_t *gtab, uint64_t *piece_cuts,
                        uint64_t *pstatus, uint32_t *ctr, uint32_t blocks, hipStream_t stream) {
@@ -1134,6 +1182,15 @@ hipError_t launch_walk(const uint8_t *arena, const StreamDesc *sds, const WalkUn
     if (e == hipSuccess)
         e = hipMemsetAsync(prm.stats, 0, kWalkStats * sizeof(unsigned long long), stream);
     if (e != hipSuccess) return e;
+    if (prm.order_in && prm.order_out) {
+        // the key bytes follow order_out in the same buffer (plan_build)
+        uint8_t *key = reinterpret_cast<uint8_t *>(prm.order_out + prm.nunits);
+        const uint32_t cb = std::min<uint32_t>((prm.nunits + 3) / 4, 4096);
+        hipLaunchKernelGGL(rcdc_walk_cost_kernel, dim3(cb), dim3(256), 0, stream, arena, sds, units,
+                           prm, key);
+        hipLaunchKernelGGL(rcdc_walk_sort_kernel, dim3(1), dim3(1024), 0, stream, prm,
+                           (const uint8_t *)key);
+    }
     const bool small = prm.mask < 0xFFFFu;
 #define RCDC_WALK_LAUNCH(TSH, SM)                                                                  \
     hipLaunchKernelGGL((rcdc_walk_kernel<TSH, SM>), dim3(blocks), dim3(1024), 0, stream, arena,   \

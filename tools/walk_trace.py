@@ -78,8 +78,27 @@ def run(kind, nstreams, sgib):
     rounds = tr[:, 2].astype(np.float64)
     rr = dur / np.maximum(rounds, 1)
     lane_bytes = st["rounds"] * 64 * (2048 + 64) + st["zones"] * 64 * 64
+    # list scheduling of the measured durations on 4096 slots: the queue's
+    # own order vs longest-first (what a perfect cost-ordered queue would give)
+    import heapq
+
+    def makespan(durs):
+        h = [0.0] * slots
+        for x in durs:
+            t = heapq.heappop(h)
+            heapq.heappush(h, t + x)
+        return max(h)
+    q_order = np.argsort(a, kind="stable")
+    sim_queue = makespan(dur[q_order])
+    sim_lpt = makespan(np.sort(dur)[::-1])
+    top = np.argsort(dur)[::-1][:8]
+    longest = [{"unit": int(i), "start_us": round(float(a[i]), 1), "us": round(float(dur[i]), 1),
+                "rounds": int(tr[i, 2]), "chunks": int(tr[i, 3])} for i in top]
     out = {
         "kind": kind, "streams": nstreams, "gib_per_stream": sgib,
+        "sim_makespan_queue_order_us": round(sim_queue, 1),
+        "sim_makespan_longest_first_us": round(sim_lpt, 1),
+        "longest_pieces": longest,
         "walk_ms": walk_ms / runs, "chain_ms": chain_ms / runs,
         "stats": st, "pieces": int(len(tr)),
         "ref_slide_bytes": ref, "lane_slide_bytes": lane_bytes,
