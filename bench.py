@@ -461,7 +461,8 @@ def run_c4(args, torch, dist, dev, rank, world, local):
                 inf = plan.info()
                 if inf["walk_pieces"]:
                     wst = plan.walk_stats()
-                    lane_hashed += wst["rounds"] * 64 * (2048 + 64) + wst["zones"] * 4096
+                    lane_hashed += (wst["rounds"] * 64 * (inf["walk_seg_bytes"] + 64) +
+                                    wst["zones"] * 4096)
                     walked_batches += 1
                 else:
                     lane_hashed += inf["scanned_bytes"] + 64 * inf["segments"]
@@ -779,7 +780,7 @@ def main():
     ref_hashed = ref_slide_bytes(got_cuts, MIN)
     if walked:
         st = plan.walk_stats()
-        seg = int(os.environ.get("RCDC_WALK_SEG", "2048"))
+        seg = info["walk_seg_bytes"]
         lane_hashed = st["rounds"] * 64 * (seg + 64) + st["zones"] * 64 * 64
         kernel = "rcdc_walk_kernel"
     else:
@@ -808,7 +809,7 @@ def main():
         "lane_hashed_bytes_per_launch": lane_hashed,
         "achieved_lane_hashed_gbs": round(lane_hashed / scan_s / 1e9, 1),
         "frac_lane_hashed": round(lane_hashed / scan_s / 1e9 / HBM_PEAK_GBS, 4),
-        "segment_bytes": int(os.environ.get("RCDC_WALK_SEG", "2048")) if walked
+        "segment_bytes": info["walk_seg_bytes"] if walked
         else info["segment_bytes"],
         "limiter": "VALU issue (~7 VALU + 2 LDS reads per hashed byte; DESIGN.md 3)",
         "pipelined": pipelined,

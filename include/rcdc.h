@@ -190,6 +190,8 @@ typedef struct {
     uint32_t work_items;      /* 64-segment wave work items               */
     uint32_t scan_blocks;     /* workgroups of the scan launch            */
     uint32_t walk_pieces;     /* pieces of long streams on the walk path  */
+    uint32_t walk_seg_bytes;  /* S of the walk kernel's 64-lane rounds    */
+    uint32_t pad;
 } rcdc_plan_info;
 rcdc_status rcdc_plan_get_info(const rcdc_plan *plan, rcdc_plan_info *info);
 
@@ -206,7 +208,7 @@ rcdc_status rcdc_plan_kernel_times(rcdc_plan *plan, uint64_t *runs,
 
 /* Work counters of the walk path (long streams) of the last run, after it
  * completes: stats[0] 64-lane hashing rounds of rcdc_walk_kernel (64 x
- * (S + 64) bytes hashed by lanes each, S = 2048), [1] its min-zone
+ * (S + 64) bytes hashed by lanes each, S = walk_seg_bytes), [1] its min-zone
  * evaluations (64 windows of 64 bytes), [2] chunks it emitted, [3] 1024-lane
  * rounds of the fixup kernel (1024 x (512 + 64) bytes each), [4] fixup zones,
  * [5] cuts the fixups walked, [6] 64-lane rounds of the boundary check

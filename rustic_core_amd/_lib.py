@@ -46,6 +46,8 @@ class PlanInfo(ctypes.Structure):
         ("work_items", ctypes.c_uint32),
         ("scan_blocks", ctypes.c_uint32),
         ("walk_pieces", ctypes.c_uint32),
+        ("walk_seg_bytes", ctypes.c_uint32),
+        ("pad", ctypes.c_uint32),
     ]
 
 

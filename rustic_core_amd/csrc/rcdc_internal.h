@@ -138,6 +138,8 @@ struct WalkParams {
     uint32_t *order_out;
     uint32_t nbig_units;   // order_in[0, nbig_units) are big pieces
     uint32_t pad2;
+    uint64_t chk_budget;   // bytes of gap hashing a boundary check may do before
+                           // it hands the boundary to the fixup kernel
 };
 
 // WalkParams.stats slots

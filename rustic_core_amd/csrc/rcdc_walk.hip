@@ -526,7 +526,6 @@ struct CheckCtx {
     uint64_t budget;  // bytes this boundary may still hash
 };
 
-constexpr uint64_t kCheckBudgetMax = 4;  // x max bytes of gap hashing per boundary
 
 // Piece index k (within the stream of unit0, npieces pieces) holding
 // position p: the last piece with start <= p (pieces differ in size).
@@ -678,7 +677,7 @@ __global__ __launch_bounds__(kChkThreads, 1) void rcdc_walk_check_kernel(
         C.mx = mx;
         C.Lp = prm.piece_bytes;
         C.Ls = prm.small_bytes;
-        C.budget = kCheckBudgetMax * mx;
+        C.budget = prm.chk_budget;
         // result (wave-uniform scalars; the hop entries in LDS, not in a
         // dynamically indexed register array, which would go to scratch)
         struct {
