@@ -216,7 +216,9 @@ rcdc_status rcdc_plan_kernel_times(rcdc_plan *plan, uint64_t *runs,
  * zone evaluations.  With the environment variable
  * RCDC_WALK_TRACE=1 at plan creation, `trace` (if not NULL) receives 4
  * words per walk piece: wall clock (100 MHz) at the piece's start and end,
- * rounds, chunks -- at most trace_cap words.  All zero for plans without
+ * rounds, chunks; then 4 words per piece boundary (rows of piece 0 unused)
+ * from the check kernel: start, end, gap rounds, hop entries -- at most
+ * trace_cap words (2 x walk_pieces x 4 in all).  All zero for plans without
  * walked streams.                                                          */
 #define RCDC_WALK_STATS 8
 rcdc_status rcdc_plan_walk_stats(rcdc_plan *plan, uint64_t *stats, uint64_t *trace,

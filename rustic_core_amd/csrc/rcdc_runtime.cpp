@@ -615,7 +615,8 @@ rcdc_status plan_build(rcdc_ctx *ctx, rcdc_plan *pl, const uint64_t *offs, const
         pl->wprm.stats = pl->d_wstats;
         pl->wprm.trace = nullptr;
         if (const char *e = getenv("RCDC_WALK_TRACE"); e && atoi(e) > 0) {
-            if ((st = ensure_dev(&pl->d_wtrace, &pl->cap_wtrace, nw * kTraceWords))) return st;
+            if ((st = ensure_dev(&pl->d_wtrace, &pl->cap_wtrace, 2 * nw * kTraceWords))) return st;
+            HIP_TRY(hipMemset(pl->d_wtrace, 0, 2 * nw * kTraceWords * 8));
             pl->wprm.trace = pl->d_wtrace;
         }
         HIP_TRY(upload(pl->d_wunits, pl->wunits.data(), nw * sizeof(WalkUnit)));
@@ -1327,7 +1328,7 @@ rcdc_status rcdc_plan_walk_stats(rcdc_plan *plan, uint64_t *stats, uint64_t *tra
     HIP_TRY(hipEventSynchronize(plan->done));
     static_assert(RCDC_WALK_STATS == kWalkStats, "stats slots");
     HIP_TRY(hipMemcpy(stats, plan->d_wstats, kWalkStats * 8, hipMemcpyDeviceToHost));
-    const uint64_t nw = plan->wunits.size() * kTraceWords;
+    const uint64_t nw = 2 * plan->wunits.size() * kTraceWords;  // walk rows, then check rows
     if (trace && trace_cap && plan->wprm.trace)
         HIP_TRY(hipMemcpy(trace, plan->d_wtrace, std::min(trace_cap, nw) * 8,
                           hipMemcpyDeviceToHost));

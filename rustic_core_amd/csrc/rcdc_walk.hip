@@ -660,6 +660,7 @@ __global__ __launch_bounds__(kChkThreads, 1) void rcdc_walk_check_kernel(
         if (u >= prm.nunits) break;
         const WalkUnit U = units[u];
         if (U.piece == 0) continue;
+        const uint64_t t0 = prm.trace ? (uint64_t)wall_clock64() : 0;
         W.rounds = W.zones = 0;
         const StreamDesc d = sds[U.stream];
         W.off = d.off;
@@ -806,6 +807,13 @@ __global__ __launch_bounds__(kChkThreads, 1) void rcdc_walk_check_kernel(
             if (R.kind == kBoundFixup) fixlist[atomicAdd(&ctr[1], 1u)] = u;
             stats_add(s_st, kWalkStatChkRounds, W.rounds);
             stats_add(s_st, kWalkStatChkZones, W.zones);
+            if (prm.trace) {
+                unsigned long long *tr = prm.trace + ((uint64_t)prm.nunits + u) * kTraceWords;
+                tr[0] = t0;
+                tr[1] = (uint64_t)wall_clock64();
+                tr[2] = W.rounds;
+                tr[3] = R.nhops;
+            }
         }
     }
     stats_flush(s_st, prm.stats);

@@ -132,20 +132,25 @@ class DevicePlan:
     WALK_STAT_NAMES = ("rounds", "zones", "chunks", "fix_rounds", "fix_zones", "fix_cuts",
                        "chk_rounds", "chk_zones")
 
-    def walk_stats(self, trace: bool = False):
+    def walk_stats(self, trace: bool = False, check_trace: bool = False):
         """Work counters of the last run's walk path (rcdc_plan_walk_stats):
         a dict, plus the ``(pieces, 4)`` per-piece trace (t0, t1 in 100 MHz
         ticks, rounds, chunks) when ``trace`` (plan built with
-        RCDC_WALK_TRACE=1)."""
+        RCDC_WALK_TRACE=1), plus the per-boundary check trace (t0, t1, gap
+        rounds, hop entries; row 0 of each stream unused) when
+        ``check_trace``."""
         stats = np.zeros(8, dtype=np.uint64)
         pieces = self.info()["walk_pieces"]
-        tr = np.zeros((max(pieces, 1), 4), dtype=np.uint64) if trace else None
+        trace = trace or check_trace
+        tr = np.zeros((2 * max(pieces, 1), 4), dtype=np.uint64) if trace else None
         st = _lib.lib().rcdc_plan_walk_stats(self._h, stats.ctypes.data,
                                              tr.ctypes.data if trace else None,
                                              tr.size if trace else 0)
         if st:
             raise status_error(st, _lib.last_error())
         d = {k: int(v) for k, v in zip(self.WALK_STAT_NAMES, stats)}
+        if check_trace:
+            return d, tr[:pieces], tr[pieces:2 * pieces]
         return (d, tr[:pieces]) if trace else d
 
     def close(self):

@@ -52,7 +52,7 @@ def run(kind, nstreams, sgib):
     torch.cuda.synchronize()
     plan.set_timing(False)
     runs, walk_ms, chain_ms = plan.kernel_times()
-    st, tr = plan.walk_stats(trace=True)
+    st, tr, ct = plan.walk_stats(check_trace=True)
     cuts = plan.results()
     # reference slides (what rabin.rs:127-188 hashes): per chunk that is not the
     # short final one, 63 prefill bytes + (cut - (s + min))
@@ -94,8 +94,26 @@ def run(kind, nstreams, sgib):
     top = np.argsort(dur)[::-1][:8]
     longest = [{"unit": int(i), "start_us": round(float(a[i]), 1), "us": round(float(dur[i]), 1),
                 "rounds": int(tr[i, 2]), "chunks": int(tr[i, 3])} for i in top]
+    # the check kernel: per boundary (rows with t0 = 0 are first pieces)
+    cv = ct[:, 0] > 0
+    c0 = ct[cv, 0].astype(np.int64)
+    c1 = ct[cv, 1].astype(np.int64)
+    cb = c0.min()
+    cdur = (c1 - c0) / 100.0
+    crounds = ct[cv, 2].astype(np.int64)
+    check = {
+        "boundaries": int(cv.sum()), "span_us": float((c1.max() - cb) / 100.0),
+        "us_p50_p90_p99_max": [float(np.percentile(cdur, q)) for q in (50, 90, 99)] + [float(cdur.max())],
+        "with_gap_rounds": int(np.count_nonzero(crounds)),
+        "us_p50_with_rounds": float(np.median(cdur[crounds > 0])) if np.any(crounds) else None,
+        "us_p50_without_rounds": float(np.median(cdur[crounds == 0])),
+        "rounds_max": int(crounds.max()),
+        "last_start_us": float((c0.max() - cb) / 100.0),
+        "walk_end_to_check_start_us": float((cb - (t1.max())) / 100.0),
+    }
     out = {
         "kind": kind, "streams": nstreams, "gib_per_stream": sgib,
+        "check": check,
         "sim_makespan_queue_order_us": round(sim_queue, 1),
         "sim_makespan_longest_first_us": round(sim_lpt, 1),
         "longest_pieces": longest,
