@@ -159,6 +159,7 @@ struct rcdc_plan {
     std::vector<uint32_t> wstream_u0;  // unit0 of every walked stream
     std::vector<uint32_t> worder;      // walk queue order (big pieces first)
     uint32_t nsmall_units = 0;         // the split pieces at worder's end
+    bool walk_many = false;            // pieces outnumber 2x the wave slots
     uint64_t walk_small = 0;           // Ls of the split pieces
     std::vector<uint8_t> walked;       // per stream: on the walk path
     uint64_t nwpiece_cuts = 0;
@@ -502,7 +503,8 @@ rcdc_status plan_build(rcdc_ctx *ctx, rcdc_plan *pl, const uint64_t *offs, const
         for (uint32_t i = 0; i < n && Lp; i++)
             if (pl->walked[i]) big_total += std::max<uint64_t>(lens[i] / Lp, 1);
         const uint64_t slots = (uint64_t)std::max(ctx->num_cus, 1) * 16;
-        uint64_t split_pct = big_total >= 2 * slots ? 20 : 0;
+        pl->walk_many = big_total >= 2 * slots;
+        uint64_t split_pct = pl->walk_many ? 20 : 0;
         if (const char *e = getenv("RCDC_WALK_SPLIT")) split_pct = std::min<uint64_t>(atoll(e), 100);
         const uint64_t Ls = Lp ? std::max<uint64_t>(Lp / 4 / ctx->min, 1) * ctx->min : 0;
         pl->walk_small = Ls;
@@ -596,7 +598,11 @@ rcdc_status plan_build(rcdc_ctx *ctx, rcdc_plan *pl, const uint64_t *offs, const
         if ((st = ensure_dev(&pl->d_wsu0, &pl->cap_wsu0, pl->wstream_u0.size()))) return st;
         // d_worder: the static order, then (cost ordering) the per-run
         // sorted order and one key byte per piece
-        const bool cost = !getenv("RCDC_WALK_COSTSORT") || atoi(getenv("RCDC_WALK_COSTSORT")) != 0;
+        // (only when waves take several pieces each: with about one piece
+        // per wave slot the order hardly matters and the two extra launches
+        // are most of C5's latency-bound step)
+        bool cost = pl->walk_many;
+        if (const char *e = getenv("RCDC_WALK_COSTSORT")) cost = atoi(e) != 0;
         if ((st = ensure_dev(&pl->d_worder, &pl->cap_worder, cost ? 2 * nw + (nw + 3) / 4 : nw)))
             return st;
         pl->wprm.order = cost ? pl->d_worder + nw : pl->d_worder;

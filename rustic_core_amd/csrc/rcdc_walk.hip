@@ -553,10 +553,81 @@ __device__ __forceinline__ uint32_t piece_of(const CheckCtx &C, uint64_t p) {
     return piece_at(C.U, C.Lp, C.Ls, p);
 }
 
+// ---- gap rounds shared inside a check workgroup ----------------------------
+// The chain phase lasts as long as its slowest boundary, and the slow ones
+// hash unsearched gaps (up to min + 64 bytes: 8 sequential 64-lane rounds).
+// A wave with a gap of >= 2 rounds posts them as jobs in an LDS ring; every
+// wave of the workgroup that waits -- for its own jobs, or because no
+// boundaries are left -- pops and runs jobs, so in the tail up to 8 waves
+// hash one gap.  No barriers: LDS atomics, per-slot ready flags, s_sleep.
+// Termination: a waiting wave runs jobs itself (its own included), so every
+// posted job is run; idle waves leave when no wave is active and the ring is
+// empty.
+constexpr uint32_t kGapSlots = 128;  // >= 8 waves x 9 outstanding rounds
+constexpr uint32_t kChkWaves = 8;
+struct GapQueue {
+    uint32_t head, tail, active, pad;
+    uint32_t ready[kGapSlots];
+    uint32_t req[kGapSlots];
+    uint64_t A[kGapSlots], lo[kGapSlots], hi[kGapSlots], off[kGapSlots];
+    unsigned long long hit[kChkWaves];  // per requesting wave: min over its rounds
+    uint32_t left[kChkWaves];           // its rounds not yet run
+};
+
+__device__ __forceinline__ uint32_t lds_load(const uint32_t *p) {
+    return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+__device__ __forceinline__ void lds_store(uint32_t *p, uint32_t v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+// Pop one job (wave-uniform): its ring slot, or kGapSlots if the ring is empty.
+__device__ uint32_t gap_pop(GapQueue &Q, uint32_t lane) {
+    uint32_t got = 0xFFFFFFFFu;
+    if (lane == 0) {
+        uint32_t h = lds_load(&Q.head);
+        while (h < lds_load(&Q.tail)) {
+            const uint32_t prev = atomicCAS(&Q.head, h, h + 1);
+            if (prev == h) {
+                got = h;
+                break;
+            }
+            h = prev;
+        }
+    }
+    got = __builtin_amdgcn_readfirstlane(got);
+    if (got == 0xFFFFFFFFu) return kGapSlots;
+    const uint32_t sl = got % kGapSlots, lap = got / kGapSlots + 1;
+    // ready[sl] holds the lap of the job it carries (0: empty), so a job of
+    // an earlier lap not yet copied out is never taken for this one
+    while (__builtin_amdgcn_readfirstlane(lds_load(&Q.ready[sl])) != lap) __builtin_amdgcn_s_sleep(1);
+    return sl;
+}
+
+// Run the job in slot sl: one 64-lane round, its first hit into hit[req].
+template <int TSH, bool SMALL>
+__device__ void gap_run(GapQueue &Q, const Walk &W, uint32_t sl, uint64_t *rounds) {
+    Walk H = W;
+    const uint64_t A = Q.A[sl], lo = Q.lo[sl], hi = Q.hi[sl];
+    H.off = Q.off[sl];
+    const uint32_t r = Q.req[sl];
+    wave_sync();
+    if (W.lane == 0) lds_store(&Q.ready[sl], 0);  // fields copied: the slot is free
+    const uint64_t h = round_first<64, TSH, SMALL>(H, A, lo, hi);
+    (*rounds)++;
+    if (W.lane == 0) {
+        if (h != kNoCut) atomicMin(&Q.hit[r], (unsigned long long)h);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        atomicSub(&Q.left[r], 1u);
+    }
+}
+
 // First pure-window hit in [lo, lim) of the stream, or lim if none;
 // kNoCut if the hashing budget ran out.
 template <int TSH, bool SMALL>
-__device__ uint64_t check_first_hit(Walk &W, CheckCtx &C, uint64_t lo, uint64_t lim) {
+__device__ uint64_t check_first_hit(Walk &W, CheckCtx &C, uint64_t lo, uint64_t lim,
+                                    GapQueue *Q, uint32_t wave, uint64_t *shared_rounds) {
     uint64_t p = lo;
     // every iteration passes one searched interval or one gap: at most ~2 per
     // min bytes of [lo, lim); the cap only guarantees termination
@@ -585,11 +656,47 @@ __device__ uint64_t check_first_hit(Walk &W, CheckCtx &C, uint64_t lo, uint64_t 
         if (gap_end - p > C.budget) return kNoCut;
         C.budget -= gap_end - p;
         uint64_t A = ((W.off + p - 1) & ~63ull) - W.off;
-        while (A < gap_end) {
-            W.rounds++;
-            const uint64_t h = round_first<64, TSH, SMALL>(W, A, p, gap_end);
+        const uint64_t step = 64ull * W.S;
+        const uint64_t R = (gap_end - A + step - 1) / step;
+        if (Q && R >= 2 && R <= kGapSlots / kChkWaves) {  // (ring capacity: 8 waves x 16)
+            // post the R rounds, then run jobs until ours are done
+            uint32_t t = 0;
+            if (W.lane == 0) {
+                Q->hit[wave] = kNoCut;
+                lds_store(&Q->left[wave], (uint32_t)R);
+                t = atomicAdd(&Q->tail, (uint32_t)R);
+            }
+            t = __builtin_amdgcn_readfirstlane(t);
+            if (W.lane == 0) {
+                for (uint32_t r = 0; r < (uint32_t)R; r++) {
+                    const uint32_t sl = (t + r) % kGapSlots, lap = (t + r) / kGapSlots + 1;
+                    while (lds_load(&Q->ready[sl]) != 0) __builtin_amdgcn_s_sleep(1);
+                    Q->A[sl] = A + r * step;
+                    Q->lo[sl] = p;
+                    Q->hi[sl] = gap_end;
+                    Q->off[sl] = W.off;
+                    Q->req[sl] = wave;
+                    lds_store(&Q->ready[sl], lap);
+                }
+            }
+            wave_sync();
+            while (__builtin_amdgcn_readfirstlane(lds_load(&Q->left[wave])) != 0) {
+                const uint32_t sl = gap_pop(*Q, W.lane);
+                if (sl < kGapSlots) gap_run<TSH, SMALL>(*Q, W, sl, shared_rounds);
+                else __builtin_amdgcn_s_sleep(2);
+            }
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+            uint64_t h = 0;
+            if (W.lane == 0) h = Q->hit[wave];
+            h = readlane64(h, 0);
             if (h != kNoCut) return h;
-            A += 64ull * W.S;
+        } else {
+            while (A < gap_end) {
+                W.rounds++;
+                const uint64_t h = round_first<64, TSH, SMALL>(W, A, p, gap_end);
+                if (h != kNoCut) return h;
+                A += step;
+            }
         }
         p = gap_end;
     }
@@ -633,8 +740,15 @@ __global__ __launch_bounds__(kChkThreads, 1) void rcdc_walk_check_kernel(
     __shared__ __attribute__((aligned(16))) uint8_t s_win[kChkThreads / 64][128];
     __shared__ uint64_t s_hops[kChkThreads / 64][kMaxHops];  // the wave's hop entries
     __shared__ BlockStats s_st;
+    __shared__ GapQueue s_q;
     stats_init(s_st);
-    fill_tables(s_tab, gtab, prm.idx_shift, threadIdx.x, kChkThreads);
+    if (threadIdx.x == 0) {
+        s_q.head = s_q.tail = 0;
+        s_q.active = kChkThreads / 64;
+    }
+    for (uint32_t i = threadIdx.x; i < kGapSlots; i += blockDim.x) s_q.ready[i] = 0;
+    fill_tables(s_tab, gtab, prm.idx_shift, threadIdx.x, kChkThreads);  // (ends with a barrier)
+    uint64_t shared_rounds = 0;
     const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
     Walk W;
     W.arena = arena;
@@ -737,7 +851,7 @@ __global__ __launch_bounds__(kChkThreads, 1) void rcdc_walk_check_kernel(
                     else if (lim <= z + 64) nxt = lim;
                     else lo = z + 64;
                 }
-                if (lo) nxt = check_first_hit<TSH, SMALL>(W, C, lo, lim);
+                if (lo) nxt = check_first_hit<TSH, SMALL>(W, C, lo, lim, &s_q, wave, &shared_rounds);
                 if (nxt == kNoCut) {
                     R.kind = kBoundFixup;
                     R.fix_from = c;
@@ -816,6 +930,21 @@ __global__ __launch_bounds__(kChkThreads, 1) void rcdc_walk_check_kernel(
             }
         }
     }
+    // no boundaries left: run the other waves' gap rounds until none can come
+    if (lane == 0) atomicSub(&s_q.active, 1u);
+    for (;;) {
+        const uint32_t sl = gap_pop(s_q, lane);
+        if (sl < kGapSlots) {
+            gap_run<TSH, SMALL>(s_q, W, sl, &shared_rounds);
+            continue;
+        }
+        const uint32_t act = __builtin_amdgcn_readfirstlane(lds_load(&s_q.active));
+        const uint32_t hd = __builtin_amdgcn_readfirstlane(lds_load(&s_q.head));
+        const uint32_t tl = __builtin_amdgcn_readfirstlane(lds_load(&s_q.tail));
+        if (act == 0 && hd == tl) break;
+        __builtin_amdgcn_s_sleep(2);
+    }
+    if (lane == 0) stats_add(s_st, kWalkStatChkRounds, shared_rounds);
     stats_flush(s_st, prm.stats);
 }
 

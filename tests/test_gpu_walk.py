@@ -181,11 +181,14 @@ def test_walk_selected_by_default_for_large_batches():
         assert np.array_equal(got[i], oracle.chunk_cuts(host, oracle.DEFAULT_POLY, mn, avg, mx))
 
 
-def test_walk_split_pieces(walk_env, monkeypatch):
+@pytest.mark.parametrize("costsort", ["0", "1"])
+def test_walk_split_pieces(walk_env, monkeypatch, costsort):
     """The split tail pieces (RCDC_WALK_SPLIT: the last share of a stream's
-    pieces cut in four, handed out last) on every data kind."""
+    pieces cut in four, handed out last) on every data kind, with and
+    without the per-run cost-ordered queue (RCDC_WALK_COSTSORT)."""
     walk_env(256 * KiB)
     monkeypatch.setenv("RCDC_WALK_SPLIT", "50")
+    monkeypatch.setenv("RCDC_WALK_COSTSORT", costsort)
     _run(SMALL, [_rand(95, 6 * MiB + 5), np.zeros(5 * MiB, np.uint8),
                  _mixed(96, 8 * MiB, 4 * KiB, 512 * KiB, 1 * KiB, 600 * KiB),
                  np.concatenate([_rand(97, 999), np.zeros(3 * MiB, np.uint8), _rand(98, MiB)])])
