@@ -264,6 +264,27 @@ def _read(reader, n: int) -> bytes:
         return b if b is not None else b""
 
 
+def _read_into(reader, mv: memoryview) -> int:
+    """reader.readinto(mv) (no intermediate bytes object) with the same error
+    mapping; readers without readinto go through read()."""
+    readinto = getattr(reader, "readinto", None)
+    while True:
+        try:
+            if readinto is None:
+                raise NotImplementedError
+            n = readinto(mv)
+        except NotImplementedError:  # e.g. an io.RawIOBase that only has read()
+            b = _read(reader, len(mv))
+            mv[:len(b)] = b
+            return len(b)
+        except InterruptedError:
+            continue  # ErrorKind::Interrupted -> retry (rabin.rs:173)
+        except OSError as e:
+            raise RusticError(ErrorKind.InputOutput,
+                              f"Failed to read from reader in iterator: {e}") from e
+        return n or 0
+
+
 class RabinChunkIter:
     """rabin.rs ChunkIter with device-computed cut points.
 
@@ -277,8 +298,9 @@ class RabinChunkIter:
         self._reader = reader
         self.size_hint = size_hint  # capacity hint only; never affects cuts
         self._stream = _Stream(ctx)
-        self._buf = bytearray()      # bytes read, not yet compacted away
-        self._off = 0                # _buf[_off:] not yet yielded
+        self._buf = bytearray()      # _buf[:_len] read, not yet compacted away
+        self._len = 0
+        self._off = 0                # _buf[_off:_len] not yet yielded
         self._base = 0               # absolute offset of _buf[_off]
         self._cuts = collections.deque()
         self._eof = False
@@ -289,16 +311,23 @@ class RabinChunkIter:
 
     def _fill(self) -> None:
         while not self._cuts and not self._eof:
-            data = _read(self._reader, READ_SIZE)
-            if not data:
-                self._eof = True
             # compact what was yielded once it dominates the buffer (amortised
             # O(1) per byte instead of a memmove per chunk)
-            if self._off and self._off >= len(self._buf) // 2:
-                del self._buf[:self._off]
-                self._off = 0
-            self._buf += data
-            self._cuts.extend(int(c) for c in self._stream.feed(data, self._eof))
+            if self._off and self._off >= self._len // 2:
+                rem = self._len - self._off
+                self._buf[:rem] = self._buf[self._off:self._len]
+                self._off, self._len = 0, rem
+            if len(self._buf) < self._len + READ_SIZE:
+                self._buf.extend(bytes(self._len + READ_SIZE - len(self._buf)))
+            # the reader fills the buffer in place (one copy fewer than
+            # read() + append)
+            with memoryview(self._buf) as mv:
+                n = _read_into(self._reader, mv[self._len:self._len + READ_SIZE])
+                if not n:
+                    self._eof = True
+                cuts = self._stream.feed(mv[self._len:self._len + n], self._eof)
+            self._len += n
+            self._cuts.extend(int(c) for c in cuts)
 
     def __next__(self) -> bytes:
         if self._finished:
