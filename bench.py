@@ -85,6 +85,9 @@ def parse():
                     help="--aead: blobs = the chunks of the first N streams")
     ap.add_argument("--pack", action="store_true",
                     help="also build pack files of the chunks on the device (rcdc_pack_build)")
+    ap.add_argument("--zstd", action="store_true",
+                    help="also compress the chunks as blobs on the device (rcdc_zstd_compress)")
+    ap.add_argument("--zstd-level", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-parity", action="store_true")
     ap.add_argument("--abi-e2e", action="store_true",
@@ -846,6 +849,9 @@ def main():
                                          world == 1 and not args.no_cpu_baseline)
     if args.pack and rank == 0:
         out_extra["pack"] = pack_measure(torch, plan, arena, offs, lens, dev, args)
+    if args.zstd and rank == 0:
+        out_extra["zstd"] = zstd_measure(torch, plan, arena, offs, lens, dev, args,
+                                         world == 1 and not args.no_cpu_baseline)
     if args.e2e and rank == 0:
         out_extra["e2e"] = e2e_rate(torch, arena, offs, lens, plan, args.workload)
     if args.abi_e2e and rank == 0 and os.path.exists(os.path.join(ROOT, "tools", "abi_e2e")):
@@ -1104,6 +1110,101 @@ def aead_measure(torch, plan, arena, offs, lens, dev, args, cpu: bool) -> dict:
                                "unit": "GiB/s", "cores": 1, "kind": "port",
                                "sample": f"oracle seal of {len(sample) >> 20} MiB, repeated 3 s"}
     del sealed, plain
+    torch.cuda.empty_cache()
+    return out
+
+
+def zstd_measure(torch, plan, arena, offs, lens, dev, args, cpu: bool) -> dict:
+    """Blob compression of the chunks just cut (the
+    zstd half): every chunk of the first --aead-streams streams becomes one
+    zstd frame (backend/decrypt.rs:489-503 encode_all, per blob as
+    blob/packer.rs:268-270), one rcdc_zstd_compress call.  Time by HIP events
+    on the launch stream; a sample of frames decoded with libzstd (the
+    checker); libzstd level 3 on the host's threads as the CPU rate."""
+    from concurrent.futures import ThreadPoolExecutor
+    from oracle import zstd_ref as zr
+    from rustic_core_amd.compress import compress_blobs, frame_layout, make_refs
+    ns = min(len(lens), max(args.aead_streams, 1))
+    cuts = plan.results()[:ns]
+    in_offs, blens = [], []
+    for i in range(ns):
+        prev = 0
+        for c in cuts[i]:
+            in_offs.append(int(offs[i]) + prev)
+            blens.append(int(c) - prev)
+            prev = int(c)
+    nb, tot = len(blens), int(sum(blens))
+    f_offs, ftot = frame_layout(blens)
+    frames = torch.empty(ftot + 64, dtype=torch.uint8, device=dev)
+    refs = make_refs(in_offs, blens, f_offs)
+    side = torch.cuda.Stream(dev)
+    sp = side.cuda_stream
+    ctx = plan.ctx
+    a, f = arena.data_ptr(), frames.data_ptr()
+    out_lens = compress_blobs(ctx, a, refs, f, args.zstd_level, sp)
+    torch.cuda.synchronize(dev)
+    k = 5
+    e = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    t0 = time.perf_counter()
+    e[0].record(side)
+    for _ in range(k):
+        out_lens = compress_blobs(ctx, a, refs, f, args.zstd_level, sp)
+    e[1].record(side)
+    torch.cuda.synchronize(dev)
+    wall_ms = (time.perf_counter() - t0) * 1e3 / k
+    ms = e[0].elapsed_time(e[1]) / k
+    flen = int(np.sum(out_lens))
+    rng = np.random.default_rng(0x2575)
+    idx = sorted(set([0, nb - 1] + [int(x) for x in rng.integers(0, nb, 10)]))
+    mism = 0
+    for i in idx:
+        d = arena[in_offs[i]:in_offs[i] + blens[i]].cpu().numpy().tobytes()
+        fr = frames[int(f_offs[i]):int(f_offs[i]) + int(out_lens[i])].cpu().numpy().tobytes()
+        mism += zr.decompress(fr) != d
+    out = {
+        "kernels": "rcdc_zstd_block_kernel + rcdc_zstd_frame_kernel + rcdc_zstd_copy_kernel",
+        "level": args.zstd_level, "blobs": nb, "bytes": tot, "frame_bytes": flen,
+        "ratio": round(flen / max(tot, 1), 4),
+        "ms_per_call": round(ms, 3), "wall_ms_per_call": round(wall_ms, 3),
+        "gibs": round(tot / (ms / 1e3) / GiB, 2),
+        "hbm_frac": round((tot + flen) / (ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
+        "check": {"blobs": len(idx), "mismatches": int(mism),
+                  "checker": f"libzstd {zr.version()} ZSTD_decompress (oracle/zstd_ref.py)"},
+    }
+    if cpu:
+        # libzstd level 3 (the library rustic links, another version) on the
+        # same chunks, one chunk per task on the process's threads, ~5 s
+        thr = cpu_threads()[0]
+        host = {}
+        sample, sb = [], 0
+        for i in range(nb):
+            if sb >= (2 << 30):
+                break
+            sample.append(i)
+            sb += blens[i]
+        for i in sample:
+            host[i] = arena[in_offs[i]:in_offs[i] + blens[i]].cpu().numpy()
+        bufs = {i: np.empty(zr.lib().ZSTD_compressBound(blens[i]), np.uint8) for i in sample}
+
+        def one(i):
+            h, b = host[i], bufs[i]
+            return zr.compress_into(b.ctypes.data, len(b), h.ctypes.data, len(h), 3)
+
+        done, clen, t0 = 0, 0, time.perf_counter()
+        with ThreadPoolExecutor(thr) as ex:
+            while time.perf_counter() - t0 < 5.0:
+                clen = sum(ex.map(one, sample))
+                done += sb
+        dt = time.perf_counter() - t0
+        out["cpu_baseline"] = {
+            "value": round(done / dt / GiB, 3), "unit": "GiB/s", "cores": thr,
+            "kind": "reference",
+            "sample": f"libzstd {zr.version()} ZSTD_compress level 3 over the first {len(sample)} "
+                      f"chunks ({sb / GiB:.2f} GiB), repeated ~5 s, one chunk per task",
+            "ratio_level3": round(clen / max(sb, 1), 4),
+            "device_ratio_same_chunks": round(int(np.sum(out_lens[:len(sample)])) / max(sb, 1), 4),
+        }
+    del frames
     torch.cuda.empty_cache()
     return out
 

@@ -336,6 +336,38 @@ rcdc_status rcdc_pack_build(rcdc_ctx *ctx, const uint8_t *key, const void *d_in,
                             uint32_t npacks, void *d_out, uint64_t out_len,
                             uint32_t *blob_offsets, void *hip_stream);
 
+/* ---- blob compression: backend/decrypt.rs:478-506 (`encode_all(data,
+ * level)` before `Key::encrypt_data` when the repository is version 2,
+ * configfile.rs:177-186), applied by the packer's process_data
+ * (blob/packer.rs:268-270) -- here to chunks already in HBM.  Each blob
+ * becomes one zstd frame (RFC 8878) that any zstd decoder reads back (rustic's
+ * decode_all, decrypt.rs:71-95); the bytes are this library's own, not
+ * libzstd's (no zstd version promises another's output).               ---- */
+
+/* One blob: bytes [in_off, in_off + len) of d_in become a frame at out_off of
+ * d_out, at most rcdc_zstd_bound(len) bytes.  Any alignment. */
+typedef struct {
+    uint64_t in_off;
+    uint64_t len;      /* < 2^32 (decrypt.rs:479-487: the length is a u32) */
+    uint64_t out_off;
+} rcdc_zstd_ref;
+
+/* Worst-case frame size of a len-byte blob (header + stored blocks). */
+uint64_t rcdc_zstd_bound(uint64_t len);
+
+/* Compress n blobs (refs is a HOST array).  level: zstd's range
+ * [-131072, 22] (0 = zstd's default, rustic's choice for version 2);
+ * out-of-range -> InvalidInput.  On return (synchronous) out_lens[i] (host)
+ * holds blob i's frame length.  Calls on one context take turns.          */
+rcdc_status rcdc_zstd_compress(rcdc_ctx *ctx, int level, const void *d_in,
+                               const rcdc_zstd_ref *refs, uint32_t n, void *d_out,
+                               uint64_t *out_lens, void *hip_stream);
+
+/* The FSE coding tables the kernels use (predefined distributions, RFC 8878
+ * 3.1.1.3.2.2), copied to out (rcdc_zstd_tables_size() bytes): for tests. */
+void rcdc_zstd_tables(void *out);
+uint64_t rcdc_zstd_tables_size(void);
+
 /* ABI version of the loaded library (== RCDC_ABI_VERSION). */
 uint32_t rcdc_abi_version(void);
 

@@ -26,6 +26,7 @@ EXPORTS = (
     "rcdc_plan_set_pipeline", "rcdc_plan_hash_many", "rcdc_plan_walk_stats",
     "rcdc_plan_finish", "rcdc_stream_queued", "rcdc_stream_batch_bytes",
     "rcdc_aead_seal", "rcdc_aead_open", "rcdc_pack_build",
+    "rcdc_zstd_bound", "rcdc_zstd_compress", "rcdc_zstd_tables", "rcdc_zstd_tables_size",
 )
 ABI_VERSION = 1
 
@@ -154,6 +155,14 @@ def lib() -> ctypes.CDLL:
     L.rcdc_aead_open.argtypes = [vp, vp, vp, vp, u32, vp, vp, vp]
     L.rcdc_pack_build.restype = st
     L.rcdc_pack_build.argtypes = [vp, vp, vp, vp, u32, vp, u32, vp, u64, vp, vp]
+    L.rcdc_zstd_bound.restype = u64
+    L.rcdc_zstd_bound.argtypes = [u64]
+    L.rcdc_zstd_compress.restype = st
+    L.rcdc_zstd_compress.argtypes = [vp, ctypes.c_int, vp, vp, u32, vp, vp, vp]
+    L.rcdc_zstd_tables.restype = None
+    L.rcdc_zstd_tables.argtypes = [vp]
+    L.rcdc_zstd_tables_size.restype = u64
+    L.rcdc_zstd_tables_size.argtypes = []
     L.rcdc_plan_device_digests.restype = st
     L.rcdc_plan_device_digests.argtypes = [vp, P(u64)]
     _lib = L

@@ -206,4 +206,53 @@ struct AeadUnit {  // 16 B
     uint32_t pad;
 };
 
+// ---- blob compression (rcdc_zstd.hip) --------------------------------------
+// A blob becomes one zstd frame (RFC 8878): header, then its bytes cut into
+// blocks of kZstdBlock, each stored raw, as RLE, or compressed (raw literals +
+// sequences coded with the predefined FSE tables).  Matches stay inside their
+// block.
+constexpr uint32_t kZstdBlock = 128u * 1024u;     // ZSTD_BLOCKSIZE_MAX
+constexpr uint32_t kZstdSlot = kZstdBlock + 64u;  // scratch per block: compressed content
+constexpr uint32_t kZstdMaxSeq = kZstdBlock / 4u + 1u;  // matches are >= 4 bytes
+constexpr uint32_t kZstdTypeRaw = 0, kZstdTypeRle = 1, kZstdTypeComp = 2;
+
+struct ZstdBlob {  // 32 B
+    uint64_t in_off;   // the blob's bytes in the input
+    uint64_t out_off;  // where its frame starts in the output
+    uint32_t len;
+    uint32_t blk0;     // its blocks: [blk0, blk0 + nblk) of this launch
+    uint32_t nblk;
+    uint32_t pad;
+};
+static_assert(sizeof(ZstdBlob) == 32, "ZstdBlob is 32 B");
+
+struct ZstdBlk {  // 16 B
+    uint32_t blob;
+    uint32_t start;    // offset in the blob
+    uint32_t len;      // <= kZstdBlock
+    uint32_t flags;    // bit 0: the blob's first block, bit 1: its last
+};
+
+// FSE compression tables of the predefined distributions (RFC 8878
+// 3.1.1.3.2.2) in the layout of zstd's FSE_buildCTable: per symbol
+// {deltaFindState, deltaNbBits}, then the state tables; plus the code tables.
+struct ZstdFseSym {
+    int32_t find;
+    uint32_t nbits;
+};
+struct ZstdTables {
+    ZstdFseSym ll[36];
+    ZstdFseSym ml[53];
+    ZstdFseSym of[32];
+    uint16_t llst[64];
+    uint16_t mlst[64];
+    uint16_t ofst[32];
+    uint8_t llcode[64];   // literal length < 64 -> code
+    uint8_t mlcode[128];  // match length - 3 < 128 -> code
+    uint8_t llbits[36];
+    uint8_t mlbits[53];
+    uint8_t pad[3];
+};
+static_assert(sizeof(ZstdTables) % 4 == 0, "ZstdTables is copied as words");
+
 }  // namespace rcdc

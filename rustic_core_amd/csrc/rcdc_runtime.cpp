@@ -65,6 +65,11 @@ hipError_t launch_aead(bool open, const uint8_t *in, uint8_t *out, const AeadBlo
                        uint32_t nblobs, const AeadUnit *units, uint32_t nunits,
                        const uint32_t *unit0, const AeadKeyDev *key, uint32_t *partials,
                        uint32_t *status, uint32_t cus, hipStream_t stream);
+uint32_t zstd_block_grid(uint32_t cus);
+hipError_t launch_zstd(const uint8_t *in, uint8_t *out, const ZstdBlob *blobs, uint32_t nblobs,
+                       const ZstdBlk *blks, uint32_t nblk, const ZstdTables *tabs, uint8_t *slots,
+                       uint64_t *seqbuf, uint32_t grid, uint2 *res, uint64_t *bpos,
+                       uint64_t *out_lens, hipStream_t stream);
 }  // namespace rcdc
 
 using namespace rcdc;
@@ -254,6 +259,16 @@ struct rcdc_ctx {
     uint64_t cap_aead_key = 0, cap_aead_blobs = 0, cap_aead_units = 0, cap_aead_unit0 = 0,
              cap_aead_partials = 0, cap_aead_status = 0, cap_aead_stage = 0;
     hipEvent_t aead_done = nullptr;
+    // blob compression (rcdc_zstd_compress): calls on one context take turns
+    std::mutex zstd_mu;
+    ZstdTables *d_zstd_tabs = nullptr;
+    ZstdBlob *d_zstd_blobs = nullptr;
+    ZstdBlk *d_zstd_blks = nullptr;
+    uint2 *d_zstd_res = nullptr;
+    uint64_t *d_zstd_bpos = nullptr, *d_zstd_lens = nullptr, *d_zstd_seq = nullptr;
+    uint8_t *d_zstd_slots = nullptr;
+    uint64_t cap_zstd_tabs = 0, cap_zstd_blobs = 0, cap_zstd_blks = 0, cap_zstd_res = 0,
+             cap_zstd_bpos = 0, cap_zstd_lens = 0, cap_zstd_seq = 0, cap_zstd_slots = 0;
 };
 
 struct rcdc_stream {
@@ -1230,6 +1245,14 @@ void rcdc_ctx_destroy(rcdc_ctx *c) {
         (void)hipFree(c->d_aead_status);
         (void)hipFree(c->d_aead_stage);
         if (c->aead_done) (void)hipEventDestroy(c->aead_done);
+        (void)hipFree(c->d_zstd_tabs);
+        (void)hipFree(c->d_zstd_blobs);
+        (void)hipFree(c->d_zstd_blks);
+        (void)hipFree(c->d_zstd_res);
+        (void)hipFree(c->d_zstd_bpos);
+        (void)hipFree(c->d_zstd_lens);
+        (void)hipFree(c->d_zstd_seq);
+        (void)hipFree(c->d_zstd_slots);
         if (c->stream) (void)hipStreamDestroy(c->stream);
     }
     delete c;
@@ -1795,6 +1818,174 @@ rcdc_status pack_build(rcdc_ctx *ctx, const uint8_t key[64], const void *d_in,
     return aead_launch(ctx, false, key, bt, (uint8_t *)d_out, st, &hdr, nullptr);
 }
 
+// ---- blob compression (zstd frames, RFC 8878) --------------------------------
+
+// FSE_buildCTable of a normalized distribution (the format's symbol spread:
+// RFC 8878 4.1.1; zstd lib/compress/fse_compress.c): state table sorted by
+// symbol, and per symbol {deltaFindState, deltaNbBits}.
+void fse_build_ctable(const int16_t *norm, int nsym, int tlog, ZstdFseSym *tt, uint16_t *st) {
+    const int size = 1 << tlog, mask = size - 1, step = (size >> 1) + (size >> 3) + 3;
+    std::vector<int> sym(size), cumul(nsym + 1);
+    int high = size - 1;
+    for (int u = 1; u <= nsym; u++) {
+        if (norm[u - 1] == -1) {
+            cumul[u] = cumul[u - 1] + 1;
+            sym[high--] = u - 1;
+        } else {
+            cumul[u] = cumul[u - 1] + norm[u - 1];
+        }
+    }
+    int pos = 0;
+    for (int s = 0; s < nsym; s++)
+        for (int k = 0; k < norm[s]; k++) {
+            sym[pos] = s;
+            pos = (pos + step) & mask;
+            while (pos > high) pos = (pos + step) & mask;
+        }
+    for (int u = 0; u < size; u++) st[cumul[sym[u]]++] = (uint16_t)(size + u);
+    int total = 0;
+    for (int s = 0; s < nsym; s++) {
+        const int c = norm[s];
+        if (c == -1 || c == 1) {
+            tt[s].nbits = ((uint32_t)tlog << 16) - (uint32_t)size;
+            tt[s].find = total - 1;
+            total++;
+        } else if (c > 1) {
+            const int mbo = tlog - (31 - __builtin_clz((uint32_t)(c - 1)));
+            tt[s].nbits = ((uint32_t)mbo << 16) - ((uint32_t)c << mbo);
+            tt[s].find = total - c;
+            total += c;
+        } else {
+            tt[s].nbits = ((uint32_t)(tlog + 1) << 16) - (uint32_t)size;
+            tt[s].find = 0;
+        }
+    }
+}
+
+// The predefined distributions and code tables (RFC 8878 3.1.1.3.2.1-2).
+const ZstdTables &zstd_tables() {
+    static ZstdTables T;
+    static std::once_flag once;
+    std::call_once(once, [] {
+        static const int16_t ll_norm[36] = {4, 3, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 1, 1, 1, 2, 2,
+                                            2, 2, 2, 2, 2, 2, 2, 3, 2, 1, 1, 1, 1, 1, -1, -1, -1, -1};
+        static const int16_t ml_norm[53] = {1, 4, 3, 2, 2, 2, 2, 2, 2, 1, 1, 1, 1, 1, 1, 1, 1, 1,
+                                            1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1,
+                                            1, 1, 1, 1, 1, 1, 1, 1, 1, 1, -1, -1, -1, -1, -1, -1, -1};
+        static const int16_t of_norm[29] = {1, 1, 1, 1, 1, 1, 2, 2, 2, 1, 1, 1, 1, 1, 1,
+                                            1, 1, 1, 1, 1, 1, 1, 1, 1, -1, -1, -1, -1, -1};
+        static const uint32_t ll_base[36] = {0,  1,  2,   3,   4,   5,   6,    7,    8,    9,
+                                             10, 11, 12,  13,  14,  15,  16,   18,   20,   22,
+                                             24, 28, 32,  40,  48,  64,  128,  256,  512,  1024,
+                                             2048, 4096, 8192, 16384, 32768, 65536};
+        static const uint8_t ll_bits[36] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 1, 1,
+                                            1, 1, 2, 2, 3, 3, 4, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16};
+        static const uint32_t ml_base[53] = {
+            3,  4,  5,  6,  7,  8,  9,  10, 11,  12,  13,  14,   15,   16,   17,   18,   19, 20,
+            21, 22, 23, 24, 25, 26, 27, 28, 29,  30,  31,  32,   33,   34,   35,   37,   39, 41,
+            43, 47, 51, 59, 67, 83, 99, 131, 259, 515, 1027, 2051, 4099, 8195, 16387, 32771, 65539};
+        static const uint8_t ml_bits[53] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0,
+                                            0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 1, 1, 1, 1,
+                                            2, 2, 3, 3, 4, 4, 5, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16};
+        memset(&T, 0, sizeof T);
+        fse_build_ctable(ll_norm, 36, 6, T.ll, T.llst);
+        fse_build_ctable(ml_norm, 53, 6, T.ml, T.mlst);
+        fse_build_ctable(of_norm, 29, 5, T.of, T.ofst);
+        for (uint32_t v = 0; v < 64; v++) {
+            int c = 0;
+            while (c + 1 < 36 && ll_base[c + 1] <= v) c++;
+            T.llcode[v] = (uint8_t)c;
+        }
+        for (uint32_t v = 0; v < 128; v++) {
+            int c = 0;
+            while (c + 1 < 53 && ml_base[c + 1] - 3 <= v) c++;
+            T.mlcode[v] = (uint8_t)c;
+        }
+        memcpy(T.llbits, ll_bits, sizeof ll_bits);
+        memcpy(T.mlbits, ml_bits, sizeof ml_bits);
+    });
+    return T;
+}
+
+uint64_t zstd_blocks(uint64_t len) { return len ? (len + kZstdBlock - 1) / kZstdBlock : 1; }
+
+// Blocks per launch window (bounds the per-block scratch: 16384 x 128 KiB)
+constexpr uint64_t kZstdWindowBlocks = 16384;
+
+rcdc_status zstd_compress(rcdc_ctx *ctx, int level, const void *d_in, const rcdc_zstd_ref *refs,
+                          uint32_t n, void *d_out, uint64_t *out_lens, void *hip_stream) {
+    if (!valid_ctx(ctx) || (n && (!refs || !d_in || !d_out || !out_lens)))
+        return fail(RCDC_ERR_INVALID_INPUT, "null argument");
+    // zstd's accepted levels (ZSTD_minCLevel() .. ZSTD_maxCLevel(); decrypt.rs:20-24)
+    if (level < -(1 << 17) || level > 22)
+        return fail(RCDC_ERR_INVALID_INPUT, "zstd level %d outside [-131072, 22]", level);
+    for (uint32_t i = 0; i < n; i++)
+        if (refs[i].len > 0xFFFFFFFFull)  // decrypt.rs:479-487: data length must fit u32
+            return fail(RCDC_ERR_UNSUPPORTED, "blob %u: %llu bytes", i,
+                        (unsigned long long)refs[i].len);
+    if (!n) return RCDC_OK;
+    std::lock_guard<std::mutex> lk(ctx->zstd_mu);
+    DeviceGuard g(ctx->device);
+    hipStream_t st = hip_stream ? (hipStream_t)hip_stream : ctx->stream;
+    rcdc_status rs;
+    if (!ctx->d_zstd_tabs) {
+        if ((rs = ensure_dev(&ctx->d_zstd_tabs, &ctx->cap_zstd_tabs, 1))) return rs;
+        HIP_TRY(hipMemcpy(ctx->d_zstd_tabs, &zstd_tables(), sizeof(ZstdTables),
+                          hipMemcpyHostToDevice));
+    }
+    const uint32_t grid = zstd_block_grid((uint32_t)std::max(ctx->num_cus, 1));
+    if ((rs = ensure_dev(&ctx->d_zstd_seq, &ctx->cap_zstd_seq, (uint64_t)grid * kZstdMaxSeq)))
+        return rs;
+    std::vector<ZstdBlob> blobs;
+    std::vector<ZstdBlk> blks;
+    uint32_t i = 0;
+    while (i < n) {
+        // a window: whole blobs, up to kZstdWindowBlocks blocks (at least one blob)
+        blobs.clear();
+        blks.clear();
+        const uint32_t i0 = i;
+        while (i < n) {
+            const uint64_t nb = zstd_blocks(refs[i].len);
+            if (!blks.empty() && blks.size() + nb > kZstdWindowBlocks) break;
+            ZstdBlob B{};
+            B.in_off = refs[i].in_off;
+            B.out_off = refs[i].out_off;
+            B.len = (uint32_t)refs[i].len;
+            B.blk0 = (uint32_t)blks.size();
+            B.nblk = (uint32_t)nb;
+            for (uint64_t k = 0; k < nb; k++) {
+                ZstdBlk b{};
+                b.blob = (uint32_t)blobs.size();
+                b.start = (uint32_t)(k * kZstdBlock);
+                b.len = (uint32_t)std::min<uint64_t>(kZstdBlock, refs[i].len - k * kZstdBlock);
+                b.flags = (k == 0 ? 1u : 0u) | (k + 1 == nb ? 2u : 0u);
+                blks.push_back(b);
+            }
+            blobs.push_back(B);
+            i++;
+        }
+        const uint64_t nbl = blks.size(), nbo = blobs.size();
+        if ((rs = ensure_dev(&ctx->d_zstd_blobs, &ctx->cap_zstd_blobs, nbo))) return rs;
+        if ((rs = ensure_dev(&ctx->d_zstd_blks, &ctx->cap_zstd_blks, nbl))) return rs;
+        if ((rs = ensure_dev(&ctx->d_zstd_res, &ctx->cap_zstd_res, nbl))) return rs;
+        if ((rs = ensure_dev(&ctx->d_zstd_bpos, &ctx->cap_zstd_bpos, nbl))) return rs;
+        if ((rs = ensure_dev(&ctx->d_zstd_lens, &ctx->cap_zstd_lens, nbo))) return rs;
+        if ((rs = ensure_dev(&ctx->d_zstd_slots, &ctx->cap_zstd_slots, nbl * kZstdSlot))) return rs;
+        HIP_TRY(hipMemcpyAsync(ctx->d_zstd_blobs, blobs.data(), nbo * sizeof(ZstdBlob),
+                               hipMemcpyHostToDevice, st));
+        HIP_TRY(hipMemcpyAsync(ctx->d_zstd_blks, blks.data(), nbl * sizeof(ZstdBlk),
+                               hipMemcpyHostToDevice, st));
+        HIP_TRY(launch_zstd((const uint8_t *)d_in, (uint8_t *)d_out, ctx->d_zstd_blobs,
+                            (uint32_t)nbo, ctx->d_zstd_blks, (uint32_t)nbl, ctx->d_zstd_tabs,
+                            ctx->d_zstd_slots, ctx->d_zstd_seq, grid, ctx->d_zstd_res,
+                            ctx->d_zstd_bpos, ctx->d_zstd_lens, st));
+        HIP_TRY(hipMemcpyAsync(out_lens + i0, ctx->d_zstd_lens, nbo * 8, hipMemcpyDeviceToHost, st));
+        // the host arrays of this window are reused by the next one
+        HIP_TRY(hipStreamSynchronize(st));
+    }
+    return RCDC_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -1817,6 +2008,18 @@ rcdc_status rcdc_pack_build(rcdc_ctx *ctx, const uint8_t *key, const void *d_in,
     return pack_build(ctx, key, d_in, blobs, nblobs, packs, npacks, d_out, out_len, blob_offsets,
                       hip_stream);
 }
+
+uint64_t rcdc_zstd_bound(uint64_t len) { return len + 3 * zstd_blocks(len) + 9; }
+
+rcdc_status rcdc_zstd_compress(rcdc_ctx *ctx, int level, const void *d_in,
+                               const rcdc_zstd_ref *refs, uint32_t n, void *d_out,
+                               uint64_t *out_lens, void *hip_stream) {
+    return zstd_compress(ctx, level, d_in, refs, n, d_out, out_lens, hip_stream);
+}
+
+void rcdc_zstd_tables(void *out) { memcpy(out, &zstd_tables(), sizeof(ZstdTables)); }
+
+uint64_t rcdc_zstd_tables_size(void) { return sizeof(ZstdTables); }
 
 // ---- streaming: one file fed in pieces -------------------------------------
 

@@ -1,0 +1,154 @@
+"""CPU: the zstd checker and the device encoder's coding tables -- SURVEY.md
+8(f) row 3 (blob compression, backend/decrypt.rs:478-506).
+
+- The checker (oracle/zstd_ref.py: the system libzstd through ctypes, and
+  pyarrow's bundled zstd) round-trips libzstd's own frames and agrees with
+  itself across both builds.
+- tests/zstd_model.py codes sequences with the library's FSE tables
+  (rcdc_zstd_tables) exactly as the kernel's lane 0 does; both decoders must
+  read every block back: every literal-length, match-length and offset code,
+  the 1/2/3-byte section headers (including >= 0x7F00 sequences) and the
+  frame-header size classes.  Compressed bytes themselves are parity-unpinned
+  (library-version specific); decoding is the contract.
+"""
+import numpy as np
+import pytest
+
+from oracle import zstd_ref as zr
+from tests import zstd_model as zm
+
+
+@pytest.fixture(scope="module")
+def T(rcdc_lib):
+    return zm.tables()
+
+
+def _synth(seqs, tail, rng):
+    """Bytes whose parse is exactly ``seqs`` (+ ``tail`` literals)."""
+    out = bytearray()
+    for ll, ml, off in seqs:
+        out += rng.integers(0, 256, ll, dtype=np.uint8).tobytes()
+        assert off <= len(out)
+        for _ in range(ml):  # overlapping copy, as the decoder does
+            out.append(out[-off])
+    out += rng.integers(0, 256, tail, dtype=np.uint8).tobytes()
+    return bytes(out)
+
+
+def _roundtrip(T, data, seqs):
+    blk = zm.compressed_block(T, data, seqs)
+    fr = zm.frame([(2, blk, len(data))], len(data))
+    assert zr.decompress(fr) == data
+    if len(blk) <= len(data):
+        # zstd >= 1.5 rejects a compressed block larger than the frame's
+        # window (its content size); the device never writes one
+        assert zr.decompress_pyarrow(fr, len(data)) == data
+    assert zr.content_size(fr) == len(data)
+    assert zr.blocks(fr) == [(2, len(blk), True)]
+    return fr
+
+
+def test_checker_roundtrip():
+    rng = np.random.default_rng(7)
+    for n in (0, 1, 100, 70000, 300000):
+        d = rng.integers(0, 4, n, dtype=np.uint8).tobytes()
+        fr = zr.compress(d, 3)
+        assert zr.decompress(fr) == d
+        assert zr.decompress_pyarrow(fr, n) == d
+        assert zr.frame_size(fr) == len(fr)
+    assert zr.version().startswith("1.")
+
+
+def test_tables_shape(T):
+    # state tables are permutations of [size, 2 size)
+    assert sorted(T["llst"]) == list(range(64, 128))
+    assert sorted(T["mlst"]) == list(range(64, 128))
+    assert sorted(T["ofst"][:32]) == list(range(32, 64))
+    assert T["llcode"][15] == 15 and T["llcode"][16] == 16 and T["llcode"][63] == 24
+    assert T["mlcode"][31] == 31 and T["mlcode"][32] == 32 and T["mlcode"][127] == 42
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_model_every_code(T, seed):
+    rng = np.random.default_rng(seed)
+    # literal lengths over every LL code, match lengths over every ML code,
+    # offsets over every OF code a 128 KiB block can reach
+    lls = [0, 1, 15, 16, 17, 63, 64, 65, 127, 128, 255, 256, 1000, 5000]
+    mls = [3, 4, 34, 35, 36, 130, 131, 258, 259, 1000, 4098, 4099, 9000]
+    seqs, size = [], 0
+    for i in range(40):
+        ll = int(rng.choice(lls))
+        ml = int(rng.choice(mls))
+        cap = size + ll
+        if cap < 1:
+            ll, cap = 1, size + 1
+        off = int(min(cap, rng.choice([1, 2, 3, 4, 7, 100, 1 << 10, 1 << 14, 1 << 16, cap])))
+        seqs.append((ll, ml, off))
+        size += ll + ml
+        if size > 100000:
+            break
+    data = _synth(seqs, int(rng.integers(0, 40)), rng)
+    _roundtrip(T, data, seqs)
+
+
+def test_model_long_lengths(T):
+    rng = np.random.default_rng(11)
+    # LL code 35 (>= 65536 literals), ML code 52 (>= 65539), the max offset
+    seqs = [(70000, 3, 70000), (5, 60000, 1)]
+    _roundtrip(T, _synth(seqs, 3, rng), seqs)
+    seqs = [(4, 3, 4), (1, 65539 + 1000, 1)]
+    _roundtrip(T, _synth(seqs, 0, rng), seqs)
+
+
+@pytest.mark.parametrize("nseq", [1, 127, 128, 0x7EFF, 0x7F00, 0x7F00 + 300])
+def test_model_sequence_counts(T, nseq):
+    rng = np.random.default_rng(nseq)
+    seqs = [(0 if i else 4, 3, 4 if i == 0 else int(rng.integers(1, 4 + 3 * i)))
+            for i in range(nseq)]
+    seqs = [(ll, ml, min(off, 4 + 3 * i)) for i, (ll, ml, off) in enumerate(seqs)]
+    data = _synth(seqs, 5, rng)
+    assert len(data) <= 131072
+    _roundtrip(T, data, seqs)
+
+
+def test_model_literal_header_classes(T):
+    rng = np.random.default_rng(3)
+    for lits in (5, 31, 32, 4095, 4096, 70000):
+        seqs = [(lits, 40, min(lits, 8))]
+        _roundtrip(T, _synth(seqs, 0, rng), seqs)
+
+
+def test_frame_header_classes():
+    # single-segment content-size classes: 1 byte < 256, 2 bytes (size - 256)
+    # < 65792, 4 bytes otherwise (the device frame kernel's choice)
+    for n in (0, 1, 255, 256, 257, 65791, 65792, 200000):
+        data = bytes(range(256)) * (n // 256 + 1)
+        data = data[:n]
+        blocks_, pos = [], 0
+        while True:
+            k = min(131072, n - pos)
+            blocks_.append((0, data[pos:pos + k], k))
+            pos += k
+            if pos >= n:
+                break
+        fr = zm.frame(blocks_, n)
+        assert zr.content_size(fr) == n
+        assert zr.decompress(fr) == data
+
+
+def test_greedy_model_text(T):
+    rng = np.random.default_rng(5)
+    words = [bytes(rng.integers(97, 123, size=int(rng.integers(2, 9))).astype(np.uint8))
+             for _ in range(300)]
+    data = b" ".join(words[int(i)] for i in rng.integers(0, 300, size=20000))[:100000]
+    seqs = zm.greedy_sequences(data)
+    fr = _roundtrip(T, data, seqs)
+    assert len(fr) < len(data) // 2
+
+
+def test_abi_rejects(rcdc_lib):
+    # NULL context / arguments: InvalidInput (2) before any HIP call
+    assert rcdc_lib.rcdc_zstd_compress(None, 0, None, None, 0, None, None, None) == 2
+    assert rcdc_lib.rcdc_zstd_bound(0) == 12
+    assert rcdc_lib.rcdc_zstd_bound(131072) == 131072 + 3 + 9
+    assert rcdc_lib.rcdc_zstd_bound(131073) == 131073 + 6 + 9
