@@ -66,6 +66,7 @@ hipError_t launch_aead(bool open, const uint8_t *in, uint8_t *out, const AeadBlo
                        const uint32_t *unit0, const AeadKeyDev *key, uint32_t *partials,
                        uint32_t *status, uint32_t cus, hipStream_t stream);
 uint32_t zstd_block_grid(uint32_t cus);
+void zstd_prof_dump();
 hipError_t launch_zstd(const uint8_t *in, uint8_t *out, const ZstdBlob *blobs, uint32_t nblobs,
                        const ZstdBlk *blks, uint32_t nblk, const ZstdTables *tabs, uint8_t *slots,
                        uint64_t *seqbuf, uint32_t grid, uint2 *res, uint64_t *bpos,
@@ -1909,8 +1910,9 @@ const ZstdTables &zstd_tables() {
 
 uint64_t zstd_blocks(uint64_t len) { return len ? (len + kZstdBlock - 1) / kZstdBlock : 1; }
 
-// Blocks per launch window (bounds the per-block scratch: 16384 x 128 KiB)
-constexpr uint64_t kZstdWindowBlocks = 16384;
+// Blocks per launch window: bounds the per-block scratch (32768 x 128 KiB);
+// windows run back to back on the stream, reusing it.
+constexpr uint64_t kZstdWindowBlocks = 32768;
 
 rcdc_status zstd_compress(rcdc_ctx *ctx, int level, const void *d_in, const rcdc_zstd_ref *refs,
                           uint32_t n, void *d_out, uint64_t *out_lens, void *hip_stream) {
@@ -1924,6 +1926,42 @@ rcdc_status zstd_compress(rcdc_ctx *ctx, int level, const void *d_in, const rcdc
             return fail(RCDC_ERR_UNSUPPORTED, "blob %u: %llu bytes", i,
                         (unsigned long long)refs[i].len);
     if (!n) return RCDC_OK;
+    // descriptors of every window (block indices relative to the window,
+    // blob indices too), uploaded once
+    struct Win {
+        uint64_t blob0, nblob, blk0, nblk;
+    };
+    std::vector<ZstdBlob> blobs;
+    std::vector<ZstdBlk> blks;
+    std::vector<Win> wins;
+    uint64_t maxw = 0;
+    for (uint32_t i = 0; i < n;) {
+        Win w{blobs.size(), 0, blks.size(), 0};
+        while (i < n) {
+            const uint64_t nb = zstd_blocks(refs[i].len);
+            if (w.nblk && w.nblk + nb > kZstdWindowBlocks) break;
+            ZstdBlob B{};
+            B.in_off = refs[i].in_off;
+            B.out_off = refs[i].out_off;
+            B.len = (uint32_t)refs[i].len;
+            B.blk0 = (uint32_t)w.nblk;
+            B.nblk = (uint32_t)nb;
+            for (uint64_t k = 0; k < nb; k++) {
+                ZstdBlk b{};
+                b.blob = (uint32_t)w.nblob;
+                b.start = (uint32_t)(k * kZstdBlock);
+                b.len = (uint32_t)std::min<uint64_t>(kZstdBlock, refs[i].len - k * kZstdBlock);
+                b.flags = (k == 0 ? 1u : 0u) | (k + 1 == nb ? 2u : 0u);
+                blks.push_back(b);
+            }
+            blobs.push_back(B);
+            w.nblk += nb;
+            w.nblob++;
+            i++;
+        }
+        maxw = std::max(maxw, w.nblk);
+        wins.push_back(w);
+    }
     std::lock_guard<std::mutex> lk(ctx->zstd_mu);
     DeviceGuard g(ctx->device);
     hipStream_t st = hip_stream ? (hipStream_t)hip_stream : ctx->stream;
@@ -1936,53 +1974,28 @@ rcdc_status zstd_compress(rcdc_ctx *ctx, int level, const void *d_in, const rcdc
     const uint32_t grid = zstd_block_grid((uint32_t)std::max(ctx->num_cus, 1));
     if ((rs = ensure_dev(&ctx->d_zstd_seq, &ctx->cap_zstd_seq, (uint64_t)grid * kZstdMaxSeq)))
         return rs;
-    std::vector<ZstdBlob> blobs;
-    std::vector<ZstdBlk> blks;
-    uint32_t i = 0;
-    while (i < n) {
-        // a window: whole blobs, up to kZstdWindowBlocks blocks (at least one blob)
-        blobs.clear();
-        blks.clear();
-        const uint32_t i0 = i;
-        while (i < n) {
-            const uint64_t nb = zstd_blocks(refs[i].len);
-            if (!blks.empty() && blks.size() + nb > kZstdWindowBlocks) break;
-            ZstdBlob B{};
-            B.in_off = refs[i].in_off;
-            B.out_off = refs[i].out_off;
-            B.len = (uint32_t)refs[i].len;
-            B.blk0 = (uint32_t)blks.size();
-            B.nblk = (uint32_t)nb;
-            for (uint64_t k = 0; k < nb; k++) {
-                ZstdBlk b{};
-                b.blob = (uint32_t)blobs.size();
-                b.start = (uint32_t)(k * kZstdBlock);
-                b.len = (uint32_t)std::min<uint64_t>(kZstdBlock, refs[i].len - k * kZstdBlock);
-                b.flags = (k == 0 ? 1u : 0u) | (k + 1 == nb ? 2u : 0u);
-                blks.push_back(b);
-            }
-            blobs.push_back(B);
-            i++;
-        }
-        const uint64_t nbl = blks.size(), nbo = blobs.size();
-        if ((rs = ensure_dev(&ctx->d_zstd_blobs, &ctx->cap_zstd_blobs, nbo))) return rs;
-        if ((rs = ensure_dev(&ctx->d_zstd_blks, &ctx->cap_zstd_blks, nbl))) return rs;
-        if ((rs = ensure_dev(&ctx->d_zstd_res, &ctx->cap_zstd_res, nbl))) return rs;
-        if ((rs = ensure_dev(&ctx->d_zstd_bpos, &ctx->cap_zstd_bpos, nbl))) return rs;
-        if ((rs = ensure_dev(&ctx->d_zstd_lens, &ctx->cap_zstd_lens, nbo))) return rs;
-        if ((rs = ensure_dev(&ctx->d_zstd_slots, &ctx->cap_zstd_slots, nbl * kZstdSlot))) return rs;
-        HIP_TRY(hipMemcpyAsync(ctx->d_zstd_blobs, blobs.data(), nbo * sizeof(ZstdBlob),
-                               hipMemcpyHostToDevice, st));
-        HIP_TRY(hipMemcpyAsync(ctx->d_zstd_blks, blks.data(), nbl * sizeof(ZstdBlk),
-                               hipMemcpyHostToDevice, st));
-        HIP_TRY(launch_zstd((const uint8_t *)d_in, (uint8_t *)d_out, ctx->d_zstd_blobs,
-                            (uint32_t)nbo, ctx->d_zstd_blks, (uint32_t)nbl, ctx->d_zstd_tabs,
-                            ctx->d_zstd_slots, ctx->d_zstd_seq, grid, ctx->d_zstd_res,
-                            ctx->d_zstd_bpos, ctx->d_zstd_lens, st));
-        HIP_TRY(hipMemcpyAsync(out_lens + i0, ctx->d_zstd_lens, nbo * 8, hipMemcpyDeviceToHost, st));
-        // the host arrays of this window are reused by the next one
-        HIP_TRY(hipStreamSynchronize(st));
-    }
+    const uint64_t nbl = blks.size(), nbo = blobs.size();
+    if ((rs = ensure_dev(&ctx->d_zstd_blobs, &ctx->cap_zstd_blobs, nbo))) return rs;
+    if ((rs = ensure_dev(&ctx->d_zstd_blks, &ctx->cap_zstd_blks, nbl))) return rs;
+    if ((rs = ensure_dev(&ctx->d_zstd_res, &ctx->cap_zstd_res, nbl))) return rs;
+    if ((rs = ensure_dev(&ctx->d_zstd_bpos, &ctx->cap_zstd_bpos, nbl))) return rs;
+    if ((rs = ensure_dev(&ctx->d_zstd_lens, &ctx->cap_zstd_lens, nbo))) return rs;
+    if ((rs = ensure_dev(&ctx->d_zstd_slots, &ctx->cap_zstd_slots, maxw * kZstdSlot))) return rs;
+    HIP_TRY(hipMemcpyAsync(ctx->d_zstd_blobs, blobs.data(), nbo * sizeof(ZstdBlob),
+                           hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemcpyAsync(ctx->d_zstd_blks, blks.data(), nbl * sizeof(ZstdBlk),
+                           hipMemcpyHostToDevice, st));
+    for (const Win &w : wins)
+        HIP_TRY(launch_zstd((const uint8_t *)d_in, (uint8_t *)d_out, ctx->d_zstd_blobs + w.blob0,
+                            (uint32_t)w.nblob, ctx->d_zstd_blks + w.blk0, (uint32_t)w.nblk,
+                            ctx->d_zstd_tabs, ctx->d_zstd_slots, ctx->d_zstd_seq, grid,
+                            ctx->d_zstd_res + w.blk0, ctx->d_zstd_bpos + w.blk0,
+                            ctx->d_zstd_lens + w.blob0, st));
+    HIP_TRY(hipMemcpyAsync(out_lens, ctx->d_zstd_lens, nbo * 8, hipMemcpyDeviceToHost, st));
+    // the host descriptors die with this call
+    HIP_TRY(hipStreamSynchronize(st));
+    if (const char *e = getenv("RCDC_ZSTD_DBG"))
+        if (atoi(e) & 4) zstd_prof_dump();
     return RCDC_OK;
 }
 

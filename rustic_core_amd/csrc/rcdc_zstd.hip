@@ -37,18 +37,24 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
 
 #include "rcdc_internal.h"
 
 using namespace rcdc;
 
 namespace rcdc {
-constexpr int kZstdHashLog = 11;           // 2048 buckets x 8 B = 16 KiB of LDS per wave
 constexpr uint32_t kZstdNone = 0xFFFFFFFFu;
 constexpr int kZstdAccelShift = 8;         // stride = 1 + (bytes since the anchor >> 8)
 constexpr uint32_t kZstdMaxStride = 32;
 constexpr int kZstdCopyThreads = 256;
 }  // namespace rcdc
+
+// RCDC_ZSTD_DBG bit 2: per-phase clock sums (wall clock, 100 MHz) over all
+// blocks: RLE check, parse, FSE, literal copy, blocks, sequences
+__device__ unsigned long long g_zstd_prof[8];
 
 namespace {
 
@@ -70,6 +76,26 @@ __device__ __forceinline__ uint32_t ld4(const uint8_t *p) {
     return __builtin_amdgcn_alignbit(hi, lo, sh);
 }
 
+// 16 bytes at any alignment (5 aligned dwords when misaligned).
+__device__ __forceinline__ uint4 ld16(const uint8_t *p) {
+    const uintptr_t a = (uintptr_t)p & ~(uintptr_t)3;
+    const uint32_t sh = ((uint32_t)(uintptr_t)p & 3u) * 8u;
+    const uint32_t *w = (const uint32_t *)a;
+    const uint32_t w0 = w[0], w1 = w[1], w2 = w[2], w3 = w[3];
+    const uint32_t w4 = sh ? w[4] : 0u;
+    return make_uint4(__builtin_amdgcn_alignbit(w1, w0, sh), __builtin_amdgcn_alignbit(w2, w1, sh),
+                      __builtin_amdgcn_alignbit(w3, w2, sh), __builtin_amdgcn_alignbit(w4, w3, sh));
+}
+
+// First differing byte of two 16-byte groups (16 if equal).
+__device__ __forceinline__ uint32_t first_diff16(uint4 a, uint4 b) {
+    const uint32_t x0 = a.x ^ b.x, x1 = a.y ^ b.y, x2 = a.z ^ b.z, x3 = a.w ^ b.w;
+    return x0 ? (uint32_t)__builtin_ctz(x0) >> 3
+         : x1 ? 4u + ((uint32_t)__builtin_ctz(x1) >> 3)
+         : x2 ? 8u + ((uint32_t)__builtin_ctz(x2) >> 3)
+         : x3 ? 12u + ((uint32_t)__builtin_ctz(x3) >> 3) : 16u;
+}
+
 // 4 bytes at p where only [p, lim) may be read; missing bytes read as 0.
 __device__ __forceinline__ uint32_t ld4_hi(const uint8_t *p, const uint8_t *lim) {
     if (p + 4 <= lim) return ld4(p);
@@ -88,31 +114,48 @@ __device__ __forceinline__ uint32_t ld4_lo(const uint8_t *p, const uint8_t *lo) 
     return v;
 }
 
+template <int HL>
 __device__ __forceinline__ uint32_t zhash(uint32_t w) {
-    return (w * 2654435761u) >> (32 - kZstdHashLog);
+    return (w * 2654435761u) >> (32 - HL);
 }
 
+// Table entry: position (17 bits) | a 15-bit tag of its 4 bytes << 17, so a
+// candidate touches memory only when its tag agrees (random data: ~2^-15).
+// A position is at most kZstdBlock - 8, so the empty entry (all ones) is none.
+__device__ __forceinline__ uint32_t ztag(uint32_t w) { return (w * 0x85EBCA77u) >> 17; }
+constexpr uint32_t kZstdPosMask = (1u << 17) - 1u;
+
 // Equal bytes of a[0..) and b[0..), at most maxlen (wave-uniform result).
+// Lane l compares 16 bytes per round (1 KiB per wave round); the last,
+// partial groups go byte-safe.
 __device__ uint32_t wave_match_fwd(const uint8_t *a, const uint8_t *b, uint32_t maxlen,
                                    const uint8_t *lim) {
     const uint32_t lane = lane_id();
     uint32_t len = 0;
     while (len < maxlen) {
-        const uint32_t o = len + lane * 4u;
-        uint32_t x = 0xFFFFFFFFu;
-        if (o < maxlen) {
-            x = ld4_hi(a + o, lim) ^ ld4_hi(b + o, lim);
-            const uint32_t rem = maxlen - o;
-            if (rem < 4) x |= 0xFFFFFFFFu << (8 * rem);
+        const uint32_t o = len + lane * 16u;
+        uint32_t d = 0;  // first differing byte in this lane's group (16: none)
+        if (o + 16 <= maxlen) {
+            d = first_diff16(ld16(a + o), ld16(b + o));
+        } else if (o < maxlen) {
+            d = 16;
+            for (uint32_t q = 0; q < 16; q += 4) {
+                uint32_t x = ld4_hi(a + o + q, lim) ^ ld4_hi(b + o + q, lim);
+                const uint32_t rem = maxlen - o - q;
+                if (rem < 4) x |= 0xFFFFFFFFu << (8 * rem);
+                if (x) {
+                    d = q + ((uint32_t)__builtin_ctz(x) >> 3);
+                    break;
+                }
+            }
         }
-        const uint64_t m = __ballot(x != 0);
+        const uint64_t m = __ballot(o < maxlen ? d < 16 : true);
         if (m) {
             const int j = __builtin_ctzll(m);
-            const uint32_t xj = rdl(x, j);
-            len += (uint32_t)j * 4u + ((uint32_t)__builtin_ctz(xj) >> 3);
+            len += (uint32_t)j * 16u + rdl(d, j);
             return len < maxlen ? len : maxlen;
         }
-        len += 256;
+        len += 1024;
     }
     return maxlen;
 }
@@ -158,43 +201,13 @@ __device__ void wave_copy(uint8_t *dst, const uint8_t *src, uint32_t n) {
     if (lane < n - t) dst[t + lane] = src[t + lane];
 }
 
-struct BitW {
-    uint64_t acc;
-    uint32_t nb;
-    uint8_t *o, *end;
-    bool over;
-    __device__ void add(uint32_t v, uint32_t bits) {
-        acc |= (uint64_t)(v & ((1u << bits) - 1u)) << nb;
-        nb += bits;
-    }
-    __device__ void flush() {
-        while (nb >= 8) {
-            if (o < end) *o++ = (uint8_t)acc;
-            else over = true;
-            acc >>= 8;
-            nb -= 8;
-        }
-    }
-};
-
-struct FseState {
-    uint32_t v;
-};
-
-__device__ __forceinline__ void fse_init(FseState &s, const ZstdFseSym *tt, const uint16_t *st,
-                                         uint32_t sym) {
-    const ZstdFseSym t = tt[sym];
-    const uint32_t nbo = (t.nbits + (1u << 15)) >> 16;
-    const uint32_t v = (nbo << 16) - t.nbits;
-    s.v = st[(int)(v >> nbo) + t.find];
-}
-
-__device__ __forceinline__ void fse_enc(BitW &w, FseState &s, const ZstdFseSym *tt,
-                                        const uint16_t *st, uint32_t sym) {
-    const ZstdFseSym t = tt[sym];
-    const uint32_t nbo = (s.v + t.nbits) >> 16;
-    w.add(s.v, nbo);
-    s.v = st[(int)(s.v >> nbo) + t.find];
+// Equal bytes counted down from the top of two 16-byte groups (16 if equal).
+__device__ __forceinline__ uint32_t last_eq16(uint4 a, uint4 b) {
+    const uint32_t x0 = a.x ^ b.x, x1 = a.y ^ b.y, x2 = a.z ^ b.z, x3 = a.w ^ b.w;
+    return x3 ? (uint32_t)__builtin_clz(x3) >> 3
+         : x2 ? 4u + ((uint32_t)__builtin_clz(x2) >> 3)
+         : x1 ? 8u + ((uint32_t)__builtin_clz(x1) >> 3)
+         : x0 ? 12u + ((uint32_t)__builtin_clz(x0) >> 3) : 16u;
 }
 
 // sequence record: literal length | match length << 20 | offset << 40
@@ -218,60 +231,174 @@ __device__ __forceinline__ SeqCodes seq_codes(uint64_t s, const ZstdTables &T) {
     return c;
 }
 
-// Lane 0: the sequences section's bitstream (ZSTD_encodeSequences order).
-// Returns its bytes, or kZstdNone if it would pass `end`.
-__device__ uint32_t fse_sequences(const uint64_t *seqs, uint32_t nseq, const ZstdTables &T,
-                                  uint8_t *out, uint8_t *end) {
-    BitW w{0, 0, out, end, false};
-    FseState sll, sml, sof;
-    SeqCodes c = seq_codes(seqs[nseq - 1], T);
-    fse_init(sml, T.ml, T.mlst, c.mlc);
-    fse_init(sof, T.of, T.ofst, c.ofc);
-    fse_init(sll, T.ll, T.llst, c.llc);
-    w.add(c.ll, T.llbits[c.llc]);
-    w.add(c.mlb, T.mlbits[c.mlc]);
-    w.flush();
-    w.add(c.ofv, c.ofc);
-    w.flush();
-    for (int64_t i = (int64_t)nseq - 2; i >= 0; i--) {
-        c = seq_codes(seqs[i], T);
-        fse_enc(w, sof, T.of, T.ofst, c.ofc);
-        fse_enc(w, sml, T.ml, T.mlst, c.mlc);
-        w.flush();
-        fse_enc(w, sll, T.ll, T.llst, c.llc);
-        w.add(c.ll, T.llbits[c.llc]);
-        w.flush();
-        w.add(c.mlb, T.mlbits[c.mlc]);
-        w.flush();
-        w.add(c.ofv, c.ofc);
-        w.flush();
-        if (w.over) return kZstdNone;
-    }
-    w.add(sml.v, 6);
-    w.flush();
-    w.add(sof.v, 5);
-    w.flush();
-    w.add(sll.v, 6);
-    w.add(1, 1);  // end mark (BIT_closeCStream)
-    w.flush();
-    if (w.nb) {
-        if (w.o < w.end) *w.o++ = (uint8_t)w.acc;
-        else w.over = true;
-    }
-    return w.over ? kZstdNone : (uint32_t)(w.o - out);
+// The FSE tables in VGPRs, for the scalar state chains: lane s holds symbol
+// s's {deltaFindState, deltaNbBits}, lane t the state table's entry t.
+struct FseRegs {
+    uint32_t llF, llN, mlF, mlN, ofF, ofN, llS, mlS, ofS;
+};
+
+__device__ FseRegs fse_regs(const ZstdTables &T) {
+    const uint32_t l = lane_id();
+    FseRegs r;
+    r.llF = l < 36 ? (uint32_t)T.ll[l].find : 0u;
+    r.llN = l < 36 ? T.ll[l].nbits : 0u;
+    r.mlF = l < 53 ? (uint32_t)T.ml[l].find : 0u;
+    r.mlN = l < 53 ? T.ml[l].nbits : 0u;
+    r.ofF = l < 32 ? (uint32_t)T.of[l].find : 0u;
+    r.ofN = l < 32 ? T.of[l].nbits : 0u;
+    r.llS = T.llst[l];
+    r.mlS = T.mlst[l];
+    r.ofS = l < 32 ? T.ofst[l] : 0u;
+    return r;
 }
 
-// All n bytes of the block equal to its first?  (wave-uniform)
+// FSE_initCState2 / FSE_encodeSymbol on wave-uniform values (SALU + readlane).
+__device__ __forceinline__ uint32_t fse_init_s(uint32_t F, uint32_t N, uint32_t S, uint32_t sym) {
+    const uint32_t nb = rdl(N, (int)sym);
+    const int32_t f = (int32_t)rdl(F, (int)sym);
+    const uint32_t nbo = (nb + (1u << 15)) >> 16;
+    const uint32_t v = (nbo << 16) - nb;
+    return rdl(S, (int)((int32_t)(v >> nbo) + f));
+}
+
+__device__ __forceinline__ uint32_t fse_enc_s(uint32_t F, uint32_t N, uint32_t S, uint32_t sym,
+                                              uint32_t st, uint32_t &field) {
+    const uint32_t nb = rdl(N, (int)sym);
+    const int32_t f = (int32_t)rdl(F, (int)sym);
+    const uint32_t nbo = (st + nb) >> 16;
+    field = (st & ((1u << nbo) - 1u)) | nbo << 16;
+    return rdl(S, (int)((int32_t)(st >> nbo) + f));
+}
+
+// OR n bits of v (n <= 25) into the LDS bit buffer at bit q.
+__device__ __forceinline__ void put_bits(uint32_t *buf, uint32_t q, uint32_t v, uint32_t n) {
+    if (!n) return;
+    v &= (1u << n) - 1u;
+    const uint32_t w = q >> 5, sh = q & 31u;
+    atomicOr(&buf[w], v << sh);
+    if (sh + n > 32) atomicOr(&buf[w + 1], v >> (32 - sh));
+}
+
+// LDS ordering inside the one-wave workgroup: a wave's LDS operations run in
+// order, so only the compiler must not move them (no wait for global stores).
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+}
+
+__device__ __forceinline__ uint32_t wl(uint32_t v, int lane, uint32_t old) {
+    return lane_id() == (uint32_t)lane ? v : old;
+}
+
+// The sequences section's bitstream (ZSTD_encodeSequences order: the last
+// sequence first, its states initialised from it; then per sequence OF, ML,
+// LL state bits and LL, ML, OF extra bits; the final states; the end mark),
+// by the whole wave: 64 sequences per round, the three state chains stepped
+// as scalar code, every field OR-ed into an LDS bit buffer at its prefix-sum
+// position, full words stored.  Returns its bytes, or kZstdNone past cap.
+__device__ uint32_t wave_fse_sequences(const uint64_t *seqs, uint32_t nseq, const ZstdTables &T,
+                                       const FseRegs &R, uint32_t *buf, uint8_t *out,
+                                       uint32_t cap) {
+    const uint32_t lane = lane_id();
+    uint32_t sLL = 0, sML = 0, sOF = 0;
+    uint32_t bitpos = 0, wbase = 0;  // bits written; bit index of buf[0] (multiple of 32)
+    if (lane == 0) buf[0] = 0;
+    wave_lds_sync();
+    for (int64_t hi = (int64_t)nseq - 1; hi >= 0; hi -= 64) {
+        const uint32_t cnt = hi + 1 < 64 ? (uint32_t)hi + 1 : 64u;
+        const bool val = lane < cnt;
+        SeqCodes c{0, 0, 0, 0, 0, 0};
+        if (val) c = seq_codes(seqs[hi - lane], T);
+        const uint32_t nll = val ? T.llbits[c.llc] : 0u, nml = val ? T.mlbits[c.mlc] : 0u;
+        uint32_t fOF = 0, fML = 0, fLL = 0;
+        for (uint32_t L = 0; L < cnt; L++) {
+            const uint32_t a = rdl(c.llc, (int)L), bm = rdl(c.mlc, (int)L), o = rdl(c.ofc, (int)L);
+            uint32_t f1 = 0, f2 = 0, f3 = 0;
+            if ((uint64_t)(hi - L) == (uint64_t)nseq - 1) {
+                sML = fse_init_s(R.mlF, R.mlN, R.mlS, bm);
+                sOF = fse_init_s(R.ofF, R.ofN, R.ofS, o);
+                sLL = fse_init_s(R.llF, R.llN, R.llS, a);
+            } else {
+                sOF = fse_enc_s(R.ofF, R.ofN, R.ofS, o, sOF, f1);
+                sML = fse_enc_s(R.mlF, R.mlN, R.mlS, bm, sML, f2);
+                sLL = fse_enc_s(R.llF, R.llN, R.llS, a, sLL, f3);
+            }
+            fOF = wl(f1, (int)L, fOF);
+            fML = wl(f2, (int)L, fML);
+            fLL = wl(f3, (int)L, fLL);
+        }
+        const uint32_t total =
+            val ? (fOF >> 16) + (fML >> 16) + (fLL >> 16) + nll + nml + c.ofc : 0u;
+        uint32_t incl = total;
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint32_t y = __shfl_up(incl, d);
+            if ((int)lane >= d) incl += y;
+        }
+        const uint32_t chunk_bits = rdl(incl, 63);
+        const uint32_t start = bitpos - wbase, endbit = start + chunk_bits;
+        for (uint32_t w = 1 + lane; w <= (endbit >> 5) + 1; w += 64) buf[w] = 0;
+        wave_lds_sync();
+        if (val) {
+            uint32_t q = start + incl - total;
+            put_bits(buf, q, fOF, fOF >> 16);
+            q += fOF >> 16;
+            put_bits(buf, q, fML, fML >> 16);
+            q += fML >> 16;
+            put_bits(buf, q, fLL, fLL >> 16);
+            q += fLL >> 16;
+            put_bits(buf, q, c.ll, nll);
+            q += nll;
+            put_bits(buf, q, c.mlb, nml);
+            q += nml;
+            put_bits(buf, q, c.ofv, c.ofc);
+        }
+        wave_lds_sync();
+        const uint32_t full = endbit >> 5;
+        if ((wbase >> 3) + full * 4u > cap) return kZstdNone;
+        uint8_t *o = out + (wbase >> 3);
+        for (uint32_t w = lane; w < full; w += 64) {
+            const uint32_t v = buf[w];
+            o[4 * w] = (uint8_t)v;
+            o[4 * w + 1] = (uint8_t)(v >> 8);
+            o[4 * w + 2] = (uint8_t)(v >> 16);
+            o[4 * w + 3] = (uint8_t)(v >> 24);
+        }
+        const uint32_t carry = buf[full];
+        wave_lds_sync();
+        if (lane == 0) buf[0] = carry;
+        wave_lds_sync();
+        wbase += full * 32u;
+        bitpos += chunk_bits;
+    }
+    // final states (FSE_flushCState: ML, OF, LL) and the end mark
+    const uint32_t start = bitpos - wbase;
+    if (lane == 0) {
+        buf[1] = 0;
+        put_bits(buf, start, sML, 6);
+        put_bits(buf, start + 6, sOF, 5);
+        put_bits(buf, start + 11, sLL, 6);
+        put_bits(buf, start + 17, 1, 1);
+    }
+    wave_lds_sync();
+    const uint32_t nbytes = (start + 18 + 7) >> 3;  // <= 8
+    if ((wbase >> 3) + nbytes > cap) return kZstdNone;
+    if (lane < nbytes) out[(wbase >> 3) + lane] = (uint8_t)(buf[lane >> 2] >> (8 * (lane & 3)));
+    return (wbase >> 3) + nbytes;
+}
+
+// All n bytes of the block equal to its first?  (wave-uniform; 1 KiB per
+// wave round, the first round decides most non-RLE blocks)
 __device__ bool wave_is_rle(const uint8_t *src, uint32_t n, const uint8_t *lim) {
     const uint32_t lane = lane_id();
     const uint32_t b4 = (uint32_t)src[0] * 0x01010101u;
-    for (uint32_t o = 0; o < n; o += 256) {
-        const uint32_t q = o + lane * 4u;
+    for (uint32_t o = 0; o < n; o += 1024) {
+        const uint32_t q = o + lane * 16u;
         uint32_t x = 0;
-        if (q < n) {
-            x = ld4_hi(src + q, lim) ^ b4;
-            const uint32_t rem = n - q;
-            if (rem < 4) x &= ~(0xFFFFFFFFu << (8 * rem));
+        if (q + 16 <= n) {
+            const uint4 v = ld16(src + q);
+            x = (v.x ^ b4) | (v.y ^ b4) | (v.z ^ b4) | (v.w ^ b4);
+        } else {
+            for (uint32_t k = q; k < n && k < q + 16; k++) x |= src[k] ^ (b4 & 0xFF);
         }
         if (__ballot(x != 0)) return false;
     }
@@ -280,17 +407,22 @@ __device__ bool wave_is_rle(const uint8_t *src, uint32_t n, const uint8_t *lim) 
 
 }  // namespace
 
-// res[b] = {type | rle byte << 8, content bytes}
+// res[b] = {type | rle byte << 8, content bytes}.  HL: hash table of 2^HL
+// positions (LDS 4 * 2^HL bytes per wave: more buckets, or more waves per CU)
+template <int HL>
 __global__ __launch_bounds__(64) void rcdc_zstd_block_kernel(
     const uint8_t *__restrict__ in, const ZstdBlob *__restrict__ blobs,
     const ZstdBlk *__restrict__ blks, uint32_t nblk, const ZstdTables *__restrict__ tabs,
-    uint8_t *__restrict__ slots, uint64_t *__restrict__ seqbuf, uint2 *__restrict__ res) {
-    __shared__ uint2 table[1 << kZstdHashLog];
+    uint8_t *__restrict__ slots, uint64_t *__restrict__ seqbuf, uint2 *__restrict__ res,
+    uint32_t dbg) {
+    __shared__ uint32_t table[1 << HL];
     __shared__ ZstdTables T;
     const uint32_t lane = lane_id();
     for (uint32_t i = lane; i < sizeof(ZstdTables) / 4; i += 64)
         ((uint32_t *)&T)[i] = ((const uint32_t *)tabs)[i];
     uint64_t *seqs = seqbuf + (uint64_t)blockIdx.x * kZstdMaxSeq;
+    __syncthreads();
+    const FseRegs R = fse_regs(T);
     for (uint32_t b = blockIdx.x; b < nblk; b += gridDim.x) {
         const ZstdBlk k = blks[b];
         const ZstdBlob B = blobs[k.blob];
@@ -303,7 +435,11 @@ __global__ __launch_bounds__(64) void rcdc_zstd_block_kernel(
             continue;
         }
         uint32_t nseq = 0, anchor = 0, matched = 0;
-        if (wave_is_rle(src, n, lim)) {
+        const bool prof = dbg & 4u;
+        uint64_t t0 = prof ? wall_clock64() : 0, t1 = t0, t2 = t0, t3 = t0;
+        const bool rle = wave_is_rle(src, n, lim);
+        if (prof) t1 = wall_clock64();
+        if (rle) {
             if (!(k.flags & 1u)) {
                 if (lane == 0) res[b] = make_uint2(kZstdTypeRle | (uint32_t)src[0] << 8, 1);
                 continue;
@@ -314,8 +450,7 @@ __global__ __launch_bounds__(64) void rcdc_zstd_block_kernel(
             anchor = n;
             matched = n - 1;
         } else {
-            for (uint32_t i = lane; i < (1u << kZstdHashLog); i += 64)
-                table[i] = make_uint2(kZstdNone, 0);
+            for (uint32_t i = lane; i < (1u << HL); i += 64) table[i] = kZstdNone;
             __builtin_amdgcn_wave_barrier();
             const uint32_t ilimit = n - 8;  // last position a match may start at
             uint32_t base = 0;
@@ -324,25 +459,67 @@ __global__ __launch_bounds__(64) void rcdc_zstd_block_kernel(
                 if (stride > kZstdMaxStride) stride = kZstdMaxStride;
                 const uint32_t p = base + lane * stride;
                 const bool act = p <= ilimit;
-                uint32_t w = 0, h = 0;
-                uint2 e = make_uint2(kZstdNone, 0);
+                uint32_t w = 0, h = 0, tg = 0, c = kZstdNone;
                 if (act) {
                     w = ld4(src + p);
-                    h = zhash(w);
-                    e = table[h];
+                    h = zhash<HL>(w);
+                    tg = ztag(w);
+                    const uint32_t e = table[h];
+                    if (e != kZstdNone && (e >> 17) == tg) c = e & kZstdPosMask;
                 }
                 __builtin_amdgcn_wave_barrier();
-                if (act) table[h] = make_uint2(p, w);
+                if (act) table[h] = p | tg << 17;
                 __builtin_amdgcn_wave_barrier();
-                const bool ok = act && e.x != kZstdNone && e.y == w;
+                // a candidate's 4 bytes are checked from memory, in the same
+                // round trip as its extension: every candidate lane extends
+                // its own match by up to 16 bytes each way (most matches end
+                // there); longer ones are finished by the wave once selected
+                bool ok = false;
+                uint32_t fl = 0, bl = 0;
+                if (act && c != kZstdNone) {
+                    const uint32_t limf = n - p - 4;
+                    uint32_t wc;
+                    if (limf >= 16) {
+                        wc = ld4(src + c);
+                        fl = first_diff16(ld16(src + p + 4), ld16(src + c + 4));
+                    } else {  // the block's last bytes: independent 4-byte loads
+                        uint4 va, vb;
+                        wc = ld4(src + c);
+                        va.x = ld4_hi(src + p + 4, lim);
+                        va.y = ld4_hi(src + p + 8, lim);
+                        va.z = ld4_hi(src + p + 12, lim);
+                        va.w = 0;
+                        vb.x = ld4_hi(src + c + 4, lim);
+                        vb.y = ld4_hi(src + c + 8, lim);
+                        vb.z = ld4_hi(src + c + 12, lim);
+                        vb.w = 0xFFFFFFFFu;
+                        fl = first_diff16(va, vb);
+                        if (fl > limf) fl = limf;
+                    }
+                    // 16 bytes before both (the bytes before the anchor are
+                    // readable, merely not matchable: clamp)
+                    const uint32_t limb = p - anchor < c ? p - anchor : c;
+                    if (c >= 16) {
+                        bl = last_eq16(ld16(src + p - 16), ld16(src + c - 16));
+                        if (bl > limb) bl = limb;
+                    }
+                    ok = wc == w;
+                    if (ok && c < 16)
+                        while (bl < limb && src[p - 1 - bl] == src[c - 1 - bl]) bl++;
+                }
                 uint64_t m = __ballot(ok);
                 while (m) {
                     const int j = __builtin_ctzll(m);
                     uint32_t pj = base + (uint32_t)j * stride;
-                    uint32_t cj = rdl(e.x, j);
-                    uint32_t len = 4 + wave_match_fwd(src + pj + 4, src + cj + 4, n - pj - 4, lim);
+                    uint32_t cj = rdl(c, j);
+                    const uint32_t f = rdl(fl, j), bb = rdl(bl, j);
+                    uint32_t len = 4 + f;
+                    if (f == 16 && n - pj > 20)
+                        len += wave_match_fwd(src + pj + 20, src + cj + 20, n - pj - 20, lim);
                     const uint32_t mb = pj - anchor < cj ? pj - anchor : cj;
-                    const uint32_t bk = wave_match_back(src + pj, src + cj, mb, src);
+                    uint32_t bk = bb < mb ? bb : mb;
+                    if (bb == 16 && mb > 16)
+                        bk += wave_match_back(src + pj - 16, src + cj - 16, mb - 16, src);
                     pj -= bk;
                     cj -= bk;
                     len += bk;
@@ -356,7 +533,16 @@ __global__ __launch_bounds__(64) void rcdc_zstd_block_kernel(
                 base = next > anchor ? next : anchor;
             }
         }
-        if (nseq == 0) {
+        if (prof) {
+            t2 = wall_clock64();
+            if (lane == 0) {
+                atomicAdd(&g_zstd_prof[0], t1 - t0);
+                atomicAdd(&g_zstd_prof[1], t2 - t1);
+                atomicAdd(&g_zstd_prof[4], 1ull);
+                atomicAdd(&g_zstd_prof[5], (unsigned long long)nseq);
+            }
+        }
+        if (nseq == 0 || (dbg & 1u)) {  // dbg bit 0: measure the parse alone
             if (lane == 0) res[b] = make_uint2(kZstdTypeRaw, n);
             continue;
         }
@@ -368,11 +554,15 @@ __global__ __launch_bounds__(64) void rcdc_zstd_block_kernel(
         const uint32_t min_gain = (n >> 6) + 2u;
         const uint32_t keep_below = n - min_gain;
         uint32_t bsz = kZstdNone;
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        if (bs0 < keep_below && lane == 0)
-            bsz = fse_sequences(seqs, nseq, T, slot + bs0, slot + keep_below);
-        bsz = rdl(bsz, 0);
-        if (bsz == kZstdNone || bs0 + bsz >= keep_below) {
+        __threadfence_block();  // lane 0's sequence records, for every lane
+        if (bs0 < keep_below)
+            bsz = wave_fse_sequences(seqs, nseq, T, R, table, slot + bs0,
+                                     keep_below - bs0);
+        if (prof) {
+            t3 = wall_clock64();
+            if (lane == 0) atomicAdd(&g_zstd_prof[2], t3 - t2);
+        }
+        if (bsz == kZstdNone || bs0 + bsz >= keep_below || (dbg & 2u)) {
             if (lane == 0) res[b] = make_uint2(kZstdTypeRaw, n);
             continue;
         }
@@ -439,6 +629,7 @@ __global__ __launch_bounds__(64) void rcdc_zstd_block_kernel(
         }
         wave_copy(lout + dst_pos, src + src_pos, n - src_pos);
         if (lane == 0) res[b] = make_uint2(kZstdTypeComp, bs0 + bsz);
+        if (prof && lane == 0) atomicAdd(&g_zstd_prof[3], wall_clock64() - t3);
     }
 }
 
@@ -520,17 +711,40 @@ __global__ __launch_bounds__(kZstdCopyThreads) void rcdc_zstd_copy_kernel(
 
 namespace rcdc {
 
-uint32_t zstd_block_grid(uint32_t cus) { return cus * 8u; }
+void zstd_prof_dump() {
+    unsigned long long h[8];
+    if (hipMemcpyFromSymbol(h, HIP_SYMBOL(g_zstd_prof), sizeof h) != hipSuccess) return;
+    fprintf(stderr, "rcdc zstd phases (wave-ms, 100 MHz clock): rle %.1f parse %.1f fse %.1f "
+            "litcopy %.1f; blocks %llu sequences %llu\n", h[0] / 1e5, h[1] / 1e5, h[2] / 1e5,
+            h[3] / 1e5, h[4], h[5]);
+    memset(h, 0, sizeof h);
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(g_zstd_prof), h, sizeof h);
+}
+
+// RCDC_ZSTD_HLOG: 11 (default; 8 KiB table, 16 waves per CU) or 12 (16 KiB,
+// 8 waves per CU: more buckets, better ratio on text, fewer waves)
+static int zstd_hlog() {
+    static const int h = getenv("RCDC_ZSTD_HLOG") ? atoi(getenv("RCDC_ZSTD_HLOG")) : 11;
+    return h == 11 ? 11 : 12;
+}
+
+uint32_t zstd_block_grid(uint32_t cus) { return cus * (zstd_hlog() == 11 ? 16u : 8u); }
 
 hipError_t launch_zstd(const uint8_t *in, uint8_t *out, const ZstdBlob *blobs, uint32_t nblobs,
                        const ZstdBlk *blks, uint32_t nblk, const ZstdTables *tabs, uint8_t *slots,
                        uint64_t *seqbuf, uint32_t grid, uint2 *res, uint64_t *bpos,
                        uint64_t *out_lens, hipStream_t stream) {
     if (nblobs == 0) return hipSuccess;
+    static const uint32_t dbg = getenv("RCDC_ZSTD_DBG") ? (uint32_t)atoi(getenv("RCDC_ZSTD_DBG")) : 0u;
     const uint32_t g = nblk < grid ? nblk : grid;
-    if (g)
-        hipLaunchKernelGGL(rcdc_zstd_block_kernel, dim3(g), dim3(64), 0, stream, in, blobs, blks,
-                           nblk, tabs, slots, seqbuf, res);
+    if (g) {
+        if (zstd_hlog() == 11)
+            hipLaunchKernelGGL(rcdc_zstd_block_kernel<11>, dim3(g), dim3(64), 0, stream, in, blobs,
+                               blks, nblk, tabs, slots, seqbuf, res, dbg);
+        else
+            hipLaunchKernelGGL(rcdc_zstd_block_kernel<12>, dim3(g), dim3(64), 0, stream, in, blobs,
+                               blks, nblk, tabs, slots, seqbuf, res, dbg);
+    }
     hipLaunchKernelGGL(rcdc_zstd_frame_kernel, dim3((nblobs + 255) / 256), dim3(256), 0, stream,
                        blobs, nblobs, res, bpos, out, out_lens);
     if (nblk)
