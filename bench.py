@@ -88,6 +88,10 @@ def parse():
     ap.add_argument("--zstd", action="store_true",
                     help="also compress the chunks as blobs on the device (rcdc_zstd_compress)")
     ap.add_argument("--zstd-level", type=int, default=0)
+    ap.add_argument("--ingest", action="store_true",
+                    help="also run the whole version-2 backup byte path on the device: chunk, "
+                         "blob ids, dedup, zstd, seal into packs (--ingest-streams streams)")
+    ap.add_argument("--ingest-streams", type=int, default=32)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-parity", action="store_true")
     ap.add_argument("--abi-e2e", action="store_true",
@@ -849,6 +853,8 @@ def main():
                                          world == 1 and not args.no_cpu_baseline)
     if args.pack and rank == 0:
         out_extra["pack"] = pack_measure(torch, plan, arena, offs, lens, dev, args)
+    if args.ingest and rank == 0:
+        out_extra["ingest"] = ingest_measure(torch, arena, offs, lens, dev, args)
     if args.zstd and rank == 0:
         out_extra["zstd"] = zstd_measure(torch, plan, arena, offs, lens, dev, args,
                                          world == 1 and not args.no_cpu_baseline)
@@ -1112,6 +1118,125 @@ def aead_measure(torch, plan, arena, offs, lens, dev, args, cpu: bool) -> dict:
     del sealed, plain
     torch.cuda.empty_cache()
     return out
+
+
+def ingest_measure(torch, arena, offs, lens, dev, args) -> dict:
+    """The backup data path of a version-2 repository on the device, end to
+    end over the first --ingest-streams streams (SURVEY.md 8(a) + 8(f)):
+    chunk (rcdc_plan_run, 8 plans), blob ids (rcdc_plan_hash_many: one
+    launch for the 8 plans), dedup by id on the host (the indexer's has(),
+    packer.rs:304-315), zstd of every new blob (rcdc_zstd_compress,
+    decrypt.rs:489-503), then seal into 32 MiB packs with their headers
+    (rcdc_pack_build, packer.rs:615-735).  Wall time of the whole sequence
+    (host steps included) after one untimed pass; one pack checked: its blob
+    opened, decoded by libzstd and hashed back to its id."""
+    import hashlib
+    from oracle import oracle, zstd_ref as zr
+    from rustic_core_amd.chunker import ConfigFile
+    from rustic_core_amd.compress import compress_blobs, frame_layout, make_refs
+    from rustic_core_amd.device import DevicePlan, hash_many
+    from rustic_core_amd.pack import PackSizer, build_packs, group_blobs, make_blobs, pack_layout
+    ns = min(len(lens), max(args.ingest_streams, 8))
+    from rustic_core_amd.chunker import Context
+    ctx = Context.get(POLY, MIN, AVG, MAX, device=dev.index or 0)
+    groups_s = [list(range(g, ns, 8)) for g in range(8)]
+    plans = [DevicePlan(ctx, [int(offs[i]) for i in g], [int(lens[i]) for i in g], arena.numel())
+             for g in groups_s]
+    side = torch.cuda.Stream(dev)
+    sp = side.cuda_stream
+    ptr = arena.data_ptr()
+    rng = np.random.default_rng(0x1A6E)
+    key = rng.integers(0, 256, 64, dtype=np.uint8).tobytes()
+    bufs = {}
+
+    def buf(name, n):
+        t = bufs.get(name)
+        if t is None or t.numel() < n:
+            bufs[name] = t = torch.empty(int(n * 1.1) + 64, dtype=torch.uint8, device=dev)
+        return t
+
+    def ingest(times):
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+        t0 = time.perf_counter()
+        ev[0].record(side)
+        for p in plans:
+            p.run(ptr, sp)
+        ev[1].record(side)
+        hash_many(plans, [ptr] * len(plans), sp)
+        ev[2].record(side)
+        seen, in_offs, blens, ids = set(), [], [], []
+        nchunks = 0
+        for p, g in zip(plans, groups_s):
+            cuts, digs = p.results(), p.digests()
+            for j, i in enumerate(g):
+                prev = 0
+                for c, d in zip(cuts[j], digs[j]):
+                    nchunks += 1
+                    k = d.tobytes()
+                    if k not in seen:
+                        seen.add(k)
+                        in_offs.append(int(offs[i]) + prev)
+                        blens.append(int(c) - prev)
+                        ids.append(d)
+                    prev = int(c)
+        t1 = time.perf_counter()
+        f_offs, ftot = frame_layout(blens)
+        frames = buf("frames", ftot)
+        flens = compress_blobs(ctx, ptr, make_refs(in_offs, blens, f_offs), frames.data_ptr(),
+                               args.zstd_level, sp)
+        t2 = time.perf_counter()
+        nb = len(blens)
+        blobs = make_blobs(f_offs, flens, np.stack(ids) if ids else np.zeros((0, 32), np.uint8),
+                           rng.integers(0, 256, (nb, 16), dtype=np.uint8), uncompressed=blens)
+        groups = group_blobs([int(x) for x in flens],
+                             PackSizer.from_config(ConfigFile.new(2, POLY), 0, 0))
+        packs, total = pack_layout(blobs, groups,
+                                   rng.integers(0, 256, (len(groups), 16), dtype=np.uint8))
+        out = buf("packs", total)
+        build_packs(ctx, key, frames.data_ptr(), blobs, packs, out.data_ptr(), total, sp)
+        torch.cuda.synchronize(dev)
+        t3 = time.perf_counter()
+        times.append({"total_ms": (t3 - t0) * 1e3, "chunk_ms": ev[0].elapsed_time(ev[1]),
+                      "ids_ms": ev[1].elapsed_time(ev[2]),
+                      "ids_to_dedup_done_ms": (t1 - t0) * 1e3,
+                      "zstd_ms": (t2 - t1) * 1e3, "pack_ms": (t3 - t2) * 1e3})
+        return nchunks, in_offs, blens, flens, blobs, packs, groups, total, out
+
+    warm = []
+    ingest(warm)
+    times = []
+    for _ in range(3):
+        nchunks, in_offs, blens, flens, blobs, packs, groups, total, out = ingest(times)
+    best = min(times, key=lambda t: t["total_ms"])
+    inb = int(sum(int(lens[i]) for i in range(ns)))
+    # check one pack: header ids, each blob opened, decoded and hashed back
+    j = len(groups) // 2
+    p = packs[j]
+    f = out[int(p["out_off"]):int(p["out_off"]) + int(p["size"])].cpu().numpy().tobytes()
+    parsed = oracle.parse_pack(key, f)
+    b0 = int(p["blob0"])
+    ok = len(parsed) == int(p["nblobs"])
+    for k, (tpe, off, ln, ulen, bid) in enumerate(parsed[:8]):
+        plain = zr.decompress(oracle.open_(key, f[off:off + ln]))
+        src = arena[in_offs[b0 + k]:in_offs[b0 + k] + blens[b0 + k]].cpu().numpy().tobytes()
+        ok &= plain == src and hashlib.sha256(plain).digest() == bytes(bid) and ulen == len(src)
+    for pl in plans:
+        pl.close()
+    bufs.clear()
+    torch.cuda.empty_cache()
+    return {
+        "path": "chunk (8 plans) -> blob ids (hash_many) -> host dedup -> zstd (new blobs) -> "
+                "seal into packs + headers; all bytes stay in HBM",
+        "streams": ns, "input_bytes": inb, "chunks": nchunks, "unique_blobs": len(blens),
+        "unique_bytes": int(sum(blens)), "frame_bytes": int(np.sum(flens)),
+        "packs": len(groups), "pack_bytes": int(total),
+        "ms": {k: round(v, 2) for k, v in best.items()},
+        "gibs_input": round(inb / (best["total_ms"] / 1e3) / GiB, 2),
+        "check": {"pack": j, "ok": bool(ok),
+                  "checker": "oracle.parse_pack + oracle.open_ + libzstd decode + sha256 == id "
+                             "for its first 8 blobs"},
+        "note": "pack ids (SHA-256 of each pack file, packer.rs:833) are left to the writer",
+    }
 
 
 def zstd_measure(torch, plan, arena, offs, lens, dev, args, cpu: bool) -> dict:
