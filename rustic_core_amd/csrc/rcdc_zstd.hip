@@ -386,6 +386,290 @@ __device__ uint32_t wave_fse_sequences(const uint64_t *seqs, uint32_t nseq, cons
     return (wbase >> 3) + nbytes;
 }
 
+
+// ---- literals section (RFC 8878 3.1.1.3.1): raw, RLE or Huffman (4 streams,
+// direct 4-bit weights) -------------------------------------------------------
+
+constexpr uint32_t kHufMaxBits = 11;
+
+__device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
+    for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d);
+    return v;
+}
+
+__device__ __forceinline__ uint32_t wave_max(uint32_t v) {
+    for (int d = 32; d >= 1; d >>= 1) {
+        const uint32_t o = __shfl_xor(v, d);
+        v = o > v ? o : v;
+    }
+    return v;
+}
+
+__device__ __forceinline__ uint32_t wave_min(uint32_t v) {
+    for (int d = 32; d >= 1; d >>= 1) {
+        const uint32_t o = __shfl_xor(v, d);
+        v = o < v ? o : v;
+    }
+    return v;
+}
+
+__device__ __forceinline__ uint32_t byte_of(uint4 v, uint32_t k) {
+    const uint32_t w = k < 8 ? (k < 4 ? v.x : v.y) : (k < 12 ? v.z : v.w);
+    return (w >> (8 * (k & 3))) & 0xFFu;
+}
+
+// Raw/RLE literals header (Size_Format by size: 1, 2 or 3 bytes).
+__device__ uint32_t lit_hdr_raw(uint8_t *out, uint32_t type, uint32_t n) {
+    if (n < 32) {
+        out[0] = (uint8_t)(type | n << 3);
+        return 1;
+    }
+    if (n < 4096) {
+        const uint32_t v = type | 1u << 2 | n << 4;
+        out[0] = (uint8_t)v;
+        out[1] = (uint8_t)(v >> 8);
+        return 2;
+    }
+    const uint32_t v = type | 3u << 2 | n << 4;
+    out[0] = (uint8_t)v;
+    out[1] = (uint8_t)(v >> 8);
+    out[2] = (uint8_t)(v >> 16);
+    return 3;
+}
+
+// One Huffman stream: literals [a, b) of lbuf, the last one first (as
+// HUF_compress1X), then the end mark; rounds of 1024 literals (lane l takes
+// 16 of them), codes OR-ed into the LDS bit buffer at prefix-sum positions.
+__device__ void huf_stream(const uint8_t *lbuf, uint32_t a, uint32_t b, const uint32_t *code,
+                           uint32_t *buf, uint8_t *out) {
+    const uint32_t lane = lane_id();
+    uint32_t bitpos = 0, wbase = 0;
+    if (lane == 0) buf[0] = 0;
+    wave_lds_sync();
+    const uint32_t len = b - a;
+    for (uint32_t t0 = 0; t0 < len; t0 += 1024) {
+        const uint32_t tl = t0 + 16u * lane;
+        uint32_t cnt = 0, bits = 0;
+        uint4 v = make_uint4(0, 0, 0, 0);
+        if (tl < len) {
+            cnt = len - tl < 16 ? len - tl : 16u;
+            v = ld16(lbuf + b - tl - 16);  // literal b-1-tl is byte 15
+            for (uint32_t k = 0; k < cnt; k++) bits += code[byte_of(v, 15 - k)] >> 16;
+        }
+        uint32_t incl = bits;
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint32_t y = __shfl_up(incl, d);
+            if ((int)lane >= d) incl += y;
+        }
+        const uint32_t chunk_bits = rdl(incl, 63);
+        const uint32_t start = bitpos - wbase, endbit = start + chunk_bits;
+        for (uint32_t w = 1 + lane; w <= (endbit >> 5) + 1; w += 64) buf[w] = 0;
+        wave_lds_sync();
+        uint32_t q = start + incl - bits;
+        for (uint32_t k = 0; k < cnt; k++) {
+            const uint32_t cd = code[byte_of(v, 15 - k)];
+            put_bits(buf, q, cd & 0xFFFFu, cd >> 16);
+            q += cd >> 16;
+        }
+        wave_lds_sync();
+        const uint32_t full = endbit >> 5;
+        uint8_t *o = out + (wbase >> 3);
+        for (uint32_t w = lane; w < full; w += 64) {
+            const uint32_t x = buf[w];
+            o[4 * w] = (uint8_t)x;
+            o[4 * w + 1] = (uint8_t)(x >> 8);
+            o[4 * w + 2] = (uint8_t)(x >> 16);
+            o[4 * w + 3] = (uint8_t)(x >> 24);
+        }
+        const uint32_t carry = buf[full];
+        wave_lds_sync();
+        if (lane == 0) buf[0] = carry;
+        wave_lds_sync();
+        wbase += full * 32u;
+        bitpos += chunk_bits;
+    }
+    const uint32_t start = bitpos - wbase;
+    if (lane == 0) {
+        buf[1] = 0;
+        put_bits(buf, start, 1, 1);  // end mark
+    }
+    wave_lds_sync();
+    const uint32_t nbytes = (start + 1 + 7) >> 3;
+    if (lane < nbytes) out[(wbase >> 3) + lane] = (uint8_t)(buf[lane >> 2] >> (8 * (lane & 3)));
+    wave_lds_sync();
+}
+
+// The literals section of a block into out; returns its bytes.  Huffman with
+// 4 streams when the literal alphabet fits direct weights (bytes <= 128) and
+// it is smaller than raw; RLE when one byte value; raw otherwise.  Code
+// lengths: Shannon lengths ceil(log2(n / count)) clamped to 11 bits, the
+// Kraft sum repaired (lengthen the shortest code below 11 while above 1) and
+// filled (shortest codes first, shorten while the slack allows);
+// tests/zstd_model.py restates it.  lds: 2048 words of LDS.
+__device__ uint32_t encode_literals(const uint8_t *lbuf, uint32_t nl, uint8_t *out,
+                                    uint32_t *lds) {
+    const uint32_t lane = lane_id();
+    if (nl >= 64) {
+        uint32_t *hist = lds, *code = lds + 256, *wts = lds + 512, *st = lds + 768;
+        uint32_t *buf = lds + 1024;
+        for (uint32_t i = lane; i < 256; i += 64) hist[i] = 0;
+        wave_lds_sync();
+        for (uint32_t k = lane * 16u; k < nl; k += 1024) {
+            const uint4 v = ld16(lbuf + k);
+            const uint32_t c = nl - k < 16 ? nl - k : 16u;
+            for (uint32_t j = 0; j < c; j++) atomicAdd(&hist[byte_of(v, j)], 1u);
+        }
+        wave_lds_sync();
+        uint32_t c[4], L[4];
+        uint32_t mx = 0, ns = 0;
+        for (int j = 0; j < 4; j++) {
+            c[j] = hist[lane + 64 * j];
+            if (c[j]) {
+                mx = lane + 64u * j;
+                ns++;
+            }
+        }
+        const uint32_t maxsym = wave_max(mx), nsym = wave_sum(ns);
+        if (nsym == 1) {  // RLE literals
+            const uint32_t h = lit_hdr_raw(out, 1, nl);
+            if (lane == 0) out[h] = (uint8_t)maxsym;
+            return h + 1;
+        }
+        if (maxsym <= 128) {
+            uint32_t k2 = 0;
+            for (int j = 0; j < 4; j++) {
+                L[j] = 0;
+                if (c[j]) {
+                    const uint32_t q = (nl + c[j] - 1) / c[j];
+                    const uint32_t l = q <= 1 ? 1u : 32u - (uint32_t)__clz(q - 1);
+                    L[j] = l > kHufMaxBits ? kHufMaxBits : l;
+                    k2 += 2048u >> L[j];
+                }
+            }
+            uint32_t K = wave_sum(k2);
+            while (K > 2048u) {  // lengthen the shortest code below 11 (lowest symbol)
+                uint32_t key = 0xFFFFFFFFu;
+                for (int j = 0; j < 4; j++)
+                    if (L[j] && L[j] < kHufMaxBits) {
+                        const uint32_t kk = L[j] << 16 | (lane + 64u * j);
+                        key = kk < key ? kk : key;
+                    }
+                key = wave_min(key);
+                if (key == 0xFFFFFFFFu) break;
+                const uint32_t sym = key & 0xFFFFu, lw = key >> 16;
+                for (int j = 0; j < 4; j++) L[j] += (lane + 64u * j == sym) ? 1u : 0u;
+                K -= 1024u >> lw;
+            }
+            for (int j = 0; j < 4; j++) wts[lane + 64 * j] = L[j];
+            wave_lds_sync();
+            if (K < 2048u && lane == 0) {  // fill the slack, shortest codes first
+                for (uint32_t ln = 1; ln <= kHufMaxBits; ln++)
+                    for (uint32_t sy = 0; sy <= maxsym; sy++) {
+                        uint32_t l = wts[sy];
+                        if (l != ln) continue;
+                        while (l > 1 && K + (2048u >> l) <= 2048u) {
+                            K += 2048u >> l;
+                            l--;
+                        }
+                        wts[sy] = l;
+                    }
+            }
+            K = rdl(K, 0);
+            wave_lds_sync();
+            if (K == 2048u) {
+                uint32_t lm = 0;
+                for (int j = 0; j < 4; j++) {
+                    L[j] = wts[lane + 64 * j];
+                    lm = L[j] > lm ? L[j] : lm;
+                }
+                const uint32_t M = wave_max(lm);  // the table log
+                uint32_t w[4];
+                for (int j = 0; j < 4; j++) w[j] = L[j] ? M + 1 - L[j] : 0u;
+                // rank starts per weight (HUF_readDTableX1: weights ascending)
+                uint32_t acc = 0;
+                for (uint32_t x = 1; x <= M; x++) {
+                    uint32_t cx = 0;
+                    for (int j = 0; j < 4; j++) cx += w[j] == x;
+                    cx = wave_sum(cx);
+                    if (lane == 0) st[x] = acc;
+                    acc += cx << (x - 1);
+                }
+                wave_lds_sync();
+                for (int j = 0; j < 4; j++) wts[lane + 64 * j] = w[j];
+                // codes: start[w] >> (w - 1) + rank among the weight's symbols
+                uint32_t cd[4] = {0, 0, 0, 0};
+                const uint64_t lt = (1ull << lane) - 1ull;
+                for (uint32_t x = 1; x <= M; x++) {
+                    uint32_t carry = 0;
+                    const uint32_t base_x = st[x] >> (x - 1);
+                    for (int j = 0; j < 4; j++) {
+                        const uint64_t m = __ballot(w[j] == x);
+                        if (w[j] == x)
+                            cd[j] = (base_x + carry + (uint32_t)__popcll(m & lt)) | (M + 1 - x) << 16;
+                        carry += (uint32_t)__popcll(m);
+                    }
+                }
+                for (int j = 0; j < 4; j++) code[lane + 64 * j] = cd[j];
+                wave_lds_sync();
+                // stream sizes
+                const uint32_t seg = (nl + 3) / 4;
+                uint32_t sb[4] = {0, 0, 0, 0};
+                for (uint32_t k = lane * 16u; k < nl; k += 1024) {
+                    const uint4 v = ld16(lbuf + k);
+                    const uint32_t cc = nl - k < 16 ? nl - k : 16u;
+                    for (uint32_t j = 0; j < cc; j++) {
+                        const uint32_t s4 = (k + j) / seg;
+                        const uint32_t nb = code[byte_of(v, j)] >> 16;
+                        sb[0] += s4 == 0 ? nb : 0u;
+                        sb[1] += s4 == 1 ? nb : 0u;
+                        sb[2] += s4 == 2 ? nb : 0u;
+                        sb[3] += s4 == 3 ? nb : 0u;
+                    }
+                }
+                uint32_t sbytes[4], comp = 1 + (maxsym + 1) / 2 + 6;
+                for (int j = 0; j < 4; j++) {
+                    sbytes[j] = (wave_sum(sb[j]) + 1 + 7) >> 3;
+                    comp += sbytes[j];
+                }
+                const uint32_t hl = nl < 1024 ? 3u : nl < 16384 ? 4u : 5u;
+                const uint32_t rawsz = (nl < 32 ? 1u : nl < 4096 ? 2u : 3u) + nl;
+                if (hl + comp < rawsz) {
+                    if (lane == 0) {
+                        const uint64_t hv = hl == 3 ? (2ull | 1ull << 2 | (uint64_t)nl << 4 |
+                                                       (uint64_t)comp << 14)
+                                            : hl == 4 ? (2ull | 2ull << 2 | (uint64_t)nl << 4 |
+                                                         (uint64_t)comp << 18)
+                                                      : (2ull | 3ull << 2 | (uint64_t)nl << 4 |
+                                                         (uint64_t)comp << 22);
+                        for (uint32_t k = 0; k < hl; k++) out[k] = (uint8_t)(hv >> (8 * k));
+                        out[hl] = (uint8_t)(127 + maxsym);
+                        uint8_t *jt = out + hl + 1 + (maxsym + 1) / 2;
+                        for (int j = 0; j < 3; j++) {
+                            jt[2 * j] = (uint8_t)sbytes[j];
+                            jt[2 * j + 1] = (uint8_t)(sbytes[j] >> 8);
+                        }
+                    }
+                    // weights of symbols 0 .. maxsym - 1, two per byte, high nibble first
+                    for (uint32_t k = lane; 2 * k < maxsym; k += 64) {
+                        const uint32_t lo = 2 * k + 1 < maxsym ? wts[2 * k + 1] : 0u;
+                        out[hl + 1 + k] = (uint8_t)(wts[2 * k] << 4 | lo);
+                    }
+                    uint8_t *so = out + hl + 1 + (maxsym + 1) / 2 + 6;
+                    for (uint32_t j = 0; j < 4; j++) {
+                        const uint32_t a = j * seg, bnd = j == 3 ? nl : (j + 1) * seg;
+                        huf_stream(lbuf, a, bnd, code, buf, so);
+                        so += sbytes[j];
+                    }
+                    return hl + comp;
+                }
+            }
+        }
+    }
+    const uint32_t h = lit_hdr_raw(out, 0, nl);
+    wave_copy(out + h, lbuf, nl);
+    return h + nl;
+}
+
 // All n bytes of the block equal to its first?  (wave-uniform; 1 KiB per
 // wave round, the first round decides most non-RLE blocks)
 __device__ bool wave_is_rle(const uint8_t *src, uint32_t n, const uint8_t *lim) {
@@ -547,17 +831,55 @@ __global__ __launch_bounds__(64) void rcdc_zstd_block_kernel(
             continue;
         }
         const uint32_t lits = n - matched;
-        const uint32_t lh = lits < 32 ? 1u : lits < 4096 ? 2u : 3u;
         const uint32_t sh = (nseq < 128 ? 1u : nseq < 0x7F00 ? 2u : 3u) + 1u;
-        const uint32_t bs0 = lh + lits + sh;
         // zstd keeps a compressed block only if it saves more than minGain
         const uint32_t min_gain = (n >> 6) + 2u;
         const uint32_t keep_below = n - min_gain;
-        uint32_t bsz = kZstdNone;
         __threadfence_block();  // lane 0's sequence records, for every lane
+        // the literals, gathered into the wave's scratch after its sequences
+        // (8 nseq + lits <= 2 kZstdBlock): a lane per short run, the wave per
+        // long run, then the tail
+        uint8_t *lbuf = (uint8_t *)(seqs + nseq);
+        {
+            uint32_t src_pos = 0, dst_pos = 0;
+            for (uint32_t c = 0; c < nseq; c += 64) {
+                const uint32_t i = c + lane;
+                uint32_t ll = 0, adv = 0;
+                if (i < nseq) {
+                    const uint64_t s = seqs[i];
+                    ll = (uint32_t)(s & 0xFFFFF);
+                    adv = ll + (uint32_t)((s >> 20) & 0xFFFFF);
+                }
+                // inclusive prefix sums over the 64 sequences
+                uint32_t xs = adv, xl = ll;
+                for (int d = 1; d < 64; d <<= 1) {
+                    const uint32_t ys = __shfl_up(xs, d), yl = __shfl_up(xl, d);
+                    if ((int)lane >= d) {
+                        xs += ys;
+                        xl += yl;
+                    }
+                }
+                const uint32_t sp = src_pos + xs - adv, dp = dst_pos + xl - ll;
+                const bool small = ll < 64;
+                if (small)
+                    for (uint32_t t = 0; t < ll; t++) lbuf[dp + t] = src[sp + t];
+                uint64_t big = __ballot(!small);
+                while (big) {
+                    const int j = __builtin_ctzll(big);
+                    big &= big - 1;
+                    wave_copy(lbuf + rdl(dp, j), src + rdl(sp, j), rdl(ll, j));
+                }
+                src_pos = rdl(src_pos + xs, 63);
+                dst_pos = rdl(dst_pos + xl, 63);
+            }
+            wave_copy(lbuf + dst_pos, src + src_pos, n - src_pos);
+        }
+        __threadfence_block();
+        const uint32_t lsz = encode_literals(lbuf, lits, slot, table);
+        const uint32_t bs0 = lsz + sh;
+        uint32_t bsz = kZstdNone;
         if (bs0 < keep_below)
-            bsz = wave_fse_sequences(seqs, nseq, T, R, table, slot + bs0,
-                                     keep_below - bs0);
+            bsz = wave_fse_sequences(seqs, nseq, T, R, table, slot + bs0, keep_below - bs0);
         if (prof) {
             t3 = wall_clock64();
             if (lane == 0) atomicAdd(&g_zstd_prof[2], t3 - t2);
@@ -566,22 +888,9 @@ __global__ __launch_bounds__(64) void rcdc_zstd_block_kernel(
             if (lane == 0) res[b] = make_uint2(kZstdTypeRaw, n);
             continue;
         }
-        // literals section header (Raw_Literals_Block, RFC 8878 3.1.1.3.1.1)
+        // sequences section header: Number_of_Sequences, modes (all predefined)
         if (lane == 0) {
-            if (lh == 1) {
-                slot[0] = (uint8_t)(lits << 3);
-            } else if (lh == 2) {
-                const uint32_t v = 1u << 2 | lits << 4;
-                slot[0] = (uint8_t)v;
-                slot[1] = (uint8_t)(v >> 8);
-            } else {
-                const uint32_t v = 3u << 2 | lits << 4;
-                slot[0] = (uint8_t)v;
-                slot[1] = (uint8_t)(v >> 8);
-                slot[2] = (uint8_t)(v >> 16);
-            }
-            // sequences section header: Number_of_Sequences, modes (all predefined)
-            uint8_t *q = slot + lh + lits;
+            uint8_t *q = slot + lsz;
             if (nseq < 128) {
                 q[0] = (uint8_t)nseq;
             } else if (nseq < 0x7F00) {
@@ -594,40 +903,6 @@ __global__ __launch_bounds__(64) void rcdc_zstd_block_kernel(
             }
             q[sh - 1] = 0;
         }
-        // literals: lane per short run, the wave per long run, then the tail
-        uint8_t *lout = slot + lh;
-        uint32_t src_pos = 0, dst_pos = 0;
-        for (uint32_t c = 0; c < nseq; c += 64) {
-            const uint32_t i = c + lane;
-            uint32_t ll = 0, adv = 0;
-            if (i < nseq) {
-                const uint64_t s = seqs[i];
-                ll = (uint32_t)(s & 0xFFFFF);
-                adv = ll + (uint32_t)((s >> 20) & 0xFFFFF);
-            }
-            // exclusive prefix sums over the 64 sequences
-            uint32_t xs = adv, xl = ll;
-            for (int d = 1; d < 64; d <<= 1) {
-                const uint32_t ys = __shfl_up(xs, d), yl = __shfl_up(xl, d);
-                if ((int)lane >= d) {
-                    xs += ys;
-                    xl += yl;
-                }
-            }
-            const uint32_t sp = src_pos + xs - adv, dp = dst_pos + xl - ll;
-            const bool small = ll < 64;
-            if (small)
-                for (uint32_t t = 0; t < ll; t++) lout[dp + t] = src[sp + t];
-            uint64_t big = __ballot(!small);
-            while (big) {
-                const int j = __builtin_ctzll(big);
-                big &= big - 1;
-                wave_copy(lout + rdl(dp, j), src + rdl(sp, j), rdl(ll, j));
-            }
-            src_pos = rdl(src_pos + xs, 63);
-            dst_pos = rdl(dst_pos + xl, 63);
-        }
-        wave_copy(lout + dst_pos, src + src_pos, n - src_pos);
         if (lane == 0) res[b] = make_uint2(kZstdTypeComp, bs0 + bsz);
         if (prof && lane == 0) atomicAdd(&g_zstd_prof[3], wall_clock64() - t3);
     }

@@ -152,3 +152,36 @@ def test_abi_rejects(rcdc_lib):
     assert rcdc_lib.rcdc_zstd_bound(0) == 12
     assert rcdc_lib.rcdc_zstd_bound(131072) == 131072 + 3 + 9
     assert rcdc_lib.rcdc_zstd_bound(131073) == 131073 + 6 + 9
+
+
+@pytest.mark.parametrize("kind", ["two", "ascii-text", "skewed", "flat-129", "clamped"])
+def test_model_huffman_literals(T, kind):
+    """Compressed_Literals_Block (4 streams, direct weights) as the device
+    builds it (tests/zstd_model.py restates rcdc_zstd.hip encode_literals):
+    every decoder reads it back, and the code is complete (Kraft sum 1)."""
+    rng = np.random.default_rng(len(kind))
+    if kind == "two":
+        lits = bytes(rng.choice([97, 98], 5000, p=[0.9, 0.1]).astype(np.uint8))
+    elif kind == "ascii-text":
+        words = [bytes(rng.integers(97, 123, int(rng.integers(2, 9))).astype(np.uint8))
+                 for _ in range(3000)]
+        lits = b" ".join(words)[:100000]
+    elif kind == "skewed":
+        lits = bytes(rng.choice(129, 60000, p=rng.dirichlet(np.ones(129) * 0.05)).astype(np.uint8))
+    elif kind == "flat-129":
+        lits = bytes(rng.integers(0, 129, 70000).astype(np.uint8))
+    else:  # many symbols rarer than 2^-11: the Kraft repair path
+        p = np.r_[[0.9], np.full(128, 0.1 / 128)]
+        lits = bytes(rng.choice(129, 131000, p=p).astype(np.uint8))
+    counts = np.bincount(np.frombuffer(lits, np.uint8), minlength=256)
+    L = zm.huf_lengths(counts)
+    assert L is not None and max(L) <= 11
+    assert sum(2.0 ** -l for l in L if l) == 1.0
+    sec = zm.huf_literals_section(lits)
+    assert sec is not None and len(sec) < len(lits)
+    blk = sec + b"\x00"  # no sequences
+    fr = zm.frame([(2, blk, len(lits))], len(lits))
+    assert zr.decompress(fr) == lits
+    assert zr.decompress_pyarrow(fr, len(lits)) == lits
+    if kind in ("skewed", "two"):  # Huffman at least as small as libzstd here
+        assert len(fr) <= 1.05 * len(zr.compress(lits, 3)) + 64

@@ -164,3 +164,349 @@ def greedy_sequences(data: bytes, min_match: int = 4):
         else:
             p += 1
     return seqs
+
+
+# ---- Huffman-coded literals (RFC 8878 4.2), the device's algorithm ---------
+
+HUF_MAX_BITS = 11
+
+
+def huf_lengths(counts):
+    """Code lengths (<= 11 bits, Kraft sum exactly 1) as the device builds
+    them: Shannon lengths ceil(log2(total / count)) clamped to 11; while the
+    Kraft sum exceeds 1, lengthen the shortest code below 11 (lowest symbol
+    first); then, shortest codes first, shorten every code while the slack
+    allows.  None if that cannot close the sum (never seen) or < 2 symbols."""
+    M = HUF_MAX_BITS
+    total = int(sum(counts))
+    L = [0] * 256
+    for s in range(256):
+        c = int(counts[s])
+        if c:
+            q = -(-total // c)
+            L[s] = min(M, max(1, (q - 1).bit_length()))
+    syms = [s for s in range(256) if L[s]]
+    if len(syms) < 2:
+        return None
+    K = sum(1 << (M - L[s]) for s in syms)
+    while K > (1 << M):
+        s = min((s for s in syms if L[s] < M), key=lambda s: (L[s], s))
+        K -= 1 << (M - L[s] - 1)
+        L[s] += 1
+    for ln in range(1, M + 1):
+        for s in syms:
+            if L[s] == ln:
+                while L[s] > 1 and K + (1 << (M - L[s])) <= (1 << M):
+                    K += 1 << (M - L[s])
+                    L[s] -= 1
+    return L if K == (1 << M) else None
+
+
+def huf_codes(L):
+    """Canonical codes of the decoder's table (HUF_readDTableX1): weights
+    ascending, symbols in order within a weight; the table log is the
+    longest code (HUF_readStats wants >= 2 symbols of weight 1).  Returns
+    (vals, nbits, weights)."""
+    M = max(L)
+    w = [M + 1 - l if l else 0 for l in L]
+    cnt = [0] * (M + 2)
+    for x in w:
+        if x:
+            cnt[x] += 1
+    start, acc = [0] * (M + 2), 0
+    for x in range(1, M + 1):
+        start[x] = acc
+        acc += cnt[x] << (x - 1)
+    vals = [0] * 256
+    for s in range(256):
+        if w[s]:
+            vals[s] = start[w[s]] >> (w[s] - 1)
+            start[w[s]] += 1 << (w[s] - 1)
+    return vals, L, w
+
+
+def huf_literals_section(lits: bytes):
+    """Compressed_Literals_Block with 4 streams and direct weights, or None
+    (max symbol > 128, < 2 symbols, no gain)."""
+    n = len(lits)
+    counts = np.bincount(np.frombuffer(lits, np.uint8), minlength=256)
+    maxsym = int(np.nonzero(counts)[0].max())
+    if maxsym > 128 or n < 64:
+        return None
+    L = huf_lengths(counts)
+    if L is None:
+        return None
+    vals, nb, w = huf_codes(L)
+    tree = bytes([127 + maxsym]) + bytes(
+        (w[k] << 4 | (w[k + 1] if k + 1 < maxsym else 0)) for k in range(0, maxsym, 2))
+    seg = (n + 3) // 4
+    streams = []
+    for k in range(4):
+        part = lits[k * seg:min(n, (k + 1) * seg)]
+        bw = BitWriter()
+        for b in reversed(part):
+            bw.add(vals[b], nb[b])
+            bw.flush()
+        bw.add(1, 1)
+        bw.flush()
+        if bw.nb:
+            bw.out.append(bw.acc & 0xFF)
+        streams.append(bytes(bw.out))
+    jump = b"".join(len(s).to_bytes(2, "little") for s in streams[:3])
+    comp = len(tree) + 6 + sum(len(s) for s in streams)
+    if n < 1024:
+        hdr = (2 | 1 << 2 | n << 4 | comp << 14).to_bytes(3, "little")
+    elif n < 16384:
+        hdr = (2 | 2 << 2 | n << 4 | comp << 18).to_bytes(4, "little")
+    else:
+        hdr = (2 | 3 << 2 | n << 4 | comp << 22).to_bytes(5, "little")
+    return hdr + tree + jump + b"".join(streams)
+
+
+def compressed_block_huf(T, data: bytes, seqs):
+    """compressed_block with Huffman literals where they apply."""
+    lits = bytearray()
+    pos = 0
+    for ll, ml, off in seqs:
+        lits += data[pos:pos + ll]
+        pos += ll + ml
+    lits += data[pos:]
+    sec = huf_literals_section(bytes(lits))
+    raw = compressed_block(T, data, seqs)
+    if sec is None:
+        return raw
+    n = len(lits)
+    lh = 1 if n < 32 else 2 if n < 4096 else 3
+    return sec + raw[lh + n:]
+
+
+# ---- adaptive FSE tables for the sequences (FSE_Compressed mode, log 6) ---
+
+FSE_ADAPT_LOG = 6
+PREDEF_NORM = {
+    "ll": ([4, 3, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 1, 1, 1, 2, 2, 2, 2, 2, 2, 2, 2, 2, 3, 2, 1, 1, 1,
+            1, 1, -1, -1, -1, -1], 6),
+    "ml": ([1, 4, 3, 2, 2, 2, 2, 2, 2, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1,
+            1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, -1, -1, -1, -1, -1, -1, -1], 6),
+    "of": ([1, 1, 1, 1, 1, 1, 2, 2, 2, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, -1, -1, -1, -1,
+            -1], 5),
+}
+
+
+def fse_normalize(counts, tl=FSE_ADAPT_LOG):
+    """Counts -> normalized counts summing to 2^tl, every present symbol >= 1
+    (no low-probability -1 symbols): rounded shares, the difference taken
+    from / given to the largest symbols (the device's rule)."""
+    size = 1 << tl
+    total = int(sum(counts))
+    norm = [0] * len(counts)
+    for s, c in enumerate(counts):
+        if c:
+            norm[s] = max(1, (int(c) * size + total // 2) // total)
+    diff = size - sum(norm)
+    order = sorted((s for s in range(len(counts)) if counts[s]), key=lambda s: (-norm[s], s))
+    if diff > 0:
+        norm[order[0]] += diff
+    i = 0
+    while diff < 0:
+        s = order[i % len(order)]
+        if norm[s] > 1:
+            norm[s] -= 1
+            diff += 1
+        i += 1
+    return norm
+
+
+def fse_write_ncount(norm, tl):
+    """FSE_writeNCount (RFC 8878 4.1.1): the table description bytes."""
+    bw = BitWriter()
+    bw.add(tl - 5, 4)
+    remaining = (1 << tl) + 1
+    threshold = 1 << tl
+    nbits = tl + 1
+    s, n = 0, len(norm)
+    prev0 = False
+    while s < n and remaining > 1:
+        if prev0:
+            start = s
+            while s < n and norm[s] == 0:
+                s += 1
+            while s >= start + 24:
+                start += 24
+                bw.add(0xFFFF, 16)
+                bw.flush()
+            while s >= start + 3:
+                start += 3
+                bw.add(3, 2)
+            bw.add(s - start, 2)
+            bw.flush()
+        count = norm[s]
+        s += 1
+        mx = (2 * threshold - 1) - remaining
+        remaining -= abs(count)
+        count += 1
+        if count >= threshold:
+            count += mx
+        bw.add(count, nbits - (1 if count < mx else 0))
+        bw.flush()
+        prev0 = count == 1
+        while remaining < threshold:
+            nbits -= 1
+            threshold >>= 1
+    assert remaining == 1
+    if bw.nb:
+        bw.out.append(bw.acc & 0xFF)
+    return bytes(bw.out)
+
+
+def fse_ctable(norm, tl):
+    """FSE_buildCTable: (symbol transforms [(find, nbits)], state table)."""
+    size, mask, step = 1 << tl, (1 << tl) - 1, (1 << tl >> 1) + (1 << tl >> 3) + 3
+    sym, cumul, high = [0] * size, [0] * (len(norm) + 1), size - 1
+    for u in range(1, len(norm) + 1):
+        if norm[u - 1] == -1:
+            cumul[u] = cumul[u - 1] + 1
+            sym[high] = u - 1
+            high -= 1
+        else:
+            cumul[u] = cumul[u - 1] + norm[u - 1]
+    pos = 0
+    for s, c in enumerate(norm):
+        for _ in range(max(c, 0)):
+            sym[pos] = s
+            pos = (pos + step) & mask
+            while pos > high:
+                pos = (pos + step) & mask
+    st = [0] * size
+    cu = list(cumul)
+    for u in range(size):
+        st[cu[sym[u]]] = size + u
+        cu[sym[u]] += 1
+    tt, total = [], 0
+    for c in norm:
+        if c in (-1, 1):
+            tt.append((total - 1, (tl << 16) - size))
+            total += 1
+        elif c > 1:
+            mbo = tl - ((c - 1).bit_length() - 1)
+            tt.append((total - c, (mbo << 16) - (c << mbo)))
+            total += c
+        else:
+            tt.append((0, ((tl + 1) << 16) - size))
+    return tt, st
+
+
+def encode_sequences_tabs(tabs, seqs, T):
+    """encode_sequences with per-stream tables tabs[name] = (tt, st, tl)."""
+    w = BitWriter()
+
+    def init(name, sym):
+        tt, st, _ = tabs[name]
+        find, nbits = tt[sym]
+        nbo = (nbits + (1 << 15)) >> 16
+        v = (nbo << 16) - nbits
+        return st[(v >> nbo) + find]
+
+    def enc(name, state, sym):
+        tt, st, _ = tabs[name]
+        find, nbits = tt[sym]
+        nbo = (state + nbits) >> 16
+        w.add(state, nbo)
+        return st[(state >> nbo) + find]
+
+    ll, ml, off = seqs[-1]
+    llc, mlc, ofc, mlb, ofv = _codes(T, ll, ml, off)
+    sml, sof, sll = init("ml", mlc), init("of", ofc), init("ll", llc)
+    w.add(ll, T["llbits"][llc])
+    w.add(mlb, T["mlbits"][mlc])
+    w.flush()
+    w.add(ofv, ofc)
+    w.flush()
+    for ll, ml, off in reversed(seqs[:-1]):
+        llc, mlc, ofc, mlb, ofv = _codes(T, ll, ml, off)
+        sof = enc("of", sof, ofc)
+        sml = enc("ml", sml, mlc)
+        w.flush()
+        sll = enc("ll", sll, llc)
+        w.add(ll, T["llbits"][llc])
+        w.flush()
+        w.add(mlb, T["mlbits"][mlc])
+        w.flush()
+        w.add(ofv, ofc)
+        w.flush()
+    w.add(sml, tabs["ml"][2])
+    w.flush()
+    w.add(sof, tabs["of"][2])
+    w.flush()
+    w.add(sll, tabs["ll"][2])
+    w.add(1, 1)
+    w.flush()
+    if w.nb:
+        w.out.append(w.acc & 0xFF)
+    return bytes(w.out)
+
+
+def _cost_bits(counts, norm, tl):
+    import math
+    return sum(c * (tl - math.log2(norm[s])) for s, c in enumerate(counts) if c)
+
+
+def sequences_section_adaptive(T, seqs):
+    """Sequences section choosing, per stream, predefined or an adaptive
+    log-6 table by estimated bits (the device's rule)."""
+    k = len(seqs)
+    codes = [_codes(T, *s) for s in seqs]
+    hist = {"ll": [0] * 36, "ml": [0] * 53, "of": [0] * 32}
+    for llc, mlc, ofc, _, _ in codes:
+        hist["ll"][llc] += 1
+        hist["ml"][mlc] += 1
+        hist["of"][ofc] += 1
+    modes, descs, tabs = {}, {}, {}
+    for name in ("ll", "of", "ml"):
+        pn, ptl = PREDEF_NORM[name]
+        cnt = hist[name]
+        pnorm = [abs(x) for x in pn] + [0] * (len(cnt) - len(pn))
+        if any(c and not pnorm[s] for s, c in enumerate(cnt)):
+            pcost = float("inf")
+        else:
+            pcost = _cost_bits(cnt, pnorm, ptl)
+        an = fse_normalize(cnt)
+        last = max(s for s in range(len(cnt)) if cnt[s])
+        desc = fse_write_ncount(an[:last + 1], FSE_ADAPT_LOG)
+        acost = _cost_bits(cnt, an, FSE_ADAPT_LOG) + 8 * len(desc)
+        if acost < pcost:
+            modes[name], descs[name] = 2, desc
+            tt, st = fse_ctable(an[:last + 1], FSE_ADAPT_LOG)
+            tabs[name] = (tt, st, FSE_ADAPT_LOG)
+        else:
+            modes[name], descs[name] = 0, b""
+            tt, st = fse_ctable(pn, ptl)
+            tabs[name] = (tt, st, ptl)
+    if k < 128:
+        sh = bytes([k])
+    elif k < 0x7F00:
+        sh = bytes([(k >> 8) + 0x80, k & 0xFF])
+    else:
+        sh = bytes([0xFF]) + (k - 0x7F00).to_bytes(2, "little")
+    sh += bytes([modes["ll"] << 6 | modes["of"] << 4 | modes["ml"] << 2])
+    return sh + descs["ll"] + descs["of"] + descs["ml"] + encode_sequences_tabs(tabs, seqs, T)
+
+
+def compressed_block_adaptive(T, data: bytes, seqs):
+    """Huffman literals (where they apply) + adaptive sequences."""
+    lits = bytearray()
+    pos = 0
+    for ll, ml, off in seqs:
+        lits += data[pos:pos + ll]
+        pos += ll + ml
+    lits += data[pos:]
+    sec = huf_literals_section(bytes(lits))
+    if sec is None:
+        n = len(lits)
+        if n < 32:
+            sec = bytes([n << 3]) + bytes(lits)
+        elif n < 4096:
+            sec = (1 << 2 | n << 4).to_bytes(2, "little") + bytes(lits)
+        else:
+            sec = (3 << 2 | n << 4).to_bytes(3, "little") + bytes(lits)
+    return sec + (sequences_section_adaptive(T, seqs) if seqs else b"\x00")
