@@ -270,6 +270,27 @@ __device__ __forceinline__ uint32_t fse_enc_s(uint32_t F, uint32_t N, uint32_t S
     return rdl(S, (int)((int32_t)(st >> nbo) + f));
 }
 
+__device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
+    for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d);
+    return v;
+}
+
+__device__ __forceinline__ uint32_t wave_max(uint32_t v) {
+    for (int d = 32; d >= 1; d >>= 1) {
+        const uint32_t o = __shfl_xor(v, d);
+        v = o > v ? o : v;
+    }
+    return v;
+}
+
+__device__ __forceinline__ uint32_t wave_min(uint32_t v) {
+    for (int d = 32; d >= 1; d >>= 1) {
+        const uint32_t o = __shfl_xor(v, d);
+        v = o < v ? o : v;
+    }
+    return v;
+}
+
 // OR n bits of v (n <= 25) into the LDS bit buffer at bit q.
 __device__ __forceinline__ void put_bits(uint32_t *buf, uint32_t q, uint32_t v, uint32_t n) {
     if (!n) return;
@@ -290,16 +311,183 @@ __device__ __forceinline__ uint32_t wl(uint32_t v, int lane, uint32_t old) {
     return lane_id() == (uint32_t)lane ? v : old;
 }
 
-// The sequences section's bitstream (ZSTD_encodeSequences order: the last
-// sequence first, its states initialised from it; then per sequence OF, ML,
-// LL state bits and LL, ML, OF extra bits; the final states; the end mark),
-// by the whole wave: 64 sequences per round, the three state chains stepped
-// as scalar code, every field OR-ed into an LDS bit buffer at its prefix-sum
-// position, full words stored.  Returns its bytes, or kZstdNone past cap.
+// Per stream (LL, OF, ML): predefined table, or an adaptive one of accuracy
+// log 6 (FSE_Compressed mode) when its estimated bits, description included,
+// are fewer.  Adaptive counts: rounded shares of 64, present symbols >= 1, the
+// difference given to / taken from the largest (tests/zstd_model.py
+// fse_normalize).  Log 6 keeps every table at <= 64 entries: one per lane,
+// so the scalar state chains read them with v_readlane as the predefined
+// ones.  Writes the description (FSE_writeNCount) at out and returns its
+// bytes; updates the stream's registers and table log.
+__device__ uint32_t fse_choose(uint32_t t, uint32_t nsymt, const uint32_t *hist, uint32_t nseq,
+                               uint32_t tlp, uint32_t predN, uint32_t &F, uint32_t &N, uint32_t &S,
+                               uint32_t &tl, uint32_t *lds, uint8_t *out, uint32_t cap) {
+    const uint32_t lane = lane_id();
+    uint32_t *nrm = lds, *cum = lds + 64, *occ = lds + 128, *pos = lds + 192, *stt = lds + 256;
+    const uint32_t cnt = lane < nsymt ? hist[t * 64 + lane] : 0u;
+    // predefined cost: its count c from deltaNbBits (c = ((mbo << 16) - nb) >> mbo, mbo = nb >> 16 + 1)
+    float pc = 0.f, ac = 0.f;
+    if (cnt) {
+        const uint32_t mbo = (predN >> 16) + 1;
+        const uint32_t cp = ((mbo << 16) - predN) >> mbo;
+        pc = (float)cnt * ((float)tlp - __log2f((float)cp));
+    }
+    uint32_t an = cnt ? (cnt * 64u + nseq / 2) / nseq : 0u;
+    if (cnt && an == 0) an = 1;
+    int32_t diff = 64 - (int32_t)wave_sum(an);
+    // give to / take from the largest (lowest symbol on ties)
+    while (diff != 0) {
+        const uint32_t key = wave_max(cnt ? an << 8 | (255u - lane) : 0u);
+        const uint32_t big = 255u - (key & 0xFFu);
+        if (diff > 0) {
+            if (lane == big) an += (uint32_t)diff;
+            diff = 0;
+        } else {
+            if (lane == big) an -= 1;
+            diff += 1;
+        }
+    }
+    if (cnt) ac = (float)cnt * (6.f - __log2f((float)an));
+    for (int d = 32; d >= 1; d >>= 1) {
+        pc += __shfl_xor(pc, d);
+        ac += __shfl_xor(ac, d);
+    }
+    nrm[lane] = an;
+    wave_lds_sync();
+    // the description (FSE_writeNCount), by lane 0
+    uint32_t nbytes = 0;
+    if (lane == 0) {
+        uint64_t acc = 6u - 5u;  // accuracy log - 5, in 4 bits
+        uint32_t nb = 4, o = 0;
+        uint32_t remaining = 65, threshold = 64, nbits = 7, sy = 0;
+        bool prev0 = false;
+        while (sy < nsymt && remaining > 1) {
+            if (prev0) {
+                uint32_t st0 = sy;
+                while (sy < nsymt && nrm[sy] == 0) sy++;
+                while (sy >= st0 + 24) {
+                    st0 += 24;
+                    acc |= (uint64_t)0xFFFF << nb;
+                    nb += 16;
+                    while (nb >= 8) {
+                        if (o < cap) out[o] = (uint8_t)acc;
+                        o++;
+                        acc >>= 8;
+                        nb -= 8;
+                    }
+                }
+                while (sy >= st0 + 3) {
+                    st0 += 3;
+                    acc |= (uint64_t)3 << nb;
+                    nb += 2;
+                }
+                acc |= (uint64_t)(sy - st0) << nb;
+                nb += 2;
+            }
+            uint32_t count = nrm[sy++];
+            const uint32_t mx = (2 * threshold - 1) - remaining;
+            remaining -= count;
+            count += 1;
+            if (count >= threshold) count += mx;
+            acc |= (uint64_t)count << nb;
+            nb += nbits - (count < mx ? 1u : 0u);
+            prev0 = count == 1;
+            while (remaining < threshold) {
+                nbits--;
+                threshold >>= 1;
+            }
+            while (nb >= 8) {
+                if (o < cap) out[o] = (uint8_t)acc;
+                o++;
+                acc >>= 8;
+                nb -= 8;
+            }
+        }
+        if (nb) {
+            if (o < cap) out[o] = (uint8_t)acc;
+            o++;
+        }
+        nbytes = o;
+    }
+    nbytes = rdl(nbytes, 0);
+    if (ac + 8.f * (float)nbytes >= pc || nbytes > cap) return 0;  // predefined
+    // the adaptive table (FSE_buildCTable, log 6: no low-probability symbols)
+    uint32_t inc = an;
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t y = __shfl_up(inc, d);
+        if ((int)lane >= d) inc += y;
+    }
+    const uint32_t c0 = inc - an;  // cumulative count before this symbol
+    cum[lane] = c0;
+    for (uint32_t j = 0; j < an; j++) occ[c0 + j] = lane;  // occurrence -> symbol
+    wave_lds_sync();
+    pos[(lane * 43u) & 63u] = occ[lane];  // the spread: step 64/2 + 64/8 + 3
+    wave_lds_sync();
+    const uint32_t sym = pos[lane];
+    uint32_t rank = 0;
+    for (uint32_t u = 0; u < lane; u++) rank += pos[u] == sym;
+    stt[cum[sym] + rank] = 64u + lane;
+    wave_lds_sync();
+    S = stt[lane];
+    if (an == 0) {
+        N = (7u << 16) - 64u;
+        F = 0;
+    } else if (an == 1) {
+        N = (6u << 16) - 64u;
+        F = c0 - 1u;
+    } else {
+        const uint32_t mbo = 6u - (31u - (uint32_t)__clz(an - 1));
+        N = (mbo << 16) - (an << mbo);
+        F = c0 - an;
+    }
+    tl = 6;
+    wave_lds_sync();
+    return nbytes;
+}
+
+// The sequences section after Number_of_Sequences: the modes byte, the
+// adaptive tables' descriptions (LL, OF, ML) and the bitstream
+// (ZSTD_encodeSequences order: the last sequence first, its states
+// initialised from it; then per sequence OF, ML, LL state bits and LL, ML,
+// OF extra bits; the final states; the end mark), by the whole wave: 64
+// sequences per round, the three state chains stepped as scalar code, every
+// field OR-ed into an LDS bit buffer at its prefix-sum position, full words
+// stored.  Returns its bytes, or kZstdNone past cap.
 __device__ uint32_t wave_fse_sequences(const uint64_t *seqs, uint32_t nseq, const ZstdTables &T,
-                                       const FseRegs &R, uint32_t *buf, uint8_t *out,
+                                       const FseRegs &R0, uint32_t *buf, uint8_t *out,
                                        uint32_t cap) {
     const uint32_t lane = lane_id();
+    // code histograms (LL, OF, ML) for the table choice
+    uint32_t *hist = buf + 1024;
+    for (uint32_t i = lane; i < 192; i += 64) hist[i] = 0;
+    wave_lds_sync();
+    for (uint32_t c0 = 0; c0 < nseq; c0 += 64) {
+        if (c0 + lane < nseq) {
+            const SeqCodes c = seq_codes(seqs[c0 + lane], T);
+            atomicAdd(&hist[c.llc], 1u);
+            atomicAdd(&hist[64 + c.ofc], 1u);
+            atomicAdd(&hist[128 + c.mlc], 1u);
+        }
+    }
+    wave_lds_sync();
+    FseRegs R = R0;
+    uint32_t tll = 6, tof = 5, tml = 6;
+    if (cap < 2) return kZstdNone;
+    uint32_t o = 1;
+    const uint32_t dl = fse_choose(0, 36, hist, nseq, 6, R0.llN, R.llF, R.llN, R.llS, tll,
+                                   buf + 1216, out + o, cap - o);
+    o += dl;
+    const uint32_t dof = fse_choose(1, 32, hist, nseq, 5, R0.ofN, R.ofF, R.ofN, R.ofS, tof,
+                                    buf + 1216, out + o, cap - o);
+    o += dof;
+    const uint32_t dml = fse_choose(2, 53, hist, nseq, 6, R0.mlN, R.mlF, R.mlN, R.mlS, tml,
+                                    buf + 1216, out + o, cap - o);
+    o += dml;
+    if (lane == 0) out[0] = (uint8_t)((dl ? 2u : 0u) << 6 | (dof ? 2u : 0u) << 4 | (dml ? 2u : 0u) << 2);
+    if (o >= cap) return kZstdNone;
+    uint8_t *const out0 = out;
+    out += o;
+    cap -= o;
     uint32_t sLL = 0, sML = 0, sOF = 0;
     uint32_t bitpos = 0, wbase = 0;  // bits written; bit index of buf[0] (multiple of 32)
     if (lane == 0) buf[0] = 0;
@@ -374,44 +562,22 @@ __device__ uint32_t wave_fse_sequences(const uint64_t *seqs, uint32_t nseq, cons
     const uint32_t start = bitpos - wbase;
     if (lane == 0) {
         buf[1] = 0;
-        put_bits(buf, start, sML, 6);
-        put_bits(buf, start + 6, sOF, 5);
-        put_bits(buf, start + 11, sLL, 6);
-        put_bits(buf, start + 17, 1, 1);
+        put_bits(buf, start, sML, tml);
+        put_bits(buf, start + tml, sOF, tof);
+        put_bits(buf, start + tml + tof, sLL, tll);
+        put_bits(buf, start + tml + tof + tll, 1, 1);
     }
     wave_lds_sync();
-    const uint32_t nbytes = (start + 18 + 7) >> 3;  // <= 8
+    const uint32_t nbytes = (start + tml + tof + tll + 1 + 7) >> 3;  // <= 8
     if ((wbase >> 3) + nbytes > cap) return kZstdNone;
     if (lane < nbytes) out[(wbase >> 3) + lane] = (uint8_t)(buf[lane >> 2] >> (8 * (lane & 3)));
-    return (wbase >> 3) + nbytes;
+    return (uint32_t)(out - out0) + (wbase >> 3) + nbytes;
 }
-
 
 // ---- literals section (RFC 8878 3.1.1.3.1): raw, RLE or Huffman (4 streams,
 // direct 4-bit weights) -------------------------------------------------------
 
 constexpr uint32_t kHufMaxBits = 11;
-
-__device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
-    for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d);
-    return v;
-}
-
-__device__ __forceinline__ uint32_t wave_max(uint32_t v) {
-    for (int d = 32; d >= 1; d >>= 1) {
-        const uint32_t o = __shfl_xor(v, d);
-        v = o > v ? o : v;
-    }
-    return v;
-}
-
-__device__ __forceinline__ uint32_t wave_min(uint32_t v) {
-    for (int d = 32; d >= 1; d >>= 1) {
-        const uint32_t o = __shfl_xor(v, d);
-        v = o < v ? o : v;
-    }
-    return v;
-}
 
 __device__ __forceinline__ uint32_t byte_of(uint4 v, uint32_t k) {
     const uint32_t w = k < 8 ? (k < 4 ? v.x : v.y) : (k < 12 ? v.z : v.w);
@@ -694,7 +860,7 @@ __device__ bool wave_is_rle(const uint8_t *src, uint32_t n, const uint8_t *lim) 
 // res[b] = {type | rle byte << 8, content bytes}.  HL: hash table of 2^HL
 // positions (LDS 4 * 2^HL bytes per wave: more buckets, or more waves per CU)
 template <int HL>
-__global__ __launch_bounds__(64) void rcdc_zstd_block_kernel(
+__global__ __launch_bounds__(64, 4) void rcdc_zstd_block_kernel(
     const uint8_t *__restrict__ in, const ZstdBlob *__restrict__ blobs,
     const ZstdBlk *__restrict__ blks, uint32_t nblk, const ZstdTables *__restrict__ tabs,
     uint8_t *__restrict__ slots, uint64_t *__restrict__ seqbuf, uint2 *__restrict__ res,
@@ -876,9 +1042,9 @@ __global__ __launch_bounds__(64) void rcdc_zstd_block_kernel(
         }
         __threadfence_block();
         const uint32_t lsz = encode_literals(lbuf, lits, slot, table);
-        const uint32_t bs0 = lsz + sh;
+        const uint32_t bs0 = lsz + sh - 1;  // after Number_of_Sequences
         uint32_t bsz = kZstdNone;
-        if (bs0 < keep_below)
+        if (bs0 + 1 < keep_below)
             bsz = wave_fse_sequences(seqs, nseq, T, R, table, slot + bs0, keep_below - bs0);
         if (prof) {
             t3 = wall_clock64();
@@ -888,7 +1054,7 @@ __global__ __launch_bounds__(64) void rcdc_zstd_block_kernel(
             if (lane == 0) res[b] = make_uint2(kZstdTypeRaw, n);
             continue;
         }
-        // sequences section header: Number_of_Sequences, modes (all predefined)
+        // Number_of_Sequences (the modes byte follows it, written above)
         if (lane == 0) {
             uint8_t *q = slot + lsz;
             if (nseq < 128) {
@@ -901,7 +1067,6 @@ __global__ __launch_bounds__(64) void rcdc_zstd_block_kernel(
                 q[1] = (uint8_t)(nseq - 0x7F00);
                 q[2] = (uint8_t)((nseq - 0x7F00) >> 8);
             }
-            q[sh - 1] = 0;
         }
         if (lane == 0) res[b] = make_uint2(kZstdTypeComp, bs0 + bsz);
         if (prof && lane == 0) atomicAdd(&g_zstd_prof[3], wall_clock64() - t3);

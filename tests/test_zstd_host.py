@@ -185,3 +185,41 @@ def test_model_huffman_literals(T, kind):
     assert zr.decompress_pyarrow(fr, len(lits)) == lits
     if kind in ("skewed", "two"):  # Huffman at least as small as libzstd here
         assert len(fr) <= 1.05 * len(zr.compress(lits, 3)) + 64
+
+
+@pytest.mark.parametrize("case", ["text", "one-ml-code", "short-block", "long-offsets"])
+def test_model_adaptive_sequences(T, case):
+    """Sequences section with adaptive log-6 FSE tables where they beat the
+    predefined ones (FSE_Compressed mode: FSE_writeNCount descriptions),
+    as rcdc_zstd.hip codes it: both decoders read it back."""
+    rng = np.random.default_rng(len(case))
+    if case == "text":
+        words = [bytes(rng.integers(97, 123, int(rng.integers(2, 9))).astype(np.uint8))
+                 for _ in range(300)]
+        data = b" ".join(words[int(i)] for i in rng.integers(0, 300, 30000))[:131072]
+        seqs = zm.greedy_sequences(data)
+    else:
+        if case == "one-ml-code":
+            seqs = [(int(rng.integers(0, 20)), 4, int(rng.integers(1, 200))) for _ in range(3000)]
+        elif case == "short-block":
+            seqs = [(3, 5, 2), (0, 6, 7), (1, 4, 3)]
+        else:
+            seqs = [(int(rng.integers(0, 40)), int(rng.integers(3, 300)), 0) for _ in range(300)]
+        fixed, size = [], 0
+        for ll, ml, off in seqs:
+            size += ll
+            off = off or int(rng.integers(1, max(2, size)))
+            off = max(1, min(off, size))
+            fixed.append((max(ll, 1) if size == ll else ll, ml, off))
+            size += ml
+        seqs = fixed
+        if seqs[0][0] == 0:
+            seqs[0] = (1,) + seqs[0][1:]
+        data = _synth(seqs, 5, rng)
+    blk = zm.compressed_block_adaptive(T, data, seqs)
+    fr = zm.frame([(2, blk, len(data))], len(data))
+    assert zr.decompress(fr) == data
+    if len(blk) <= len(data):
+        assert zr.decompress_pyarrow(fr, len(data)) == data
+    if case == "text":
+        assert len(fr) < 1.15 * len(zr.compress(data, 3))

@@ -304,16 +304,13 @@ def fse_normalize(counts, tl=FSE_ADAPT_LOG):
         if c:
             norm[s] = max(1, (int(c) * size + total // 2) // total)
     diff = size - sum(norm)
-    order = sorted((s for s in range(len(counts)) if counts[s]), key=lambda s: (-norm[s], s))
+    big = max(range(len(counts)), key=lambda s: (norm[s], -s))
     if diff > 0:
-        norm[order[0]] += diff
-    i = 0
-    while diff < 0:
-        s = order[i % len(order)]
-        if norm[s] > 1:
-            norm[s] -= 1
-            diff += 1
-        i += 1
+        norm[big] += diff
+    while diff < 0:  # take one from the current largest (lowest symbol on ties)
+        big = max(range(len(counts)), key=lambda s: (norm[s], -s))
+        norm[big] -= 1
+        diff += 1
     return norm
 
 
