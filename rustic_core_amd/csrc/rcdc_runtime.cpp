@@ -279,6 +279,11 @@ struct rcdc_stream {
     uint64_t batch = 0;            // bytes buffered before a device pass
     bool done = false;
     std::deque<uint64_t> out;      // final cuts not yet handed to the caller
+    // the same pending bytes, kept on the device after a pass, so the next
+    // pass sends only the new bytes over PCIe (tail_len == pending.size()
+    // when valid, 0 otherwise)
+    uint8_t *d_tail = nullptr;
+    uint64_t cap_tail = 0, tail_len = 0;
 };
 
 namespace {
@@ -1019,9 +1024,12 @@ struct HostPiece {
 // stream.  Stream i of the batch is the concatenation of its pieces (a
 // streaming caller's buffered tail and its new read need no intermediate
 // copy).  The plan is rebuilt only when the batch layout changes.
+// d_prefix (optional): the first prefix_len bytes of the arena come from
+// device memory (a stream's tail kept from its previous pass), not the host.
 rcdc_status run_host_pieces(rcdc_ctx *ctx, Lane *L, const std::vector<uint64_t> &lens,
                             const std::vector<HostPiece> &pieces, uint64_t *cuts, uint64_t cap,
-                            uint64_t *counts) {
+                            uint64_t *counts, const uint8_t *d_prefix = nullptr,
+                            uint64_t prefix_len = 0) {
     const uint32_t n = (uint32_t)lens.size();
     std::vector<uint64_t> offs(n);
     uint64_t total = 0;
@@ -1039,10 +1047,13 @@ rcdc_status run_host_pieces(rcdc_ctx *ctx, Lane *L, const std::vector<uint64_t> 
             HIP_TRY(hipHostMalloc((void **)&L->pinned[k], L->stage, hipHostMallocDefault));
     }
     uint64_t t_copy = 0, t_wait = 0, t0 = g_hprof_on ? now_ns() : 0;
+    if (prefix_len)
+        HIP_TRY(hipMemcpyAsync(L->d_arena, d_prefix, prefix_len, hipMemcpyDeviceToDevice,
+                               L->stream));
     // staged copies: block k of the arena goes through slot k & 1
     size_t pi = 0;  // first piece that may overlap the block
     uint64_t k = 0;
-    for (uint64_t p = 0; p < total; p += L->stage, k++) {
+    for (uint64_t p = prefix_len; p < total; p += L->stage, k++) {
         const uint64_t e = std::min(p + L->stage, total);
         const int slot = (int)(k & 1);
         if (k >= 2) {
@@ -2046,7 +2057,13 @@ rcdc_status rcdc_stream_open(rcdc_ctx *ctx, rcdc_stream **out) {
     return RCDC_OK;
 }
 
-void rcdc_stream_close(rcdc_stream *st) { delete st; }
+void rcdc_stream_close(rcdc_stream *st) {
+    if (st && st->d_tail) {
+        DeviceGuard g(st->ctx->device);
+        (void)hipFree(st->d_tail);
+    }
+    delete st;
+}
 
 uint64_t rcdc_stream_batch_bytes(const rcdc_ctx *ctx) {
     if (!ctx) return 0;
@@ -2072,19 +2089,35 @@ static rcdc_status stream_pass(rcdc_stream *st, const uint8_t *data, uint64_t le
     std::vector<uint64_t> tmp(rcdc_max_cuts(ctx, N));
     std::vector<uint64_t> lens{N};
     std::vector<HostPiece> pieces;
-    if (P) pieces.push_back({0, st->pending.data(), P});
+    // the pending bytes come from the device copy of the last pass's tail
+    // when there is one; otherwise from the host buffer
+    const bool dev_tail = P && st->d_tail && st->tail_len == P;
+    if (P && !dev_tail) pieces.push_back({0, st->pending.data(), P});
     if (len) pieces.push_back({P, data, len});
     uint64_t cnt = 0;
     Lane *L = nullptr;
     rcdc_status s2 = lane_acquire(ctx, &L);
     if (s2) return s2;
-    s2 = run_host_pieces(ctx, L, lens, pieces, tmp.data(), tmp.size(), &cnt);
+    st->tail_len = 0;
+    s2 = run_host_pieces(ctx, L, lens, pieces, tmp.data(), tmp.size(), &cnt,
+                         dev_tail ? st->d_tail : nullptr, dev_tail ? P : 0);
+    uint64_t keep = cnt;
+    if (!s2 && !is_final && cnt && tmp[cnt - 1] == N) keep = cnt - 1;
+    const uint64_t consumed = keep ? tmp[keep - 1] : 0;
+    if (!s2 && !is_final && N > consumed) {
+        // keep the unfinished tail on the device for the next pass (the lane's
+        // arena is reused as soon as the lane is released)
+        DeviceGuard g(ctx->device);
+        s2 = ensure_dev(&st->d_tail, &st->cap_tail, N - consumed);
+        if (!s2 && hipMemcpyAsync(st->d_tail, L->d_arena + consumed, N - consumed,
+                                  hipMemcpyDeviceToDevice, L->stream) == hipSuccess &&
+            hipStreamSynchronize(L->stream) == hipSuccess)
+            st->tail_len = N - consumed;
+        s2 = RCDC_OK;  // without a device tail the next pass sends the host copy
+    }
     lane_release(ctx, L);
     if (s2) return s2;
-    uint64_t keep = cnt;
-    if (!is_final && cnt && tmp[cnt - 1] == N) keep = cnt - 1;
     for (uint64_t i = 0; i < keep; i++) st->out.push_back(st->base + tmp[i]);
-    const uint64_t consumed = keep ? tmp[keep - 1] : 0;
     // the unfinished tail [consumed, N) becomes the new pending bytes (in
     // place: the buffer keeps its capacity)
     if (consumed < P) {
