@@ -260,6 +260,11 @@ struct rcdc_ctx {
     uint64_t cap_aead_key = 0, cap_aead_blobs = 0, cap_aead_units = 0, cap_aead_unit0 = 0,
              cap_aead_partials = 0, cap_aead_status = 0, cap_aead_stage = 0;
     hipEvent_t aead_done = nullptr;
+    // device tails of open streams (max + 256 bytes each): a pool, so opening
+    // and closing streams never calls hipMalloc / hipFree (which synchronise
+    // the device) once warm
+    std::mutex tail_mu;
+    std::vector<uint8_t *> tail_pool, tail_all;
     // blob compression (rcdc_zstd_compress): calls on one context take turns
     std::mutex zstd_mu;
     ZstdTables *d_zstd_tabs = nullptr;
@@ -282,8 +287,8 @@ struct rcdc_stream {
     // the same pending bytes, kept on the device after a pass, so the next
     // pass sends only the new bytes over PCIe (tail_len == pending.size()
     // when valid, 0 otherwise)
-    uint8_t *d_tail = nullptr;
-    uint64_t cap_tail = 0, tail_len = 0;
+    uint8_t *d_tail = nullptr;  // from the context's pool, ctx->max + 256 bytes
+    uint64_t tail_len = 0;
 };
 
 namespace {
@@ -1257,6 +1262,7 @@ void rcdc_ctx_destroy(rcdc_ctx *c) {
         (void)hipFree(c->d_aead_status);
         (void)hipFree(c->d_aead_stage);
         if (c->aead_done) (void)hipEventDestroy(c->aead_done);
+        for (uint8_t *t : c->tail_all) (void)hipFree(t);
         (void)hipFree(c->d_zstd_tabs);
         (void)hipFree(c->d_zstd_blobs);
         (void)hipFree(c->d_zstd_blks);
@@ -2058,9 +2064,9 @@ rcdc_status rcdc_stream_open(rcdc_ctx *ctx, rcdc_stream **out) {
 }
 
 void rcdc_stream_close(rcdc_stream *st) {
-    if (st && st->d_tail) {
-        DeviceGuard g(st->ctx->device);
-        (void)hipFree(st->d_tail);
+    if (st && st->d_tail) {  // back to the context's pool
+        std::lock_guard<std::mutex> lk(st->ctx->tail_mu);
+        st->ctx->tail_pool.push_back(st->d_tail);
     }
     delete st;
 }
@@ -2104,13 +2110,26 @@ static rcdc_status stream_pass(rcdc_stream *st, const uint8_t *data, uint64_t le
     uint64_t keep = cnt;
     if (!s2 && !is_final && cnt && tmp[cnt - 1] == N) keep = cnt - 1;
     const uint64_t consumed = keep ? tmp[keep - 1] : 0;
-    if (!s2 && !is_final && N > consumed) {
+    static const bool devtail = !getenv("RCDC_STREAM_HOSTTAIL");
+    if (!s2 && !is_final && N > consumed && devtail) {
         // keep the unfinished tail on the device for the next pass (the lane's
         // arena is reused as soon as the lane is released)
+        // (the tail is the last, unfinished chunk: at most max bytes)
         DeviceGuard g(ctx->device);
-        s2 = ensure_dev(&st->d_tail, &st->cap_tail, N - consumed);
-        if (!s2 && hipMemcpyAsync(st->d_tail, L->d_arena + consumed, N - consumed,
-                                  hipMemcpyDeviceToDevice, L->stream) == hipSuccess &&
+        if (!st->d_tail) {
+            std::lock_guard<std::mutex> lk(ctx->tail_mu);
+            if (!ctx->tail_pool.empty()) {
+                st->d_tail = ctx->tail_pool.back();
+                ctx->tail_pool.pop_back();
+            } else if (hipMalloc((void **)&st->d_tail, ctx->max + 256) == hipSuccess) {
+                ctx->tail_all.push_back(st->d_tail);
+            } else {
+                st->d_tail = nullptr;
+            }
+        }
+        if (st->d_tail && N - consumed <= ctx->max + 256 &&
+            hipMemcpyAsync(st->d_tail, L->d_arena + consumed, N - consumed,
+                           hipMemcpyDeviceToDevice, L->stream) == hipSuccess &&
             hipStreamSynchronize(L->stream) == hipSuccess)
             st->tail_len = N - consumed;
         s2 = RCDC_OK;  // without a device tail the next pass sends the host copy
