@@ -311,52 +311,12 @@ __device__ __forceinline__ uint32_t wl(uint32_t v, int lane, uint32_t old) {
     return lane_id() == (uint32_t)lane ? v : old;
 }
 
-// Per stream (LL, OF, ML): predefined table, or an adaptive one of accuracy
-// log 6 (FSE_Compressed mode) when its estimated bits, description included,
-// are fewer.  Adaptive counts: rounded shares of 64, present symbols >= 1, the
-// difference given to / taken from the largest (tests/zstd_model.py
-// fse_normalize).  Log 6 keeps every table at <= 64 entries: one per lane,
-// so the scalar state chains read them with v_readlane as the predefined
-// ones.  Writes the description (FSE_writeNCount) at out and returns its
-// bytes; updates the stream's registers and table log.
-__device__ uint32_t fse_choose(uint32_t t, uint32_t nsymt, const uint32_t *hist, uint32_t nseq,
-                               uint32_t tlp, uint32_t predN, uint32_t &F, uint32_t &N, uint32_t &S,
-                               uint32_t &tl, uint32_t *lds, uint8_t *out, uint32_t cap) {
-    const uint32_t lane = lane_id();
-    uint32_t *nrm = lds, *cum = lds + 64, *occ = lds + 128, *pos = lds + 192, *stt = lds + 256;
-    const uint32_t cnt = lane < nsymt ? hist[t * 64 + lane] : 0u;
-    // predefined cost: its count c from deltaNbBits (c = ((mbo << 16) - nb) >> mbo, mbo = nb >> 16 + 1)
-    float pc = 0.f, ac = 0.f;
-    if (cnt) {
-        const uint32_t mbo = (predN >> 16) + 1;
-        const uint32_t cp = ((mbo << 16) - predN) >> mbo;
-        pc = (float)cnt * ((float)tlp - __log2f((float)cp));
-    }
-    uint32_t an = cnt ? (cnt * 64u + nseq / 2) / nseq : 0u;
-    if (cnt && an == 0) an = 1;
-    int32_t diff = 64 - (int32_t)wave_sum(an);
-    // give to / take from the largest (lowest symbol on ties)
-    while (diff != 0) {
-        const uint32_t key = wave_max(cnt ? an << 8 | (255u - lane) : 0u);
-        const uint32_t big = 255u - (key & 0xFFu);
-        if (diff > 0) {
-            if (lane == big) an += (uint32_t)diff;
-            diff = 0;
-        } else {
-            if (lane == big) an -= 1;
-            diff += 1;
-        }
-    }
-    if (cnt) ac = (float)cnt * (6.f - __log2f((float)an));
-    for (int d = 32; d >= 1; d >>= 1) {
-        pc += __shfl_xor(pc, d);
-        ac += __shfl_xor(ac, d);
-    }
-    nrm[lane] = an;
-    wave_lds_sync();
-    // the description (FSE_writeNCount), by lane 0
+// FSE_writeNCount of normalized counts nrm[0 .. nsymt) at accuracy log 6
+// (RFC 8878 4.1.1), by lane 0; returns the bytes (wave-uniform).
+__device__ uint32_t ncount_write(const uint32_t *nrm, uint32_t nsymt, uint8_t *out,
+                                 uint32_t cap) {
     uint32_t nbytes = 0;
-    if (lane == 0) {
+    if (lane_id() == 0) {
         uint64_t acc = 6u - 5u;  // accuracy log - 5, in 4 bits
         uint32_t nb = 4, o = 0;
         uint32_t remaining = 65, threshold = 64, nbits = 7, sy = 0;
@@ -409,9 +369,17 @@ __device__ uint32_t fse_choose(uint32_t t, uint32_t nsymt, const uint32_t *hist,
         }
         nbytes = o;
     }
-    nbytes = rdl(nbytes, 0);
-    if (ac + 8.f * (float)nbytes >= pc || nbytes > cap) return 0;  // predefined
-    // the adaptive table (FSE_buildCTable, log 6: no low-probability symbols)
+    return rdl(nbytes, 0);
+}
+
+// FSE_buildCTable of a log-6 table with no low-probability symbols, lane s
+// holding symbol s's normalized count an: returns the lane's {find, nbits}
+// (symbol s) and state-table entry (state lane).  The spread is position
+// (43 k) mod 64 for occurrence k; the state table comes from ranks.
+__device__ void fse_build_log6(uint32_t an, uint32_t *lds, uint32_t &F, uint32_t &N,
+                               uint32_t &S) {
+    const uint32_t lane = lane_id();
+    uint32_t *cum = lds + 64, *occ = lds + 128, *pos = lds + 192, *stt = lds + 256;
     uint32_t inc = an;
     for (int d = 1; d < 64; d <<= 1) {
         const uint32_t y = __shfl_up(inc, d);
@@ -440,6 +408,57 @@ __device__ uint32_t fse_choose(uint32_t t, uint32_t nsymt, const uint32_t *hist,
         N = (mbo << 16) - (an << mbo);
         F = c0 - an;
     }
+    wave_lds_sync();
+}
+
+// Per stream (LL, OF, ML): predefined table, or an adaptive one of accuracy
+// log 6 (FSE_Compressed mode) when its estimated bits, description included,
+// are fewer.  Adaptive counts: rounded shares of 64, present symbols >= 1, the
+// difference given to / taken from the largest (tests/zstd_model.py
+// fse_normalize).  Log 6 keeps every table at <= 64 entries: one per lane,
+// so the scalar state chains read them with v_readlane as the predefined
+// ones.  Writes the description (FSE_writeNCount) at out and returns its
+// bytes; updates the stream's registers and table log.
+__device__ uint32_t fse_choose(uint32_t t, uint32_t nsymt, const uint32_t *hist, uint32_t nseq,
+                               uint32_t tlp, uint32_t predN, uint32_t &F, uint32_t &N, uint32_t &S,
+                               uint32_t &tl, uint32_t *lds, uint8_t *out, uint32_t cap) {
+    const uint32_t lane = lane_id();
+    uint32_t *nrm = lds;
+    const uint32_t cnt = lane < nsymt ? hist[t * 64 + lane] : 0u;
+    // predefined cost: its count c from deltaNbBits (c = ((mbo << 16) - nb) >> mbo, mbo = nb >> 16 + 1)
+    float pc = 0.f, ac = 0.f;
+    if (cnt) {
+        const uint32_t mbo = (predN >> 16) + 1;
+        const uint32_t cp = ((mbo << 16) - predN) >> mbo;
+        pc = (float)cnt * ((float)tlp - __log2f((float)cp));
+    }
+    uint32_t an = cnt ? (cnt * 64u + nseq / 2) / nseq : 0u;
+    if (cnt && an == 0) an = 1;
+    int32_t diff = 64 - (int32_t)wave_sum(an);
+    // give to / take from the largest (lowest symbol on ties)
+    while (diff != 0) {
+        const uint32_t key = wave_max(cnt ? an << 8 | (255u - lane) : 0u);
+        const uint32_t big = 255u - (key & 0xFFu);
+        if (diff > 0) {
+            if (lane == big) an += (uint32_t)diff;
+            diff = 0;
+        } else {
+            if (lane == big) an -= 1;
+            diff += 1;
+        }
+    }
+    if (cnt) ac = (float)cnt * (6.f - __log2f((float)an));
+    for (int d = 32; d >= 1; d >>= 1) {
+        pc += __shfl_xor(pc, d);
+        ac += __shfl_xor(ac, d);
+    }
+    nrm[lane] = an;
+    wave_lds_sync();
+    // the description (FSE_writeNCount), by lane 0
+    const uint32_t nbytes = ncount_write(nrm, nsymt, out, cap);
+
+    if (ac + 8.f * (float)nbytes >= pc || nbytes > cap) return 0;  // predefined
+    fse_build_log6(an, lds, F, N, S);
     tl = 6;
     wave_lds_sync();
     return nbytes;
@@ -665,6 +684,100 @@ __device__ void huf_stream(const uint8_t *lbuf, uint32_t a, uint32_t b, const ui
     wave_lds_sync();
 }
 
+
+// Huffman weights of symbols 0 .. n-1 (n <= 255, in wts) as an FSE stream
+// (RFC 8878 4.2.1.2): accuracy log 6, NCount description, then two
+// interleaved states in FSE_compress_usingCTable order (tests/zstd_model.py
+// fse_compress_weights).  Returns the bytes (< 128), or 0 if not codable.
+__device__ uint32_t fse_weights(const uint32_t *wts, uint32_t n, uint32_t *lds, uint8_t *out,
+                                uint32_t cap) {
+    const uint32_t lane = lane_id();
+    uint32_t cnt = 0;
+    for (uint32_t i = 0; i < n; i++) cnt += wts[i] == lane;  // lane v counts weight v
+    if (lane >= 12) cnt = 0;
+    if (wave_sum(cnt ? 1u : 0u) < 2) return 0;
+    uint32_t an = cnt ? (cnt * 64u + n / 2) / n : 0u;
+    if (cnt && an == 0) an = 1;
+    int32_t diff = 64 - (int32_t)wave_sum(an);
+    while (diff != 0) {
+        const uint32_t key = wave_max(cnt ? an << 8 | (255u - lane) : 0u);
+        const uint32_t big = 255u - (key & 0xFFu);
+        if (diff > 0) {
+            if (lane == big) an += (uint32_t)diff;
+            diff = 0;
+        } else {
+            if (lane == big) an -= 1;
+            diff += 1;
+        }
+    }
+    uint32_t *nrm = lds;
+    nrm[lane] = an;
+    wave_lds_sync();
+    const uint32_t nb0 = ncount_write(nrm, 12, out, cap);
+    uint32_t F, N, S;
+    fse_build_log6(an, lds, F, N, S);
+    // the stream, as scalar code: the last weight first, two states
+    uint64_t acc = 0;
+    uint32_t nb = 0, o = nb0;
+    auto add = [&](uint32_t v, uint32_t bits) {
+        acc |= (uint64_t)(v & ((1u << bits) - 1u)) << nb;
+        nb += bits;
+    };
+    auto flush = [&]() {
+        while (nb >= 8) {
+            if (lane == 0 && o < cap) out[o] = (uint8_t)acc;
+            o++;
+            acc >>= 8;
+            nb -= 8;
+        }
+    };
+    auto sym_at = [&](uint32_t i) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)wts[i]); };
+    auto init = [&](uint32_t sy) { return fse_init_s(F, N, S, sy); };
+    auto enc = [&](uint32_t st, uint32_t sy) {
+        uint32_t field;
+        const uint32_t ns = fse_enc_s(F, N, S, sy, st, field);
+        add(field & 0xFFFFu, field >> 16);
+        return ns;
+    };
+    uint32_t ip = n, s1, s2;
+    if (n & 1) {
+        s1 = init(sym_at(ip - 1));
+        s2 = init(sym_at(ip - 2));
+        s1 = enc(s1, sym_at(ip - 3));
+        ip -= 3;
+        flush();
+    } else {
+        s2 = init(sym_at(ip - 1));
+        s1 = init(sym_at(ip - 2));
+        ip -= 2;
+    }
+    if ((n - 2) & 2) {
+        s2 = enc(s2, sym_at(ip - 1));
+        s1 = enc(s1, sym_at(ip - 2));
+        ip -= 2;
+        flush();
+    }
+    while (ip > 0) {
+        s2 = enc(s2, sym_at(ip - 1));
+        s1 = enc(s1, sym_at(ip - 2));
+        s2 = enc(s2, sym_at(ip - 3));
+        s1 = enc(s1, sym_at(ip - 4));
+        ip -= 4;
+        flush();
+    }
+    add(s2, 6);
+    flush();
+    add(s1, 6);
+    add(1, 1);
+    flush();
+    if (nb) {
+        if (lane == 0 && o < cap) out[o] = (uint8_t)acc;
+        o++;
+    }
+    wave_lds_sync();
+    return o < 128 && o <= cap ? o : 0u;
+}
+
 // The literals section of a block into out; returns its bytes.  Huffman with
 // 4 streams when the literal alphabet fits direct weights (bytes <= 128) and
 // it is smaller than raw; RLE when one byte value; raw otherwise.  Code
@@ -701,7 +814,13 @@ __device__ uint32_t encode_literals(const uint8_t *lbuf, uint32_t nl, uint8_t *o
             if (lane == 0) out[h] = (uint8_t)maxsym;
             return h + 1;
         }
-        if (maxsym <= 128) {
+        // order-0 entropy bound: skip the Huffman work when it cannot pay
+        // (random literals: every block of incompressible runs next to zeros)
+        float hbits = 0.f;
+        for (int j = 0; j < 4; j++)
+            if (c[j]) hbits += (float)c[j] * __log2f((float)nl / (float)c[j]);
+        for (int d = 32; d >= 1; d >>= 1) hbits += __shfl_xor(hbits, d);
+        if (hbits * 0.125f + 64.f < (float)nl) {
             uint32_t k2 = 0;
             for (int j = 0; j < 4; j++) {
                 L[j] = 0;
@@ -792,14 +911,21 @@ __device__ uint32_t encode_literals(const uint8_t *lbuf, uint32_t nl, uint8_t *o
                         sb[3] += s4 == 3 ? nb : 0u;
                     }
                 }
-                uint32_t sbytes[4], comp = 1 + (maxsym + 1) / 2 + 6;
+                // tree description: direct 4-bit weights up to symbol 128, else
+                // FSE-compressed weights (written now, after the literals header)
+                const uint32_t hl = nl < 1024 ? 3u : nl < 16384 ? 4u : 5u;
+                uint32_t tree = 1 + (maxsym + 1) / 2;
+                if (maxsym > 128) {
+                    const uint32_t fw = fse_weights(wts, maxsym, lds + 1536, out + hl + 1, nl);
+                    tree = fw ? 1 + fw : 0u;
+                }
+                uint32_t sbytes[4], comp = tree + 6;
                 for (int j = 0; j < 4; j++) {
                     sbytes[j] = (wave_sum(sb[j]) + 1 + 7) >> 3;
                     comp += sbytes[j];
                 }
-                const uint32_t hl = nl < 1024 ? 3u : nl < 16384 ? 4u : 5u;
                 const uint32_t rawsz = (nl < 32 ? 1u : nl < 4096 ? 2u : 3u) + nl;
-                if (hl + comp < rawsz) {
+                if (tree && hl + comp < rawsz) {
                     if (lane == 0) {
                         const uint64_t hv = hl == 3 ? (2ull | 1ull << 2 | (uint64_t)nl << 4 |
                                                        (uint64_t)comp << 14)
@@ -808,19 +934,20 @@ __device__ uint32_t encode_literals(const uint8_t *lbuf, uint32_t nl, uint8_t *o
                                                       : (2ull | 3ull << 2 | (uint64_t)nl << 4 |
                                                          (uint64_t)comp << 22);
                         for (uint32_t k = 0; k < hl; k++) out[k] = (uint8_t)(hv >> (8 * k));
-                        out[hl] = (uint8_t)(127 + maxsym);
-                        uint8_t *jt = out + hl + 1 + (maxsym + 1) / 2;
+                        out[hl] = (uint8_t)(maxsym > 128 ? tree - 1 : 127 + maxsym);
+                        uint8_t *jt = out + hl + tree;
                         for (int j = 0; j < 3; j++) {
                             jt[2 * j] = (uint8_t)sbytes[j];
                             jt[2 * j + 1] = (uint8_t)(sbytes[j] >> 8);
                         }
                     }
                     // weights of symbols 0 .. maxsym - 1, two per byte, high nibble first
-                    for (uint32_t k = lane; 2 * k < maxsym; k += 64) {
-                        const uint32_t lo = 2 * k + 1 < maxsym ? wts[2 * k + 1] : 0u;
-                        out[hl + 1 + k] = (uint8_t)(wts[2 * k] << 4 | lo);
-                    }
-                    uint8_t *so = out + hl + 1 + (maxsym + 1) / 2 + 6;
+                    if (maxsym <= 128)
+                        for (uint32_t k = lane; 2 * k < maxsym; k += 64) {
+                            const uint32_t lo = 2 * k + 1 < maxsym ? wts[2 * k + 1] : 0u;
+                            out[hl + 1 + k] = (uint8_t)(wts[2 * k] << 4 | lo);
+                        }
+                    uint8_t *so = out + hl + tree + 6;
                     for (uint32_t j = 0; j < 4; j++) {
                         const uint32_t a = j * seg, bnd = j == 3 ? nl : (j + 1) * seg;
                         huf_stream(lbuf, a, bnd, code, buf, so);
@@ -860,7 +987,7 @@ __device__ bool wave_is_rle(const uint8_t *src, uint32_t n, const uint8_t *lim) 
 // res[b] = {type | rle byte << 8, content bytes}.  HL: hash table of 2^HL
 // positions (LDS 4 * 2^HL bytes per wave: more buckets, or more waves per CU)
 template <int HL>
-__global__ __launch_bounds__(64, 4) void rcdc_zstd_block_kernel(
+__global__ __launch_bounds__(64, HL == 11 ? 4 : 3) void rcdc_zstd_block_kernel(
     const uint8_t *__restrict__ in, const ZstdBlob *__restrict__ blobs,
     const ZstdBlk *__restrict__ blks, uint32_t nblk, const ZstdTables *__restrict__ tabs,
     uint8_t *__restrict__ slots, uint64_t *__restrict__ seqbuf, uint2 *__restrict__ res,

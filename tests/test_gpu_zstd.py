@@ -49,6 +49,9 @@ def _kinds(rng, n, kind):
     if kind == "skewed":  # literal-heavy, skewed alphabet below 129: Huffman literals
         p = np.random.default_rng(99).dirichlet(np.ones(129) * 0.1)
         return bytes(rng.choice(129, n, p=p).astype(np.uint8))
+    if kind == "binary":  # skewed bytes over all 256 values: FSE-compressed Huffman weights
+        p = np.random.default_rng(98).dirichlet(np.ones(256) * 0.2)
+        return bytes(rng.choice(256, n, p=p).astype(np.uint8))
     if kind == "periodic":
         pat = rng.integers(0, 256, int(rng.integers(1, 300)), dtype=np.uint8).tobytes()
         return (pat * (n // len(pat) + 1))[:n]
@@ -109,15 +112,16 @@ EDGE = [0, 1, 15, 16, 17, 100, 255, 256, 257, 4096, 65791, 65792, 131071, 131072
         131073, 262144 + 5, MiB + 3]
 
 
-@pytest.mark.parametrize("kind", ["random", "zeros", "text", "mixed", "periodic", "skewed"])
+@pytest.mark.parametrize("kind", ["random", "zeros", "text", "mixed", "periodic", "skewed",
+                                  "binary"])
 def test_ragged_lengths(gpu_ctx, kind):
     rng = np.random.default_rng(hash(kind) & 0xFFFF)
     datas = [_kinds(rng, n, kind) for n in EDGE]
     pads = [int(rng.integers(0, 16)) for _ in datas]
     frames = _compress(gpu_ctx, datas, in_pad=pads, out_pad=pads[::-1], runs=2)
     _check(frames, datas)
-    if kind == "skewed":  # no long matches: Huffman-coded literals carry the ratio
-        assert len(frames[-1]) < 0.75 * len(datas[-1])
+    if kind in ("skewed", "binary"):  # few long matches: Huffman literals carry the ratio
+        assert len(frames[-1]) < (0.75 if kind == "skewed" else 0.85) * len(datas[-1])
         assert len(frames[-1]) < 1.2 * len(zr.compress(datas[-1], 3)) + 64
     if kind in ("zeros", "periodic", "text"):
         big = frames[-1]

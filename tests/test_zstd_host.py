@@ -223,3 +223,21 @@ def test_model_adaptive_sequences(T, case):
         assert zr.decompress_pyarrow(fr, len(data)) == data
     if case == "text":
         assert len(fr) < 1.15 * len(zr.compress(data, 3))
+
+
+@pytest.mark.parametrize("nsym,n,alpha", [(200, 5000, 0.05), (256, 50000, 0.3), (140, 131000, 1.0),
+                                          (255, 777, 3.0), (256, 3333, 0.05)])
+def test_model_huffman_fse_weights(T, nsym, n, alpha):
+    """Literal bytes above 128: the Huffman weights go FSE-compressed (log 6,
+    two interleaved states, FSE_compress_usingCTable order), as the device
+    writes them (rcdc_zstd.hip fse_weights); both decoders read them."""
+    rng = np.random.default_rng(nsym + n)
+    lits = bytes(rng.choice(nsym, n, p=rng.dirichlet(np.ones(nsym) * alpha)).astype(np.uint8))
+    sec = zm.huf_literals_section(lits)
+    if sec is None:  # weights >= 128 bytes or no gain: raw literals
+        return
+    assert sec[{True: 3, False: 4}[n < 1024] if n < 16384 else 5] < 128  # FSE weights header byte
+    fr = zm.frame([(2, sec + b"\x00", n)], n)
+    assert zr.decompress(fr) == lits
+    if len(sec) + 1 <= n:
+        assert zr.decompress_pyarrow(fr, n) == lits

@@ -231,14 +231,20 @@ def huf_literals_section(lits: bytes):
     n = len(lits)
     counts = np.bincount(np.frombuffer(lits, np.uint8), minlength=256)
     maxsym = int(np.nonzero(counts)[0].max())
-    if maxsym > 128 or n < 64:
+    if n < 64:
         return None
     L = huf_lengths(counts)
     if L is None:
         return None
     vals, nb, w = huf_codes(L)
-    tree = bytes([127 + maxsym]) + bytes(
-        (w[k] << 4 | (w[k + 1] if k + 1 < maxsym else 0)) for k in range(0, maxsym, 2))
+    if maxsym <= 128:  # direct representation: 4-bit weights
+        tree = bytes([127 + maxsym]) + bytes(
+            (w[k] << 4 | (w[k + 1] if k + 1 < maxsym else 0)) for k in range(0, maxsym, 2))
+    else:  # FSE-compressed weights
+        fw = fse_compress_weights(w[:maxsym])
+        if fw is None:
+            return None
+        tree = bytes([len(fw)]) + fw
     seg = (n + 3) // 4
     streams = []
     for k in range(4):
@@ -507,3 +513,69 @@ def compressed_block_adaptive(T, data: bytes, seqs):
         else:
             sec = (3 << 2 | n << 4).to_bytes(3, "little") + bytes(lits)
     return sec + (sequences_section_adaptive(T, seqs) if seqs else b"\x00")
+
+
+# ---- FSE-compressed Huffman weights (RFC 8878 4.2.1.2), for maxsym > 128 ---
+
+def fse_compress_weights(weights):
+    """Huffman weights (symbols 0 .. n-1) as an FSE stream of accuracy log 6
+    with two interleaved states (FSE_compress_usingCTable order), NCount
+    description first; None when < 2 distinct weights or >= 128 bytes."""
+    n = len(weights)
+    counts = [0] * 12
+    for w in weights:
+        counts[w] += 1
+    if sum(1 for c in counts if c) < 2:
+        return None
+    tl = 6
+    norm = fse_normalize(counts, tl)
+    last = max(s for s in range(12) if counts[s])
+    desc = fse_write_ncount(norm[:last + 1], tl)
+    tt, st = fse_ctable(norm[:last + 1], tl)
+    w = BitWriter()
+
+    def init(sym):
+        find, nbits = tt[sym]
+        nbo = (nbits + (1 << 15)) >> 16
+        v = (nbo << 16) - nbits
+        return st[(v >> nbo) + find]
+
+    def enc(state, sym):
+        find, nbits = tt[sym]
+        nbo = (state + nbits) >> 16
+        w.add(state, nbo)
+        return st[(state >> nbo) + find]
+
+    ip = n
+    if n & 1:
+        s1 = init(weights[ip - 1])
+        s2 = init(weights[ip - 2])
+        s1 = enc(s1, weights[ip - 3])
+        ip -= 3
+        w.flush()
+    else:
+        s2 = init(weights[ip - 1])
+        s1 = init(weights[ip - 2])
+        ip -= 2
+    rest = n - 2
+    if rest & 2:
+        s2 = enc(s2, weights[ip - 1])
+        s1 = enc(s1, weights[ip - 2])
+        ip -= 2
+        w.flush()
+    while ip > 0:
+        s2 = enc(s2, weights[ip - 1])
+        s1 = enc(s1, weights[ip - 2])
+        s2 = enc(s2, weights[ip - 3])
+        s1 = enc(s1, weights[ip - 4])
+        ip -= 4
+        w.flush()
+    w.add(s2, tl)
+    w.flush()
+    w.add(s1, tl)
+    w.add(1, 1)
+    w.flush()
+    if w.nb:
+        w.out.append(w.acc & 0xFF)
+    out = desc + bytes(w.out)
+    return out if len(out) < 128 else None
