@@ -1086,10 +1086,20 @@ __global__ __launch_bounds__(64, HL == 11 ? 4 : 3) void rcdc_zstd_block_kernel(
                 }
                 uint64_t m = __ballot(ok);
                 while (m) {
-                    const int j = __builtin_ctzll(m);
+                    int j = __builtin_ctzll(m);
+                    uint32_t f = rdl(fl, j);
+                    // lazy step: the next position's match, if it reaches at
+                    // least two bytes further, wins (zstd's lazy parsers)
+                    if (stride == 1 && f < 16 && j < 63 && ((m >> (j + 1)) & 1ull)) {
+                        const uint32_t f2 = rdl(fl, j + 1);
+                        if (f2 > f + 1) {
+                            j += 1;
+                            f = f2;
+                        }
+                    }
                     uint32_t pj = base + (uint32_t)j * stride;
                     uint32_t cj = rdl(c, j);
-                    const uint32_t f = rdl(fl, j), bb = rdl(bl, j);
+                    const uint32_t bb = rdl(bl, j);
                     uint32_t len = 4 + f;
                     if (f == 16 && n - pj > 20)
                         len += wave_match_fwd(src + pj + 20, src + cj + 20, n - pj - 20, lim);

@@ -241,3 +241,32 @@ def test_model_huffman_fse_weights(T, nsym, n, alpha):
     assert zr.decompress(fr) == lits
     if len(sec) + 1 <= n:
         assert zr.decompress_pyarrow(fr, n) == lits
+
+
+def test_model_repeat_offsets(T):
+    """Repeat offset codes with a block-local history (RFC 8878 3.1.2.5:
+    offset values 1-3, the LL = 0 shift, history updates): both decoders
+    read them back.  (The device codes offsets literally; this pins the
+    rules for a repeat-aware parse.)"""
+    rng = np.random.default_rng(12)
+    words = [bytes(rng.integers(97, 123, int(rng.integers(2, 9))).astype(np.uint8))
+             for _ in range(400)]
+    rows = b"".join(b"%08d,%s,%d,%s\n" % (i, words[i % 400], (i * 7919) % 100000,
+                                          words[(i * 31) % 400]) for i in range(6000))[:131072]
+    seqs = zm.greedy_sequences_rep(rows)
+    vals = zm.offsets_to_values(seqs)
+    assert any(v <= 3 for _, _, v in vals)
+    # the LL = 0 rules too: force back-to-back matches at repeat offsets
+    seqs2 = [(5, 4, 3), (0, 4, 3 + 0), (2, 5, 7), (0, 6, 3), (0, 4, 6), (1, 4, 3)]
+    fixed = []
+    size = 0
+    for ll, ml, off in seqs2:
+        size += ll
+        fixed.append((ll, ml, min(off, size)))
+        size += ml
+    for d, s in [(rows, seqs), (_synth(fixed, 3, rng), fixed)]:
+        blk = zm.compressed_block_adaptive(T, d, s, reps=True)
+        fr = zm.frame([(2, blk, len(d))], len(d))
+        assert zr.decompress(fr) == d
+        if len(blk) <= len(d):
+            assert zr.decompress_pyarrow(fr, len(d)) == d

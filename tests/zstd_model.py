@@ -47,8 +47,8 @@ class BitWriter:
             self.nb -= 8
 
 
-def _codes(T, ll, ml, off):
-    mlb, ofv = ml - 3, off + 3
+def _codes(T, ll, ml, off, is_value=False):
+    mlb, ofv = ml - 3, (off if is_value else off + 3)
     llc = int(T["llcode"][ll]) if ll < 64 else ll.bit_length() - 1 + 19
     mlc = int(T["mlcode"][mlb]) if mlb < 128 else mlb.bit_length() - 1 + 36
     return llc, mlc, ofv.bit_length() - 1, mlb, ofv
@@ -399,8 +399,9 @@ def fse_ctable(norm, tl):
     return tt, st
 
 
-def encode_sequences_tabs(tabs, seqs, T):
-    """encode_sequences with per-stream tables tabs[name] = (tt, st, tl)."""
+def encode_sequences_tabs(tabs, seqs, T, values=False):
+    """encode_sequences with per-stream tables tabs[name] = (tt, st, tl);
+    values: seqs carry offset values (repeat codes) instead of offsets."""
     w = BitWriter()
 
     def init(name, sym):
@@ -418,7 +419,7 @@ def encode_sequences_tabs(tabs, seqs, T):
         return st[(state >> nbo) + find]
 
     ll, ml, off = seqs[-1]
-    llc, mlc, ofc, mlb, ofv = _codes(T, ll, ml, off)
+    llc, mlc, ofc, mlb, ofv = _codes(T, ll, ml, off, values)
     sml, sof, sll = init("ml", mlc), init("of", ofc), init("ll", llc)
     w.add(ll, T["llbits"][llc])
     w.add(mlb, T["mlbits"][mlc])
@@ -426,7 +427,7 @@ def encode_sequences_tabs(tabs, seqs, T):
     w.add(ofv, ofc)
     w.flush()
     for ll, ml, off in reversed(seqs[:-1]):
-        llc, mlc, ofc, mlb, ofv = _codes(T, ll, ml, off)
+        llc, mlc, ofc, mlb, ofv = _codes(T, ll, ml, off, values)
         sof = enc("of", sof, ofc)
         sml = enc("ml", sml, mlc)
         w.flush()
@@ -454,11 +455,11 @@ def _cost_bits(counts, norm, tl):
     return sum(c * (tl - math.log2(norm[s])) for s, c in enumerate(counts) if c)
 
 
-def sequences_section_adaptive(T, seqs):
+def sequences_section_adaptive(T, seqs, values=False):
     """Sequences section choosing, per stream, predefined or an adaptive
     log-6 table by estimated bits (the device's rule)."""
     k = len(seqs)
-    codes = [_codes(T, *s) for s in seqs]
+    codes = [_codes(T, *s, values) for s in seqs]
     hist = {"ll": [0] * 36, "ml": [0] * 53, "of": [0] * 32}
     for llc, mlc, ofc, _, _ in codes:
         hist["ll"][llc] += 1
@@ -492,11 +493,13 @@ def sequences_section_adaptive(T, seqs):
     else:
         sh = bytes([0xFF]) + (k - 0x7F00).to_bytes(2, "little")
     sh += bytes([modes["ll"] << 6 | modes["of"] << 4 | modes["ml"] << 2])
-    return sh + descs["ll"] + descs["of"] + descs["ml"] + encode_sequences_tabs(tabs, seqs, T)
+    return sh + descs["ll"] + descs["of"] + descs["ml"] + encode_sequences_tabs(tabs, seqs, T,
+                                                                               values)
 
 
-def compressed_block_adaptive(T, data: bytes, seqs):
-    """Huffman literals (where they apply) + adaptive sequences."""
+def compressed_block_adaptive(T, data: bytes, seqs, reps=False):
+    """Huffman literals (where they apply) + adaptive sequences; reps: code
+    offsets with block-local repeat codes (offsets_to_values)."""
     lits = bytearray()
     pos = 0
     for ll, ml, off in seqs:
@@ -512,7 +515,11 @@ def compressed_block_adaptive(T, data: bytes, seqs):
             sec = (1 << 2 | n << 4).to_bytes(2, "little") + bytes(lits)
         else:
             sec = (3 << 2 | n << 4).to_bytes(3, "little") + bytes(lits)
-    return sec + (sequences_section_adaptive(T, seqs) if seqs else b"\x00")
+    if not seqs:
+        return sec + b"\x00"
+    if reps:
+        return sec + sequences_section_adaptive(T, offsets_to_values(seqs), True)
+    return sec + sequences_section_adaptive(T, seqs)
 
 
 # ---- FSE-compressed Huffman weights (RFC 8878 4.2.1.2), for maxsym > 128 ---
@@ -579,3 +586,66 @@ def fse_compress_weights(weights):
         w.out.append(w.acc & 0xFF)
     out = desc + bytes(w.out)
     return out if len(out) < 128 else None
+
+
+# ---- repeat offsets (RFC 8878 3.1.2.5), block-local history ---------------
+
+def offsets_to_values(seqs):
+    """[(ll, ml, off)] -> [(ll, ml, offset_value)] with repeat codes where
+    the offset is one of the repeat history entries set inside this block
+    (entries inherited from earlier blocks are unknown to a block coded in
+    parallel, so never referenced): the device's rule."""
+    rep = [None, None, None]
+    out = []
+    for ll, ml, off in seqs:
+        if ll > 0:
+            if rep[0] == off:
+                v = 1
+            elif rep[1] == off:
+                v, rep = 2, [rep[1], rep[0], rep[2]]
+            elif rep[2] == off:
+                v, rep = 3, [rep[2], rep[0], rep[1]]
+            else:
+                v, rep = off + 3, [off, rep[0], rep[1]]
+        else:
+            if rep[1] == off:
+                v, rep = 1, [rep[1], rep[0], rep[2]]
+            elif rep[2] == off:
+                v, rep = 2, [rep[2], rep[0], rep[1]]
+            elif rep[0] is not None and rep[0] - 1 == off:
+                v, rep = 3, [off, rep[0], rep[1]]
+            else:
+                v, rep = off + 3, [off, rep[0], rep[1]]
+        out.append((ll, ml, v))
+    return out
+
+
+def greedy_sequences_rep(data: bytes):
+    """greedy_sequences with zstd_fast's repeat check first (the last offset
+    at the current position)."""
+    seqs, last, anchor, p, n = [], {}, 0, 0, len(data)
+    rep = None
+    while p + 8 <= n:
+        if rep and p - rep >= 0 and data[p:p + 4] == data[p - rep:p - rep + 4]:
+            m = 4
+            while p + m < n and data[p + m] == data[p - rep + m]:
+                m += 1
+            seqs.append((p - anchor, m, rep))
+            last[data[p:p + 4]] = p
+            p += m
+            anchor = p
+            continue
+        key = data[p:p + 4]
+        c = last.get(key)
+        last[key] = p
+        if c is not None:
+            m = 4
+            while p + m < n and data[c + m] == data[p + m]:
+                m += 1
+            seqs.append((p - anchor, m, p - c))
+            rep = p - c
+            p += m
+            anchor = p
+        else:
+            p += 1
+    return seqs

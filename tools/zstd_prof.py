@@ -1,6 +1,7 @@
 """Device zstd throughput per data kind (rcdc_zstd_compress): 8 GiB of
 chunk-sized blobs (0.5-8 MiB) of random bytes, zeros, C3-style mixed runs,
-and word text; GiB/s by HIP events, ratio, and a decode check of a sample.
+word text and CSV-like rows; GiB/s by HIP events, ratio, and a decode check
+of a sample (and libzstd level 3's ratio on a 16 MiB piece of each kind).
 Run under rocprofv3 --kernel-trace --stats for the per-kernel split."""
 import argparse
 import sys
@@ -17,7 +18,7 @@ from rustic_core_amd.compress import compress_blobs, frame_layout, make_refs  # 
 ap = argparse.ArgumentParser()
 ap.add_argument("--gib", type=float, default=8)
 ap.add_argument("--reps", type=int, default=3)
-ap.add_argument("--kinds", default="random,zeros,mixed,text")
+ap.add_argument("--kinds", default="random,zeros,mixed,text,csv")
 args = ap.parse_args()
 dev = torch.device("cuda:0")
 n = int(args.gib * (1 << 30))
@@ -36,6 +37,9 @@ refs = make_refs(offs, lens, f_offs)
 words = [bytes(rng.integers(97, 123, size=int(rng.integers(2, 9))).astype(np.uint8)) for _ in range(400)]
 text = np.frombuffer(b" ".join(words[int(i)] for i in rng.integers(0, 400, 16 << 20 >> 2)), np.uint8)
 text = torch.from_numpy(text[:16 << 20].copy()).to(dev)
+csv_rows = b"".join(b"%08d,%s,%d,%s\n" % (i, words[i % 400], (i * 7919) % 100000, words[(i * 31) % 400])
+                    for i in range(600000))
+csv_rows = torch.from_numpy(np.frombuffer(csv_rows, np.uint8)[:16 << 20].copy()).to(dev)
 
 
 def fill(kind):
@@ -43,10 +47,11 @@ def fill(kind):
         arena.random_(0, 256)
     elif kind == "zeros":
         arena.zero_()
-    elif kind == "text":
-        t = text.numel()
+    elif kind in ("text", "csv"):
+        src = text if kind == "text" else csv_rows
+        t = src.numel()
         for o in range(0, n, t):
-            arena[o:o + min(t, n - o)] = text[:min(t, n - o)]
+            arena[o:o + min(t, n - o)] = src[:min(t, n - o)]
     elif kind == "mixed":  # C3: random runs 64 KiB-16 MiB, zero runs 4 KiB-16 MiB
         arena.random_(0, 256)
         o = 0
@@ -77,6 +82,9 @@ for kind in args.kinds.split(","):
         d = arena[int(offs[i]):int(offs[i]) + lens[i]].cpu().numpy().tobytes()
         f = frames[int(f_offs[i]):int(f_offs[i]) + int(ln[i])].cpu().numpy().tobytes()
         bad += zr.decompress(f) != d
+    piece = arena[:16 << 20].cpu().numpy().tobytes()
+    ref = sum(len(zr.compress(piece[o:o + (1 << 20)], 3)) for o in range(0, len(piece), 1 << 20))
     print(f"{kind:7s} {len(lens)} blobs {n / 2**30:.1f} GiB: {ms:.2f} ms (wall {wall:.2f}) "
           f"= {n / (ms / 1e3) / 2**30:.1f} GiB/s, ratio {int(ln.sum()) / n:.4f}, "
-          f"decode mismatches {bad}", flush=True)
+          f"libzstd-3 ratio on 16 x 1 MiB {ref / len(piece):.4f}, decode mismatches {bad}",
+          flush=True)
