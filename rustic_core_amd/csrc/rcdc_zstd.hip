@@ -114,15 +114,25 @@ __device__ __forceinline__ uint32_t ld4_lo(const uint8_t *p, const uint8_t *lo) 
     return v;
 }
 
+// Positions are keyed on their first `key` bytes (4 or 6) and matches are at
+// least that long (zstd's fast levels use 5-6: on structured data shorter
+// matches cost more sequence bits than the literals they replace; 6-byte keys
+// pay only with enough buckets).
+__device__ __forceinline__ uint64_t key48(uint32_t w, uint32_t w2, uint32_t key) {
+    return key == 6 ? (uint64_t)w | (uint64_t)(w2 & 0xFFFFu) << 32 : (uint64_t)w;
+}
+
 template <int HL>
-__device__ __forceinline__ uint32_t zhash(uint32_t w) {
-    return (w * 2654435761u) >> (32 - HL);
+__device__ __forceinline__ uint32_t zhash(uint64_t k) {
+    return (uint32_t)((k * 0x9E3779B97F4A7C15ull) >> (64 - HL));
 }
 
 // Table entry: position (17 bits) | a 15-bit tag of its 4 bytes << 17, so a
 // candidate touches memory only when its tag agrees (random data: ~2^-15).
 // A position is at most kZstdBlock - 8, so the empty entry (all ones) is none.
-__device__ __forceinline__ uint32_t ztag(uint32_t w) { return (w * 0x85EBCA77u) >> 17; }
+__device__ __forceinline__ uint32_t ztag(uint64_t k) {
+    return (uint32_t)((k * 0xC2B2AE3D27D4EB4Full) >> 49);
+}
 constexpr uint32_t kZstdPosMask = (1u << 17) - 1u;
 
 // Equal bytes of a[0..) and b[0..), at most maxlen (wave-uniform result).
@@ -210,7 +220,8 @@ __device__ __forceinline__ uint32_t last_eq16(uint4 a, uint4 b) {
          : x0 ? 12u + ((uint32_t)__builtin_clz(x0) >> 3) : 16u;
 }
 
-// sequence record: literal length | match length << 20 | offset << 40
+// sequence record: literal length | match length << 20 | offset value << 40
+// (a repeat code 1-3, or offset + 3)
 __device__ __forceinline__ uint64_t seq_pack(uint32_t ll, uint32_t ml, uint32_t off) {
     return (uint64_t)ll | (uint64_t)ml << 20 | (uint64_t)off << 40;
 }
@@ -223,7 +234,7 @@ __device__ __forceinline__ SeqCodes seq_codes(uint64_t s, const ZstdTables &T) {
     SeqCodes c;
     c.ll = (uint32_t)(s & 0xFFFFF);
     const uint32_t ml = (uint32_t)((s >> 20) & 0xFFFFF);
-    c.ofv = (uint32_t)(s >> 40) + 3u;  // offset_value: never a repeat code
+    c.ofv = (uint32_t)(s >> 40);
     c.mlb = ml - 3u;
     c.llc = c.ll < 64 ? T.llcode[c.ll] : highbit(c.ll) + 19u;
     c.mlc = c.mlb < 128 ? T.mlcode[c.mlb] : highbit(c.mlb) + 36u;
@@ -991,7 +1002,7 @@ __global__ __launch_bounds__(64, HL == 11 ? 4 : 3) void rcdc_zstd_block_kernel(
     const uint8_t *__restrict__ in, const ZstdBlob *__restrict__ blobs,
     const ZstdBlk *__restrict__ blks, uint32_t nblk, const ZstdTables *__restrict__ tabs,
     uint8_t *__restrict__ slots, uint64_t *__restrict__ seqbuf, uint2 *__restrict__ res,
-    uint32_t dbg) {
+    uint32_t dbg, uint32_t key) {
     __shared__ uint32_t table[1 << HL];
     __shared__ ZstdTables T;
     const uint32_t lane = lane_id();
@@ -1022,7 +1033,7 @@ __global__ __launch_bounds__(64, HL == 11 ? 4 : 3) void rcdc_zstd_block_kernel(
                 continue;
             }
             // first block of the frame: one literal, then an offset-1 match
-            if (lane == 0) seqs[0] = seq_pack(1, n - 1, 1);
+            if (lane == 0) seqs[0] = seq_pack(1, n - 1, 1 + 3);
             nseq = 1;
             anchor = n;
             matched = n - 1;
@@ -1031,6 +1042,7 @@ __global__ __launch_bounds__(64, HL == 11 ? 4 : 3) void rcdc_zstd_block_kernel(
             __builtin_amdgcn_wave_barrier();
             const uint32_t ilimit = n - 8;  // last position a match may start at
             uint32_t base = 0;
+            uint32_t rep0 = 0, rep1 = 0, rep2 = 0;  // repeat history set in this block (0: unknown)
             while (base <= ilimit) {
                 uint32_t stride = 1u + ((base - anchor) >> kZstdAccelShift);
                 if (stride > kZstdMaxStride) stride = kZstdMaxStride;
@@ -1039,8 +1051,9 @@ __global__ __launch_bounds__(64, HL == 11 ? 4 : 3) void rcdc_zstd_block_kernel(
                 uint32_t w = 0, h = 0, tg = 0, c = kZstdNone;
                 if (act) {
                     w = ld4(src + p);
-                    h = zhash<HL>(w);
-                    tg = ztag(w);
+                    const uint64_t k6 = key48(w, key == 6 ? ld4(src + p + 4) : 0u, key);
+                    h = zhash<HL>(k6);
+                    tg = ztag(k6);
                     const uint32_t e = table[h];
                     if (e != kZstdNone && (e >> 17) == tg) c = e & kZstdPosMask;
                 }
@@ -1080,7 +1093,7 @@ __global__ __launch_bounds__(64, HL == 11 ? 4 : 3) void rcdc_zstd_block_kernel(
                         bl = last_eq16(ld16(src + p - 16), ld16(src + c - 16));
                         if (bl > limb) bl = limb;
                     }
-                    ok = wc == w;
+                    ok = wc == w && 4 + fl >= key;
                     if (ok && c < 16)
                         while (bl < limb && src[p - 1 - bl] == src[c - 1 - bl]) bl++;
                 }
@@ -1110,7 +1123,52 @@ __global__ __launch_bounds__(64, HL == 11 ? 4 : 3) void rcdc_zstd_block_kernel(
                     pj -= bk;
                     cj -= bk;
                     len += bk;
-                    if (lane == 0) seqs[nseq] = seq_pack(pj - anchor, len, pj - cj);
+                    // offset value: a repeat code when the offset is in the
+                    // block-local history (RFC 8878 3.1.2.5; entries from
+                    // earlier blocks are unknown here: 0), else offset + 3
+                    const uint32_t off = pj - cj, ll = pj - anchor;
+                    uint32_t ofv;
+                    if (ll) {
+                        if (off == rep0) {
+                            ofv = 1;
+                        } else if (off == rep1) {
+                            ofv = 2;
+                            rep1 = rep0;
+                            rep0 = off;
+                        } else if (off == rep2) {
+                            ofv = 3;
+                            rep2 = rep1;
+                            rep1 = rep0;
+                            rep0 = off;
+                        } else {
+                            ofv = off + 3;
+                            rep2 = rep1;
+                            rep1 = rep0;
+                            rep0 = off;
+                        }
+                    } else {
+                        if (off == rep1) {
+                            ofv = 1;
+                            rep1 = rep0;
+                            rep0 = off;
+                        } else if (off == rep2) {
+                            ofv = 2;
+                            rep2 = rep1;
+                            rep1 = rep0;
+                            rep0 = off;
+                        } else if (rep0 && off == rep0 - 1) {
+                            ofv = 3;
+                            rep2 = rep1;
+                            rep1 = rep0;
+                            rep0 = off;
+                        } else {
+                            ofv = off + 3;
+                            rep2 = rep1;
+                            rep1 = rep0;
+                            rep0 = off;
+                        }
+                    }
+                    if (lane == 0) seqs[nseq] = seq_pack(ll, len, ofv);
                     nseq++;
                     matched += len;
                     anchor = pj + len;
@@ -1129,12 +1187,35 @@ __global__ __launch_bounds__(64, HL == 11 ? 4 : 3) void rcdc_zstd_block_kernel(
                 atomicAdd(&g_zstd_prof[5], (unsigned long long)nseq);
             }
         }
-        if (nseq == 0 || (dbg & 1u)) {  // dbg bit 0: measure the parse alone
+        if (dbg & 1u) {  // dbg bit 0: measure the parse alone
             if (lane == 0) res[b] = make_uint2(kZstdTypeRaw, n);
             continue;
         }
+        if (nseq == 0) {
+            // no match: a literals-only block can still pay (Huffman) when the
+            // bytes are skewed; an order-0 entropy sample of the first 4 KiB
+            // decides before any copy (random blocks end here)
+            uint32_t *hs = table;
+            for (uint32_t i = lane; i < 256; i += 64) hs[i] = 0;
+            wave_lds_sync();
+            const uint32_t ns = (n < 4096 ? n : 4096u) & ~15u;  // >= 16; k + 16 <= n
+            for (uint32_t k = lane * 16u; k < ns; k += 1024) {
+                const uint4 v = ld16(src + k);
+                for (uint32_t j = 0; j < 16; j++) atomicAdd(&hs[byte_of(v, j)], 1u);
+            }
+            wave_lds_sync();
+            float hb = 0.f;
+            for (uint32_t i = lane; i < 256; i += 64)
+                if (hs[i]) hb += (float)hs[i] * __log2f((float)ns / (float)hs[i]);
+            for (int d = 32; d >= 1; d >>= 1) hb += __shfl_xor(hb, d);
+            if (hb > 7.5f * (float)ns) {
+                if (lane == 0) res[b] = make_uint2(kZstdTypeRaw, n);
+                continue;
+            }
+        }
         const uint32_t lits = n - matched;
-        const uint32_t sh = (nseq < 128 ? 1u : nseq < 0x7F00 ? 2u : 3u) + 1u;
+        // Number_of_Sequences bytes, + the modes byte when there are sequences
+        const uint32_t sh = nseq == 0 ? 1u : (nseq < 128 ? 1u : nseq < 0x7F00 ? 2u : 3u) + 1u;
         // zstd keeps a compressed block only if it saves more than minGain
         const uint32_t min_gain = (n >> 6) + 2u;
         const uint32_t keep_below = n - min_gain;
@@ -1179,9 +1260,9 @@ __global__ __launch_bounds__(64, HL == 11 ? 4 : 3) void rcdc_zstd_block_kernel(
         }
         __threadfence_block();
         const uint32_t lsz = encode_literals(lbuf, lits, slot, table);
-        const uint32_t bs0 = lsz + sh - 1;  // after Number_of_Sequences
-        uint32_t bsz = kZstdNone;
-        if (bs0 + 1 < keep_below)
+        const uint32_t bs0 = nseq ? lsz + sh - 1 : lsz + 1;  // after Number_of_Sequences
+        uint32_t bsz = nseq ? kZstdNone : 0u;
+        if (nseq && bs0 + 1 < keep_below)
             bsz = wave_fse_sequences(seqs, nseq, T, R, table, slot + bs0, keep_below - bs0);
         if (prof) {
             t3 = wall_clock64();
@@ -1300,6 +1381,12 @@ void zstd_prof_dump() {
 
 // RCDC_ZSTD_HLOG: 11 (default; 8 KiB table, 16 waves per CU) or 12 (16 KiB,
 // 8 waves per CU: more buckets, better ratio on text, fewer waves)
+// RCDC_ZSTD_KEY: key bytes / minimum match, 4 or 6 (default below)
+static uint32_t zstd_key() {
+    static const uint32_t k = getenv("RCDC_ZSTD_KEY") ? (uint32_t)atoi(getenv("RCDC_ZSTD_KEY")) : 4u;
+    return k == 6 ? 6u : 4u;
+}
+
 static int zstd_hlog() {
     static const int h = getenv("RCDC_ZSTD_HLOG") ? atoi(getenv("RCDC_ZSTD_HLOG")) : 11;
     return h == 11 ? 11 : 12;
@@ -1317,10 +1404,10 @@ hipError_t launch_zstd(const uint8_t *in, uint8_t *out, const ZstdBlob *blobs, u
     if (g) {
         if (zstd_hlog() == 11)
             hipLaunchKernelGGL(rcdc_zstd_block_kernel<11>, dim3(g), dim3(64), 0, stream, in, blobs,
-                               blks, nblk, tabs, slots, seqbuf, res, dbg);
+                               blks, nblk, tabs, slots, seqbuf, res, dbg, zstd_key());
         else
             hipLaunchKernelGGL(rcdc_zstd_block_kernel<12>, dim3(g), dim3(64), 0, stream, in, blobs,
-                               blks, nblk, tabs, slots, seqbuf, res, dbg);
+                               blks, nblk, tabs, slots, seqbuf, res, dbg, zstd_key());
     }
     hipLaunchKernelGGL(rcdc_zstd_frame_kernel, dim3((nblobs + 255) / 256), dim3(256), 0, stream,
                        blobs, nblobs, res, bpos, out, out_lens);
