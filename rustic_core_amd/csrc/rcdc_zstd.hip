@@ -1051,7 +1051,8 @@ __global__ __launch_bounds__(64, HL == 11 ? 4 : 3) void rcdc_zstd_block_kernel(
                 uint32_t w = 0, h = 0, tg = 0, c = kZstdNone;
                 if (act) {
                     w = ld4(src + p);
-                    const uint64_t k6 = key48(w, key == 6 ? ld4(src + p + 4) : 0u, key);
+                    const uint64_t k6 = key48(w, (key & 0xFFu) == 6 ? ld4(src + p + 4) : 0u,
+                                              key & 0xFFu);
                     h = zhash<HL>(k6);
                     tg = ztag(k6);
                     const uint32_t e = table[h];
@@ -1093,7 +1094,7 @@ __global__ __launch_bounds__(64, HL == 11 ? 4 : 3) void rcdc_zstd_block_kernel(
                         bl = last_eq16(ld16(src + p - 16), ld16(src + c - 16));
                         if (bl > limb) bl = limb;
                     }
-                    ok = wc == w && 4 + fl >= key;
+                    ok = wc == w && 4 + fl >= (key & 0xFFu);
                     if (ok && c < 16)
                         while (bl < limb && src[p - 1 - bl] == src[c - 1 - bl]) bl++;
                 }
@@ -1128,7 +1129,9 @@ __global__ __launch_bounds__(64, HL == 11 ? 4 : 3) void rcdc_zstd_block_kernel(
                     // earlier blocks are unknown here: 0), else offset + 3
                     const uint32_t off = pj - cj, ll = pj - anchor;
                     uint32_t ofv;
-                    if (ll) {
+                    if (!(key & 0x100u)) {  // RCDC_ZSTD_REP=0 (A/B): literal offsets only
+                        ofv = off + 3;
+                    } else if (ll) {
                         if (off == rep0) {
                             ofv = 1;
                         } else if (off == rep1) {
@@ -1382,9 +1385,11 @@ void zstd_prof_dump() {
 // RCDC_ZSTD_HLOG: 11 (default; 8 KiB table, 16 waves per CU) or 12 (16 KiB,
 // 8 waves per CU: more buckets, better ratio on text, fewer waves)
 // RCDC_ZSTD_KEY: key bytes / minimum match, 4 or 6 (default below)
+// | 0x100: repeat codes on (RCDC_ZSTD_REP=0 turns them off, for A/B runs)
 static uint32_t zstd_key() {
     static const uint32_t k = getenv("RCDC_ZSTD_KEY") ? (uint32_t)atoi(getenv("RCDC_ZSTD_KEY")) : 4u;
-    return k == 6 ? 6u : 4u;
+    static const bool rep = !(getenv("RCDC_ZSTD_REP") && atoi(getenv("RCDC_ZSTD_REP")) == 0);
+    return (k == 6 ? 6u : 4u) | (rep ? 0x100u : 0u);
 }
 
 static int zstd_hlog() {

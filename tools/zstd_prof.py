@@ -1,6 +1,6 @@
 """Device zstd throughput per data kind (rcdc_zstd_compress): 8 GiB of
 chunk-sized blobs (0.5-8 MiB) of random bytes, zeros, C3-style mixed runs,
-word text and CSV-like rows; GiB/s by HIP events, ratio, and a decode check
+word text, CSV-like rows and code-like lines; GiB/s by HIP events, ratio, and a decode check
 of a sample (and libzstd level 3's ratio on a 16 MiB piece of each kind).
 Run under rocprofv3 --kernel-trace --stats for the per-kernel split."""
 import argparse
@@ -18,7 +18,7 @@ from rustic_core_amd.compress import compress_blobs, frame_layout, make_refs  # 
 ap = argparse.ArgumentParser()
 ap.add_argument("--gib", type=float, default=8)
 ap.add_argument("--reps", type=int, default=3)
-ap.add_argument("--kinds", default="random,zeros,mixed,text,csv")
+ap.add_argument("--kinds", default="random,zeros,mixed,text,csv,code")
 args = ap.parse_args()
 dev = torch.device("cuda:0")
 n = int(args.gib * (1 << 30))
@@ -40,6 +40,9 @@ text = torch.from_numpy(text[:16 << 20].copy()).to(dev)
 csv_rows = b"".join(b"%08d,%s,%d,%s\n" % (i, words[i % 400], (i * 7919) % 100000, words[(i * 31) % 400])
                     for i in range(600000))
 csv_rows = torch.from_numpy(np.frombuffer(csv_rows, np.uint8)[:16 << 20].copy()).to(dev)
+code_lines = b"".join(b"    x_%d = foo(%s, %d) + bar[%d];\n" % (i % 97, words[i % 50], i, (i * 13) % 1000)
+                      for i in range(600000))
+code_lines = torch.from_numpy(np.frombuffer(code_lines, np.uint8)[:16 << 20].copy()).to(dev)
 
 
 def fill(kind):
@@ -47,8 +50,8 @@ def fill(kind):
         arena.random_(0, 256)
     elif kind == "zeros":
         arena.zero_()
-    elif kind in ("text", "csv"):
-        src = text if kind == "text" else csv_rows
+    elif kind in ("text", "csv", "code"):
+        src = {"text": text, "csv": csv_rows, "code": code_lines}[kind]
         t = src.numel()
         for o in range(0, n, t):
             arena[o:o + min(t, n - o)] = src[:min(t, n - o)]
