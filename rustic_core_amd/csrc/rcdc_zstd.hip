@@ -1038,6 +1038,30 @@ __global__ __launch_bounds__(64, HL == 11 ? 4 : 3) void rcdc_zstd_block_kernel(
             anchor = n;
             matched = n - 1;
         } else {
+            // incompressible blocks (random runs, already-compressed files):
+            // order-0 entropy of four 1 KiB windows spread over the block;
+            // all near 8 bits per byte -> stored raw without a parse (the
+            // plug-in estimate of random bytes over 4 KiB is ~7.95)
+            if (n >= 8192) {
+                uint32_t *hs = table;
+                for (uint32_t i = lane; i < 256; i += 64) hs[i] = 0;
+                wave_lds_sync();
+                const uint32_t w0 = lane >> 4, k = (lane & 15u) * 64u;  // 16 lanes per window
+                const uint32_t base_w = ((n / 4) * w0) & ~15u;
+                for (uint32_t j = 0; j < 64; j += 16) {
+                    const uint4 v = ld16(src + base_w + k + j);
+                    for (uint32_t q = 0; q < 16; q++) atomicAdd(&hs[byte_of(v, q)], 1u);
+                }
+                wave_lds_sync();
+                float hb = 0.f;
+                for (uint32_t i = lane; i < 256; i += 64)
+                    if (hs[i]) hb += (float)hs[i] * __log2f(4096.f / (float)hs[i]);
+                for (int d = 32; d >= 1; d >>= 1) hb += __shfl_xor(hb, d);
+                if (hb > 7.9f * 4096.f) {
+                    if (lane == 0) res[b] = make_uint2(kZstdTypeRaw, n);
+                    continue;
+                }
+            }
             for (uint32_t i = lane; i < (1u << HL); i += 64) table[i] = kZstdNone;
             __builtin_amdgcn_wave_barrier();
             const uint32_t ilimit = n - 8;  // last position a match may start at
