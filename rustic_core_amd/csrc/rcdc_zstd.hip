@@ -974,19 +974,29 @@ __device__ uint32_t encode_literals(const uint8_t *lbuf, uint32_t nl, uint8_t *o
     return h + nl;
 }
 
-// All n bytes of the block equal to its first?  (wave-uniform; 1 KiB per
-// wave round, the first round decides most non-RLE blocks)
+// All n bytes of the block equal to its first?  (wave-uniform; 4 KiB per
+// wave round, four independent 16-byte loads per lane in flight; the first
+// round decides most non-RLE blocks)
 __device__ bool wave_is_rle(const uint8_t *src, uint32_t n, const uint8_t *lim) {
     const uint32_t lane = lane_id();
     const uint32_t b4 = (uint32_t)src[0] * 0x01010101u;
-    for (uint32_t o = 0; o < n; o += 1024) {
-        const uint32_t q = o + lane * 16u;
+    for (uint32_t o = 0; o < n; o += 4096) {
         uint32_t x = 0;
-        if (q + 16 <= n) {
-            const uint4 v = ld16(src + q);
-            x = (v.x ^ b4) | (v.y ^ b4) | (v.z ^ b4) | (v.w ^ b4);
+        if (o + 4096 <= n) {
+            uint4 v[4];
+#pragma unroll
+            for (int u = 0; u < 4; u++) v[u] = ld16(src + o + u * 1024u + lane * 16u);
+#pragma unroll
+            for (int u = 0; u < 4; u++) x |= (v[u].x ^ b4) | (v[u].y ^ b4) | (v[u].z ^ b4) | (v[u].w ^ b4);
         } else {
-            for (uint32_t k = q; k < n && k < q + 16; k++) x |= src[k] ^ (b4 & 0xFF);
+            for (uint32_t q = o + lane * 16u; q < n; q += 1024) {
+                if (q + 16 <= n) {
+                    const uint4 v = ld16(src + q);
+                    x |= (v.x ^ b4) | (v.y ^ b4) | (v.z ^ b4) | (v.w ^ b4);
+                } else {
+                    for (uint32_t k = q; k < n; k++) x |= src[k] ^ (b4 & 0xFF);
+                }
+            }
         }
         if (__ballot(x != 0)) return false;
     }
@@ -1354,6 +1364,8 @@ __global__ void rcdc_zstd_frame_kernel(const ZstdBlob *__restrict__ blobs, uint3
 }
 
 // A workgroup per block: 3-byte block header, then the content.
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+template <bool NT>
 __global__ __launch_bounds__(kZstdCopyThreads) void rcdc_zstd_copy_kernel(
     const uint8_t *__restrict__ in, const ZstdBlob *__restrict__ blobs,
     const ZstdBlk *__restrict__ blks, const uint2 *__restrict__ res,
@@ -1381,15 +1393,47 @@ __global__ __launch_bounds__(kZstdCopyThreads) void rcdc_zstd_copy_kernel(
     o += head;
     src += head;
     const uint32_t rest = n - head, n16 = rest >> 4;
-    for (uint32_t q = t; q < n16; q += kZstdCopyThreads) {
-        const uint8_t *s = src + 16u * q;
-        uint4 v;
-        v.x = ld4(s);
-        v.y = ld4(s + 4);
-        v.z = ld4(s + 8);
-        v.w = ld4(s + 12);
-        *(uint4 *)(o + 16u * q) = v;
+    // src's byte offset within a dword is the same for every thread: one
+    // dwordx4 from the dword-aligned base plus the next dword (which holds
+    // byte 15 when misaligned, so nothing past the content is touched)
+    const uint32_t sh = ((uint32_t)(uintptr_t)src & 3u) * 8u;
+    const uint32_t *w = (const uint32_t *)((uintptr_t)src & ~(uintptr_t)3);
+    auto piece = [&](uint32_t q) {
+        uint4 a;
+        if (NT) {
+            const u32x4 x = __builtin_nontemporal_load((const u32x4 *)(w + 4u * q));
+            a = make_uint4(x.x, x.y, x.z, x.w);
+        } else {
+            a = *(const uint4 *)(w + 4u * q);
+        }
+        uint4 v = a;
+        if (sh) {
+            const uint32_t e = w[4u * q + 4u];
+            v = make_uint4(__builtin_amdgcn_alignbit(a.y, a.x, sh),
+                           __builtin_amdgcn_alignbit(a.z, a.y, sh),
+                           __builtin_amdgcn_alignbit(a.w, a.z, sh),
+                           __builtin_amdgcn_alignbit(e, a.w, sh));
+        }
+        return v;
+    };
+    auto put = [&](uint32_t q, uint4 v) {
+        if (NT) {
+            u32x4 x = {v.x, v.y, v.z, v.w};
+            __builtin_nontemporal_store(x, (u32x4 *)(o + 16u * q));
+        } else {
+            *(uint4 *)(o + 16u * q) = v;
+        }
+    };
+    constexpr uint32_t U = 4, S = U * kZstdCopyThreads;
+    uint32_t q0 = 0;
+    for (; q0 + S <= n16; q0 += S) {
+        uint4 v[U];
+#pragma unroll
+        for (uint32_t u = 0; u < U; u++) v[u] = piece(q0 + u * kZstdCopyThreads + t);
+#pragma unroll
+        for (uint32_t u = 0; u < U; u++) put(q0 + u * kZstdCopyThreads + t, v[u]);
     }
+    for (uint32_t q = q0 + t; q < n16; q += kZstdCopyThreads) put(q, piece(q));
     const uint32_t d = n16 * 16u;
     if (t < rest - d) o[d + t] = src[d + t];
 }
@@ -1440,9 +1484,11 @@ hipError_t launch_zstd(const uint8_t *in, uint8_t *out, const ZstdBlob *blobs, u
     }
     hipLaunchKernelGGL(rcdc_zstd_frame_kernel, dim3((nblobs + 255) / 256), dim3(256), 0, stream,
                        blobs, nblobs, res, bpos, out, out_lens);
+    static const bool nt = !(getenv("RCDC_ZSTD_NT") && atoi(getenv("RCDC_ZSTD_NT")) == 0);
     if (nblk)
-        hipLaunchKernelGGL(rcdc_zstd_copy_kernel, dim3(nblk), dim3(kZstdCopyThreads), 0, stream,
-                           in, blobs, blks, res, bpos, slots, out);
+        hipLaunchKernelGGL(nt ? rcdc_zstd_copy_kernel<true> : rcdc_zstd_copy_kernel<false>,
+                           dim3(nblk), dim3(kZstdCopyThreads), 0, stream, in, blobs, blks, res,
+                           bpos, slots, out);
     return hipGetLastError();
 }
 

@@ -70,7 +70,8 @@ for kind in args.kinds.split(","):
     fill(kind)
     torch.cuda.synchronize()
     st = torch.cuda.current_stream().cuda_stream
-    ln = compress_blobs(ctx, arena.data_ptr(), refs, frames.data_ptr(), 0, st)
+    for _ in range(3):  # warm-up (the first kind otherwise runs at a lower clock)
+        ln = compress_blobs(ctx, arena.data_ptr(), refs, frames.data_ptr(), 0, st)
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
     e0.record()
