@@ -1297,6 +1297,7 @@ __global__ __launch_bounds__(64, HL == 11 ? 4 : 3) void rcdc_zstd_block_kernel(
         }
         __threadfence_block();
         const uint32_t lsz = encode_literals(lbuf, lits, slot, table);
+        if (prof && lane == 0) atomicAdd(&g_zstd_prof[6], wall_clock64() - t2);
         const uint32_t bs0 = nseq ? lsz + sh - 1 : lsz + 1;  // after Number_of_Sequences
         uint32_t bsz = nseq ? kZstdNone : 0u;
         if (nseq && bs0 + 1 < keep_below)
@@ -1443,9 +1444,9 @@ namespace rcdc {
 void zstd_prof_dump() {
     unsigned long long h[8];
     if (hipMemcpyFromSymbol(h, HIP_SYMBOL(g_zstd_prof), sizeof h) != hipSuccess) return;
-    fprintf(stderr, "rcdc zstd phases (wave-ms, 100 MHz clock): rle %.1f parse %.1f fse %.1f "
-            "litcopy %.1f; blocks %llu sequences %llu\n", h[0] / 1e5, h[1] / 1e5, h[2] / 1e5,
-            h[3] / 1e5, h[4], h[5]);
+    fprintf(stderr, "rcdc zstd phases (wave-ms, 100 MHz clock): rle %.1f parse %.1f "
+            "literals+sequences %.1f (literals %.1f) tail %.1f; blocks %llu sequences %llu\n",
+            h[0] / 1e5, h[1] / 1e5, h[2] / 1e5, h[6] / 1e5, h[3] / 1e5, h[4], h[5]);
     memset(h, 0, sizeof h);
     (void)hipMemcpyToSymbol(HIP_SYMBOL(g_zstd_prof), h, sizeof h);
 }
