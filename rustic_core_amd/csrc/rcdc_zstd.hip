@@ -518,7 +518,22 @@ __device__ uint32_t wave_fse_sequences(const uint64_t *seqs, uint32_t nseq, cons
     uint8_t *const out0 = out;
     out += o;
     cap -= o;
-    uint32_t sLL = 0, sML = 0, sOF = 0;
+    // the three state chains run on lanes 0 (OF), 1 (ML), 2 (LL) in VALU over
+    // LDS copies of the tables (the scalar unit, shared by the CU's waves, is
+    // the parse's bottleneck): buf[256, 832) tables, [832, 1024) the round's
+    // symbol codes, [1024, 1216) (the histograms, done) the state fields
+    uint32_t *ctN = buf + 256, *ctF = buf + 448, *ctS = buf + 640, *csym = buf + 832,
+             *cfld = buf + 1024;
+    ctN[lane] = R.ofN;
+    ctN[64 + lane] = R.mlN;
+    ctN[128 + lane] = R.llN;
+    ctF[lane] = R.ofF;
+    ctF[64 + lane] = R.mlF;
+    ctF[128 + lane] = R.llF;
+    ctS[lane] = R.ofS;
+    ctS[64 + lane] = R.mlS;
+    ctS[128 + lane] = R.llS;
+    uint32_t sch = 0;  // lane k < 3: chain k's state
     uint32_t bitpos = 0, wbase = 0;  // bits written; bit index of buf[0] (multiple of 32)
     if (lane == 0) buf[0] = 0;
     wave_lds_sync();
@@ -528,22 +543,39 @@ __device__ uint32_t wave_fse_sequences(const uint64_t *seqs, uint32_t nseq, cons
         SeqCodes c{0, 0, 0, 0, 0, 0};
         if (val) c = seq_codes(seqs[hi - lane], T);
         const uint32_t nll = val ? T.llbits[c.llc] : 0u, nml = val ? T.mlbits[c.mlc] : 0u;
-        uint32_t fOF = 0, fML = 0, fLL = 0;
-        for (uint32_t L = 0; L < cnt; L++) {
-            const uint32_t a = rdl(c.llc, (int)L), bm = rdl(c.mlc, (int)L), o = rdl(c.ofc, (int)L);
-            uint32_t f1 = 0, f2 = 0, f3 = 0;
-            if ((uint64_t)(hi - L) == (uint64_t)nseq - 1) {
-                sML = fse_init_s(R.mlF, R.mlN, R.mlS, bm);
-                sOF = fse_init_s(R.ofF, R.ofN, R.ofS, o);
-                sLL = fse_init_s(R.llF, R.llN, R.llS, a);
-            } else {
-                sOF = fse_enc_s(R.ofF, R.ofN, R.ofS, o, sOF, f1);
-                sML = fse_enc_s(R.mlF, R.mlN, R.mlS, bm, sML, f2);
-                sLL = fse_enc_s(R.llF, R.llN, R.llS, a, sLL, f3);
+        if (val) {
+            csym[3 * lane] = c.ofc;
+            csym[3 * lane + 1] = c.mlc;
+            csym[3 * lane + 2] = c.llc;
+        }
+        wave_lds_sync();
+        if (lane < 3) {
+            // FSE_initCState2 from the last sequence, then FSE_encodeSymbol
+            const uint32_t tb = lane * 64u;
+            uint32_t L = 0;
+            if ((uint64_t)hi == (uint64_t)nseq - 1) {
+                const uint32_t sy = csym[lane], nb = ctN[tb + sy];
+                const uint32_t nbo = (nb + (1u << 15)) >> 16;
+                const uint32_t v = (nbo << 16) - nb;
+                sch = ctS[tb + (uint32_t)((int32_t)(v >> nbo) + (int32_t)ctF[tb + sy])];
+                cfld[lane] = 0;
+                L = 1;
             }
-            fOF = wl(f1, (int)L, fOF);
-            fML = wl(f2, (int)L, fML);
-            fLL = wl(f3, (int)L, fLL);
+            for (; L < cnt; L++) {
+                const uint32_t sy = csym[3 * L + lane];
+                const uint32_t nb = ctN[tb + sy];
+                const int32_t f = (int32_t)ctF[tb + sy];
+                const uint32_t nbo = (sch + nb) >> 16;
+                cfld[3 * L + lane] = (sch & ((1u << nbo) - 1u)) | nbo << 16;
+                sch = ctS[tb + (uint32_t)((int32_t)(sch >> nbo) + f)];
+            }
+        }
+        wave_lds_sync();
+        uint32_t fOF = 0, fML = 0, fLL = 0;
+        if (val) {
+            fOF = cfld[3 * lane];
+            fML = cfld[3 * lane + 1];
+            fLL = cfld[3 * lane + 2];
         }
         const uint32_t total =
             val ? (fOF >> 16) + (fML >> 16) + (fLL >> 16) + nll + nml + c.ofc : 0u;
@@ -590,6 +622,7 @@ __device__ uint32_t wave_fse_sequences(const uint64_t *seqs, uint32_t nseq, cons
     }
     // final states (FSE_flushCState: ML, OF, LL) and the end mark
     const uint32_t start = bitpos - wbase;
+    const uint32_t sOF = rdl(sch, 0), sML = rdl(sch, 1), sLL = rdl(sch, 2);
     if (lane == 0) {
         buf[1] = 0;
         put_bits(buf, start, sML, tml);
