@@ -68,32 +68,35 @@ __device__ __forceinline__ uint32_t highbit(uint32_t v) { return 31u - (uint32_t
 
 // 4 bytes at any alignment from the aligned dwords that hold them (a dword
 // that holds a readable byte is readable: allocations are 4-byte granular).
+// Branch-free: when aligned, alignbit(hi, lo, 0) is lo whatever hi is, so hi
+// is loaded from the dword itself (no exec-masked load, no scalar unit work);
+// the aligned pointer comes from p by arithmetic so the loads stay global.
 __device__ __forceinline__ uint32_t ld4(const uint8_t *p) {
-    const uintptr_t a = (uintptr_t)p & ~(uintptr_t)3;
-    const uint32_t sh = ((uint32_t)(uintptr_t)p & 3u) * 8u;
-    const uint32_t lo = *(const uint32_t *)a;
-    const uint32_t hi = sh ? *(const uint32_t *)(a + 4) : 0u;
-    return __builtin_amdgcn_alignbit(hi, lo, sh);
+    const uint32_t b = (uint32_t)(uintptr_t)p & 3u;
+    const uint32_t *w = (const uint32_t *)(p - b);
+    const uint32_t lo = w[0];
+    const uint32_t hi = w[b ? 1 : 0];
+    return __builtin_amdgcn_alignbit(hi, lo, b * 8u);
 }
 
 // 16 bytes at any alignment (5 aligned dwords when misaligned).
 __device__ __forceinline__ uint4 ld16(const uint8_t *p) {
-    const uintptr_t a = (uintptr_t)p & ~(uintptr_t)3;
-    const uint32_t sh = ((uint32_t)(uintptr_t)p & 3u) * 8u;
-    const uint32_t *w = (const uint32_t *)a;
+    const uint32_t b = (uint32_t)(uintptr_t)p & 3u, sh = b * 8u;
+    const uint32_t *w = (const uint32_t *)(p - b);
     const uint32_t w0 = w[0], w1 = w[1], w2 = w[2], w3 = w[3];
-    const uint32_t w4 = sh ? w[4] : 0u;
+    const uint32_t w4 = w[b ? 4 : 3];
     return make_uint4(__builtin_amdgcn_alignbit(w1, w0, sh), __builtin_amdgcn_alignbit(w2, w1, sh),
                       __builtin_amdgcn_alignbit(w3, w2, sh), __builtin_amdgcn_alignbit(w4, w3, sh));
 }
 
-// First differing byte of two 16-byte groups (16 if equal).
+// First differing byte of two 16-byte groups (16 if equal); branch-free: a
+// zero word counts as 128 bits, the first differing bit is the minimum.
 __device__ __forceinline__ uint32_t first_diff16(uint4 a, uint4 b) {
     const uint32_t x0 = a.x ^ b.x, x1 = a.y ^ b.y, x2 = a.z ^ b.z, x3 = a.w ^ b.w;
-    return x0 ? (uint32_t)__builtin_ctz(x0) >> 3
-         : x1 ? 4u + ((uint32_t)__builtin_ctz(x1) >> 3)
-         : x2 ? 8u + ((uint32_t)__builtin_ctz(x2) >> 3)
-         : x3 ? 12u + ((uint32_t)__builtin_ctz(x3) >> 3) : 16u;
+    const uint32_t z0 = __builtin_ctzg(x0, 128), z1 = 32u + __builtin_ctzg(x1, 96);
+    const uint32_t z2 = 64u + __builtin_ctzg(x2, 64), z3 = 96u + __builtin_ctzg(x3, 32);
+    const uint32_t m01 = z0 < z1 ? z0 : z1, m23 = z2 < z3 ? z2 : z3;
+    return (m01 < m23 ? m01 : m23) >> 3;
 }
 
 // 4 bytes at p where only [p, lim) may be read; missing bytes read as 0.
@@ -214,10 +217,10 @@ __device__ void wave_copy(uint8_t *dst, const uint8_t *src, uint32_t n) {
 // Equal bytes counted down from the top of two 16-byte groups (16 if equal).
 __device__ __forceinline__ uint32_t last_eq16(uint4 a, uint4 b) {
     const uint32_t x0 = a.x ^ b.x, x1 = a.y ^ b.y, x2 = a.z ^ b.z, x3 = a.w ^ b.w;
-    return x3 ? (uint32_t)__builtin_clz(x3) >> 3
-         : x2 ? 4u + ((uint32_t)__builtin_clz(x2) >> 3)
-         : x1 ? 8u + ((uint32_t)__builtin_clz(x1) >> 3)
-         : x0 ? 12u + ((uint32_t)__builtin_clz(x0) >> 3) : 16u;
+    const uint32_t z3 = __builtin_clzg(x3, 128), z2 = 32u + __builtin_clzg(x2, 96);
+    const uint32_t z1 = 64u + __builtin_clzg(x1, 64), z0 = 96u + __builtin_clzg(x0, 32);
+    const uint32_t m32 = z3 < z2 ? z3 : z2, m10 = z1 < z0 ? z1 : z0;
+    return (m32 < m10 ? m32 : m10) >> 3;
 }
 
 // sequence record: literal length | match length << 20 | offset value << 40
@@ -1166,18 +1169,24 @@ __global__ __launch_bounds__(64, HL == 11 ? 4 : 3) void rcdc_zstd_block_kernel(
                         while (bl < limb && src[p - 1 - bl] == src[c - 1 - bl]) bl++;
                 }
                 uint64_t m = __ballot(ok);
+                // lazy step, per lane in VALU: the next position's match, if
+                // it reaches at least two bytes further, wins (zstd's lazy
+                // parsers).  Lanes past an accepted match leave m only below
+                // it, so the next lane's bit in the round's mask is its bit
+                // in m whenever this lane is picked.
+                uint32_t tgt = lane;
+                {
+                    const uint32_t fn = __shfl_down(fl, 1);
+                    const bool okn = lane < 63 && ((m >> (lane + 1)) & 1ull);
+                    if (stride == 1 && ok && fl < 16 && okn && fn > fl + 1) tgt = lane + 1;
+                }
+                // the round's sequences stay in the picked lanes' registers
+                // and are stored together after the loop
+                uint32_t vll = 0, vml = 0, vof = 0;
+                uint64_t sel = 0;
                 while (m) {
-                    int j = __builtin_ctzll(m);
-                    uint32_t f = rdl(fl, j);
-                    // lazy step: the next position's match, if it reaches at
-                    // least two bytes further, wins (zstd's lazy parsers)
-                    if (stride == 1 && f < 16 && j < 63 && ((m >> (j + 1)) & 1ull)) {
-                        const uint32_t f2 = rdl(fl, j + 1);
-                        if (f2 > f + 1) {
-                            j += 1;
-                            f = f2;
-                        }
-                    }
+                    const int j = (int)rdl(tgt, __builtin_ctzll(m));
+                    const uint32_t f = rdl(fl, j);
                     uint32_t pj = base + (uint32_t)j * stride;
                     uint32_t cj = rdl(c, j);
                     const uint32_t bb = rdl(bl, j);
@@ -1238,12 +1247,18 @@ __global__ __launch_bounds__(64, HL == 11 ? 4 : 3) void rcdc_zstd_block_kernel(
                             rep0 = off;
                         }
                     }
-                    if (lane == 0) seqs[nseq] = seq_pack(ll, len, ofv);
-                    nseq++;
+                    const bool me = lane == (uint32_t)j;
+                    vll = me ? ll : vll;
+                    vml = me ? len : vml;
+                    vof = me ? ofv : vof;
+                    sel |= 1ull << j;
                     matched += len;
                     anchor = pj + len;
                     m &= __ballot(p >= anchor);
                 }
+                if ((sel >> lane) & 1ull)
+                    seqs[nseq + __popcll(sel & ((1ull << lane) - 1ull))] = seq_pack(vll, vml, vof);
+                nseq += __popcll(sel);
                 const uint32_t next = base + 64u * stride;
                 base = next > anchor ? next : anchor;
             }
