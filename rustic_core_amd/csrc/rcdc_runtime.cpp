@@ -70,7 +70,7 @@ void zstd_prof_dump();
 hipError_t launch_zstd(const uint8_t *in, uint8_t *out, const ZstdBlob *blobs, uint32_t nblobs,
                        const ZstdBlk *blks, uint32_t nblk, const ZstdTables *tabs, uint8_t *slots,
                        uint64_t *seqbuf, uint32_t grid, uint2 *res, uint64_t *bpos,
-                       uint64_t *out_lens, hipStream_t stream);
+                       uint64_t *out_lens, uint32_t *queue, hipStream_t stream);
 }  // namespace rcdc
 
 using namespace rcdc;
@@ -272,6 +272,8 @@ struct rcdc_ctx {
     ZstdBlk *d_zstd_blks = nullptr;
     uint2 *d_zstd_res = nullptr;
     uint64_t *d_zstd_bpos = nullptr, *d_zstd_lens = nullptr, *d_zstd_seq = nullptr;
+    uint32_t *d_zstd_queue = nullptr;  // per window: blocks taken past the first grid
+    uint64_t cap_zstd_queue = 0;
     uint8_t *d_zstd_slots = nullptr;
     uint64_t cap_zstd_tabs = 0, cap_zstd_blobs = 0, cap_zstd_blks = 0, cap_zstd_res = 0,
              cap_zstd_bpos = 0, cap_zstd_lens = 0, cap_zstd_seq = 0, cap_zstd_slots = 0;
@@ -1269,6 +1271,7 @@ void rcdc_ctx_destroy(rcdc_ctx *c) {
         (void)hipFree(c->d_zstd_res);
         (void)hipFree(c->d_zstd_bpos);
         (void)hipFree(c->d_zstd_lens);
+        (void)hipFree(c->d_zstd_queue);
         (void)hipFree(c->d_zstd_seq);
         (void)hipFree(c->d_zstd_slots);
         if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -1998,16 +2001,21 @@ rcdc_status zstd_compress(rcdc_ctx *ctx, int level, const void *d_in, const rcdc
     if ((rs = ensure_dev(&ctx->d_zstd_bpos, &ctx->cap_zstd_bpos, nbl))) return rs;
     if ((rs = ensure_dev(&ctx->d_zstd_lens, &ctx->cap_zstd_lens, nbo))) return rs;
     if ((rs = ensure_dev(&ctx->d_zstd_slots, &ctx->cap_zstd_slots, maxw * kZstdSlot))) return rs;
+    // the block kernel's queue: 8 counters 64 B apart per window
+    if ((rs = ensure_dev(&ctx->d_zstd_queue, &ctx->cap_zstd_queue, wins.size() * 128))) return rs;
+    HIP_TRY(hipMemsetAsync(ctx->d_zstd_queue, 0, wins.size() * 128 * 4, st));
     HIP_TRY(hipMemcpyAsync(ctx->d_zstd_blobs, blobs.data(), nbo * sizeof(ZstdBlob),
                            hipMemcpyHostToDevice, st));
     HIP_TRY(hipMemcpyAsync(ctx->d_zstd_blks, blks.data(), nbl * sizeof(ZstdBlk),
                            hipMemcpyHostToDevice, st));
-    for (const Win &w : wins)
+    for (size_t k = 0; k < wins.size(); k++) {
+        const Win &w = wins[k];
         HIP_TRY(launch_zstd((const uint8_t *)d_in, (uint8_t *)d_out, ctx->d_zstd_blobs + w.blob0,
                             (uint32_t)w.nblob, ctx->d_zstd_blks + w.blk0, (uint32_t)w.nblk,
                             ctx->d_zstd_tabs, ctx->d_zstd_slots, ctx->d_zstd_seq, grid,
                             ctx->d_zstd_res + w.blk0, ctx->d_zstd_bpos + w.blk0,
-                            ctx->d_zstd_lens + w.blob0, st));
+                            ctx->d_zstd_lens + w.blob0, ctx->d_zstd_queue + 128 * k, st));
+    }
     HIP_TRY(hipMemcpyAsync(out_lens, ctx->d_zstd_lens, nbo * 8, hipMemcpyDeviceToHost, st));
     // the host descriptors die with this call
     HIP_TRY(hipStreamSynchronize(st));

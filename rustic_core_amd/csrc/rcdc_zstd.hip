@@ -1048,7 +1048,7 @@ __global__ __launch_bounds__(64, HL == 11 ? 4 : 3) void rcdc_zstd_block_kernel(
     const uint8_t *__restrict__ in, const ZstdBlob *__restrict__ blobs,
     const ZstdBlk *__restrict__ blks, uint32_t nblk, const ZstdTables *__restrict__ tabs,
     uint8_t *__restrict__ slots, uint64_t *__restrict__ seqbuf, uint2 *__restrict__ res,
-    uint32_t dbg, uint32_t key) {
+    uint32_t dbg, uint32_t key, uint32_t *__restrict__ queue) {
     __shared__ uint32_t table[1 << HL];
     __shared__ ZstdTables T;
     const uint32_t lane = lane_id();
@@ -1057,7 +1057,20 @@ __global__ __launch_bounds__(64, HL == 11 ? 4 : 3) void rcdc_zstd_block_kernel(
     uint64_t *seqs = seqbuf + (uint64_t)blockIdx.x * kZstdMaxSeq;
     __syncthreads();
     const FseRegs R = fse_regs(T);
-    for (uint32_t b = blockIdx.x; b < nblk; b += gridDim.x) {
+    // Blocks [0, S) go by a static stride; the last one to two grids' worth,
+    // [S, nblk), are taken from a queue (blocks cost from ~0 to a full parse:
+    // a static stride left the last waves running alone).  The queue is 8
+    // counters, one per residue x = blockIdx & 7 (its own 64-byte line): set
+    // x's k-th take is block S + x + 8k.  Few takes on 8 addresses keep the
+    // device-scope atomics off the cheap kernels' path; lane 0's vector atomic
+    // is issued as a block starts, so its round trip overlaps the block.
+    // Every wave leaves once its set's count passes nblk.
+    const uint32_t G = gridDim.x, rounds = nblk / G;
+    const uint32_t S = rounds >= 2 ? (rounds - 1) * G : (G < nblk ? G : nblk);
+    const uint32_t qx = blockIdx.x & 7u;
+    uint32_t nx = 0;
+    for (uint32_t b = blockIdx.x; b < nblk; b = b + G < S ? b + G : S + qx + 8u * rdl(nx, 0)) {
+        if (b + G >= S && lane == 0) nx = atomicAdd(queue + 16u * qx, 1u);
         const ZstdBlk k = blks[b];
         const ZstdBlob B = blobs[k.blob];
         const uint8_t *src = in + B.in_off + k.start;
@@ -1519,17 +1532,17 @@ uint32_t zstd_block_grid(uint32_t cus) { return cus * (zstd_hlog() == 11 ? 16u :
 hipError_t launch_zstd(const uint8_t *in, uint8_t *out, const ZstdBlob *blobs, uint32_t nblobs,
                        const ZstdBlk *blks, uint32_t nblk, const ZstdTables *tabs, uint8_t *slots,
                        uint64_t *seqbuf, uint32_t grid, uint2 *res, uint64_t *bpos,
-                       uint64_t *out_lens, hipStream_t stream) {
+                       uint64_t *out_lens, uint32_t *queue, hipStream_t stream) {
     if (nblobs == 0) return hipSuccess;
     static const uint32_t dbg = getenv("RCDC_ZSTD_DBG") ? (uint32_t)atoi(getenv("RCDC_ZSTD_DBG")) : 0u;
     const uint32_t g = nblk < grid ? nblk : grid;
     if (g) {
         if (zstd_hlog() == 11)
             hipLaunchKernelGGL(rcdc_zstd_block_kernel<11>, dim3(g), dim3(64), 0, stream, in, blobs,
-                               blks, nblk, tabs, slots, seqbuf, res, dbg, zstd_key());
+                               blks, nblk, tabs, slots, seqbuf, res, dbg, zstd_key(), queue);
         else
             hipLaunchKernelGGL(rcdc_zstd_block_kernel<12>, dim3(g), dim3(64), 0, stream, in, blobs,
-                               blks, nblk, tabs, slots, seqbuf, res, dbg, zstd_key());
+                               blks, nblk, tabs, slots, seqbuf, res, dbg, zstd_key(), queue);
     }
     hipLaunchKernelGGL(rcdc_zstd_frame_kernel, dim3((nblobs + 255) / 256), dim3(256), 0, stream,
                        blobs, nblobs, res, bpos, out, out_lens);
