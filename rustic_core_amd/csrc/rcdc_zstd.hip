@@ -1427,7 +1427,7 @@ __global__ void rcdc_zstd_frame_kernel(const ZstdBlob *__restrict__ blobs, uint3
 
 // A workgroup per block: 3-byte block header, then the content.
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-template <bool NT>
+template <bool NT, bool AL>
 __global__ __launch_bounds__(kZstdCopyThreads) void rcdc_zstd_copy_kernel(
     const uint8_t *__restrict__ in, const ZstdBlob *__restrict__ blobs,
     const ZstdBlk *__restrict__ blks, const uint2 *__restrict__ res,
@@ -1488,6 +1488,67 @@ __global__ __launch_bounds__(kZstdCopyThreads) void rcdc_zstd_copy_kernel(
     };
     constexpr uint32_t U = 4, S = U * kZstdCopyThreads;
     uint32_t q0 = 0;
+    if (AL) {
+        // 16-aligned loads; the next 16 bytes come from the neighbour lane
+        // (lane 63 and the last chunk load them), funnelled by the
+        // block-uniform byte shift
+        const uint32_t sb = (uint32_t)(uintptr_t)src & 15u, kk = sb >> 2, rr = (sb & 3u) * 8u;
+        const uint8_t *s16 = src - sb;
+        const uint32_t ln = t & 63u;
+        auto lda = [&](uint32_t q) {
+            const u32x4 x = __builtin_nontemporal_load((const u32x4 *)(s16 + 16u * q));
+            return make_uint4(x.x, x.y, x.z, x.w);
+        };
+        auto funnel = [&](uint4 A, uint4 B) {
+            uint32_t x0, x1, x2, x3, x4;
+            if (kk == 0) {
+                x0 = A.x; x1 = A.y; x2 = A.z; x3 = A.w; x4 = B.x;
+            } else if (kk == 1) {
+                x0 = A.y; x1 = A.z; x2 = A.w; x3 = B.x; x4 = B.y;
+            } else if (kk == 2) {
+                x0 = A.z; x1 = A.w; x2 = B.x; x3 = B.y; x4 = B.z;
+            } else {
+                x0 = A.w; x1 = B.x; x2 = B.y; x3 = B.z; x4 = B.w;
+            }
+            return make_uint4(__builtin_amdgcn_alignbit(x1, x0, rr), __builtin_amdgcn_alignbit(x2, x1, rr),
+                              __builtin_amdgcn_alignbit(x3, x2, rr), __builtin_amdgcn_alignbit(x4, x3, rr));
+        };
+        auto nbr = [&](uint4 A) {
+            return make_uint4(__shfl_down(A.x, 1), __shfl_down(A.y, 1), __shfl_down(A.z, 1),
+                              __shfl_down(A.w, 1));
+        };
+        for (; q0 + S <= n16; q0 += S) {
+            uint4 A[U], E[U];
+#pragma unroll
+            for (uint32_t u = 0; u < U; u++) {
+                const uint32_t q = q0 + u * kZstdCopyThreads + t;
+                A[u] = lda(q);
+                E[u] = make_uint4(0, 0, 0, 0);
+                if (sb && ln == 63u) E[u] = lda(q + 1);  // q + 1 <= n16: holds content bytes
+            }
+#pragma unroll
+            for (uint32_t u = 0; u < U; u++) {
+                const uint32_t q = q0 + u * kZstdCopyThreads + t;
+                if (sb) {
+                    uint4 B = nbr(A[u]);
+                    if (ln == 63u) B = E[u];
+                    put(q, funnel(A[u], B));
+                } else {
+                    put(q, A[u]);
+                }
+            }
+        }
+        for (uint32_t q = q0 + t; q < n16; q += kZstdCopyThreads) {
+            const uint4 A = lda(q);
+            if (sb) {
+                uint4 B = nbr(A);  // valid when lane + 1 holds q + 1 (< n16)
+                if (ln == 63u || q + 1 >= n16) B = lda(q + 1);
+                put(q, funnel(A, B));
+            } else {
+                put(q, A);
+            }
+        }
+    } else {
     for (; q0 + S <= n16; q0 += S) {
         uint4 v[U];
 #pragma unroll
@@ -1496,6 +1557,7 @@ __global__ __launch_bounds__(kZstdCopyThreads) void rcdc_zstd_copy_kernel(
         for (uint32_t u = 0; u < U; u++) put(q0 + u * kZstdCopyThreads + t, v[u]);
     }
     for (uint32_t q = q0 + t; q < n16; q += kZstdCopyThreads) put(q, piece(q));
+    }
     const uint32_t d = n16 * 16u;
     if (t < rest - d) o[d + t] = src[d + t];
 }
@@ -1546,11 +1608,17 @@ hipError_t launch_zstd(const uint8_t *in, uint8_t *out, const ZstdBlob *blobs, u
     }
     hipLaunchKernelGGL(rcdc_zstd_frame_kernel, dim3((nblobs + 255) / 256), dim3(256), 0, stream,
                        blobs, nblobs, res, bpos, out, out_lens);
+    // A/B knobs: RCDC_ZSTD_COPY=1 loads dword-aligned dwordx4 + one dword per
+    // 16 B instead of 16-aligned loads with a lane shuffle (default, random
+    // blocks +13 %); RCDC_ZSTD_NT=0 (with COPY=1) plain loads and stores
     static const bool nt = !(getenv("RCDC_ZSTD_NT") && atoi(getenv("RCDC_ZSTD_NT")) == 0);
+    static const bool al = !(getenv("RCDC_ZSTD_COPY") && atoi(getenv("RCDC_ZSTD_COPY")) == 1);
+    auto *copy = al   ? rcdc_zstd_copy_kernel<true, true>
+                 : nt ? rcdc_zstd_copy_kernel<true, false>
+                      : rcdc_zstd_copy_kernel<false, false>;
     if (nblk)
-        hipLaunchKernelGGL(nt ? rcdc_zstd_copy_kernel<true> : rcdc_zstd_copy_kernel<false>,
-                           dim3(nblk), dim3(kZstdCopyThreads), 0, stream, in, blobs, blks, res,
-                           bpos, slots, out);
+        hipLaunchKernelGGL(copy, dim3(nblk), dim3(kZstdCopyThreads), 0, stream, in, blobs, blks,
+                           res, bpos, slots, out);
     return hipGetLastError();
 }
 
