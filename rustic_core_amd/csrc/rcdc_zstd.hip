@@ -1010,29 +1010,44 @@ __device__ uint32_t encode_literals(const uint8_t *lbuf, uint32_t nl, uint8_t *o
     return h + nl;
 }
 
-// All n bytes of the block equal to its first?  (wave-uniform; 4 KiB per
-// wave round, four independent 16-byte loads per lane in flight; the first
-// round decides most non-RLE blocks)
+// All n bytes of the block equal to its first?  (wave-uniform; 16-aligned
+// 16-byte loads, bytes outside [src, src + n) in the first and last chunk
+// masked off (an aligned chunk that holds a readable byte is readable); 4 KiB
+// per wave round, four loads in flight per lane; the first round decides
+// most non-RLE blocks)
 __device__ bool wave_is_rle(const uint8_t *src, uint32_t n, const uint8_t *lim) {
     const uint32_t lane = lane_id();
     const uint32_t b4 = (uint32_t)src[0] * 0x01010101u;
-    for (uint32_t o = 0; o < n; o += 4096) {
+    const uint32_t sb = (uint32_t)(uintptr_t)src & 15u, end = sb + n;
+    const uint8_t *s16 = src - sb;
+    const uint32_t nch = (end + 15u) >> 4;
+    // bytes of the dword at offset p (from s16) that lie in [sb, end)
+    auto dmask = [&](uint32_t p) {
+        uint32_t m = 0xFFFFFFFFu;
+        if (p < sb) m = sb - p >= 4 ? 0u : m << (8 * (sb - p));
+        if (p + 4 > end) m = p >= end ? 0u : m & (0xFFFFFFFFu >> (8 * (p + 4 - end)));
+        return m;
+    };
+    auto diff = [&](uint32_t q) {
+        const uint4 v = *(const uint4 *)(s16 + 16u * q);
+        uint32_t x0 = v.x ^ b4, x1 = v.y ^ b4, x2 = v.z ^ b4, x3 = v.w ^ b4;
+        if (q == 0 || q + 1 == nch) {
+            x0 &= dmask(16u * q);
+            x1 &= dmask(16u * q + 4);
+            x2 &= dmask(16u * q + 8);
+            x3 &= dmask(16u * q + 12);
+        }
+        return x0 | x1 | x2 | x3;
+    };
+    for (uint32_t o = 0; o < nch; o += 256) {
         uint32_t x = 0;
-        if (o + 4096 <= n) {
-            uint4 v[4];
+        if (o + 256 <= nch) {
+            uint32_t d[4];
 #pragma unroll
-            for (int u = 0; u < 4; u++) v[u] = ld16(src + o + u * 1024u + lane * 16u);
-#pragma unroll
-            for (int u = 0; u < 4; u++) x |= (v[u].x ^ b4) | (v[u].y ^ b4) | (v[u].z ^ b4) | (v[u].w ^ b4);
+            for (int u = 0; u < 4; u++) d[u] = diff(o + u * 64u + lane);
+            x = d[0] | d[1] | d[2] | d[3];
         } else {
-            for (uint32_t q = o + lane * 16u; q < n; q += 1024) {
-                if (q + 16 <= n) {
-                    const uint4 v = ld16(src + q);
-                    x |= (v.x ^ b4) | (v.y ^ b4) | (v.z ^ b4) | (v.w ^ b4);
-                } else {
-                    for (uint32_t k = q; k < n; k++) x |= src[k] ^ (b4 & 0xFF);
-                }
-            }
+            for (uint32_t q = o + lane; q < nch; q += 64) x |= diff(q);
         }
         if (__ballot(x != 0)) return false;
     }

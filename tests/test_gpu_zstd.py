@@ -246,3 +246,23 @@ def test_compressed_packs(gpu_ctx):
             assert len(plain) == ulen and hashlib.sha256(plain).digest() == bytes(bid)
             seen += 1
     assert seen == len(datas)
+
+
+def test_rle_edges(gpu_ctx):
+    """One differing byte at a block's edges or middle: never coded as RLE.
+    The RLE check reads 16-aligned chunks and masks the bytes outside the
+    block in its first and last chunk (rcdc_zstd.hip wave_is_rle); blobs start
+    at every offset mod 16 so both masks are exercised."""
+    blk = 131072
+    datas, pads = [], []
+    for i, pos in enumerate([0, 1, 3, 4, 15, 16, 17, 4095, 65536, blk - 17, blk - 16, blk - 5,
+                             blk - 4, blk - 2, blk - 1]):
+        for which in (0, 1):  # the frame's first block (never RLE-coded) or its second
+            d = bytearray(b"\x07" * (2 * blk - 3))
+            at = which * blk + pos
+            if at < len(d):
+                d[at] = 0x08
+            datas.append(bytes(d))
+            pads.append((i * 2 + which) % 16)
+    frames = _compress(gpu_ctx, datas, in_pad=pads)
+    _check(frames, datas)
