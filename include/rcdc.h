@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define RCDC_ABI_VERSION 1u
+#define RCDC_ABI_VERSION 2u
 
 /* Status codes map onto rustic_core ErrorKind (crates/core/src/error.rs:108-124). */
 typedef enum {

@@ -268,6 +268,10 @@ typedef struct {
     size_t nfiles;
     uint64_t min, avg, max;
     uint64_t *counts;
+    /* optional cut lists: file f's cuts go to cuts[cut_base[f] ..], at most
+     * cut_cap[f] of them (cdc_ref_chunk_many_cuts) */
+    uint64_t *cuts;
+    const uint64_t *cut_base, *cut_cap;
     size_t next; /* shared work counter */
     pthread_mutex_t mu;
     uint64_t total;
@@ -291,10 +295,12 @@ static void *many_worker(void *arg) {
         it->src_len = c->lens[f];
         it->buf_len = sizeof it->buf;
         it->pos = sizeof it->buf;
-        uint64_t k = 0;
+        uint64_t k = 0, off = 0;
         for (;;) {
             size_t len = owned_next(c->t, it, &r, vec, c->avg - 1, c->min, c->max);
             if (len == 0 || len == CDC_REF_UNDERFLOW) break;
+            off += len;
+            if (c->cuts && k < c->cut_cap[f]) c->cuts[c->cut_base[f] + k] = off;
             k++;
         }
         if (c->counts) c->counts[f] = k;
@@ -316,6 +322,27 @@ uint64_t cdc_ref_chunk_many_owned(const cdc_ref_tables *t, const uint8_t *data,
     memset(&c, 0, sizeof c);
     c.t = t; c.data = data; c.offs = offs; c.lens = lens; c.nfiles = nfiles;
     c.min = min; c.avg = avg; c.max = max; c.counts = counts;
+    pthread_mutex_init(&c.mu, NULL);
+    if (nthreads < 1) nthreads = 1;
+    pthread_t *th = (pthread_t *)calloc((size_t)nthreads, sizeof *th);
+    for (int i = 0; i < nthreads; i++) pthread_create(&th[i], NULL, many_worker, &c);
+    for (int i = 0; i < nthreads; i++) pthread_join(th[i], NULL);
+    free(th);
+    pthread_mutex_destroy(&c.mu);
+    return c.total;
+}
+
+uint64_t cdc_ref_chunk_many_cuts(const cdc_ref_tables *t, const uint8_t *data,
+                                 const uint64_t *offs, const uint64_t *lens,
+                                 size_t nfiles, uint64_t min, uint64_t avg,
+                                 uint64_t max, int nthreads, uint64_t *counts,
+                                 uint64_t *cuts, const uint64_t *cut_base,
+                                 const uint64_t *cut_cap) {
+    many_ctx c;
+    memset(&c, 0, sizeof c);
+    c.t = t; c.data = data; c.offs = offs; c.lens = lens; c.nfiles = nfiles;
+    c.min = min; c.avg = avg; c.max = max; c.counts = counts;
+    c.cuts = cuts; c.cut_base = cut_base; c.cut_cap = cut_cap;
     pthread_mutex_init(&c.mu, NULL);
     if (nthreads < 1) nthreads = 1;
     pthread_t *th = (pthread_t *)calloc((size_t)nthreads, sizeof *th);

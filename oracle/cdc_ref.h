@@ -91,6 +91,16 @@ uint64_t cdc_ref_chunk_many_owned(const cdc_ref_tables *t, const uint8_t *data,
                                   size_t nfiles, uint64_t min, uint64_t avg,
                                   uint64_t max, int nthreads, uint64_t *counts);
 
+/* Same work, and the cut lists too: file i's cut offsets (relative to the
+ * file) land in cuts[cut_base[i] .. cut_base[i] + min(counts[i], cut_cap[i])).
+ * The parity checker of whole device batches (bench.py, tests).            */
+uint64_t cdc_ref_chunk_many_cuts(const cdc_ref_tables *t, const uint8_t *data,
+                                 const uint64_t *offs, const uint64_t *lens,
+                                 size_t nfiles, uint64_t min, uint64_t avg,
+                                 uint64_t max, int nthreads, uint64_t *counts,
+                                 uint64_t *cuts, const uint64_t *cut_base,
+                                 const uint64_t *cut_cap);
+
 /* FixedSize chunker (fixed_size.rs:41-70): cuts every `size` bytes. */
 size_t cdc_ref_fixed(size_t n, uint64_t size, uint64_t *cuts, size_t cap);
 

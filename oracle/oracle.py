@@ -72,6 +72,9 @@ def lib():
         L.cdc_ref_chunk_many_owned.argtypes = [ctypes.POINTER(_Tables), p, p, p, sz,
                                                u64, u64, u64, ctypes.c_int, p]
         L.cdc_ref_chunk_many_owned.restype = u64
+        L.cdc_ref_chunk_many_cuts.argtypes = [ctypes.POINTER(_Tables), p, p, p, sz, u64, u64,
+                                              u64, ctypes.c_int, p, p, p, p]
+        L.cdc_ref_chunk_many_cuts.restype = u64
         L.cdc_ref_fixed.argtypes = [sz, u64, p, sz]
         L.cdc_ref_fixed.restype = sz
         L.cdc_ref_candidates.argtypes = [ctypes.POINTER(_Tables), p, sz, u64, sz, sz, p]
@@ -167,6 +170,32 @@ def chunk_many_owned(arena: np.ndarray, offs, lens, poly=DEFAULT_POLY,
                                    _ptr(lens), offs.size, min_size, avg, max_size,
                                    nthreads, _ptr(counts))
     return counts
+
+
+def chunk_many_cuts(arena: np.ndarray, offs, lens, poly=DEFAULT_POLY,
+                    min_size=DEFAULT_MIN, avg=DEFAULT_AVG, max_size=DEFAULT_MAX,
+                    nthreads: int = 1) -> list:
+    """Cut lists of many files (reference-equivalent work, per-file threads as
+    archiver.rs:195): file i = arena[offs[i], offs[i] + lens[i]).  The parity
+    checker of whole device batches."""
+    arena = np.ascontiguousarray(arena, dtype=np.uint8).reshape(-1)
+    offs = np.ascontiguousarray(offs, dtype=np.uint64)
+    lens = np.ascontiguousarray(lens, dtype=np.uint64)
+    for o, n in zip(offs, lens):
+        assert int(o) + int(n) <= arena.size
+    caps = lens // np.uint64(max(min_size, 1)) + np.uint64(2)
+    base = np.concatenate([np.zeros(1, np.uint64), np.cumsum(caps)[:-1]]).astype(np.uint64)
+    cuts = np.zeros(int(caps.sum()) if caps.size else 1, dtype=np.uint64)
+    counts = np.zeros(offs.size, dtype=np.uint64)
+    lib().cdc_ref_chunk_many_cuts(ctypes.byref(tables(poly)), _ptr(arena), _ptr(offs),
+                                  _ptr(lens), offs.size, min_size, avg, max_size, nthreads,
+                                  _ptr(counts), _ptr(cuts), _ptr(base), _ptr(caps))
+    out = []
+    for i in range(offs.size):
+        k = int(counts[i])
+        assert k <= int(caps[i])
+        out.append(cuts[int(base[i]):int(base[i]) + k].copy())
+    return out
 
 
 def fixed_cuts(n: int, size: int) -> np.ndarray:

@@ -28,7 +28,7 @@ EXPORTS = (
     "rcdc_aead_seal", "rcdc_aead_open", "rcdc_pack_build",
     "rcdc_zstd_bound", "rcdc_zstd_compress", "rcdc_zstd_tables", "rcdc_zstd_tables_size",
 )
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 
 class RcdcLibraryError(RuntimeError):

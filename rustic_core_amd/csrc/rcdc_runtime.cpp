@@ -260,6 +260,9 @@ struct rcdc_ctx {
     uint64_t cap_aead_key = 0, cap_aead_blobs = 0, cap_aead_units = 0, cap_aead_unit0 = 0,
              cap_aead_partials = 0, cap_aead_status = 0, cap_aead_stage = 0;
     hipEvent_t aead_done = nullptr;
+    // ordering of calls on the context's stream (hip_stream == 0) with the
+    // legacy default stream (null_enter / null_leave)
+    hipEvent_t ev_null_in = nullptr, ev_null_out = nullptr;
     // device tails of open streams (max + 256 bytes each): a pool, so opening
     // and closing streams never calls hipMalloc / hipFree (which synchronise
     // the device) once warm
@@ -303,6 +306,30 @@ struct DeviceGuard {
     }
     ~DeviceGuard() { (void)hipSetDevice(prev); }
 };
+
+// hip_stream == 0 selects the context's own stream.  That stream is created
+// non-blocking, so on its own it is not ordered with the legacy default
+// stream (torch's default stream is that stream).  A call given 0 is ordered
+// as if it ran there: after the work queued on the default stream before
+// the call (null_enter) and before the work queued there after it
+// (null_leave).
+rcdc_status null_enter(rcdc_ctx *ctx, const void *hip_stream, hipStream_t *st) {
+    if (hip_stream) {
+        *st = (hipStream_t)hip_stream;
+        return RCDC_OK;
+    }
+    *st = ctx->stream;
+    HIP_TRY(hipEventRecord(ctx->ev_null_in, nullptr));
+    HIP_TRY(hipStreamWaitEvent(ctx->stream, ctx->ev_null_in, 0));
+    return RCDC_OK;
+}
+
+rcdc_status null_leave(rcdc_ctx *ctx, const void *hip_stream, hipStream_t st) {
+    if (hip_stream) return RCDC_OK;
+    HIP_TRY(hipEventRecord(ctx->ev_null_out, st));
+    HIP_TRY(hipStreamWaitEvent(nullptr, ctx->ev_null_out, 0));
+    return RCDC_OK;
+}
 
 // Device buffer of at least `need` elements.  Grows with 25 % headroom: a
 // reallocation's hipFree synchronises the whole device (every lane of every
@@ -675,8 +702,9 @@ rcdc_status plan_run(rcdc_plan *pl, const void *d_arena, hipStream_t stream) {
     rcdc_ctx *ctx = pl->ctx;
     if (((uintptr_t)d_arena & 255u) != 0)
         return fail(RCDC_ERR_INVALID_INPUT, "device arena %p is not 256-byte aligned", d_arena);
-    if (!stream) stream = ctx->stream;
     DeviceGuard g(ctx->device);
+    const void *caller_stream = stream;
+    if (rcdc_status ns = null_enter(ctx, caller_stream, &stream)) return ns;
     ScanParams sp{};
     sp.seg_bytes = pl->seg_bytes;
     sp.mask = (uint32_t)(ctx->avg - 1);
@@ -752,6 +780,7 @@ rcdc_status plan_run(rcdc_plan *pl, const void *d_arena, hipStream_t stream) {
     pl->last_arena = d_arena;
     pl->last_stream = stream;
     HIP_TRY(hipEventRecord(pl->done, stream));
+    if (rcdc_status ns = null_leave(ctx, caller_stream, stream)) return ns;
     pl->ran = true;
     pl->hashed = false;
     pl->finished = false;
@@ -1233,6 +1262,8 @@ rcdc_status rcdc_ctx_create(uint64_t poly, uint64_t min, uint64_t avg_pow2, uint
     uint64_t img[512];
     build_tables(poly, img);
     if ((e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking)) != hipSuccess ||
+        (e = hipEventCreateWithFlags(&c->ev_null_in, hipEventDisableTiming)) != hipSuccess ||
+        (e = hipEventCreateWithFlags(&c->ev_null_out, hipEventDisableTiming)) != hipSuccess ||
         (e = hipMalloc((void **)&c->d_tables, sizeof img)) != hipSuccess ||
         (e = hipMemcpy(c->d_tables, img, sizeof img, hipMemcpyHostToDevice)) != hipSuccess) {
         rcdc_ctx_destroy(c);
@@ -1264,6 +1295,8 @@ void rcdc_ctx_destroy(rcdc_ctx *c) {
         (void)hipFree(c->d_aead_status);
         (void)hipFree(c->d_aead_stage);
         if (c->aead_done) (void)hipEventDestroy(c->aead_done);
+        if (c->ev_null_in) (void)hipEventDestroy(c->ev_null_in);
+        if (c->ev_null_out) (void)hipEventDestroy(c->ev_null_out);
         for (uint8_t *t : c->tail_all) (void)hipFree(t);
         (void)hipFree(c->d_zstd_tabs);
         (void)hipFree(c->d_zstd_blobs);
@@ -1439,10 +1472,11 @@ rcdc_status rcdc_sha256_chunks(rcdc_ctx *ctx, const void *d_arena, const rcdc_ch
     if (((uintptr_t)d_digests & 3) || ((uintptr_t)d_refs & 15))
         return fail(RCDC_ERR_INVALID_INPUT, "digests must be 4-byte and refs 16-byte aligned");
     DeviceGuard g(ctx->device);
-    hipStream_t st = hip_stream ? (hipStream_t)hip_stream : ctx->stream;
+    hipStream_t st;
+    if (rcdc_status ns = null_enter(ctx, hip_stream, &st)) return ns;
     HIP_TRY(launch_sha256_list((const uint8_t *)d_arena, (const ulonglong2 *)d_refs, n,
                                (uint32_t *)d_digests, st));
-    return RCDC_OK;
+    return null_leave(ctx, hip_stream, st);
 }
 
 rcdc_status rcdc_plan_hash(rcdc_plan *plan, const void *d_arena, void *hip_stream) {
@@ -1451,9 +1485,9 @@ rcdc_status rcdc_plan_hash(rcdc_plan *plan, const void *d_arena, void *hip_strea
     if (d_arena != plan->last_arena)
         return fail(RCDC_ERR_INVALID_INPUT, "arena differs from the last rcdc_plan_run");
     DeviceGuard g(plan->ctx->device);
-    hipStream_t st = hip_stream ? (hipStream_t)hip_stream : plan->last_stream;
-    if (!st) st = plan->ctx->stream;
+    hipStream_t st;
     rcdc_status rs;
+    if ((rs = null_enter(plan->ctx, hip_stream, &st))) return rs;
     if ((rs = ensure_dev(&plan->d_dig, &plan->cap_dig, plan->ncuts * 8))) return rs;
     if ((rs = ensure_dev(&plan->d_shaw, &plan->cap_shaw, 256))) return rs;
     if ((rs = ensure_dev(&plan->d_order, &plan->cap_order, plan->ncuts))) return rs;
@@ -1463,7 +1497,7 @@ rcdc_status rcdc_plan_hash(rcdc_plan *plan, const void *d_arena, void *hip_strea
                                plan->d_order, plan->d_dig, st));
     HIP_TRY(hipEventRecord(plan->done, st));
     plan->hashed = true;
-    return RCDC_OK;
+    return null_leave(plan->ctx, hip_stream, st);
 }
 
 rcdc_status rcdc_plan_hash_many(rcdc_plan *const *plans, uint32_t n,
@@ -1483,7 +1517,8 @@ rcdc_status rcdc_plan_hash_many(rcdc_plan *const *plans, uint32_t n,
             if (plans[i] == pl) return fail(RCDC_ERR_INVALID_INPUT, "plan %u repeated", j);
     }
     DeviceGuard g(ctx->device);
-    hipStream_t st = hip_stream ? (hipStream_t)hip_stream : ctx->stream;
+    hipStream_t st;
+    if (rcdc_status ns = null_enter(ctx, hip_stream, &st)) return ns;
     const uint8_t *ar[8];
     const StreamDesc *sd[8];
     uint32_t ns[8];
@@ -1512,7 +1547,7 @@ rcdc_status rcdc_plan_hash_many(rcdc_plan *const *plans, uint32_t n,
         HIP_TRY(hipEventRecord(plans[j]->done, st));
         plans[j]->hashed = true;
     }
-    return RCDC_OK;
+    return null_leave(ctx, hip_stream, st);
 }
 
 rcdc_status rcdc_plan_finish(rcdc_plan *plan) {
@@ -1764,9 +1799,15 @@ rcdc_status aead_run(rcdc_ctx *ctx, bool open, const uint8_t key[64], const void
         which.push_back(i);
     }
     std::vector<uint32_t> ds;
-    hipStream_t st = hip_stream ? (hipStream_t)hip_stream : ctx->stream;
-    if ((rs = aead_launch(ctx, open, key, bt, (uint8_t *)d_out, st, nullptr, open ? &ds : nullptr)))
-        return rs;
+    hipStream_t st;
+    {
+        DeviceGuard g(ctx->device);
+        if ((rs = null_enter(ctx, hip_stream, &st))) return rs;
+        if ((rs = aead_launch(ctx, open, key, bt, (uint8_t *)d_out, st, nullptr,
+                              open ? &ds : nullptr)))
+            return rs;
+        if ((rs = null_leave(ctx, hip_stream, st))) return rs;
+    }
     if (open)
         for (size_t j = 0; j < which.size(); j++) status[which[j]] = ds[j];
     return RCDC_OK;
@@ -1835,8 +1876,11 @@ rcdc_status pack_build(rcdc_ctx *ctx, const uint8_t key[64], const void *d_in,
         if ((rs = aead_add(bt[1], h, p))) return rs;
     }
     hdr.resize(hdr.size() + 4, 0);  // the kernel may read 3 bytes past a blob
-    hipStream_t st = hip_stream ? (hipStream_t)hip_stream : ctx->stream;
-    return aead_launch(ctx, false, key, bt, (uint8_t *)d_out, st, &hdr, nullptr);
+    DeviceGuard g(ctx->device);
+    hipStream_t st;
+    if ((rs = null_enter(ctx, hip_stream, &st))) return rs;
+    if ((rs = aead_launch(ctx, false, key, bt, (uint8_t *)d_out, st, &hdr, nullptr))) return rs;
+    return null_leave(ctx, hip_stream, st);
 }
 
 // ---- blob compression (zstd frames, RFC 8878) --------------------------------
@@ -1934,6 +1978,16 @@ uint64_t zstd_blocks(uint64_t len) { return len ? (len + kZstdBlock - 1) / kZstd
 // windows run back to back on the stream, reusing it.
 constexpr uint64_t kZstdWindowBlocks = 32768;
 
+// RCDC_ZSTD_WINDOW_BLOCKS (tests): a smaller window, so a modest batch runs
+// the multi-window path (per-window queues, rebased indices, reused slots)
+static uint64_t zstd_window_blocks() {
+    if (const char *e = getenv("RCDC_ZSTD_WINDOW_BLOCKS")) {
+        const long long v = atoll(e);
+        if (v > 0) return std::min<uint64_t>((uint64_t)v, kZstdWindowBlocks);
+    }
+    return kZstdWindowBlocks;
+}
+
 rcdc_status zstd_compress(rcdc_ctx *ctx, int level, const void *d_in, const rcdc_zstd_ref *refs,
                           uint32_t n, void *d_out, uint64_t *out_lens, void *hip_stream) {
     if (!valid_ctx(ctx) || (n && (!refs || !d_in || !d_out || !out_lens)))
@@ -1955,11 +2009,12 @@ rcdc_status zstd_compress(rcdc_ctx *ctx, int level, const void *d_in, const rcdc
     std::vector<ZstdBlk> blks;
     std::vector<Win> wins;
     uint64_t maxw = 0;
+    const uint64_t wblocks = zstd_window_blocks();
     for (uint32_t i = 0; i < n;) {
         Win w{blobs.size(), 0, blks.size(), 0};
         while (i < n) {
             const uint64_t nb = zstd_blocks(refs[i].len);
-            if (w.nblk && w.nblk + nb > kZstdWindowBlocks) break;
+            if (w.nblk && w.nblk + nb > wblocks) break;
             ZstdBlob B{};
             B.in_off = refs[i].in_off;
             B.out_off = refs[i].out_off;
@@ -1984,8 +2039,9 @@ rcdc_status zstd_compress(rcdc_ctx *ctx, int level, const void *d_in, const rcdc
     }
     std::lock_guard<std::mutex> lk(ctx->zstd_mu);
     DeviceGuard g(ctx->device);
-    hipStream_t st = hip_stream ? (hipStream_t)hip_stream : ctx->stream;
+    hipStream_t st;
     rcdc_status rs;
+    if ((rs = null_enter(ctx, hip_stream, &st))) return rs;
     if (!ctx->d_zstd_tabs) {
         if ((rs = ensure_dev(&ctx->d_zstd_tabs, &ctx->cap_zstd_tabs, 1))) return rs;
         HIP_TRY(hipMemcpy(ctx->d_zstd_tabs, &zstd_tables(), sizeof(ZstdTables),
@@ -2021,7 +2077,7 @@ rcdc_status zstd_compress(rcdc_ctx *ctx, int level, const void *d_in, const rcdc
     HIP_TRY(hipStreamSynchronize(st));
     if (const char *e = getenv("RCDC_ZSTD_DBG"))
         if (atoi(e) & 4) zstd_prof_dump();
-    return RCDC_OK;
+    return null_leave(ctx, hip_stream, st);
 }
 
 }  // namespace

@@ -263,3 +263,44 @@ def test_encrypt_decrypt_data_roundtrip(gpu_ctx, oracle_mod, rng):
         key.decrypt_data(b"short")
     enc, k, r = key.to_keys()
     assert Key.from_keys(enc, k, r)._key == key._key
+
+
+def test_null_stream_orders_with_default_stream(gpu_ctx, oracle_mod, rng):
+    """hip_stream = 0 (torch's default stream) with no explicit synchronize:
+    the input is produced by a chain of async kernels on the default stream
+    right before the seal / zstd / chunk calls, and their outputs are read
+    back by default-stream copies right after (rcdc_runtime.cpp null_enter /
+    null_leave order the context's own stream with the default stream)."""
+    import torch
+    from rustic_core_amd.compress import compress_blobs, frame_layout, make_refs as zrefs
+    from rustic_core_amd.crypto import Key, make_refs, sealed_layout
+    from oracle import zstd_ref
+    n = 64 * MiB
+    base = np.arange(n, dtype=np.uint64).astype(np.uint8) * np.uint8(7)
+    want = base.copy()
+    for _ in range(48):
+        want = (want * np.uint8(3) + np.uint8(1)).astype(np.uint8)
+    assert torch.cuda.current_stream().cuda_stream == 0
+    key = Key(_rand(rng, 64))
+    nonce = _rand(rng, 16)
+    lens = [n - 69, 4]  # inputs end 64 bytes before the tensor (the kernel reads ahead)
+    offs = [0, n - 69]
+    oo, olen = sealed_layout(lens)
+    for trial in range(2):
+        x = torch.from_numpy(base).to("cuda:0")
+        for _ in range(48):
+            x.mul_(3).add_(1)
+        out = torch.empty(olen + 64, dtype=torch.uint8, device="cuda:0")
+        key.seal_blobs(x.data_ptr(), make_refs(offs, lens, oo, nonce * 2), out.data_ptr(), 0)
+        got = out[:int(oo[0]) + lens[0] + 32].cpu().numpy().tobytes()
+        assert got == oracle_mod.seal(key._key, nonce, want[:lens[0]].tobytes()), trial
+        # zstd frames of the same bytes, again straight after the producer
+        x2 = torch.from_numpy(base).to("cuda:0")
+        for _ in range(48):
+            x2.mul_(3).add_(1)
+        f_offs, ftot = frame_layout([4 * MiB])
+        fr = torch.empty(ftot + 16, dtype=torch.uint8, device="cuda:0")
+        fl = compress_blobs(gpu_ctx, x2.data_ptr(), zrefs([8 * MiB], [4 * MiB], f_offs),
+                            fr.data_ptr(), 0, 0)
+        frame = fr[:int(fl[0])].cpu().numpy().tobytes()
+        assert zstd_ref.decompress(frame) == want[8 * MiB:12 * MiB].tobytes()

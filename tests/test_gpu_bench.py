@@ -1,0 +1,33 @@
+"""The multi-rank bench launcher on the device (the path the driver's
+8-GPU run takes): `bench.py --gpus 2` re-launches itself under
+torch.distributed.run as a child process before touching the GPU
+(bench.py spawn_ranks), each rank chunks its own streams (per-file
+sharding, archiver.rs:195) and rank 0 prints one JSON line.  On a one-GPU
+box the ranks share cuda:0 and time over gloo (RCDC_BENCH_BACKEND=gloo)."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_bench_two_ranks_gloo(gpu_ctx):
+    env = dict(os.environ, RCDC_BENCH_BACKEND="gloo")
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2",
+                        "--workload", "C2", "--steps", "2", "--warmup", "1", "--prewarm", "0",
+                        "--no-cpu-baseline"], capture_output=True, text=True, timeout=300,
+                       env=env, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-3000:]
+    line = json.loads(lines[0])
+    assert line["n_gpus"] == 2
+    assert line["parity"]["mismatches"] == 0
+    assert line["parity"]["streams_checked"] == 1024
+    assert line["value"] > 0 and line["scaling"] == "weak"

@@ -202,3 +202,33 @@ def test_walk_many_pieces_per_stream(walk_env):
     shifted = np.concatenate([_rand(90, 999), np.zeros(40 * MiB, np.uint8), _rand(91, 3 * MiB)])
     _run(SMALL, [_rand(92, 40 * MiB), np.zeros(40 * MiB, np.uint8), shifted,
                  _mixed(93, 40 * MiB, 4 * KiB, 1 * MiB, 1 * KiB, 4 * MiB)])
+
+
+def test_c4_shaped_batch_default_selection():
+    """C4 as bench.py runs it (BASELINE.json configs[3]): files of
+    log-uniform 4-256 MiB (the first 96 sizes of seed 4000, uniform random
+    bytes seeded 4000 + file), one plan with the default path selection --
+    files >= 2 pieces walk, the short ones scan in the same plan -- and every
+    file diffed against the oracle (rabin.rs:107-191)."""
+    import torch
+    from bench import c4_files, c4_fill
+    from rustic_core_amd.chunker import Context
+    from rustic_core_amd.device import DevicePlan, pack_offsets
+    mn, avg, mx = DEFAULT
+    sizes = c4_files(96)
+    files = list(range(96))
+    offs, alen = pack_offsets(sizes)
+    arena = torch.empty(alen, dtype=torch.uint8, device="cuda:0")
+    c4_fill(torch, arena, offs, files, sizes, "cuda:0")
+    ctx = Context.get(oracle.DEFAULT_POLY, mn, avg, mx, device=0)
+    plan = DevicePlan(ctx, offs, sizes, alen)
+    inf = plan.info()
+    assert inf["walk_pieces"] > 0 and inf["scanned_bytes"] > 0, inf
+    assert min(sizes) < 8 * MiB <= max(sizes)
+    plan.run(arena.data_ptr())
+    got = plan.results()
+    plan.close()
+    host = arena.cpu().numpy()
+    want = oracle.chunk_many_cuts(host, offs, sizes, nthreads=16)
+    bad = [i for i in files if not np.array_equal(got[i], want[i])]
+    assert not bad, (bad[:4], _first_diff(got[bad[0]], want[bad[0]]))

@@ -159,3 +159,22 @@ def test_reference_underflows_below_4096(oracle_mod, rcdc_lib, mn):
     with pytest.raises(ReferenceUnderflow):
         oracle_mod.chunk_cuts_owned(data, oracle_mod.DEFAULT_POLY, mn, 4096, 16384)
     assert rcdc_lib.rcdc_check_params(4096, mn, 16384) == 1
+
+
+def test_chunk_many_cuts_equals_per_file(oracle_mod):
+    """The threaded batch checker (bench.py's parity leg over whole batches)
+    returns each file's cut list exactly as the single-file oracle does,
+    including empty, sub-min, unaligned and exactly-min files."""
+    kinds = _kinds(5 * (1 << 20) + 333, 77)
+    lens = [0, 100, 1 << 19, (1 << 19) + 1, 3 * (1 << 20) + 7, 5 * (1 << 20) + 333]
+    files = [kinds["random"][:lens[0]], kinds["zeros"][:lens[1]], kinds["mixed"][:lens[2]],
+             kinds["random"][:lens[3]], kinds["lowent"][:lens[4]], kinds["mixed"][:lens[5]]]
+    offs, pos = [], 3
+    arena = np.zeros(sum(lens) + 64 * len(lens), np.uint8)
+    for f in files:
+        offs.append(pos)
+        arena[pos:pos + f.size] = f
+        pos += f.size + 17
+    got = oracle_mod.chunk_many_cuts(arena, offs, lens, nthreads=4)
+    for g, f in zip(got, files):
+        assert np.array_equal(g, oracle_mod.chunk_cuts(f))
