@@ -77,8 +77,8 @@ def parse():
     ap.add_argument("--sha-depth", type=int, default=8,
                     help="batches whose blob ids are in flight at once (pipelined ingest)")
     ap.add_argument("--pipeline", action="store_true",
-                    help="overlap run k's resolve with run k+1's scan (rcdc_plan_set_pipeline; "
-                         "measured slower on C2: the resolve waves starve behind the scan)")
+                    help="overlap run k's chain kernels with run k+1's hashing kernels "
+                         "(rcdc_plan_set_pipeline)")
     ap.add_argument("--aead", action="store_true",
                     help="also seal + open the chunks as blobs on the device (rcdc_aead_*)")
     ap.add_argument("--aead-streams", type=int, default=16,
@@ -707,8 +707,10 @@ def main():
     plan = DevicePlan(ctx, offs, lens, int(arena.numel()))
     info = plan.info()
     pipelined = False
-    if args.pipeline and args.workload != "C5" and info.get("walk_pieces", 0) == 0:
-        plan.set_pipeline(True)  # rcdc_plan_set_pipeline: resolve k overlaps scan k+1
+    if args.pipeline and args.workload != "C5":
+        # rcdc_plan_set_pipeline: run k's chain kernels (check / fixup /
+        # assemble, resolve) overlap run k + 1's hashing kernels
+        plan.set_pipeline(True)
         pipelined = True
     stream = torch.cuda.current_stream(dev)
     sptr = stream.cuda_stream

@@ -190,17 +190,31 @@ struct rcdc_plan {
     hipStream_t last_stream = nullptr;
     hipEvent_t done = nullptr;
     bool ran = false;
-    // pipelined runs (rcdc_plan_set_pipeline): scan k + 1 overlaps resolve k;
-    // summaries ping-pong between two buffer sets, resolve on its own stream
+    // pipelined runs (rcdc_plan_set_pipeline): run k's hashing kernels (scan,
+    // walk) go to hashing stream k % 2, its chain kernels (resolve, check,
+    // fixup, assemble) to the chain stream.  Hashing k + 1 thus overlaps
+    // chain k, and the next walk fills the tail of the previous one.  Every
+    // per-run buffer the chain reads ping-pongs between two sets.
     bool pipelined = false;
     uint32_t pp = 0;                  // buffer set of the next run
+    uint32_t last_set = 0;            // buffer set of the last run
     uint4 *d_sums2 = nullptr;
     uint64_t *d_masks2 = nullptr;
     uint64_t cap_sums2 = 0, cap_masks2 = 0;
     hipStream_t rstream = nullptr;
+    hipStream_t hstream[2] = {nullptr, nullptr};
+    hipEvent_t ev_in[2] = {nullptr, nullptr};
     hipEvent_t ev_scan[2] = {nullptr, nullptr};
     hipEvent_t ev_res[2] = {nullptr, nullptr};
     bool res_pending[2] = {false, false};
+    // walk buffer set 1 (set 0 is the d_w* fields above)
+    uint64_t *d_wpiece2 = nullptr, *d_pstatus2 = nullptr, *d_fixcuts2 = nullptr;
+    BoundRes *d_bres2 = nullptr;
+    uint32_t *d_ctr2 = nullptr, *d_fixlist2 = nullptr, *d_worder2 = nullptr;
+    FixRes *d_fixres2 = nullptr;
+    unsigned long long *d_wstats2 = nullptr;
+    uint64_t cap_wpiece2 = 0, cap_pstatus2 = 0, cap_fixcuts2 = 0, cap_bres2 = 0, cap_ctr2 = 0,
+             cap_fixlist2 = 0, cap_worder2 = 0, cap_fixres2 = 0, cap_wstats2 = 0;
     // SHA-256 of every chunk (rcdc_plan_hash), slot-indexed like d_cuts
     uint32_t *d_dig = nullptr;
     uint64_t cap_dig = 0;
@@ -720,13 +734,41 @@ rcdc_status plan_run(rcdc_plan *pl, const void *d_arena, hipStream_t stream) {
         }
         ev = &pl->tev[3 * pl->truns];
         pl->truns++;
-        HIP_TRY(hipEventRecord(ev[0], stream));
     }
     const uint32_t set = pl->pipelined ? pl->pp : 0;
     uint4 *sums = set ? pl->d_sums2 : pl->d_sums;
     uint64_t *masks = set ? pl->d_masks2 : pl->d_masks;
-    if (pl->pipelined && pl->res_pending[set])  // resolve k - 2 read this set
-        HIP_TRY(hipStreamWaitEvent(stream, pl->ev_res[set], 0));
+    // this run's walk buffers and parameters
+    WalkParams wprm = pl->wprm;
+    uint64_t *wpiece = pl->d_wpiece, *pstatus = pl->d_pstatus, *fixcuts = pl->d_fixcuts;
+    BoundRes *bres = pl->d_bres;
+    uint32_t *ctr = pl->d_ctr, *fixlist = pl->d_fixlist;
+    FixRes *fixres = pl->d_fixres;
+    if (set && !pl->wunits.empty()) {
+        const uint64_t nw = pl->wunits.size();
+        wpiece = pl->d_wpiece2;
+        pstatus = pl->d_pstatus2;
+        fixcuts = pl->d_fixcuts2;
+        bres = pl->d_bres2;
+        ctr = pl->d_ctr2;
+        fixlist = pl->d_fixlist2;
+        fixres = pl->d_fixres2;
+        wprm.stats = pl->d_wstats2;
+        if (wprm.order_out) {  // the cost-sorted queue (and its key bytes) of this run
+            wprm.order_out = pl->d_worder2;
+            wprm.order = pl->d_worder2;
+        }
+        (void)nw;
+    }
+    if (pl->pipelined) {
+        // hashing on this set's stream, after the caller's earlier work and
+        // after the chain that last read this set (run k - 2)
+        HIP_TRY(hipEventRecord(pl->ev_in[set], stream));
+        stream = pl->hstream[set];
+        HIP_TRY(hipStreamWaitEvent(stream, pl->ev_in[set], 0));
+        if (pl->res_pending[set]) HIP_TRY(hipStreamWaitEvent(stream, pl->ev_res[set], 0));
+    }
+    if (ev) HIP_TRY(hipEventRecord(ev[0], stream));
     HIP_TRY(launch_scan(ctx->variant, (const uint8_t *)d_arena, pl->d_items, (uint32_t)pl->items.size(),
                         ctx->d_tables, sp, sums, masks, pl->blocks, stream));
     const uint32_t cus = (uint32_t)std::max(ctx->num_cus, 1);
@@ -735,13 +777,13 @@ rcdc_status plan_run(rcdc_plan *pl, const void *d_arena, hipStream_t stream) {
         HIP_TRY(hipStreamSynchronize(stream));
         fprintf(stderr, "rcdc: scan done\n");
     }
-    HIP_TRY(launch_walk((const uint8_t *)d_arena, pl->d_sds, pl->d_wunits, pl->wprm, ctx->d_tables,
-                        pl->d_wpiece, pl->d_pstatus, pl->d_ctr,
+    HIP_TRY(launch_walk((const uint8_t *)d_arena, pl->d_sds, pl->d_wunits, wprm, ctx->d_tables,
+                        wpiece, pstatus, ctr,
                         (uint32_t)std::min<uint64_t>(cus, (pl->wunits.size() + 15) / 16), stream));
     if (dbg) {
         HIP_TRY(hipStreamSynchronize(stream));
         uint32_t h[4] = {0, 0, 0, 0};
-        if (!pl->wunits.empty()) HIP_TRY(hipMemcpy(h, pl->d_ctr, 16, hipMemcpyDeviceToHost));
+        if (!pl->wunits.empty()) HIP_TRY(hipMemcpy(h, ctr, 16, hipMemcpyDeviceToHost));
         fprintf(stderr, "rcdc: walk done (%zu units; queue %u)\n", pl->wunits.size(), h[0]);
     }
     if (ev) HIP_TRY(hipEventRecord(ev[1], stream));
@@ -767,10 +809,11 @@ rcdc_status plan_run(rcdc_plan *pl, const void *d_arena, hipStream_t stream) {
         fprintf(stderr, "rcdc: resolve done\n");
     }
     HIP_TRY(launch_walk_chain((const uint8_t *)d_arena, pl->d_sds, pl->d_wunits, pl->d_wsu0,
-                              (uint32_t)pl->wstream_u0.size(), pl->wprm, ctx->d_tables,
-                              pl->d_wpiece, pl->d_pstatus, pl->d_bres, pl->d_ctr, pl->d_fixlist,
-                              pl->d_fixcuts, pl->d_fixres, pl->d_cuts, pl->d_counts, cus, stream));
+                              (uint32_t)pl->wstream_u0.size(), wprm, ctx->d_tables,
+                              wpiece, pstatus, bres, ctr, fixlist,
+                              fixcuts, fixres, pl->d_cuts, pl->d_counts, cus, stream));
     if (ev) HIP_TRY(hipEventRecord(ev[2], stream));
+    pl->last_set = set;
     if (pl->pipelined) {
         HIP_TRY(hipEventRecord(pl->ev_res[set], stream));
         pl->res_pending[set] = true;
@@ -780,7 +823,10 @@ rcdc_status plan_run(rcdc_plan *pl, const void *d_arena, hipStream_t stream) {
     pl->last_arena = d_arena;
     pl->last_stream = stream;
     HIP_TRY(hipEventRecord(pl->done, stream));
-    if (rcdc_status ns = null_leave(ctx, caller_stream, stream)) return ns;
+    // (pipelined runs stay asynchronous beyond the caller's stream: their
+    // completion is rcdc_plan_finish / the device synchronisation)
+    if (!pl->pipelined)
+        if (rcdc_status ns = null_leave(ctx, caller_stream, stream)) return ns;
     pl->ran = true;
     pl->hashed = false;
     pl->finished = false;
@@ -959,9 +1005,20 @@ void plan_release(rcdc_plan *pl) {
     (void)hipFree(pl->d_masks);
     (void)hipFree(pl->d_sums2);
     (void)hipFree(pl->d_masks2);
+    (void)hipFree(pl->d_wpiece2);
+    (void)hipFree(pl->d_pstatus2);
+    (void)hipFree(pl->d_fixcuts2);
+    (void)hipFree(pl->d_bres2);
+    (void)hipFree(pl->d_ctr2);
+    (void)hipFree(pl->d_fixlist2);
+    (void)hipFree(pl->d_worder2);
+    (void)hipFree(pl->d_fixres2);
+    (void)hipFree(pl->d_wstats2);
     for (int k = 0; k < 2; k++) {
+        if (pl->ev_in[k]) (void)hipEventDestroy(pl->ev_in[k]);
         if (pl->ev_scan[k]) (void)hipEventDestroy(pl->ev_scan[k]);
         if (pl->ev_res[k]) (void)hipEventDestroy(pl->ev_res[k]);
+        if (pl->hstream[k]) (void)hipStreamDestroy(pl->hstream[k]);
     }
     if (pl->rstream) (void)hipStreamDestroy(pl->rstream);
     (void)hipFree(pl->d_cuts);
@@ -1367,23 +1424,50 @@ rcdc_status rcdc_plan_device_results(rcdc_plan *plan, uint64_t *d_cuts, uint64_t
 rcdc_status rcdc_plan_set_pipeline(rcdc_plan *plan, int enable) {
     if (!plan) return fail(RCDC_ERR_INVALID_INPUT, "null argument");
     if (!enable) {
+        if (plan->pipelined && plan->ran) {
+            DeviceGuard g(plan->ctx->device);
+            HIP_TRY(hipEventSynchronize(plan->done));
+        }
         plan->pipelined = false;
+        plan->pp = 0;
         return RCDC_OK;
     }
-    if (!plan->wunits.empty())
-        return fail(RCDC_ERR_UNSUPPORTED, "pipelined runs need a plan without walked streams");
+    if (plan->pipelined) return RCDC_OK;
     DeviceGuard g(plan->ctx->device);
+    if (plan->ran) HIP_TRY(hipEventSynchronize(plan->done));  // set 0's buffers are free
     rcdc_status st;
-    if ((st = ensure_dev(&plan->d_sums2, &plan->cap_sums2, plan->cap_sums))) return st;
-    if ((st = ensure_dev(&plan->d_masks2, &plan->cap_masks2, plan->cap_masks))) return st;
+    if ((st = ensure_dev(&plan->d_sums2, &plan->cap_sums2, std::max<uint64_t>(plan->cap_sums, 1))))
+        return st;
+    if ((st = ensure_dev(&plan->d_masks2, &plan->cap_masks2, std::max<uint64_t>(plan->cap_masks, 1))))
+        return st;
+    if (const uint64_t nw = plan->wunits.size()) {
+        if ((st = ensure_dev(&plan->d_wpiece2, &plan->cap_wpiece2, plan->nwpiece_cuts))) return st;
+        if ((st = ensure_dev(&plan->d_pstatus2, &plan->cap_pstatus2, nw))) return st;
+        if ((st = ensure_dev(&plan->d_bres2, &plan->cap_bres2, nw))) return st;
+        if ((st = ensure_dev(&plan->d_ctr2, &plan->cap_ctr2, 4))) return st;
+        if ((st = ensure_dev(&plan->d_fixlist2, &plan->cap_fixlist2, nw))) return st;
+        if ((st = ensure_dev(&plan->d_fixcuts2, &plan->cap_fixcuts2, nw * plan->wprm.fix_cap)))
+            return st;
+        if ((st = ensure_dev(&plan->d_fixres2, &plan->cap_fixres2, nw))) return st;
+        if ((st = ensure_dev(&plan->d_wstats2, &plan->cap_wstats2, kWalkStats))) return st;
+        if (plan->wprm.order_out &&
+            (st = ensure_dev(&plan->d_worder2, &plan->cap_worder2, nw + (nw + 3) / 4)))
+            return st;
+    }
     if (!plan->rstream)
         HIP_TRY(hipStreamCreateWithFlags(&plan->rstream, hipStreamNonBlocking));
     for (int k = 0; k < 2; k++) {
+        if (!plan->hstream[k])
+            HIP_TRY(hipStreamCreateWithFlags(&plan->hstream[k], hipStreamNonBlocking));
+        if (!plan->ev_in[k])
+            HIP_TRY(hipEventCreateWithFlags(&plan->ev_in[k], hipEventDisableTiming));
         if (!plan->ev_scan[k])
             HIP_TRY(hipEventCreateWithFlags(&plan->ev_scan[k], hipEventDisableTiming));
         if (!plan->ev_res[k])
             HIP_TRY(hipEventCreateWithFlags(&plan->ev_res[k], hipEventDisableTiming));
+        plan->res_pending[k] = false;
     }
+    plan->pp = 0;
     plan->pipelined = true;
     return RCDC_OK;
 }
@@ -1410,7 +1494,8 @@ rcdc_status rcdc_plan_walk_stats(rcdc_plan *plan, uint64_t *stats, uint64_t *tra
     DeviceGuard g(plan->ctx->device);
     HIP_TRY(hipEventSynchronize(plan->done));
     static_assert(RCDC_WALK_STATS == kWalkStats, "stats slots");
-    HIP_TRY(hipMemcpy(stats, plan->d_wstats, kWalkStats * 8, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(stats, plan->last_set ? plan->d_wstats2 : plan->d_wstats, kWalkStats * 8,
+                      hipMemcpyDeviceToHost));
     const uint64_t nw = 2 * plan->wunits.size() * kTraceWords;  // walk rows, then check rows
     if (trace && trace_cap && plan->wprm.trace)
         HIP_TRY(hipMemcpy(trace, plan->d_wtrace, std::min(trace_cap, nw) * 8,

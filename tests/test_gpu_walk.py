@@ -232,3 +232,51 @@ def test_c4_shaped_batch_default_selection():
     want = oracle.chunk_many_cuts(host, offs, sizes, nthreads=16)
     bad = [i for i in files if not np.array_equal(got[i], want[i])]
     assert not bad, (bad[:4], _first_diff(got[bad[0]], want[bad[0]]))
+
+
+@pytest.mark.parametrize("params,piece", [(SMALL, 256 * KiB), (DEFAULT, 4 * MiB)])
+def test_walk_pipelined_runs(walk_env, params, piece):
+    """rcdc_plan_set_pipeline on a walked plan: run k's check / fixup /
+    assemble (chain stream) overlap run k + 1's walk (hashing stream k % 2);
+    the walk buffers ping-pong between two sets.  Runs alternate between two
+    arenas with different bytes; each result must be its last run's cuts, and
+    a scan-path stream in the same plan (its resolve on the chain stream) too."""
+    import torch
+    from rustic_core_amd.chunker import Context
+    from rustic_core_amd.device import DevicePlan, pack_offsets
+    walk_env(piece)
+    mn, avg, mx = params
+    big = 48 * MiB if params == DEFAULT else 6 * MiB
+    lens = [big, big + 4097, 100 * KiB, big // 2 + 3]
+    offs, alen = pack_offsets(lens)
+    hosts = []
+    for a in range(2):
+        h = np.zeros(alen, np.uint8)
+        for i, (o, n) in enumerate(zip(offs, lens)):
+            h[int(o):int(o) + n] = (_mixed(100 + 10 * a + i, n, 4 * KiB, 2 * mn, 1 * KiB, 2 * mn)
+                                    if i % 2 else _rand(200 + 10 * a + i, n))
+        hosts.append(h)
+    devs = [torch.from_numpy(h).to("cuda:0") for h in hosts]
+    exp = [[oracle.chunk_cuts(h[int(o):int(o) + n], oracle.DEFAULT_POLY, mn, avg, mx)
+            for o, n in zip(offs, lens)] for h in hosts]
+    ctx = Context.get(oracle.DEFAULT_POLY, mn, avg, mx, device=0)
+    plan = DevicePlan(ctx, offs, lens, alen)
+    assert plan.info()["walk_pieces"] > 0
+    plan.set_pipeline(True)
+    s = torch.cuda.Stream()
+    for k in range(7):
+        plan.run(devs[k % 2].data_ptr(), s.cuda_stream)
+    got = plan.results()  # the last run: arena 0
+    for i, (g, e) in enumerate(zip(got, exp[0])):
+        assert np.array_equal(g, e), (i, _first_diff(g, e))
+    for k in range(4):
+        plan.run(devs[k % 2].data_ptr())  # default stream
+    got = plan.results()  # arena 1
+    for i, (g, e) in enumerate(zip(got, exp[1])):
+        assert np.array_equal(g, e), (i, _first_diff(g, e))
+    st = plan.walk_stats()
+    assert st["chunks"] > 0
+    plan.set_pipeline(False)
+    plan.run(devs[0].data_ptr())
+    assert all(np.array_equal(g, e) for g, e in zip(plan.results(), exp[0]))
+    plan.close()
