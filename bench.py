@@ -78,7 +78,9 @@ def parse():
                     help="batches whose blob ids are in flight at once (pipelined ingest)")
     ap.add_argument("--pipeline", action="store_true",
                     help="overlap run k's chain kernels with run k+1's hashing kernels "
-                         "(rcdc_plan_set_pipeline)")
+                         "(rcdc_plan_set_pipeline); the default for walked plans (C3, C4)")
+    ap.add_argument("--no-pipeline", action="store_true",
+                    help="serial runs even for walked plans")
     ap.add_argument("--aead", action="store_true",
                     help="also seal + open the chunks as blobs on the device (rcdc_aead_*)")
     ap.add_argument("--aead-streams", type=int, default=16,
@@ -468,8 +470,7 @@ def run_c4(args, torch, dist, dev, rank, world, local):
                 inf = plan.info()
                 if inf["walk_pieces"]:
                     wst = plan.walk_stats()
-                    lane_hashed += (wst["rounds"] * 64 * (inf["walk_seg_bytes"] + 64) +
-                                    wst["zones"] * 4096)
+                    lane_hashed += wst["round_bytes"] + wst["zones"] * 4096
                     walked_batches += 1
                 else:
                     lane_hashed += inf["scanned_bytes"] + 64 * inf["segments"]
@@ -707,7 +708,8 @@ def main():
     plan = DevicePlan(ctx, offs, lens, int(arena.numel()))
     info = plan.info()
     pipelined = False
-    if args.pipeline and args.workload != "C5":
+    if args.workload != "C5" and not args.no_pipeline and (
+            args.pipeline or info.get("walk_pieces", 0) > 0):
         # rcdc_plan_set_pipeline: run k's chain kernels (check / fixup /
         # assemble, resolve) overlap run k + 1's hashing kernels
         plan.set_pipeline(True)
@@ -779,7 +781,8 @@ def main():
     #   ref_hashed: the bytes the reference itself slides over (rabin.rs:127-188:
     #     per chunk 63 prefill bytes + (cut - (s + min)); from the cut lists);
     #   lane_hashed: the bytes our lanes hashed (device work counters: walk
-    #     rounds x 64 x (S + 64) + zones x 64 x 64; the scan: every position
+    #     round bytes (64 x (S + 64) per round, shorter last rounds where the
+    #     search end is known) + zones x 64 x 64; the scan: every position
     #     after the first min of a stream plus 64 B of warm-up per segment).
     walked = info.get("walk_pieces", 0) > 0
     in_bytes = int(lens.sum())
@@ -790,7 +793,7 @@ def main():
     if walked:
         st = plan.walk_stats()
         seg = info["walk_seg_bytes"]
-        lane_hashed = st["rounds"] * 64 * (seg + 64) + st["zones"] * 64 * 64
+        lane_hashed = st["round_bytes"] + st["zones"] * 64 * 64
         kernel = "rcdc_walk_kernel"
     else:
         st = None

@@ -207,20 +207,22 @@ rcdc_status rcdc_plan_kernel_times(rcdc_plan *plan, uint64_t *runs,
                                    double *resolve_ms_total);
 
 /* Work counters of the walk path (long streams) of the last run, after it
- * completes: stats[0] 64-lane hashing rounds of rcdc_walk_kernel (64 x
- * (S + 64) bytes hashed by lanes each, S = walk_seg_bytes), [1] its min-zone
- * evaluations (64 windows of 64 bytes), [2] chunks it emitted, [3] 1024-lane
- * rounds of the fixup kernel (1024 x (512 + 64) bytes each), [4] fixup zones,
- * [5] cuts the fixups walked, [6] 64-lane rounds of the boundary check
- * kernel over bytes no walker searched (64 x (S + 64) bytes each), [7] its
- * zone evaluations.  With the environment variable
+ * completes: stats[0] 64-lane hashing rounds of rcdc_walk_kernel, [1] its
+ * min-zone evaluations (64 windows of 64 bytes), [2] chunks it emitted, [3]
+ * 1024-lane rounds of the fixup kernel (1024 x (512 + 64) bytes each), [4]
+ * fixup zones, [5] cuts the fixups walked, [6] 64-lane rounds of the
+ * boundary check kernel over bytes no walker searched, [7] its zone
+ * evaluations, [8] the bytes the walk kernel's rounds hashed (64 x (S + 64)
+ * per round; the last round of a search with a known end -- a piece's stop,
+ * a chunk's max, EOF -- hashes only the 64-byte units it needs), [9] the
+ * same for the check kernel's rounds.  With the environment variable
  * RCDC_WALK_TRACE=1 at plan creation, `trace` (if not NULL) receives 4
  * words per walk piece: wall clock (100 MHz) at the piece's start and end,
  * rounds, chunks; then 4 words per piece boundary (rows of piece 0 unused)
  * from the check kernel: start, end, gap rounds, hop entries -- at most
  * trace_cap words (2 x walk_pieces x 4 in all).  All zero for plans without
  * walked streams.                                                          */
-#define RCDC_WALK_STATS 8
+#define RCDC_WALK_STATS 10
 rcdc_status rcdc_plan_walk_stats(rcdc_plan *plan, uint64_t *stats, uint64_t *trace,
                                  uint64_t trace_cap);
 

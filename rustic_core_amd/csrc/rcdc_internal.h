@@ -151,7 +151,9 @@ constexpr int kWalkStatFixZones = 4;   // fixup kernel: zone evaluations
 constexpr int kWalkStatFixCuts = 5;    // fixup kernel: cuts walked
 constexpr int kWalkStatChkRounds = 6;  // check kernel: 64-lane rounds over unsearched gaps
 constexpr int kWalkStatChkZones = 7;   // check kernel: zone evaluations
-constexpr int kWalkStats = 8;
+constexpr int kWalkStatBytes = 8;      // walk kernel: bytes its rounds hashed (64 x (S + 64) each)
+constexpr int kWalkStatChkBytes = 9;   // check kernel: bytes its gap rounds hashed
+constexpr int kWalkStats = 10;
 // trace per unit: wall clock (100 MHz) at start and end, rounds, chunks
 constexpr int kTraceWords = 4;
 

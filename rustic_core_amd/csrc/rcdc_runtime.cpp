@@ -48,7 +48,7 @@ hipError_t launch_walk_chain(const uint8_t *arena, const StreamDesc *sds, const 
                              const uint64_t *piece_cuts, const uint64_t *pstatus, BoundRes *bres,
                              uint32_t *ctr, uint32_t *fixlist, uint64_t *fix_cuts,
                              FixRes *fixres, uint64_t *cuts, uint64_t *counts,
-                             uint32_t fix_blocks, hipStream_t stream);
+                             uint32_t fix_blocks, uint32_t chk_cap, hipStream_t stream);
 hipError_t launch_sha256_list(const uint8_t *arena, const ulonglong2 *refs, uint32_t n,
                               uint32_t *digests, hipStream_t stream);
 hipError_t launch_sha256_plan(const uint8_t *arena, const StreamDesc *sds, uint32_t nstreams,
@@ -196,6 +196,10 @@ struct rcdc_plan {
     // chain k, and the next walk fills the tail of the previous one.  Every
     // per-run buffer the chain reads ping-pongs between two sets.
     bool pipelined = false;
+    // boundary-check workgroups of a pipelined run: the check is latency
+    // bound and each workgroup holds a whole CU (128 KiB of LDS tables), so
+    // overlapped with the next walk it runs on few CUs (RCDC_CHK_BLOCKS)
+    uint32_t chk_blocks_pipe = 64;
     uint32_t pp = 0;                  // buffer set of the next run
     uint32_t last_set = 0;            // buffer set of the last run
     uint4 *d_sums2 = nullptr;
@@ -811,7 +815,9 @@ rcdc_status plan_run(rcdc_plan *pl, const void *d_arena, hipStream_t stream) {
     HIP_TRY(launch_walk_chain((const uint8_t *)d_arena, pl->d_sds, pl->d_wunits, pl->d_wsu0,
                               (uint32_t)pl->wstream_u0.size(), wprm, ctx->d_tables,
                               wpiece, pstatus, bres, ctr, fixlist,
-                              fixcuts, fixres, pl->d_cuts, pl->d_counts, cus, stream));
+                              fixcuts, fixres, pl->d_cuts, pl->d_counts,
+                              pl->pipelined ? std::min<uint32_t>(cus, 32) : cus,
+                              pl->pipelined ? pl->chk_blocks_pipe : cus, stream));
     if (ev) HIP_TRY(hipEventRecord(ev[2], stream));
     pl->last_set = set;
     if (pl->pipelined) {
@@ -1454,11 +1460,33 @@ rcdc_status rcdc_plan_set_pipeline(rcdc_plan *plan, int enable) {
             (st = ensure_dev(&plan->d_worder2, &plan->cap_worder2, nw + (nw + 3) / 4)))
             return st;
     }
-    if (!plan->rstream)
-        HIP_TRY(hipStreamCreateWithFlags(&plan->rstream, hipStreamNonBlocking));
+    const int prio_mode = getenv("RCDC_PIPE_PRIO") ? atoi(getenv("RCDC_PIPE_PRIO")) : 0;
+    int prio_lo = 0, prio_hi = 0;
+    if (prio_mode) {
+        HIP_TRY(hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi));
+        if (getenv("RCDC_PIPE_PRIO_PRINT"))
+            fprintf(stderr, "rcdc: stream priorities %d..%d\n", prio_lo, prio_hi);
+    }
+    if (!plan->rstream) {
+        if (prio_mode >= 3)  // the chain kernels first on freed CUs
+            HIP_TRY(hipStreamCreateWithPriority(&plan->rstream, hipStreamNonBlocking, prio_hi));
+        else
+            HIP_TRY(hipStreamCreateWithFlags(&plan->rstream, hipStreamNonBlocking));
+    }
     for (int k = 0; k < 2; k++) {
-        if (!plan->hstream[k])
-            HIP_TRY(hipStreamCreateWithFlags(&plan->hstream[k], hipStreamNonBlocking));
+        if (!plan->hstream[k]) {
+            // RCDC_PIPE_PRIO (experiments): the two hashing streams at different
+            // priorities, so they sit on different hardware queues and run k + 1's
+            // walk can start on the CUs run k's walk frees in its tail
+            if (prio_mode == 1 || prio_mode == 2)
+                HIP_TRY(hipStreamCreateWithPriority(&plan->hstream[k], hipStreamNonBlocking,
+                                                    k ? (prio_mode == 2 ? prio_lo : prio_hi) : prio_lo));
+            else if (prio_mode == 4)  // three levels: chain high, the hashing streams low / middle
+                HIP_TRY(hipStreamCreateWithPriority(&plan->hstream[k], hipStreamNonBlocking,
+                                                    k ? (prio_lo + prio_hi) / 2 : prio_lo));
+            else
+                HIP_TRY(hipStreamCreateWithFlags(&plan->hstream[k], hipStreamNonBlocking));
+        }
         if (!plan->ev_in[k])
             HIP_TRY(hipEventCreateWithFlags(&plan->ev_in[k], hipEventDisableTiming));
         if (!plan->ev_scan[k])
@@ -1468,6 +1496,7 @@ rcdc_status rcdc_plan_set_pipeline(rcdc_plan *plan, int enable) {
         plan->res_pending[k] = false;
     }
     plan->pp = 0;
+    if (const char *e = getenv("RCDC_CHK_BLOCKS")) plan->chk_blocks_pipe = (uint32_t)std::max(atoi(e), 1);
     plan->pipelined = true;
     return RCDC_OK;
 }

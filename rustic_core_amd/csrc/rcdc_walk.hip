@@ -174,9 +174,24 @@ struct Walk {
     uint8_t *win;      // 128 B of LDS (the zone window)
     uint64_t *red;     // LDS: 16 reduction slots (workgroup walker)
     uint32_t lane, wave, tid;
-    // work counters of this walker (wave-uniform): hashing rounds, zones
+    // work counters of this walker (wave-uniform): hashing rounds, zones,
+    // and the bytes its rounds hashed (LANES x (S + 64) per round)
     uint32_t rounds, zones;
+    uint64_t lbytes;
 };
+
+// Segment of a round that starts at A and only needs positions below end:
+// the walker's S, or -- for the last round of a known end (a piece that
+// stops "open", a chunk's max, EOF, a gap of the check) -- the fewest
+// 64-byte units per lane that still cover [A + 1, end).  The round after a
+// shrunk one never runs (A + LANES x S >= end).
+template <int LANES>
+__device__ __forceinline__ uint32_t round_seg(uint32_t S, uint64_t A, uint64_t end) {
+    const uint64_t span = end > A ? end - A : 0;
+    if (span >= (uint64_t)LANES * S) return S;
+    const uint64_t per = (span + LANES - 1) / LANES;
+    return (uint32_t)max((per + 63) / 64 * 64, (uint64_t)64);
+}
 
 // First pure-window candidate p in [q, end) among the positions of one round
 // (A: stream position with off + A 64-byte aligned); kNoCut if none.  Lane t
@@ -184,19 +199,19 @@ struct Walk {
 // first slide gives the window of position A + t*S + 1, so lane t tests
 // [A + 1 + t*S, A + 1 + (t+1)*S) (the scan kernel's r = 0 <-> lane start + 65).
 template <int LANES, int TSH, bool SMALL>
-__device__ uint64_t round_first(const Walk &W, uint64_t A, uint64_t q, uint64_t end) {
-    const uint64_t P0 = A + 1 + (uint64_t)W.tid * W.S;
+__device__ uint64_t round_first(const Walk &W, uint64_t A, uint64_t q, uint64_t end, uint32_t S) {
+    const uint64_t P0 = A + 1 + (uint64_t)W.tid * S;
     // signed clamps: hipcc (ROCm 7.2) dropped the `end > P0 ?` guard of the
     // unsigned form in the workgroup instantiation (lanes past `end` then
     // counted a full segment; seen in the .s and on the device)
     const int64_t dlo = (int64_t)q - (int64_t)P0, dhi = (int64_t)end - (int64_t)P0;
-    const uint32_t rlo = (uint32_t)min(max(dlo, (int64_t)0), (int64_t)W.S);
-    const uint32_t rhi = (uint32_t)min(max(dhi, (int64_t)0), (int64_t)W.S);
+    const uint32_t rlo = (uint32_t)min(max(dlo, (int64_t)0), (int64_t)S);
+    const uint32_t rhi = (uint32_t)min(max(dhi, (int64_t)0), (int64_t)S);
     const uint64_t valid = __builtin_amdgcn_ballot_w64(rlo < rhi);
     uint64_t best = kNoCut;
     if (valid) {
         const uint64_t base = W.off + A - 64;  // >= off: A >= q - 64 >= pos + min
-        const uint64_t wbase = base + (uint64_t)W.wave * 64u * W.S;
+        const uint64_t wbase = base + (uint64_t)W.wave * 64u * S;
         const uint64_t rest = W.arena_len > wbase ? W.arena_len - wbase : 0;
         // integer clamp, made provably uniform: a descriptor hipcc cannot
         // prove uniform costs a waterfall loop per buffer load
@@ -206,7 +221,7 @@ __device__ uint64_t round_first(const Walk &W, uint64_t A, uint64_t q, uint64_t 
             (uint32_t)(rest < 0xFFFFFFFFull ? rest : 0xFFFFFFFFull));
         const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
             (void *)(W.arena + wbase), (short)0, (int)rec, 0x00020000);
-        const Chain c = scan_segment<kWR, false, TSH, SMALL, kWG>(rsrc, W.lane * W.S, W.S / kUnit,
+        const Chain c = scan_segment<kWR, false, TSH, SMALL, kWG>(rsrc, W.lane * S, S / kUnit,
                                                                    rlo, rhi, W.tab, W.k, valid,
                                                                    W.lane);
         const uint64_t hits = __builtin_amdgcn_ballot_w64(c.first != kNone) & valid;
@@ -279,8 +294,10 @@ __device__ uint64_t walk_next(Walk &W, uint64_t pos, uint64_t stop_scan, uint64_
     const uint64_t end = min(limit, stop_scan);
     uint64_t A = ((W.off + q - 1) & ~63ull) - W.off;  // A + 1 <= q: q is tested
     while (A < end) {
+        const uint32_t S = round_seg<LANES>(W.S, A, end);
         W.rounds++;
-        const uint64_t p = round_first<LANES, TSH, SMALL>(W, A, q, end);
+        W.lbytes += (uint64_t)LANES * (S + 64);
+        const uint64_t p = round_first<LANES, TSH, SMALL>(W, A, q, end, S);
         if (p != kNoCut) {
             *kind = kKindHit;
             return p;
@@ -356,6 +373,7 @@ __global__ __launch_bounds__(1024, 1) void rcdc_walk_kernel(
         const uint32_t u = __builtin_amdgcn_readfirstlane(prm.order[q]);
         const uint64_t t0 = prm.trace ? (uint64_t)wall_clock64() : 0;
         W.rounds = W.zones = 0;
+        W.lbytes = 0;
         const WalkUnit U = units[u];
         const StreamDesc d = sds[U.stream];
         W.off = d.off;
@@ -396,6 +414,7 @@ __global__ __launch_bounds__(1024, 1) void rcdc_walk_kernel(
                          (n > U.out_cap ? (kOpenFlag << 1) : 0ull);
             stats_add(s_st, kWalkStatRounds, W.rounds);
             stats_add(s_st, kWalkStatZones, W.zones);
+            stats_add(s_st, kWalkStatBytes, W.lbytes);
             stats_add(s_st, kWalkStatChunks, n);
             if (prm.trace) {
                 unsigned long long *tr = prm.trace + (uint64_t)u * kTraceWords;
@@ -607,15 +626,18 @@ __device__ uint32_t gap_pop(GapQueue &Q, uint32_t lane) {
 
 // Run the job in slot sl: one 64-lane round, its first hit into hit[req].
 template <int TSH, bool SMALL>
-__device__ void gap_run(GapQueue &Q, const Walk &W, uint32_t sl, uint64_t *rounds) {
+__device__ void gap_run(GapQueue &Q, const Walk &W, uint32_t sl, uint64_t *rounds,
+                        uint64_t *lbytes) {
     Walk H = W;
     const uint64_t A = Q.A[sl], lo = Q.lo[sl], hi = Q.hi[sl];
     H.off = Q.off[sl];
     const uint32_t r = Q.req[sl];
     wave_sync();
     if (W.lane == 0) lds_store(&Q.ready[sl], 0);  // fields copied: the slot is free
-    const uint64_t h = round_first<64, TSH, SMALL>(H, A, lo, hi);
+    const uint32_t S = round_seg<64>(W.S, A, hi);
+    const uint64_t h = round_first<64, TSH, SMALL>(H, A, lo, hi, S);
     (*rounds)++;
+    *lbytes += 64ull * (S + 64);
     if (W.lane == 0) {
         if (h != kNoCut) atomicMin(&Q.hit[r], (unsigned long long)h);
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
@@ -627,7 +649,8 @@ __device__ void gap_run(GapQueue &Q, const Walk &W, uint32_t sl, uint64_t *round
 // kNoCut if the hashing budget ran out.
 template <int TSH, bool SMALL>
 __device__ uint64_t check_first_hit(Walk &W, CheckCtx &C, uint64_t lo, uint64_t lim,
-                                    GapQueue *Q, uint32_t wave, uint64_t *shared_rounds) {
+                                    GapQueue *Q, uint32_t wave, uint64_t *shared_rounds,
+                                    uint64_t *shared_lbytes) {
     uint64_t p = lo;
     // every iteration passes one searched interval or one gap: at most ~2 per
     // min bytes of [lo, lim); the cap only guarantees termination
@@ -682,7 +705,7 @@ __device__ uint64_t check_first_hit(Walk &W, CheckCtx &C, uint64_t lo, uint64_t 
             wave_sync();
             while (__builtin_amdgcn_readfirstlane(lds_load(&Q->left[wave])) != 0) {
                 const uint32_t sl = gap_pop(*Q, W.lane);
-                if (sl < kGapSlots) gap_run<TSH, SMALL>(*Q, W, sl, shared_rounds);
+                if (sl < kGapSlots) gap_run<TSH, SMALL>(*Q, W, sl, shared_rounds, shared_lbytes);
                 else __builtin_amdgcn_s_sleep(2);
             }
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
@@ -692,8 +715,10 @@ __device__ uint64_t check_first_hit(Walk &W, CheckCtx &C, uint64_t lo, uint64_t 
             if (h != kNoCut) return h;
         } else {
             while (A < gap_end) {
+                const uint32_t S = round_seg<64>(W.S, A, gap_end);
                 W.rounds++;
-                const uint64_t h = round_first<64, TSH, SMALL>(W, A, p, gap_end);
+                W.lbytes += 64ull * (S + 64);
+                const uint64_t h = round_first<64, TSH, SMALL>(W, A, p, gap_end, S);
                 if (h != kNoCut) return h;
                 A += step;
             }
@@ -748,7 +773,7 @@ __global__ __launch_bounds__(kChkThreads, 1) void rcdc_walk_check_kernel(
     }
     for (uint32_t i = threadIdx.x; i < kGapSlots; i += blockDim.x) s_q.ready[i] = 0;
     fill_tables(s_tab, gtab, prm.idx_shift, threadIdx.x, kChkThreads);  // (ends with a barrier)
-    uint64_t shared_rounds = 0;
+    uint64_t shared_rounds = 0, shared_lbytes = 0;
     const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
     Walk W;
     W.arena = arena;
@@ -776,6 +801,7 @@ __global__ __launch_bounds__(kChkThreads, 1) void rcdc_walk_check_kernel(
         if (U.piece == 0) continue;
         const uint64_t t0 = prm.trace ? (uint64_t)wall_clock64() : 0;
         W.rounds = W.zones = 0;
+        W.lbytes = 0;
         const StreamDesc d = sds[U.stream];
         W.off = d.off;
         W.N = d.n;
@@ -851,7 +877,8 @@ __global__ __launch_bounds__(kChkThreads, 1) void rcdc_walk_check_kernel(
                     else if (lim <= z + 64) nxt = lim;
                     else lo = z + 64;
                 }
-                if (lo) nxt = check_first_hit<TSH, SMALL>(W, C, lo, lim, &s_q, wave, &shared_rounds);
+                if (lo) nxt = check_first_hit<TSH, SMALL>(W, C, lo, lim, &s_q, wave, &shared_rounds,
+                                                                &shared_lbytes);
                 if (nxt == kNoCut) {
                     R.kind = kBoundFixup;
                     R.fix_from = c;
@@ -921,6 +948,7 @@ __global__ __launch_bounds__(kChkThreads, 1) void rcdc_walk_check_kernel(
             if (R.kind == kBoundFixup) fixlist[atomicAdd(&ctr[1], 1u)] = u;
             stats_add(s_st, kWalkStatChkRounds, W.rounds);
             stats_add(s_st, kWalkStatChkZones, W.zones);
+            stats_add(s_st, kWalkStatChkBytes, W.lbytes);
             if (prm.trace) {
                 unsigned long long *tr = prm.trace + ((uint64_t)prm.nunits + u) * kTraceWords;
                 tr[0] = t0;
@@ -935,7 +963,7 @@ __global__ __launch_bounds__(kChkThreads, 1) void rcdc_walk_check_kernel(
     for (;;) {
         const uint32_t sl = gap_pop(s_q, lane);
         if (sl < kGapSlots) {
-            gap_run<TSH, SMALL>(s_q, W, sl, &shared_rounds);
+            gap_run<TSH, SMALL>(s_q, W, sl, &shared_rounds, &shared_lbytes);
             continue;
         }
         const uint32_t act = __builtin_amdgcn_readfirstlane(lds_load(&s_q.active));
@@ -944,7 +972,10 @@ __global__ __launch_bounds__(kChkThreads, 1) void rcdc_walk_check_kernel(
         if (act == 0 && hd == tl) break;
         __builtin_amdgcn_s_sleep(2);
     }
-    if (lane == 0) stats_add(s_st, kWalkStatChkRounds, shared_rounds);
+    if (lane == 0) {
+        stats_add(s_st, kWalkStatChkRounds, shared_rounds);
+        stats_add(s_st, kWalkStatChkBytes, shared_lbytes);
+    }
     stats_flush(s_st, prm.stats);
 }
 
@@ -993,6 +1024,7 @@ __global__ __launch_bounds__(1024, 1) void rcdc_walk_fixup_kernel(
         uint64_t *out = fix_cuts + (uint64_t)u * prm.fix_cap;
         uint64_t c = bres[u].fix_from, n = 0;
         W.rounds = W.zones = 0;
+        W.lbytes = 0;
         uint32_t munit = kNoUnit;
         int32_t midx = -1;
         while (c < d.n && n <= prm.fix_cap) {
@@ -1345,11 +1377,12 @@ hipError_t launch_walk_chain(const uint8_t *arena, const StreamDesc *sds, const 
                              const uint64_t *piece_cuts, const uint64_t *pstatus, BoundRes *bres,
                              uint32_t *ctr, uint32_t *fixlist, uint64_t *fix_cuts,
                              FixRes *fixres, uint64_t *cuts, uint64_t *counts,
-                             uint32_t fix_blocks, hipStream_t stream) {
+                             uint32_t fix_blocks, uint32_t chk_cap, hipStream_t stream) {
     if (prm.nunits == 0) return hipSuccess;
     static const bool dbg = getenv("RCDC_DEBUG_SYNC") != nullptr;
     const bool small = prm.mask < 0xFFFFu;
-    const uint32_t chk_blocks = std::min<uint32_t>(fix_blocks, (prm.nunits + 7) / 8);
+    const uint32_t chk_blocks =
+        std::max<uint32_t>(std::min<uint32_t>(std::min(fix_blocks, chk_cap), (prm.nunits + 7) / 8), 1);
 #define RCDC_CHK_LAUNCH(TSH, SM)                                                                   \
     hipLaunchKernelGGL((rcdc_walk_check_kernel<TSH, SM>), dim3(chk_blocks), dim3(kChkThreads), 0,  \
                        stream,                                                                     \

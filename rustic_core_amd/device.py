@@ -130,7 +130,7 @@ class DevicePlan:
         return n.value, a.value, b.value
 
     WALK_STAT_NAMES = ("rounds", "zones", "chunks", "fix_rounds", "fix_zones", "fix_cuts",
-                       "chk_rounds", "chk_zones")
+                       "chk_rounds", "chk_zones", "round_bytes", "chk_round_bytes")
 
     def walk_stats(self, trace: bool = False, check_trace: bool = False):
         """Work counters of the last run's walk path (rcdc_plan_walk_stats):
@@ -139,7 +139,7 @@ class DevicePlan:
         RCDC_WALK_TRACE=1), plus the per-boundary check trace (t0, t1, gap
         rounds, hop entries; row 0 of each stream unused) when
         ``check_trace``."""
-        stats = np.zeros(8, dtype=np.uint64)
+        stats = np.zeros(len(self.WALK_STAT_NAMES), dtype=np.uint64)
         pieces = self.info()["walk_pieces"]
         trace = trace or check_trace
         tr = np.zeros((2 * max(pieces, 1), 4), dtype=np.uint64) if trace else None

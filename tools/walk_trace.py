@@ -77,7 +77,7 @@ def run(kind, nstreams, sgib):
     below = {k: float(np.sum(dt[active < k])) for k in (4096, 2048, 1024, 256, 64)}
     rounds = tr[:, 2].astype(np.float64)
     rr = dur / np.maximum(rounds, 1)
-    lane_bytes = st["rounds"] * 64 * (plan.info()["walk_seg_bytes"] + 64) + st["zones"] * 64 * 64
+    lane_bytes = st["round_bytes"] + st["zones"] * 64 * 64
     # list scheduling of the measured durations on 4096 slots: the queue's
     # own order vs longest-first (what a perfect cost-ordered queue would give)
     import heapq
