@@ -91,9 +91,11 @@ def parse():
                     help="also compress the chunks as blobs on the device (rcdc_zstd_compress)")
     ap.add_argument("--zstd-level", type=int, default=0)
     ap.add_argument("--ingest", action="store_true",
-                    help="also run the whole version-2 backup byte path on the device: chunk, "
-                         "blob ids, dedup, zstd, seal into packs (--ingest-streams streams)")
-    ap.add_argument("--ingest-streams", type=int, default=32)
+                    help="run the whole version-2 backup byte path on the device (DeviceIngest: "
+                         "chunk, blob ids, dedup, zstd, seal, verify, packs) over "
+                         "--ingest-streams streams; on by default for C3 at N = 1")
+    ap.add_argument("--no-ingest", action="store_true")
+    ap.add_argument("--ingest-streams", type=int, default=64)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-parity", action="store_true")
     ap.add_argument("--abi-e2e", action="store_true",
@@ -858,7 +860,8 @@ def main():
                                          world == 1 and not args.no_cpu_baseline)
     if args.pack and rank == 0:
         out_extra["pack"] = pack_measure(torch, plan, arena, offs, lens, dev, args)
-    if args.ingest and rank == 0:
+    if rank == 0 and not args.no_ingest and (
+            args.ingest or (args.workload == "C3" and world == 1)):
         out_extra["ingest"] = ingest_measure(torch, arena, offs, lens, dev, args)
     if args.zstd and rank == 0:
         out_extra["zstd"] = zstd_measure(torch, plan, arena, offs, lens, dev, args,
@@ -1127,138 +1130,77 @@ def aead_measure(torch, plan, arena, offs, lens, dev, args, cpu: bool) -> dict:
 
 def ingest_measure(torch, arena, offs, lens, dev, args) -> dict:
     """The backup data path of a version-2 repository on the device, end to
-    end over the first --ingest-streams streams (SURVEY.md 8(a) + 8(f)):
-    chunk (rcdc_plan_run, 8 plans), blob ids (rcdc_plan_hash_many: one
-    launch for the 8 plans), dedup by id on the host (the indexer's has(),
-    packer.rs:304-315), zstd of every new blob (rcdc_zstd_compress,
-    decrypt.rs:489-503), then seal into 32 MiB packs with their headers
-    (rcdc_pack_build, packer.rs:615-735).  Wall time of the whole sequence
-    (host steps included) after one untimed pass; one pack checked: its blob
-    opened, decoded by libzstd and hashed back to its id."""
+    end over the first --ingest-streams streams, through the product API
+    (rustic_core_amd/ingest.py DeviceIngest: SURVEY.md 8(a) + 8(f)): chunk,
+    blob ids (short and long chunks on two streams), dedup against the
+    packer's and the index's ids (packer.rs:304-315), zstd of the new blobs
+    (the long chunks speculatively under their ids), seal, extra_verify
+    (open + decode + compare every sealed blob on the device, decrypt.rs:
+    508-529, the reference's default), and the pack files (add_raw + sealed
+    headers, packer.rs:615-735).  Wall time of the whole call (host steps
+    included) after one untimed call, each with an empty index; one pack
+    checked by the oracle: header, every blob opened, decoded by libzstd and
+    hashed back to its id."""
     import hashlib
     from oracle import oracle, zstd_ref as zr
     from rustic_core_amd.chunker import ConfigFile
-    from rustic_core_amd.compress import compress_blobs, make_refs
-    from rustic_core_amd.device import DevicePlan, hash_many
-    from rustic_core_amd.pack import PackSizer, build_packs, group_blobs, make_blobs, pack_layout
-    ns = min(len(lens), max(args.ingest_streams, 8))
-    from rustic_core_amd.chunker import Context
-    ctx = Context.get(POLY, MIN, AVG, MAX, device=dev.index or 0)
-    groups_s = [list(range(g, ns, 8)) for g in range(8)]
-    plans = [DevicePlan(ctx, [int(offs[i]) for i in g], [int(lens[i]) for i in g], arena.numel())
-             for g in groups_s]
-    side = torch.cuda.Stream(dev)
-    sp = side.cuda_stream
-    ptr = arena.data_ptr()
+    from rustic_core_amd.crypto import Key
+    from rustic_core_amd.ingest import DeviceIngest
+    ns = min(len(lens), max(args.ingest_streams, 1))
     rng = np.random.default_rng(0x1A6E)
     key = rng.integers(0, 256, 64, dtype=np.uint8).tobytes()
-    bufs = {}
-
-    def buf(name, n):
-        t = bufs.get(name)
-        if t is None or t.numel() < n:
-            bufs[name] = t = torch.empty(int(n * 1.1) + 64, dtype=torch.uint8, device=dev)
-        return t
-
-    zside = torch.cuda.Stream(dev)
-    zp = zside.cuda_stream
-
-    def ingest(times):
-        ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
-        t0 = time.perf_counter()
-        ev[0].record(side)
-        for p in plans:
-            p.run(ptr, sp)
-        ev[1].record(side)
-        # every chunk's (offset, length), from the plans' cut lists
-        in_offs, blens = [], []
-        for p, g in zip(plans, groups_s):
-            cuts = p.results()
-            for j, i in enumerate(g):
-                c = np.asarray(cuts[j], np.uint64)
-                prev = np.concatenate([np.zeros(1, np.uint64), c[:-1]])
-                in_offs.append(np.uint64(offs[i]) + prev)
-                blens.append(c - prev)
-        in_offs, blens = np.concatenate(in_offs), np.concatenate(blens)
-        t1 = time.perf_counter()
-        hash_many(plans, [ptr] * len(plans), sp)
-        ev[2].record(side)
-        # every chunk compressed speculatively on another stream while the
-        # ids run (the SHA-256 launch's tail occupies few CUs); duplicates'
-        # frames are simply not packed
-        nblk = np.maximum(1, (blens + 131071) // 131072)
-        fb = (blens + 3 * nblk + 9 + 15) // 16 * 16  # rcdc_zstd_bound, 16-aligned
-        f_offs = np.concatenate([np.zeros(1, np.uint64), np.cumsum(fb)[:-1].astype(np.uint64)])
-        frames = buf("frames", int(fb.sum()))
-        flens = compress_blobs(ctx, ptr, make_refs(in_offs, blens, f_offs), frames.data_ptr(),
-                               args.zstd_level, zp)
-        t2 = time.perf_counter()
-        ids = np.concatenate([np.concatenate([np.asarray(d, np.uint8).reshape(-1, 32)
-                                              for d in p.digests()]) for p in plans])
-        t3 = time.perf_counter()
-        # dedup: the first occurrence of every id (the indexer's has(),
-        # packer.rs:304-315), in chunk order
-        _, first = np.unique(np.ascontiguousarray(ids).view(np.dtype((np.void, 32))).ravel(),
-                             return_index=True)
-        first.sort()
-        nb = len(first)
-        blobs = make_blobs(f_offs[first], flens[first], ids[first],
-                           rng.integers(0, 256, (nb, 16), dtype=np.uint8),
-                           uncompressed=blens[first])
-        groups = group_blobs([int(x) for x in flens[first]],
-                             PackSizer.from_config(ConfigFile.new(2, POLY), 0, 0))
-        packs, total = pack_layout(blobs, groups,
-                                   rng.integers(0, 256, (len(groups), 16), dtype=np.uint8))
-        t4 = time.perf_counter()
-        out = buf("packs", total)
-        build_packs(ctx, key, frames.data_ptr(), blobs, packs, out.data_ptr(), total, sp)
+    cfg = ConfigFile.new(2, POLY)
+    cfg.compression = args.zstd_level if args.zstd_level != 0 else None
+    ing = DeviceIngest(cfg, Key(key), device=dev.index or 0)
+    o, n = [int(x) for x in offs[:ns]], [int(x) for x in lens[:ns]]
+    times, res = [], None
+    for r in range(4):
+        ing.indexed = set()
+        del res
         torch.cuda.synchronize(dev)
-        t5 = time.perf_counter()
-        times.append({"total_ms": (t5 - t0) * 1e3, "chunk_ms": ev[0].elapsed_time(ev[1]),
-                      "cut_lists_ms": (t1 - t0) * 1e3, "ids_ms": ev[1].elapsed_time(ev[2]),
-                      "zstd_all_chunks_ms (under the ids)": (t2 - t1) * 1e3,
-                      "ids_ready_ms": (t3 - t0) * 1e3, "dedup_group_ms": (t4 - t3) * 1e3,
-                      "pack_ms": (t5 - t4) * 1e3})
-        return (len(ids), in_offs[first], blens[first], flens[first], blobs, packs, groups,
-                total, out)
-
-    warm = []
-    ingest(warm)
-    times = []
-    for _ in range(3):
-        nchunks, in_offs, blens, flens, blobs, packs, groups, total, out = ingest(times)
-    best = min(times, key=lambda t: t["total_ms"])
-    inb = int(sum(int(lens[i]) for i in range(ns)))
-    # check one pack: header ids, each blob opened, decoded and hashed back
-    j = len(groups) // 2
-    p = packs[j]
-    f = out[int(p["out_off"]):int(p["out_off"]) + int(p["size"])].cpu().numpy().tobytes()
+        t0 = time.perf_counter()
+        res = ing.ingest(arena, o, n)
+        torch.cuda.synchronize(dev)
+        if r:
+            times.append((time.perf_counter() - t0, res.ms))
+    best_t, best_ms = min(times, key=lambda x: x[0])
+    inb = int(sum(n))
+    # one pack, checked by the oracle
+    j = len(res.pack_table) // 2
+    f = res.pack_file(j)
     parsed = oracle.parse_pack(key, f)
-    b0 = int(p["blob0"])
-    ok = len(parsed) == int(p["nblobs"])
-    for k, (tpe, off, ln, ulen, bid) in enumerate(parsed[:8]):
+    b0 = int(res.pack_table[j]["blob0"])
+    nidx = np.nonzero(res.new)[0]
+    ok = len(parsed) == int(res.pack_table[j]["nblobs"])
+    for k, (tpe, off, ln, ulen, bid) in enumerate(parsed):
         plain = zr.decompress(oracle.open_(key, f[off:off + ln]))
-        a0, n0 = int(in_offs[b0 + k]), int(blens[b0 + k])
+        c = nidx[b0 + k]
+        a0, n0 = int(res.chunk_offs[c]), int(res.chunk_lens[c])
         src = arena[a0:a0 + n0].cpu().numpy().tobytes()
         ok &= plain == src and hashlib.sha256(plain).digest() == bytes(bid) and ulen == len(src)
-    for pl in plans:
-        pl.close()
-    bufs.clear()
-    torch.cuda.empty_cache()
-    return {
-        "path": "chunk (8 plans) -> blob ids (hash_many) || zstd of every chunk (second stream) "
-                "-> host dedup (numpy) -> seal the new blobs' frames into packs + headers; all "
-                "bytes stay in HBM",
-        "streams": ns, "input_bytes": inb, "chunks": nchunks, "unique_blobs": len(blens),
-        "unique_bytes": int(sum(blens)), "frame_bytes": int(np.sum(flens)),
-        "packs": len(groups), "pack_bytes": int(total),
-        "ms": {k: round(v, 2) for k, v in best.items()},
-        "gibs_input": round(inb / (best["total_ms"] / 1e3) / GiB, 2),
-        "check": {"pack": j, "ok": bool(ok),
+    uniq = len(np.unique(np.ascontiguousarray(res.ids).view(np.dtype((np.void, 32)))))
+    out = {
+        "path": "rustic_core_amd.ingest.DeviceIngest: chunk -> blob ids (short || long chunks) "
+                "-> dedup -> zstd (new blobs; long chunks speculatively under their ids) -> seal "
+                "-> extra_verify (open + decode + compare, on the device) -> packs (add_raw + "
+                "sealed headers); all bytes stay in HBM",
+        "streams": ns, "input_bytes": inb, "chunks": len(res.ids), "unique_blobs": uniq,
+        "new_blobs": int(res.new.sum()), "unique_bytes": int(res.chunk_lens[res.new].sum()),
+        "pack_bytes": res.pack_bytes, "packs": len(res.pack_table),
+        "extra_verify": ing.extra_verify, "zstd_level": ing.level,
+        "ms": {k: round(v, 2) for k, v in best_ms.items()},
+        "gibs_input": round(inb / best_t / GiB, 2),
+        "check": {"pack": j, "ok": bool(ok) and uniq == int(res.new.sum()),
                   "checker": "oracle.parse_pack + oracle.open_ + libzstd decode + sha256 == id "
-                             "for its first 8 blobs"},
+                             "for every blob of one pack; new blobs == distinct ids"},
+        "floor": "the longest chunk's SHA-256 chain (one lane, ~2 us per 64-B block: ~0.27 s "
+                 "for an 8 MiB chunk) bounds one call (DESIGN.md 3c)",
         "note": "pack ids (SHA-256 of each pack file, packer.rs:833) are left to the writer",
     }
+    ing.close()
+    del res
+    torch.cuda.empty_cache()
+    return out
 
 
 def zstd_measure(torch, plan, arena, offs, lens, dev, args, cpu: bool) -> dict:

@@ -338,6 +338,15 @@ rcdc_status rcdc_pack_build(rcdc_ctx *ctx, const uint8_t *key, const void *d_in,
                             uint32_t npacks, void *d_out, uint64_t out_len,
                             uint32_t *blob_offsets, void *hip_stream);
 
+/* The same with blobs sealed already (packer.rs:615-655 add_raw: the packer
+ * appends encrypted data): blobs[i].len is the sealed length (>= 32, nonce +
+ * ciphertext + tag) of the bytes at in_off, copied into the pack as they are
+ * (nonce ignored); only the headers are sealed here.                        */
+rcdc_status rcdc_pack_build_raw(rcdc_ctx *ctx, const uint8_t *key, const void *d_in,
+                                const rcdc_pack_blob *blobs, uint32_t nblobs, rcdc_pack *packs,
+                                uint32_t npacks, void *d_out, uint64_t out_len,
+                                uint32_t *blob_offsets, void *hip_stream);
+
 /* ---- blob compression: backend/decrypt.rs:478-506 (`encode_all(data,
  * level)` before `Key::encrypt_data` when the repository is version 2,
  * configfile.rs:177-186), applied by the packer's process_data
@@ -369,6 +378,36 @@ uint64_t rcdc_zstd_bound(uint64_t len);
 rcdc_status rcdc_zstd_compress(rcdc_ctx *ctx, int level, const void *d_in,
                                const rcdc_zstd_ref *refs, uint32_t n, void *d_out,
                                uint64_t *out_lens, void *hip_stream);
+
+/* ---- frame check: backend/decrypt.rs:508-529 (`very_data`, on by default:
+ * extra_verify, repofile/configfile.rs:198): after compressing a blob the
+ * packer decodes it again and compares it with the input.  Here every frame
+ * is decoded on the device and compared with its blob in place. ---------- */
+
+/* Frame [frame_off, frame_off + frame_len) of d_frames is expected to decode
+ * to [data_off, data_off + data_len) of d_data (allow 4 readable bytes after
+ * each range). */
+typedef struct {
+    uint64_t frame_off;
+    uint64_t frame_len;
+    uint64_t data_off;
+    uint64_t data_len;
+} rcdc_zstd_check_ref;
+
+/* Decode n frames (refs is a HOST array) and compare them with their blobs:
+ * status[i] (host) = 0 the frame decodes to exactly the blob (RFC 8878: any
+ * block and literal type, 1 or 4 Huffman streams, predefined / RLE / FSE /
+ * repeat sequence tables, repeat offsets, matches into earlier blocks),
+ * 1 it decodes to other bytes or another length (ErrorKind::Verification,
+ * decrypt.rs:516-526), 2 malformed or not readable here (a dictionary, a
+ * skippable frame, bytes after the frame).  A frame checksum is skipped.
+ * flags bit 0 (RCDC_CHECK_STORED): the "frames" are stored bytes (blobs of an
+ * uncompressed repository), compared as they are.  Synchronous.  Calls on one context take turns; the context keeps a
+ * 128 KiB literal scratch per resident wave (256 MiB on 256 CUs).          */
+rcdc_status rcdc_zstd_check(rcdc_ctx *ctx, const void *d_frames, const void *d_data,
+                            const rcdc_zstd_check_ref *refs, uint32_t n, uint32_t flags,
+                            uint32_t *status, void *hip_stream);
+#define RCDC_CHECK_STORED 1u
 
 /* The FSE coding tables the kernels use (predefined distributions, RFC 8878
  * 3.1.1.3.2.2), copied to out (rcdc_zstd_tables_size() bytes): for tests. */

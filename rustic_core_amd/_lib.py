@@ -27,6 +27,7 @@ EXPORTS = (
     "rcdc_plan_finish", "rcdc_stream_queued", "rcdc_stream_batch_bytes",
     "rcdc_aead_seal", "rcdc_aead_open", "rcdc_pack_build",
     "rcdc_zstd_bound", "rcdc_zstd_compress", "rcdc_zstd_tables", "rcdc_zstd_tables_size",
+    "rcdc_zstd_check", "rcdc_pack_build_raw",
 )
 ABI_VERSION = 2
 
@@ -155,10 +156,14 @@ def lib() -> ctypes.CDLL:
     L.rcdc_aead_open.argtypes = [vp, vp, vp, vp, u32, vp, vp, vp]
     L.rcdc_pack_build.restype = st
     L.rcdc_pack_build.argtypes = [vp, vp, vp, vp, u32, vp, u32, vp, u64, vp, vp]
+    L.rcdc_pack_build_raw.restype = st
+    L.rcdc_pack_build_raw.argtypes = [vp, vp, vp, vp, u32, vp, u32, vp, u64, vp, vp]
     L.rcdc_zstd_bound.restype = u64
     L.rcdc_zstd_bound.argtypes = [u64]
     L.rcdc_zstd_compress.restype = st
     L.rcdc_zstd_compress.argtypes = [vp, ctypes.c_int, vp, vp, u32, vp, vp, vp]
+    L.rcdc_zstd_check.restype = st
+    L.rcdc_zstd_check.argtypes = [vp, vp, vp, vp, u32, u32, vp, vp]
     L.rcdc_zstd_tables.restype = None
     L.rcdc_zstd_tables.argtypes = [vp]
     L.rcdc_zstd_tables_size.restype = u64

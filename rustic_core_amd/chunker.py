@@ -65,6 +65,9 @@ class ConfigFile:
     datapack_size_limit: Optional[int] = None
     min_packsize_tolerate_percent: Optional[int] = None
     max_packsize_tolerate_percent: Optional[int] = None
+    # blob processing (configfile.rs:43-50)
+    compression: Optional[int] = None
+    extra_verify: Optional[bool] = None
 
     @classmethod
     def new(cls, version: int, poly: int) -> "ConfigFile":
@@ -97,6 +100,20 @@ class ConfigFile:
         return (30 if self.min_packsize_tolerate_percent is None
                 else self.min_packsize_tolerate_percent,
                 0xFFFFFFFF if not mx else mx)
+
+    def zstd(self) -> Optional[int]:
+        """configfile.rs:182-193: the zstd level, None = no compression."""
+        if self.version == 1 or (self.version == 2 and self.compression == 0):
+            return None
+        if self.version == 2:
+            return 0 if self.compression is None else self.compression
+        raise RusticError(ErrorKind.Unsupported,
+                          f"Config version `{self.version}` not supported. Please make sure, "
+                          "that you use the correct version.")
+
+    def extra_verify_(self) -> bool:
+        """configfile.rs:197-199 (default: verify)."""
+        return True if self.extra_verify is None else bool(self.extra_verify)
 
     def get_chunker(self) -> Chunker:
         return self.chunker or Chunker.Rabin

@@ -27,6 +27,14 @@ from .errors import ErrorKind, RusticError, status_error
 ZSTD_REF = np.dtype([("in_off", "<u8"), ("len", "<u8"), ("out_off", "<u8")])
 assert ZSTD_REF.itemsize == 24
 
+# rcdc_zstd_check_ref (include/rcdc.h)
+ZSTD_CHECK_REF = np.dtype([("frame_off", "<u8"), ("frame_len", "<u8"), ("data_off", "<u8"),
+                           ("data_len", "<u8")])
+assert ZSTD_CHECK_REF.itemsize == 32
+
+# frame check status (rcdc_zstd_check)
+CHECK_OK, CHECK_MISMATCH, CHECK_CORRUPT = 0, 1, 2
+
 # zstd's level range (decrypt.rs:20-24, zstd::compression_level_range)
 MIN_LEVEL, MAX_LEVEL = -(1 << 17), 22
 
@@ -34,6 +42,13 @@ MIN_LEVEL, MAX_LEVEL = -(1 << 17), 22
 def zstd_bound(n: int) -> int:
     """Worst-case frame bytes of an n-byte blob."""
     return int(_lib.lib().rcdc_zstd_bound(int(n)))
+
+
+def zstd_bounds(lens) -> np.ndarray:
+    """rcdc_zstd_bound of every length (numpy; the same formula)."""
+    lens = np.asarray(lens, np.int64)
+    nblk = np.maximum((lens + (128 << 10) - 1) // (128 << 10), 1)
+    return lens + 3 * nblk + 9
 
 
 def frame_layout(lens, align: int = 16):
@@ -66,6 +81,63 @@ def compress_blobs(ctx: Context, d_in: int, refs: np.ndarray, d_out: int, level:
     return out_lens[:len(refs)]
 
 
+def check_frames(ctx: Context, d_frames: int, frame_offs, frame_lens, d_data: int, data_offs,
+                 data_lens, hip_stream: Optional[int] = None, stored: bool = False) -> np.ndarray:
+    """Decode every frame on the device and compare it with its blob
+    (rcdc_zstd_check): per frame 0 = equal, 1 = other bytes or length,
+    2 = malformed / not readable here.  ``stored``: the "frames" are plain
+    bytes (uncompressed blobs), compared as they are."""
+    n = len(frame_lens)
+    refs = np.zeros(max(n, 1), ZSTD_CHECK_REF)
+    refs["frame_off"][:n] = np.asarray(frame_offs, np.uint64)
+    refs["frame_len"][:n] = np.asarray(frame_lens, np.uint64)
+    refs["data_off"][:n] = np.asarray(data_offs, np.uint64)
+    refs["data_len"][:n] = np.asarray(data_lens, np.uint64)
+    status = np.zeros(max(n, 1), np.uint32)
+    st = _lib.lib().rcdc_zstd_check(ctx.handle, ctypes.c_void_p(d_frames), ctypes.c_void_p(d_data),
+                                    refs.ctypes.data, n, 1 if stored else 0, status.ctypes.data,
+                                    ctypes.c_void_p(hip_stream or 0))
+    if st:
+        raise status_error(st, _lib.last_error())
+    return status[:n]
+
+
+VERIFY_MESSAGE = ("Verification failed: After decrypting and decompressing the data changed! "
+                  "The data may be corrupted.")  # decrypt.rs:519-521
+
+
+def verify_sealed(ctx: Context, key, d_sealed: int, sealed_offs, sealed_lens, d_data: int,
+                  data_offs, data_lens, compressed: bool, hip_stream: Optional[int] = None,
+                  scratch=None) -> None:
+    """very_data (decrypt.rs:508-529) for a batch: open every sealed blob on
+    the device (MAC checked), then decode its frame (or take the plaintext
+    when not compressed) and compare it with the input bytes.  Raises
+    ErrorKind.Verification on the first blob that does not come back."""
+    import torch
+    from .crypto import make_refs as aead_refs, sealed_layout
+    n = len(sealed_lens)
+    if n == 0:
+        return
+    plain_lens = np.asarray(sealed_lens, np.uint64) - 32
+    p_offs, total = sealed_layout(plain_lens)  # 16-aligned plaintexts
+    dev = torch.device("cuda", ctx.device)
+    if scratch is None or scratch.numel() < total + 64:
+        scratch = torch.empty(int(total) + 64, dtype=torch.uint8, device=dev)
+    st = key.open_blobs(d_sealed, aead_refs(sealed_offs, sealed_lens, p_offs), scratch.data_ptr(),
+                        hip_stream, ctx)
+    bad = np.nonzero(st)[0]
+    if len(bad):
+        raise RusticError(ErrorKind.Verification,
+                          f"{VERIFY_MESSAGE} (blob {int(bad[0])}: MAC check failed)")
+    # compressed: decode each frame; else the plaintext is compared as is
+    cs = check_frames(ctx, scratch.data_ptr(), p_offs, plain_lens, d_data, data_offs, data_lens,
+                      hip_stream, stored=not compressed)
+    bad = np.nonzero(cs)[0]
+    if len(bad):
+        raise RusticError(ErrorKind.Verification,
+                          f"{VERIFY_MESSAGE} (blob {int(bad[0])}: status {int(cs[bad[0]])})")
+
+
 def _ctx(device: int) -> Context:
     from .crypto import _ctx as c
     return c(device)
@@ -89,10 +161,13 @@ def encode_all(data: bytes, level: int = 0, device: int = 0) -> bytes:
 
 
 def process_blobs(key, d_in: int, in_offs, lens, level: Optional[int] = 0, nonces=None,
-                  device: int = 0):
+                  device: int = 0, extra_verify: bool = True):
     """DecryptWriteBackend::process_data (decrypt.rs:566-572) for a batch of
-    blobs in HBM: compress (level not None) and seal.  Returns (sealed
-    device tensor, sealed offsets, sealed lengths, data_len,
+    blobs in HBM: compress (level not None), seal, and -- with
+    ``extra_verify`` (the reference's default, configfile.rs:198) -- open and
+    decode every sealed blob again and compare it with the input
+    (``very_data``, decrypt.rs:508-529; ErrorKind.Verification).  Returns
+    (sealed device tensor, sealed offsets, sealed lengths, data_len,
     uncompressed_length) -- uncompressed_length is 0 where nothing was
     compressed (``None`` in the reference)."""
     import torch
@@ -119,6 +194,9 @@ def process_blobs(key, d_in: int, in_offs, lens, level: Optional[int] = 0, nonce
         s_offs, s_total = sealed_layout(src_lens)
         out = torch.empty(max(s_total, 1), dtype=torch.uint8, device=dev)
         key.seal_blobs(src, aead_refs(src_offs, src_lens, s_offs, nonces), out.data_ptr(), s, ctx)
+        if extra_verify:
+            verify_sealed(ctx, key, out.data_ptr(), s_offs, np.asarray(src_lens, np.uint64) + 32,
+                          d_in, in_offs, lens, level is not None, s)
         torch.cuda.synchronize(dev)
     del keep
     ulen = lens.copy() if level is not None else np.zeros(n, np.uint64)

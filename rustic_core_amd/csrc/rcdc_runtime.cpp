@@ -71,6 +71,13 @@ hipError_t launch_zstd(const uint8_t *in, uint8_t *out, const ZstdBlob *blobs, u
                        const ZstdBlk *blks, uint32_t nblk, const ZstdTables *tabs, uint8_t *slots,
                        uint64_t *seqbuf, uint32_t grid, uint2 *res, uint64_t *bpos,
                        uint64_t *out_lens, uint32_t *queue, hipStream_t stream);
+uint64_t zstd_check_scratch_bytes(uint32_t grid);
+hipError_t launch_copy_ranges(const uint8_t *in, uint8_t *out, const void *units, uint32_t n,
+                              uint32_t cus, hipStream_t stream);
+hipError_t launch_zstd_check(const uint8_t *frames, const uint8_t *data, const void *refs,
+                             const uint32_t *order, uint32_t n, bool stored, uint8_t *scratch,
+                             uint32_t grid,
+                             uint32_t *status, uint32_t *ctr, hipStream_t stream);
 }  // namespace rcdc
 
 using namespace rcdc;
@@ -298,6 +305,15 @@ struct rcdc_ctx {
     uint8_t *d_zstd_slots = nullptr;
     uint64_t cap_zstd_tabs = 0, cap_zstd_blobs = 0, cap_zstd_blks = 0, cap_zstd_res = 0,
              cap_zstd_bpos = 0, cap_zstd_lens = 0, cap_zstd_seq = 0, cap_zstd_slots = 0;
+    // frame checks (rcdc_zstd_check): calls on one context take turns
+    std::mutex zck_mu;
+    uint64_t *d_zck_refs = nullptr;
+    uint32_t *d_zck_order = nullptr, *d_zck_status = nullptr;
+    uint8_t *d_zck_scratch = nullptr;
+    uint64_t cap_zck_refs = 0, cap_zck_order = 0, cap_zck_status = 0, cap_zck_scratch = 0;
+    // pack files from sealed blobs (rcdc_pack_build_raw): copy units
+    uint64_t *d_copy_units = nullptr;
+    uint64_t cap_copy_units = 0;
 };
 
 struct rcdc_stream {
@@ -1370,6 +1386,11 @@ void rcdc_ctx_destroy(rcdc_ctx *c) {
         (void)hipFree(c->d_zstd_queue);
         (void)hipFree(c->d_zstd_seq);
         (void)hipFree(c->d_zstd_slots);
+        (void)hipFree(c->d_zck_refs);
+        (void)hipFree(c->d_zck_order);
+        (void)hipFree(c->d_zck_status);
+        (void)hipFree(c->d_zck_scratch);
+        (void)hipFree(c->d_copy_units);
         if (c->stream) (void)hipStreamDestroy(c->stream);
     }
     delete c;
@@ -1933,16 +1954,19 @@ static_assert(sizeof(rcdc_pack) == 48, "rcdc_pack is 48 B");
 // Pack files (blob/packer.rs:615-655, 693-735; repofile/packfile.rs): blobs
 // sealed back to back, then the sealed header (one HeaderEntry per blob:
 // type, u32 length, [u32 raw length], id) and its u32 length.
+// raw (add_raw): the blobs at in_off are sealed already (len = sealed bytes,
+// >= 32); they are copied into place and only the headers are sealed.
 rcdc_status pack_build(rcdc_ctx *ctx, const uint8_t key[64], const void *d_in,
                        const rcdc_pack_blob *blobs, uint32_t nblobs, rcdc_pack *packs,
                        uint32_t npacks, void *d_out, uint64_t out_len, uint32_t *blob_offsets,
-                       void *hip_stream) {
+                       void *hip_stream, bool raw = false) {
     if (!valid_ctx(ctx) || !key || (npacks && (!packs || !d_out)) || (nblobs && (!blobs || !d_in)))
         return fail(RCDC_ERR_INVALID_INPUT, "null argument");
     std::vector<AeadBatch> bt(2);
     bt[0].in = (const uint8_t *)d_in;
     bt[1].in = nullptr;  // headers: from the staging buffer
     std::vector<uint8_t> hdr;
+    std::vector<uint64_t> copies;  // raw: (src, dst, len, 0) per unit of <= 1 MiB
     rcdc_status rs;
     for (uint32_t p = 0; p < npacks; p++) {
         rcdc_pack &P = packs[p];
@@ -1954,16 +1978,27 @@ rcdc_status pack_build(rcdc_ctx *ctx, const uint8_t key[64], const void *d_in,
         for (uint32_t i = P.blob0; i < P.blob0 + P.nblobs; i++) {
             const rcdc_pack_blob &b = blobs[i];
             if (b.type > 1) return fail(RCDC_ERR_INVALID_INPUT, "blob %u: type %u", i, b.type);
-            const uint32_t sealed = b.len + 32u;
-            if (b.len > 0xFFFFFFFFu - 32u)
+            if (raw && b.len < 32)
+                return fail(RCDC_ERR_INVALID_INPUT, "blob %u: %u sealed bytes (< 32)", i, b.len);
+            if (!raw && b.len > 0xFFFFFFFFu - 32u)
                 return fail(RCDC_ERR_UNSUPPORTED, "blob %u: %u bytes", i, b.len);
+            const uint32_t sealed = raw ? b.len : b.len + 32u;
             if (blob_offsets) blob_offsets[i] = (uint32_t)off;
-            AeadBlob a{};
-            a.in_off = b.in_off;
-            a.len = b.len;
-            a.out_off = P.out_off + off;
-            memcpy(a.nonce, b.nonce, 16);
-            if ((rs = aead_add(bt[0], a, i))) return rs;
+            if (raw) {
+                for (uint64_t c = 0; c < sealed; c += 1u << 20) {
+                    copies.push_back(b.in_off + c);
+                    copies.push_back(P.out_off + off + c);
+                    copies.push_back(std::min<uint64_t>(1u << 20, sealed - c));
+                    copies.push_back(0);
+                }
+            } else {
+                AeadBlob a{};
+                a.in_off = b.in_off;
+                a.len = b.len;
+                a.out_off = P.out_off + off;
+                memcpy(a.nonce, b.nonce, 16);
+                if ((rs = aead_add(bt[0], a, i))) return rs;
+            }
             // HeaderEntry (packfile.rs:88-124, little-endian)
             hdr.push_back((uint8_t)(b.type + (b.uncompressed_len ? 2u : 0u)));
             for (int j = 0; j < 4; j++) hdr.push_back((uint8_t)(sealed >> (8 * j)));
@@ -1993,6 +2028,20 @@ rcdc_status pack_build(rcdc_ctx *ctx, const uint8_t key[64], const void *d_in,
     DeviceGuard g(ctx->device);
     hipStream_t st;
     if ((rs = null_enter(ctx, hip_stream, &st))) return rs;
+    if (!copies.empty()) {
+        // the unit list lives in the context until the copy has run (the
+        // AEAD lock below orders calls on this context's scratch)
+        std::lock_guard<std::mutex> lk(ctx->aead_mu);
+        if (ctx->aead_done) HIP_TRY(hipEventSynchronize(ctx->aead_done));
+        const uint64_t nu = copies.size() / 4;
+        if ((rs = ensure_dev(&ctx->d_copy_units, &ctx->cap_copy_units, copies.size()))) return rs;
+        HIP_TRY(hipMemcpyAsync(ctx->d_copy_units, copies.data(), copies.size() * 8,
+                               hipMemcpyHostToDevice, st));
+        HIP_TRY(launch_copy_ranges((const uint8_t *)d_in, (uint8_t *)d_out, ctx->d_copy_units,
+                                   (uint32_t)nu, (uint32_t)std::max(ctx->num_cus, 1), st));
+        // the host vector dies with this call
+        HIP_TRY(hipStreamSynchronize(st));
+    }
     if ((rs = aead_launch(ctx, false, key, bt, (uint8_t *)d_out, st, &hdr, nullptr))) return rs;
     return null_leave(ctx, hip_stream, st);
 }
@@ -2194,9 +2243,53 @@ rcdc_status zstd_compress(rcdc_ctx *ctx, int level, const void *d_in, const rcdc
     return null_leave(ctx, hip_stream, st);
 }
 
+// Frame checks: one wave per frame, longest frames first (a frame's blocks
+// are read in order, so the longest frame bounds the launch).
+rcdc_status zstd_check(rcdc_ctx *ctx, const void *d_frames, const void *d_data,
+                       const rcdc_zstd_check_ref *refs, uint32_t n, uint32_t flags,
+                       uint32_t *status, void *hip_stream) {
+    if (!valid_ctx(ctx) || (n && (!refs || !d_frames || !d_data || !status)))
+        return fail(RCDC_ERR_INVALID_INPUT, "null argument");
+    if (!n) return RCDC_OK;
+    std::vector<uint32_t> order(n);
+    for (uint32_t i = 0; i < n; i++) order[i] = i;
+    std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) {
+        return refs[a].frame_len > refs[b].frame_len;
+    });
+    std::lock_guard<std::mutex> lk(ctx->zck_mu);
+    DeviceGuard g(ctx->device);
+    hipStream_t st;
+    rcdc_status rs;
+    if ((rs = null_enter(ctx, hip_stream, &st))) return rs;
+    const uint32_t grid = (uint32_t)std::max(ctx->num_cus, 1) * 8u;
+    if ((rs = ensure_dev(&ctx->d_zck_refs, &ctx->cap_zck_refs, 4ull * n))) return rs;
+    if ((rs = ensure_dev(&ctx->d_zck_order, &ctx->cap_zck_order, (uint64_t)n + 16))) return rs;
+    if ((rs = ensure_dev(&ctx->d_zck_status, &ctx->cap_zck_status, n))) return rs;
+    if ((rs = ensure_dev(&ctx->d_zck_scratch, &ctx->cap_zck_scratch, zstd_check_scratch_bytes(grid))))
+        return rs;
+    // the queue counter sits after the order array
+    uint32_t *ctr = ctx->d_zck_order + n;
+    HIP_TRY(hipMemsetAsync(ctr, 0, 4, st));
+    HIP_TRY(hipMemcpyAsync(ctx->d_zck_refs, refs, sizeof(rcdc_zstd_check_ref) * n,
+                           hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemcpyAsync(ctx->d_zck_order, order.data(), 4ull * n, hipMemcpyHostToDevice, st));
+    HIP_TRY(launch_zstd_check((const uint8_t *)d_frames, (const uint8_t *)d_data, ctx->d_zck_refs,
+                              ctx->d_zck_order, n, (flags & RCDC_CHECK_STORED) != 0,
+                              ctx->d_zck_scratch, grid, ctx->d_zck_status, ctr, st));
+    HIP_TRY(hipMemcpyAsync(status, ctx->d_zck_status, 4ull * n, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    return null_leave(ctx, hip_stream, st);
+}
+
 }  // namespace
 
 extern "C" {
+
+rcdc_status rcdc_zstd_check(rcdc_ctx *ctx, const void *d_frames, const void *d_data,
+                            const rcdc_zstd_check_ref *refs, uint32_t n, uint32_t flags,
+                            uint32_t *status, void *hip_stream) {
+    return zstd_check(ctx, d_frames, d_data, refs, n, flags, status, hip_stream);
+}
 
 rcdc_status rcdc_aead_seal(rcdc_ctx *ctx, const uint8_t *key, const void *d_in,
                            const rcdc_aead_ref *refs, uint32_t n, void *d_out, void *hip_stream) {
@@ -2215,6 +2308,14 @@ rcdc_status rcdc_pack_build(rcdc_ctx *ctx, const uint8_t *key, const void *d_in,
                             uint32_t *blob_offsets, void *hip_stream) {
     return pack_build(ctx, key, d_in, blobs, nblobs, packs, npacks, d_out, out_len, blob_offsets,
                       hip_stream);
+}
+
+rcdc_status rcdc_pack_build_raw(rcdc_ctx *ctx, const uint8_t *key, const void *d_in,
+                                const rcdc_pack_blob *blobs, uint32_t nblobs, rcdc_pack *packs,
+                                uint32_t npacks, void *d_out, uint64_t out_len,
+                                uint32_t *blob_offsets, void *hip_stream) {
+    return pack_build(ctx, key, d_in, blobs, nblobs, packs, npacks, d_out, out_len, blob_offsets,
+                      hip_stream, true);
 }
 
 uint64_t rcdc_zstd_bound(uint64_t len) { return len + 3 * zstd_blocks(len) + 9; }

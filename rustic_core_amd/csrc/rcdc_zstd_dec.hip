@@ -1,0 +1,908 @@
+// rcdc_zstd_dec.hip -- zstd frames read back on the device: the extra_verify
+// check of rustic's packer (backend/decrypt.rs:508-529 `very_data`: after
+// compress + seal, decrypt and decompress the blob again and compare it with
+// the input; on by default, configfile.rs:198 extra_verify) for blobs in HBM.
+//
+// rcdc_zstd_check_kernel: one wave per frame (RFC 8878), frames taken from an
+// atomic queue in the host's order (longest first).  The wave decodes every
+// block the way any conforming decoder does (frame header, raw / RLE /
+// compressed blocks; raw / RLE / Huffman / treeless literals with 1 or 4
+// streams and direct or FSE-coded weights; predefined / RLE / FSE / repeat
+// sequence tables; repeat offsets; matches reaching into earlier blocks) and
+// compares what it decodes with the blob's bytes instead of writing it:
+//   - a raw or RLE block, or a sequence's literals, is compared with the
+//     blob's bytes at the output position (literals decoded into a per-wave
+//     scratch first: 4 Huffman streams on lanes 0-3);
+//   - a match of offset o at output position p is compared as
+//     data[p + i] == data[p - o + i]: by induction everything before p
+//     already equals the data, so the data itself stands in for the decoded
+//     output and the comparison has no order (overlapping matches included).
+// Sequences are decoded 64 at a time by the whole wave (uniform code: every
+// lane steps the same FSE states) and lane j keeps sequence j; a prefix sum
+// places them and each lane compares its own (sequences longer than 256 bytes
+// are compared by the whole wave afterwards).
+// Status per frame: 0 = decodes to exactly the blob, 1 = decodes to other
+// bytes or another length, 2 = malformed or a feature this reader lacks
+// (dictionaries, skippable frames, more than one frame).  A frame checksum,
+// when present, is skipped (the blob comparison is the stronger check).
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "rcdc_internal.h"
+
+using namespace rcdc;
+
+namespace {
+
+constexpr uint32_t kCkOk = 0, kCkMismatch = 1, kCkCorrupt = 2;
+constexpr uint32_t kBlockMax = 128u << 10;
+
+// Predefined distributions (RFC 8878 3.1.1.3.2.2) and code -> (baseline,
+// extra bits) of literal and match lengths (3.1.1.3.2.1.1).
+__constant__ int16_t kLLNorm[36] = {4, 3, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 1, 1, 1, 2, 2,
+                                    2, 2, 2, 2, 2, 2, 2, 3, 2, 1, 1, 1, 1, 1, -1, -1, -1, -1};
+__constant__ int16_t kMLNorm[53] = {1, 4, 3, 2, 2, 2, 2, 2, 2, 1, 1, 1, 1, 1, 1, 1, 1, 1,
+                                    1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1,
+                                    1, 1, 1, 1, 1, 1, 1, 1, 1, 1, -1, -1, -1, -1, -1, -1, -1};
+__constant__ int16_t kOFNorm[29] = {1, 1, 1, 1, 1, 1, 2, 2, 2, 1, 1, 1, 1, 1, 1,
+                                    1, 1, 1, 1, 1, 1, 1, 1, 1, -1, -1, -1, -1, -1};
+__constant__ uint32_t kLLBase[36] = {0,  1,  2,  3,  4,  5,   6,   7,   8,    9,    10,   11,
+                                     12, 13, 14, 15, 16, 18,  20,  22,  24,   28,   32,   40,
+                                     48, 64, 128, 256, 512, 1024, 2048, 4096, 8192, 16384, 32768, 65536};
+__constant__ uint8_t kLLBits[36] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0,  1,  1,
+                                    1, 1, 2, 2, 3, 3, 4, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16};
+__constant__ uint32_t kMLBase[53] = {3,  4,  5,  6,  7,  8,  9,  10, 11, 12, 13, 14, 15, 16,
+                                     17, 18, 19, 20, 21, 22, 23, 24, 25, 26, 27, 28, 29, 30,
+                                     31, 32, 33, 34, 35, 37, 39, 41, 43, 47, 51, 59, 67, 83,
+                                     99, 131, 259, 515, 1027, 2051, 4099, 8195, 16387, 32771, 65539};
+__constant__ uint8_t kMLBits[53] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0,
+                                    0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 1, 1, 1, 1,
+                                    2, 2, 3, 3, 4, 4, 5, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16};
+
+struct FseD {  // FSE decoding entry (FSE_decode_t)
+    uint8_t sym, nb;
+    uint16_t next;
+};
+struct HufD {
+    uint8_t sym, nb;
+};
+
+// LDS of one wave (workgroup = one wave)
+struct DecLds {
+    FseD ll[512], ml[512], of[256];
+    FseD hw[64];  // FSE table of Huffman weights (log <= 6)
+    HufD huf[2048];
+    int16_t norm[64];
+    uint16_t nxt[256];
+    uint8_t w[256];  // Huffman weights
+};
+
+__device__ __forceinline__ uint32_t highbit32(uint32_t v) { return 31u - (uint32_t)__clz(v); }
+
+__device__ __forceinline__ void wsync() {
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+    __syncthreads();
+}
+
+// 4 bytes at any alignment from the aligned dwords that hold them (a dword
+// holding a readable byte is readable: allocations are 4-byte granular).
+__device__ __forceinline__ uint32_t ld4u(const uint8_t *p) {
+    const uint32_t b = (uint32_t)(uintptr_t)p & 3u;
+    const uint32_t *w = (const uint32_t *)(p - b);
+    const uint32_t lo = w[0];
+    const uint32_t hi = w[b ? 1 : 0];
+    return __builtin_amdgcn_alignbit(hi, lo, b * 8u);
+}
+
+// n (<= 8) little-endian bytes at p; bytes outside [lo, hi) read as 0.
+__device__ uint64_t ld8b(const uint8_t *p, const uint8_t *lo, const uint8_t *hi) {
+    if (p >= lo && p + 8 <= hi)
+        return (uint64_t)ld4u(p) | (uint64_t)ld4u(p + 4) << 32;
+    uint64_t v = 0;
+    for (int i = 0; i < 8; i++)
+        if (p + i >= lo && p + i < hi) v |= (uint64_t)p[i] << (8 * i);
+    return v;
+}
+
+// Backward bitstream (RFC 8878 4.1): bits [0, pos) unread, read from the top;
+// bits below 0 read as zeros (a read that goes below 0 is an overflow).
+struct BRev {
+    const uint8_t *base;
+    int64_t len;
+    int64_t pos;
+    int64_t cb;      // cache holds bits [cb, cb + 64)
+    uint64_t cache;
+};
+
+__device__ __forceinline__ void brev_fill(BRev &r) {
+    r.cb = ((r.pos - 57) >> 3) << 3;  // arithmetic shift: floor
+    r.cache = ld8b(r.base + (r.cb >> 3), r.base, r.base + r.len);
+}
+
+// false: empty stream or no end mark
+__device__ bool brev_init(BRev &r, const uint8_t *p, int64_t len) {
+    r.base = p;
+    r.len = len;
+    if (len <= 0) return false;
+    const uint32_t last = p[len - 1];
+    if (last == 0) return false;
+    r.pos = 8 * (len - 1) + (int64_t)highbit32(last);
+    brev_fill(r);
+    return true;
+}
+
+__device__ __forceinline__ uint64_t brev_peek(BRev &r, uint32_t n) {
+    if (n == 0) return 0;
+    const int64_t lo = r.pos - (int64_t)n;
+    if (lo < r.cb) brev_fill(r);
+    return (r.cache >> (uint32_t)(lo - r.cb)) & ((1ull << n) - 1ull);
+}
+
+__device__ __forceinline__ uint64_t brev_bits(BRev &r, uint32_t n) {
+    const uint64_t v = brev_peek(r, n);
+    r.pos -= n;
+    return v;
+}
+
+// FSE_readNCount: a table description at p (at most `avail` bytes);
+// returns its byte length, or -1.  norm[0..*nsym) and *al are set.
+__device__ int read_ncount(const uint8_t *p, int64_t avail, uint32_t max_sym, uint32_t max_al,
+                           int16_t *norm, uint32_t *nsym, uint32_t *al) {
+    if (avail < 1) return -1;
+    const uint8_t *end = p + avail;
+    int64_t bitpos = 0;  // from p
+    auto rd32 = [&](int64_t bp) -> uint32_t {
+        const uint64_t v = ld8b(p + (bp >> 3), p, end);
+        return (uint32_t)(v >> (bp & 7));
+    };
+    uint32_t bs = rd32(0);
+    int nb = (int)(bs & 0xF) + 5;
+    if ((uint32_t)nb > max_al) return -1;
+    *al = (uint32_t)nb;
+    bitpos = 4;
+    int remaining = (1 << nb) + 1;
+    int threshold = 1 << nb;
+    nb++;
+    uint32_t s = 0;
+    bool prev0 = false;
+    while (remaining > 1 && s <= max_sym) {
+        bs = rd32(bitpos);
+        if (prev0) {
+            uint32_t n0 = s;
+            while ((bs & 0xFFFF) == 0xFFFF) {
+                n0 += 24;
+                bitpos += 16;
+                bs = rd32(bitpos);
+            }
+            while ((bs & 3) == 3) {
+                n0 += 3;
+                bs >>= 2;
+                bitpos += 2;
+            }
+            n0 += bs & 3;
+            bitpos += 2;
+            if (n0 > max_sym + 1) return -1;
+            while (s < n0) norm[s++] = 0;
+            if (s > max_sym) break;
+            bs = rd32(bitpos);
+        }
+        const int mx = (2 * threshold - 1) - remaining;
+        int count;
+        if ((int)(bs & (uint32_t)(threshold - 1)) < mx) {
+            count = (int)(bs & (uint32_t)(threshold - 1));
+            bitpos += nb - 1;
+        } else {
+            count = (int)(bs & (uint32_t)(2 * threshold - 1));
+            if (count >= threshold) count -= mx;
+            bitpos += nb;
+        }
+        count--;
+        remaining -= count < 0 ? -count : count;
+        norm[s++] = (int16_t)count;
+        prev0 = count == 0;
+        while (remaining < threshold) {
+            nb--;
+            threshold >>= 1;
+        }
+        if (bitpos > 8 * avail) return -1;
+    }
+    if (remaining != 1 || s > max_sym + 1) return -1;
+    *nsym = s;
+    const int64_t used = (bitpos + 7) >> 3;
+    return used > avail ? -1 : (int)used;
+}
+
+// FSE_buildDTable from norm[0..nsym) (accuracy al) into t; false if the
+// counts do not fill the table.  Uniform code; lane 0 writes.
+__device__ bool build_fse(FseD *t, const int16_t *norm, uint32_t nsym, uint32_t al, uint16_t *nxt,
+                          uint32_t lane) {
+    const uint32_t size = 1u << al, mask = size - 1;
+    uint32_t high = size - 1;
+    int total = 0;
+    for (uint32_t s = 0; s < nsym; s++) total += norm[s] < 0 ? 1 : norm[s];
+    if ((uint32_t)total != size) return false;
+    for (uint32_t s = 0; s < nsym; s++) {
+        if (norm[s] == -1) {
+            if (lane == 0) t[high].sym = (uint8_t)s;
+            high--;
+            if (lane == 0) nxt[s] = 1;
+        } else if (lane == 0) {
+            nxt[s] = (uint16_t)(norm[s] < 0 ? 0 : norm[s]);
+        }
+    }
+    const uint32_t step = (size >> 1) + (size >> 3) + 3;
+    uint32_t pos = 0;
+    for (uint32_t s = 0; s < nsym; s++) {
+        for (int i = 0; i < norm[s]; i++) {
+            if (lane == 0) t[pos].sym = (uint8_t)s;
+            do {
+                pos = (pos + step) & mask;
+            } while (pos > high);
+        }
+    }
+    if (pos != 0) return false;
+    wsync();
+    if (lane == 0) {
+        for (uint32_t u = 0; u < size; u++) {
+            const uint32_t s = t[u].sym;
+            const uint32_t ns = nxt[s]++;
+            const uint32_t nb = al - highbit32(ns);
+            t[u].nb = (uint8_t)nb;
+            t[u].next = (uint16_t)((ns << nb) - size);
+        }
+    }
+    wsync();
+    return true;
+}
+
+__device__ bool build_predefined(FseD *t, const int16_t *src, uint32_t nsym, uint32_t al,
+                                 int16_t *norm, uint16_t *nxt, uint32_t lane) {
+    if (lane < nsym) norm[lane] = src[lane];
+    wsync();
+    return build_fse(t, norm, nsym, al, nxt, lane);
+}
+
+// Frame-walk state of one wave.
+struct Dec {
+    const uint8_t *data;  // the blob
+    uint64_t dlen;
+    uint64_t out;         // bytes decoded (= compared) so far
+    uint32_t rep[3];
+    uint32_t huf_log;     // 0: no Huffman table yet
+    uint32_t al_ll, al_ml, al_of;  // 255: no table yet
+    uint32_t bad;         // status
+};
+
+// ---- comparisons (the whole wave) -----------------------------------------
+
+// data[p, p+n) == src[0, n) (kind 0) / == byte v (kind 1) / == data[p-o, ..)
+// (kind 2); wave-uniform arguments; returns true if equal.
+__device__ bool wave_cmp(const uint8_t *a, const uint8_t *b, uint32_t v, int kind, uint64_t n,
+                         uint32_t lane) {
+    const uint32_t rep4 = v * 0x01010101u;
+    bool ok = true;
+    for (uint64_t o = (uint64_t)lane * 4u; o < n; o += 256) {
+        const uint32_t x = ld4u(a + o);
+        const uint32_t y = kind == 1 ? rep4 : ld4u(b + o);
+        uint32_t d = x ^ y;
+        const uint64_t rem = n - o;
+        if (rem < 4) d &= (1u << (8 * rem)) - 1u;
+        ok &= d == 0;
+    }
+    return __builtin_amdgcn_ballot_w64(!ok) == 0;
+}
+
+// one lane's comparison (kinds as wave_cmp)
+__device__ bool lane_cmp(const uint8_t *a, const uint8_t *b, uint32_t v, int kind, uint32_t n) {
+    const uint32_t rep4 = v * 0x01010101u;
+    uint32_t acc = 0;
+    for (uint32_t o = 0; o < n; o += 4) {
+        const uint32_t x = ld4u(a + o);
+        const uint32_t y = kind == 1 ? rep4 : ld4u(b + o);
+        uint32_t d = x ^ y;
+        const uint32_t rem = n - o;
+        if (rem < 4) d &= (1u << (8 * rem)) - 1u;
+        acc |= d;
+    }
+    return acc == 0;
+}
+
+// ---- literals ---------------------------------------------------------------
+
+// Huffman weights (HUF_readStats) at p (avail bytes) -> L.w[0..*nw), the
+// implied last weight appended; returns the description's length or -1.
+__device__ int read_huf_weights(const uint8_t *p, int64_t avail, DecLds &L, uint32_t *nw,
+                                uint32_t lane) {
+    if (avail < 1) return -1;
+    const uint32_t hb = p[0];
+    uint32_t n = 0;
+    int used;
+    if (hb >= 128) {
+        n = hb - 127;
+        used = 1 + (int)((n + 1) / 2);
+        if (used > avail) return -1;
+        if (lane < n) {
+            const uint32_t byte = p[1 + lane / 2];
+            L.w[lane] = (uint8_t)((lane & 1) ? (byte & 15u) : (byte >> 4));
+        }
+        if (lane + 64 < n) {
+            const uint32_t k = lane + 64, byte = p[1 + k / 2];
+            L.w[k] = (uint8_t)((k & 1) ? (byte & 15u) : (byte >> 4));
+        }
+        wsync();
+    } else {
+        // FSE-compressed weights: NCount (log <= 6), then two interleaved
+        // states over a backward bitstream (FSE_decompress_usingDTable)
+        used = 1 + (int)hb;
+        if (used > avail || hb == 0) return -1;
+        uint32_t nsym = 0, al = 0;
+        const int nc = read_ncount(p + 1, hb, 255, 6, L.norm, &nsym, &al);
+        if (nc < 0) return -1;
+        wsync();
+        if (!build_fse(L.hw, L.norm, nsym, al, L.nxt, lane)) return -1;
+        BRev r;
+        if (!brev_init(r, p + 1 + nc, (int64_t)hb - nc)) return -1;
+        uint32_t s1 = (uint32_t)brev_bits(r, al), s2 = (uint32_t)brev_bits(r, al);
+        for (;;) {
+            if (n >= 255) return -1;
+            FseD e = L.hw[s1];
+            if (lane == 0) L.w[n] = e.sym;
+            n++;
+            s1 = e.next + (uint32_t)brev_bits(r, e.nb);
+            if (r.pos < 0) {
+                if (n >= 255) return -1;
+                if (lane == 0) L.w[n] = L.hw[s2].sym;
+                n++;
+                break;
+            }
+            if (n >= 255) return -1;
+            e = L.hw[s2];
+            if (lane == 0) L.w[n] = e.sym;
+            n++;
+            s2 = e.next + (uint32_t)brev_bits(r, e.nb);
+            if (r.pos < 0) {
+                if (n >= 255) return -1;
+                if (lane == 0) L.w[n] = L.hw[s1].sym;
+                n++;
+                break;
+            }
+        }
+        wsync();
+    }
+    // the last weight is implied: the weights fill a power of two
+    uint32_t total = 0;
+    for (uint32_t i = 0; i < n; i++) {
+        const uint32_t wi = L.w[i];
+        if (wi > 11) return -1;
+        total += wi ? (1u << (wi - 1)) : 0u;
+    }
+    if (total == 0) return -1;
+    const uint32_t tl = highbit32(total) + 1;
+    if (tl > 11) return -1;
+    const uint32_t rest = (1u << tl) - total;
+    if (rest & (rest - 1)) return -1;
+    wsync();
+    if (lane == 0) L.w[n] = (uint8_t)(highbit32(rest) + 1);
+    *nw = n + 1;
+    wsync();
+    return used;
+}
+
+// HUF_readDTableX1 from L.w[0..nw) -> L.huf; returns the table log.
+__device__ uint32_t build_huf(DecLds &L, uint32_t nw, uint32_t lane) {
+    uint32_t cnt[13] = {0};
+    uint32_t total = 0;
+    for (uint32_t s = 0; s < nw; s++) {
+        const uint32_t wi = L.w[s];
+        cnt[wi]++;
+        total += wi ? (1u << (wi - 1)) : 0u;
+    }
+    const uint32_t tl = highbit32(total);  // total is a power of two now
+    uint32_t start[13];
+    uint32_t nx = 0;
+    for (uint32_t wi = 1; wi <= tl; wi++) {
+        start[wi] = nx;
+        nx += cnt[wi] << (wi - 1);
+    }
+    // symbols of weight wi fill 2^(wi-1) entries each, in symbol order: lane l
+    // writes the entries of symbol s with l in the range (all lanes stride)
+    for (uint32_t s = 0; s < nw; s++) {
+        const uint32_t wi = L.w[s];
+        if (!wi) continue;
+        const uint32_t len = 1u << (wi - 1), b = start[wi];
+        start[wi] += len;
+        for (uint32_t k = lane; k < len; k += 64) {
+            L.huf[b + k].sym = (uint8_t)s;
+            L.huf[b + k].nb = (uint8_t)(tl + 1 - wi);
+        }
+    }
+    wsync();
+    return tl;
+}
+
+// One Huffman stream [p, p+len) -> n symbols at out (one lane).
+__device__ bool huf_stream(const DecLds &L, uint32_t tl, const uint8_t *p, int64_t len,
+                           uint8_t *out, uint32_t n) {
+    BRev r;
+    if (n == 0) return len == 0 || (brev_init(r, p, len) && r.pos == 0);
+    if (!brev_init(r, p, len)) return false;
+    uint32_t i = 0;
+    // four symbols per dword store once aligned
+    while (i < n && ((uintptr_t)(out + i) & 3u)) {
+        const HufD e = L.huf[brev_peek(r, tl)];
+        out[i++] = e.sym;
+        r.pos -= e.nb;
+    }
+    for (; i + 4 <= n; i += 4) {
+        uint32_t v = 0;
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const HufD e = L.huf[brev_peek(r, tl)];
+            v |= (uint32_t)e.sym << (8 * k);
+            r.pos -= e.nb;
+        }
+        *reinterpret_cast<uint32_t *>(out + i) = v;
+    }
+    for (; i < n; i++) {
+        const HufD e = L.huf[brev_peek(r, tl)];
+        out[i] = e.sym;
+        r.pos -= e.nb;
+    }
+    return r.pos == 0;
+}
+
+// ---- blocks -----------------------------------------------------------------
+
+// Compressed block [p, p + bs): literals section then sequences section.
+__device__ void check_compressed(Dec &D, DecLds &L, const uint8_t *p, uint32_t bs, uint8_t *scratch,
+                                 uint32_t lane) {
+    const uint8_t *end = p + bs;
+    // -- literals section header (3.1.1.3.1.1)
+    const uint32_t b0 = p[0];
+    const uint32_t ltype = b0 & 3u, sf = (b0 >> 2) & 3u;
+    uint32_t regen = 0, csize = 0, hdr = 0, nstreams = 1;
+    if (ltype < 2) {
+        if (sf == 0 || sf == 2) {
+            regen = b0 >> 3;
+            hdr = 1;
+        } else if (sf == 1) {
+            if (bs < 2) { D.bad = kCkCorrupt; return; }
+            regen = (b0 >> 4) | ((uint32_t)p[1] << 4);
+            hdr = 2;
+        } else {
+            if (bs < 3) { D.bad = kCkCorrupt; return; }
+            regen = (b0 >> 4) | ((uint32_t)p[1] << 4) | ((uint32_t)p[2] << 12);
+            hdr = 3;
+        }
+    } else {
+        nstreams = sf == 0 ? 1u : 4u;
+        if (sf < 2) {
+            if (bs < 3) { D.bad = kCkCorrupt; return; }
+            const uint32_t v = b0 | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16);
+            regen = (v >> 4) & 0x3FFu;
+            csize = (v >> 14) & 0x3FFu;
+            hdr = 3;
+        } else if (sf == 2) {
+            if (bs < 4) { D.bad = kCkCorrupt; return; }
+            const uint32_t v = b0 | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) |
+                               ((uint32_t)p[3] << 24);
+            regen = (v >> 4) & 0x3FFFu;
+            csize = v >> 18;
+            hdr = 4;
+        } else {
+            if (bs < 5) { D.bad = kCkCorrupt; return; }
+            const uint64_t v = b0 | ((uint64_t)p[1] << 8) | ((uint64_t)p[2] << 16) |
+                               ((uint64_t)p[3] << 24) | ((uint64_t)p[4] << 32);
+            regen = (uint32_t)((v >> 4) & 0x3FFFFu);
+            csize = (uint32_t)((v >> 22) & 0x3FFFFu);
+            hdr = 5;
+        }
+    }
+    if (regen > kBlockMax) { D.bad = kCkCorrupt; return; }
+    const uint8_t *lits = nullptr;  // the decoded literals (kind 0) or a byte (kind 1)
+    uint32_t lit_byte = 0;
+    int lkind = 0;
+    const uint8_t *q = p + hdr;
+    if (ltype == 0) {
+        if (q + regen > end) { D.bad = kCkCorrupt; return; }
+        lits = q;
+        q += regen;
+    } else if (ltype == 1) {
+        if (q + 1 > end) { D.bad = kCkCorrupt; return; }
+        lit_byte = q[0];
+        lkind = 1;
+        q += 1;
+    } else {
+        if (q + csize > end) { D.bad = kCkCorrupt; return; }
+        const uint8_t *cs = q;
+        int64_t clen = csize;
+        if (ltype == 2) {
+            uint32_t nw = 0;
+            const int tu = read_huf_weights(cs, clen, L, &nw, lane);
+            if (tu < 0) { D.bad = kCkCorrupt; return; }
+            D.huf_log = build_huf(L, nw, lane);
+            cs += tu;
+            clen -= tu;
+        } else if (D.huf_log == 0) {  // treeless: the previous block's table
+            D.bad = kCkCorrupt;
+            return;
+        }
+        const uint32_t tl = D.huf_log;
+        bool ok = true;
+        if (nstreams == 1) {
+            if (lane == 0) ok = huf_stream(L, tl, cs, clen, scratch, regen);
+        } else {
+            if (clen < 6) { D.bad = kCkCorrupt; return; }
+            const int64_t s1 = cs[0] | (cs[1] << 8), s2 = cs[2] | (cs[3] << 8),
+                          s3 = cs[4] | (cs[5] << 8);
+            const int64_t s4 = clen - 6 - s1 - s2 - s3;
+            const uint32_t seg = (regen + 3) / 4;
+            if (s4 < 0 || 3 * seg > regen) { D.bad = kCkCorrupt; return; }
+            if (lane < 4) {
+                const int64_t off = 6 + (lane > 0 ? s1 : 0) + (lane > 1 ? s2 : 0) + (lane > 2 ? s3 : 0);
+                const int64_t ln = lane == 0 ? s1 : lane == 1 ? s2 : lane == 2 ? s3 : s4;
+                const uint32_t n = lane < 3 ? seg : regen - 3 * seg;
+                ok = huf_stream(L, tl, cs + off, ln, scratch + lane * seg, n);
+            }
+        }
+        if (__builtin_amdgcn_ballot_w64(!ok)) { D.bad = kCkCorrupt; return; }
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+        __syncthreads();
+        lits = scratch;
+        q += csize;
+    }
+    // -- sequences section header (3.1.1.3.2.1)
+    if (q >= end) { D.bad = kCkCorrupt; return; }
+    uint32_t nseq = q[0];
+    if (nseq == 0) {
+        q += 1;
+    } else if (nseq < 128) {
+        q += 1;
+    } else if (nseq < 255) {
+        if (q + 2 > end) { D.bad = kCkCorrupt; return; }
+        nseq = ((nseq - 128) << 8) + q[1];
+        q += 2;
+    } else {
+        if (q + 3 > end) { D.bad = kCkCorrupt; return; }
+        nseq = q[1] + ((uint32_t)q[2] << 8) + 0x7F00u;
+        q += 3;
+    }
+    uint64_t litpos = 0;  // literals consumed
+    if (nseq) {
+        if (q >= end) { D.bad = kCkCorrupt; return; }
+        const uint32_t modes = *q++;
+        if (modes & 3u) { D.bad = kCkCorrupt; return; }
+        // tables in the order LL, OF, ML
+        for (int k = 0; k < 3; k++) {
+            const uint32_t mode = (modes >> (6 - 2 * k)) & 3u;
+            FseD *t = k == 0 ? L.ll : k == 1 ? L.of : L.ml;
+            uint32_t &al = k == 0 ? D.al_ll : k == 1 ? D.al_of : D.al_ml;
+            const uint32_t max_sym = k == 0 ? 35u : k == 1 ? 31u : 52u;
+            const uint32_t max_al = k == 0 ? 9u : k == 1 ? 8u : 9u;
+            if (mode == 0) {
+                const int16_t *nrm = k == 0 ? kLLNorm : k == 1 ? kOFNorm : kMLNorm;
+                const uint32_t ns = k == 0 ? 36u : k == 1 ? 29u : 53u;
+                const uint32_t a = k == 1 ? 5u : 6u;
+                if (!build_predefined(t, nrm, ns, a, L.norm, L.nxt, lane)) { D.bad = kCkCorrupt; return; }
+                al = a;
+            } else if (mode == 1) {
+                if (q >= end) { D.bad = kCkCorrupt; return; }
+                const uint32_t s = *q++;
+                if (s > max_sym) { D.bad = kCkCorrupt; return; }
+                if (lane == 0) {
+                    t[0].sym = (uint8_t)s;
+                    t[0].nb = 0;
+                    t[0].next = 0;
+                }
+                wsync();
+                al = 0;
+            } else if (mode == 2) {
+                uint32_t ns = 0, a = 0;
+                const int u = read_ncount(q, end - q, max_sym, max_al, L.norm, &ns, &a);
+                if (u < 0) { D.bad = kCkCorrupt; return; }
+                wsync();
+                if (!build_fse(t, L.norm, ns, a, L.nxt, lane)) { D.bad = kCkCorrupt; return; }
+                al = a;
+                q += u;
+            } else if (al == 255u) {  // repeat: needs an earlier table
+                D.bad = kCkCorrupt;
+                return;
+            }
+        }
+        BRev r;
+        if (!brev_init(r, q, end - q)) { D.bad = kCkCorrupt; return; }
+        uint32_t sll = (uint32_t)brev_bits(r, D.al_ll);
+        uint32_t sof = (uint32_t)brev_bits(r, D.al_of);
+        uint32_t sml = (uint32_t)brev_bits(r, D.al_ml);
+        uint32_t r0 = D.rep[0], r1 = D.rep[1], r2 = D.rep[2];
+        for (uint32_t s0 = 0; s0 < nseq; s0 += 64) {
+            const uint32_t nb = min(64u, nseq - s0);
+            uint32_t myll = 0, myml = 0, myoff = 0;
+            bool err = false;
+            for (uint32_t j = 0; j < nb; j++) {
+                const FseD eo = L.of[sof], el = L.ll[sll], em = L.ml[sml];
+                const uint32_t ofc = eo.sym, llc = el.sym, mlc = em.sym;
+                if (ofc > 31 || llc > 35 || mlc > 52) err = true;
+                const uint64_t ofv = (1ull << ofc) + brev_bits(r, ofc);
+                const uint32_t ml = kMLBase[mlc] + (uint32_t)brev_bits(r, kMLBits[mlc]);
+                const uint32_t ll = kLLBase[llc] + (uint32_t)brev_bits(r, kLLBits[llc]);
+                uint32_t off;
+                if (ofv > 3) {
+                    off = (uint32_t)(ofv - 3);
+                    r2 = r1;
+                    r1 = r0;
+                    r0 = off;
+                } else {
+                    const uint32_t idx = (uint32_t)ofv - 1u + (ll == 0 ? 1u : 0u);
+                    if (idx == 0) {
+                        off = r0;
+                    } else if (idx == 1) {
+                        off = r1;
+                        r1 = r0;
+                        r0 = off;
+                    } else if (idx == 2) {
+                        off = r2;
+                        r2 = r1;
+                        r1 = r0;
+                        r0 = off;
+                    } else {
+                        off = r0 - 1u;
+                        r2 = r1;
+                        r1 = r0;
+                        r0 = off;
+                    }
+                }
+                if (off == 0) err = true;
+                if (s0 + j + 1 < nseq) {
+                    sll = el.next + (uint32_t)brev_bits(r, el.nb);
+                    sml = em.next + (uint32_t)brev_bits(r, em.nb);
+                    sof = eo.next + (uint32_t)brev_bits(r, eo.nb);
+                }
+                if (lane == j) {
+                    myll = ll;
+                    myml = ml;
+                    myoff = off;
+                }
+            }
+            if (err || r.pos < 0) { D.bad = kCkCorrupt; return; }
+            // place the batch: exclusive prefix sums of ll and ll + ml
+            uint64_t incl_l = myll, incl_o = (uint64_t)myll + myml;
+            for (uint32_t d = 1; d < 64; d <<= 1) {
+                const uint64_t a = __shfl_up(incl_l, d), b = __shfl_up(incl_o, d);
+                if (lane >= d) {
+                    incl_l += a;
+                    incl_o += b;
+                }
+            }
+            const uint64_t lp = litpos + incl_l - myll;             // my literals
+            const uint64_t op = D.out + incl_o - myll - myml;       // my output position
+            const uint64_t tot_l = __shfl(incl_l, (int)nb - 1), tot_o = __shfl(incl_o, (int)nb - 1);
+            const bool mine = lane < nb;
+            // uniform verdicts: more literals than decoded or a match before
+            // the frame start (malformed), or longer than the blob (mismatch)
+            const bool c_lit = litpos + tot_l > regen;
+            const bool c_off = __builtin_amdgcn_ballot_w64(mine && (uint64_t)myoff > op + myll) != 0;
+            if (c_lit || c_off) { D.bad = kCkCorrupt; return; }
+            if (D.out + tot_o > D.dlen) { D.bad = kCkMismatch; return; }
+            const bool lng = mine && (uint64_t)myll + myml > 256;
+            bool eq = true;
+            if (mine && !lng) {
+                const uint8_t *dst = D.data + op;
+                eq = lane_cmp(dst, lits + lp, lit_byte, lkind, myll) &&
+                     lane_cmp(dst + myll, dst + myll - myoff, 0, 2, myml);
+            }
+            uint64_t longs = __builtin_amdgcn_ballot_w64(lng);
+            while (longs) {
+                const int L0 = __builtin_ctzll(longs);
+                longs &= longs - 1;
+                const uint64_t o = __shfl(op, L0), l0 = __shfl(lp, L0);
+                const uint32_t a = (uint32_t)__shfl((int)myll, L0), m = (uint32_t)__shfl((int)myml, L0),
+                               f = (uint32_t)__shfl((int)myoff, L0);
+                const uint8_t *dst = D.data + o;
+                const bool e1 = wave_cmp(dst, lits + l0, lit_byte, lkind, a, lane);
+                const bool e2 = wave_cmp(dst + a, dst + a - f, 0, 2, m, lane);
+                if (lane == (uint32_t)L0) eq = e1 && e2;
+            }
+            if (__builtin_amdgcn_ballot_w64(!eq)) { D.bad = kCkMismatch; return; }
+            litpos += tot_l;
+            D.out += tot_o;
+        }
+        if (r.pos != 0) { D.bad = kCkCorrupt; return; }
+        D.rep[0] = r0;
+        D.rep[1] = r1;
+        D.rep[2] = r2;
+    } else if (q != end) {
+        D.bad = kCkCorrupt;
+        return;
+    }
+    // the remaining literals
+    const uint64_t rest = regen - litpos;
+    if (D.out + rest > D.dlen) { D.bad = kCkMismatch; return; }
+    if (!wave_cmp(D.data + D.out, lits + litpos, lit_byte, lkind, rest, lane)) {
+        D.bad = kCkMismatch;
+        return;
+    }
+    D.out += rest;
+}
+
+// One frame; returns its status.
+__device__ uint32_t check_frame(const uint8_t *f, uint64_t flen, const uint8_t *data, uint64_t dlen,
+                                DecLds &L, uint8_t *scratch, uint32_t lane) {
+    const uint8_t *end = f + flen;
+    if (flen < 6) return kCkCorrupt;
+    const uint32_t magic = f[0] | (f[1] << 8) | (f[2] << 16) | ((uint32_t)f[3] << 24);
+    if (magic != 0xFD2FB528u) return kCkCorrupt;
+    const uint32_t fhd = f[4];
+    const uint32_t fcs_flag = fhd >> 6, single = (fhd >> 5) & 1u, cksum = (fhd >> 2) & 1u,
+                   did_flag = fhd & 3u;
+    if (fhd & 8u) return kCkCorrupt;  // reserved bit
+    const uint8_t *q = f + 5;
+    if (!single) q += 1;  // window descriptor
+    const uint32_t did_len = did_flag == 0 ? 0 : did_flag == 1 ? 1 : did_flag == 2 ? 2 : 4;
+    if (q + did_len > end) return kCkCorrupt;
+    uint32_t did = 0;
+    for (uint32_t i = 0; i < did_len; i++) did |= (uint32_t)q[i] << (8 * i);
+    if (did) return kCkCorrupt;  // dictionaries: not supported
+    q += did_len;
+    const uint32_t fcs_len = fcs_flag == 0 ? (single ? 1 : 0) : fcs_flag == 1 ? 2 : fcs_flag == 2 ? 4 : 8;
+    if (q + fcs_len > end) return kCkCorrupt;
+    uint64_t fcs = 0;
+    for (uint32_t i = 0; i < fcs_len; i++) fcs |= (uint64_t)q[i] << (8 * i);
+    if (fcs_len == 2) fcs += 256;
+    q += fcs_len;
+    if (fcs_len && fcs != dlen) return kCkMismatch;
+    Dec D;
+    D.data = data;
+    D.dlen = dlen;
+    D.out = 0;
+    D.rep[0] = 1;
+    D.rep[1] = 4;
+    D.rep[2] = 8;
+    D.huf_log = 0;
+    D.al_ll = D.al_ml = D.al_of = 255u;
+    D.bad = kCkOk;
+    for (;;) {
+        if (q + 3 > end) return kCkCorrupt;
+        const uint32_t bh = q[0] | (q[1] << 8) | ((uint32_t)q[2] << 16);
+        q += 3;
+        const uint32_t last = bh & 1u, btype = (bh >> 1) & 3u, bsize = bh >> 3;
+        if (btype == 3) return kCkCorrupt;
+        if (btype == 0) {
+            if (bsize > kBlockMax || q + bsize > end) return kCkCorrupt;
+            if (D.out + bsize > dlen) return kCkMismatch;
+            if (!wave_cmp(data + D.out, q, 0, 0, bsize, lane)) return kCkMismatch;
+            D.out += bsize;
+            q += bsize;
+        } else if (btype == 1) {
+            if (bsize > kBlockMax || q + 1 > end) return kCkCorrupt;
+            if (D.out + bsize > dlen) return kCkMismatch;
+            if (!wave_cmp(data + D.out, nullptr, q[0], 1, bsize, lane)) return kCkMismatch;
+            D.out += bsize;
+            q += 1;
+        } else {
+            if (bsize > kBlockMax || bsize == 0 || q + bsize > end) return kCkCorrupt;
+            check_compressed(D, L, q, bsize, scratch, lane);
+            if (D.bad) return D.bad;
+            q += bsize;
+        }
+        if (last) break;
+    }
+    if (cksum) q += 4;
+    if (q != end) return kCkCorrupt;  // a second frame or trailing bytes
+    return D.out == dlen ? kCkOk : kCkMismatch;
+}
+
+}  // namespace
+
+// refs: frame_off, frame_len, data_off, data_len (rcdc_zstd_check_ref);
+// order: the queue order; ctr: the queue counter (zeroed by the host).
+__global__ __launch_bounds__(64) void rcdc_zstd_check_kernel(
+    const uint8_t *__restrict__ frames, const uint8_t *__restrict__ data,
+    const ulonglong4 *__restrict__ refs, const uint32_t *__restrict__ order, uint32_t n,
+    uint32_t stored, uint8_t *scratch, uint32_t *__restrict__ status, uint32_t *ctr) {
+    __shared__ DecLds L;
+    const uint32_t lane = threadIdx.x;
+    uint8_t *scr = scratch + (uint64_t)blockIdx.x * (kBlockMax + 64);
+    for (;;) {
+        uint32_t k = 0;
+        if (lane == 0) k = atomicAdd(ctr, 1u);
+        k = __builtin_amdgcn_readfirstlane(__shfl(k, 0));
+        if (k >= n) break;
+        const uint32_t i = order[k];
+        const ulonglong4 r = refs[i];
+        uint32_t st;
+        if (stored)  // plain bytes: equal length and bytes
+            st = r.y != r.w ? kCkMismatch
+                            : (wave_cmp(data + r.z, frames + r.x, 0, 0, r.w, lane) ? kCkOk : kCkMismatch);
+        else
+            st = check_frame(frames + r.x, r.y, data + r.z, r.w, L, scr, lane);
+        if (lane == 0) status[i] = st;
+        __syncthreads();  // LDS tables are rebuilt by the next frame
+    }
+}
+
+namespace rcdc {
+
+uint64_t zstd_check_scratch_bytes(uint32_t grid) { return (uint64_t)grid * (kBlockMax + 64); }
+
+hipError_t launch_zstd_check(const uint8_t *frames, const uint8_t *data, const void *refs,
+                             const uint32_t *order, uint32_t n, bool stored, uint8_t *scratch,
+                             uint32_t grid, uint32_t *status, uint32_t *ctr, hipStream_t stream) {
+    if (n == 0) return hipSuccess;
+    const uint32_t g = n < grid ? n : grid;
+    hipLaunchKernelGGL(rcdc_zstd_check_kernel, dim3(g), dim3(64), 0, stream, frames, data,
+                       (const ulonglong4 *)refs, order, n, stored ? 1u : 0u, scratch, status, ctr);
+    return hipGetLastError();
+}
+
+}  // namespace rcdc
+
+// ---- range copies (pack files from blobs sealed elsewhere: packer.rs
+// add_raw, :615-655) -----------------------------------------------------------
+// Unit k copies len bytes from in + src to out + dst (any alignments): the
+// output's 16-aligned body in dwordx4 stores of bytes loaded at any alignment
+// (five dwords + v_alignbit), the ragged head and tail byte by byte.
+
+namespace {
+
+typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ u32x4v ld16u(const uint8_t *p) {
+    const uint32_t b = (uint32_t)(uintptr_t)p & 3u, sh = b * 8u;
+    const uint32_t *w = (const uint32_t *)(p - b);
+    const uint32_t w0 = w[0], w1 = w[1], w2 = w[2], w3 = w[3];
+    const uint32_t w4 = w[b ? 4 : 3];
+    u32x4v v;
+    v.x = __builtin_amdgcn_alignbit(w1, w0, sh);
+    v.y = __builtin_amdgcn_alignbit(w2, w1, sh);
+    v.z = __builtin_amdgcn_alignbit(w3, w2, sh);
+    v.w = __builtin_amdgcn_alignbit(w4, w3, sh);
+    return v;
+}
+
+}  // namespace
+
+__global__ __launch_bounds__(256) void rcdc_copy_ranges_kernel(const uint8_t *__restrict__ in,
+                                                               uint8_t *__restrict__ out,
+                                                               const ulonglong4 *__restrict__ units,
+                                                               uint32_t n) {
+    const uint32_t t = threadIdx.x;
+    for (uint32_t k = blockIdx.x; k < n; k += gridDim.x) {
+        const ulonglong4 u = units[k];  // src, dst, len
+        const uint8_t *s = in + u.x;
+        uint8_t *d = out + u.y;
+        const uint64_t len = u.z;
+        uint32_t head = (uint32_t)((16u - ((uintptr_t)d & 15u)) & 15u);
+        if (head > len) head = (uint32_t)len;
+        if (t < head) d[t] = s[t];
+        const uint64_t body = (len - head) / 16;
+        const uint8_t *sb = s + head;
+        u32x4v *db = reinterpret_cast<u32x4v *>(d + head);
+        uint64_t i = t;
+        for (; i + 768 < body; i += 1024) {
+            const u32x4v v0 = ld16u(sb + 16 * i), v1 = ld16u(sb + 16 * (i + 256)),
+                        v2 = ld16u(sb + 16 * (i + 512)), v3 = ld16u(sb + 16 * (i + 768));
+            __builtin_nontemporal_store(v0, db + i);
+            __builtin_nontemporal_store(v1, db + i + 256);
+            __builtin_nontemporal_store(v2, db + i + 512);
+            __builtin_nontemporal_store(v3, db + i + 768);
+        }
+        for (; i < body; i += 256) __builtin_nontemporal_store(ld16u(sb + 16 * i), db + i);
+        const uint64_t done = head + 16 * body;
+        if (t < len - done) d[done + t] = s[done + t];
+    }
+}
+
+namespace rcdc {
+
+hipError_t launch_copy_ranges(const uint8_t *in, uint8_t *out, const void *units, uint32_t n,
+                              uint32_t cus, hipStream_t stream) {
+    if (n == 0) return hipSuccess;
+    const uint32_t g = n < cus * 8u ? n : cus * 8u;
+    hipLaunchKernelGGL(rcdc_copy_ranges_kernel, dim3(g), dim3(256), 0, stream, in, out,
+                       (const ulonglong4 *)units, n);
+    return hipGetLastError();
+}
+
+}  // namespace rcdc

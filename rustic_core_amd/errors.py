@@ -15,6 +15,7 @@ class ErrorKind(enum.Enum):
     Internal = "Internal"            # device / runtime failure
     InputOutput = "InputOutput"      # rabin.rs:131-138,174-180 (reader errors)
     Cryptography = "Cryptography"    # crypto/aespoly1305.rs:89-108 (MAC check)
+    Verification = "Verification"    # backend/decrypt.rs:516-526 (extra_verify)
 
 
 class RusticError(Exception):

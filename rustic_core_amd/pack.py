@@ -122,14 +122,15 @@ def make_blobs(in_offs, lens, ids, nonces, types=None, uncompressed=None) -> np.
 
 
 def pack_layout(blobs: np.ndarray, groups: Sequence[Tuple[int, int]], header_nonces,
-                align: int = 1) -> Tuple[np.ndarray, int]:
+                align: int = 1, raw: bool = False) -> Tuple[np.ndarray, int]:
     """rcdc_pack array for `groups`, packed back to back in one output
-    buffer (each pack `align`-aligned); returns (packs, total bytes)."""
+    buffer (each pack `align`-aligned); returns (packs, total bytes).
+    ``raw``: blobs["len"] are sealed lengths already (build_packs raw)."""
     packs = np.zeros(len(groups), PACK)
     o = 0
     for k, (b0, n) in enumerate(groups):
         sel = blobs[b0:b0 + n]
-        size = int(np.sum(sel["len"].astype(np.int64) + 32))
+        size = int(np.sum(sel["len"].astype(np.int64) + (0 if raw else 32)))
         size += int(np.sum(np.where(sel["uncompressed_len"] > 0, 41, 37))) + 32 + 4
         packs[k]["out_off"] = o
         packs[k]["blob0"] = b0
@@ -140,19 +141,21 @@ def pack_layout(blobs: np.ndarray, groups: Sequence[Tuple[int, int]], header_non
 
 
 def build_packs(ctx, key: bytes, d_in: int, blobs: np.ndarray, packs: np.ndarray, d_out: int,
-                out_len: int, hip_stream: Optional[int] = None) -> np.ndarray:
+                out_len: int, hip_stream: Optional[int] = None, raw: bool = False) -> np.ndarray:
     """rcdc_pack_build: fills packs["size"], packs["header_len"] and returns
     each blob's offset in its pack (IndexBlob location.offset; length =
-    len + 32)."""
+    len + 32).  ``raw`` (rcdc_pack_build_raw, packer.rs add_raw): the blobs
+    at in_off are sealed already and blobs["len"] is their sealed length;
+    they are copied, only the headers are sealed."""
     blobs = np.ascontiguousarray(blobs, PACK_BLOB)
     if not (packs.flags["C_CONTIGUOUS"] and packs.dtype == PACK):
         raise TypeError("packs must be a C-contiguous PACK array (it receives the sizes)")
     offs = np.zeros(max(len(blobs), 1), np.uint32)
     kb = (ctypes.c_uint8 * 64).from_buffer_copy(bytes(key))
-    st = _lib.lib().rcdc_pack_build(ctx.handle, kb, ctypes.c_void_p(d_in), blobs.ctypes.data,
-                                    len(blobs), packs.ctypes.data, len(packs),
-                                    ctypes.c_void_p(d_out), int(out_len), offs.ctypes.data,
-                                    ctypes.c_void_p(hip_stream or 0))
+    fn = _lib.lib().rcdc_pack_build_raw if raw else _lib.lib().rcdc_pack_build
+    st = fn(ctx.handle, kb, ctypes.c_void_p(d_in), blobs.ctypes.data, len(blobs),
+            packs.ctypes.data, len(packs), ctypes.c_void_p(d_out), int(out_len),
+            offs.ctypes.data, ctypes.c_void_p(hip_stream or 0))
     if st:
         raise status_error(st, _lib.last_error())
     return offs[:len(blobs)]

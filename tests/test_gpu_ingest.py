@@ -1,0 +1,209 @@
+"""The device ingest path (rustic_core_amd/ingest.py): chunk -> blob ids ->
+dedup -> zstd -> seal -> verify -> packs, for streams in HBM.
+
+Reference: archiver/file_archiver.rs:138-168 (chunk + id per chunk),
+blob/packer.rs:304-315 (dedup by id against the index and the packer),
+backend/decrypt.rs:566-572 + 508-529 (process_data + very_data),
+blob/packer.rs:615-735 (add_raw, the sealed header), index/indexer.rs.
+
+Checked against the oracle: every cut (oracle/cdc_ref), every id (hashlib
+over the oracle's chunks), the dedup decision (first occurrence in chunk
+order, minus what the index holds), and every pack file parsed and opened
+by oracle.parse_pack / oracle.open_ with each blob decoded by libzstd back
+to its chunk.
+"""
+import hashlib
+
+import numpy as np
+import pytest
+
+from oracle import oracle, zstd_ref as zr
+
+pytestmark = pytest.mark.gpu
+
+MiB = 1 << 20
+
+
+def _streams(seed=1, n=8):
+    """Mixed streams (random runs, zero runs, text runs); stream 5 repeats
+    stream 1 and stream 7 starts with stream 2's first 6 MiB, so whole
+    chunks repeat across streams."""
+    rng = np.random.default_rng(seed)
+    words = [bytes(rng.integers(97, 123, int(rng.integers(2, 9))).astype(np.uint8))
+             for _ in range(300)]
+    text = b" ".join(words[int(j)] for j in rng.integers(0, 300, (8 * MiB) // 5))
+    datas = []
+    for i in range(n):
+        size = int(rng.integers(6 * MiB, 40 * MiB))
+        out = bytearray()
+        while len(out) < size:
+            k = int(rng.integers(64 << 10, 6 * MiB))
+            c = int(rng.integers(0, 3))
+            if c == 0:
+                out += rng.integers(0, 256, k, dtype=np.uint8).tobytes()
+            elif c == 1:
+                out += bytes(k)
+            else:
+                a = int(rng.integers(0, len(text) - k))
+                out += text[a:a + k]
+        datas.append(bytes(out[:size]))
+    datas[5] = datas[1]
+    datas[7] = datas[2][:6 * MiB] + datas[7][6 * MiB:]
+    return datas
+
+
+def _arena(datas):
+    import torch
+    from rustic_core_amd.device import pack_offsets
+    lens = [len(d) for d in datas]
+    offs, total = pack_offsets(lens)
+    host = np.zeros(total, np.uint8)
+    for o, d in zip(offs, datas):
+        host[int(o):int(o) + len(d)] = np.frombuffer(d, np.uint8)
+    return host, torch.from_numpy(host).to("cuda:0"), offs, lens
+
+
+def _ingest(version, indexed=None, extra_verify=None, key=bytes(range(64)), seed=1):
+    from rustic_core_amd.chunker import ConfigFile
+    from rustic_core_amd.crypto import Key
+    from rustic_core_amd.ingest import DeviceIngest
+    cfg = ConfigFile.new(version, oracle.DEFAULT_POLY)
+    datas = _streams(seed)
+    host, arena, offs, lens = _arena(datas)
+    ing = DeviceIngest(cfg, Key(key), indexed=indexed, extra_verify=extra_verify)
+    res = ing.ingest(arena, offs, lens)
+    return ing, res, host, offs, lens, datas
+
+
+def _check_result(res, host, offs, lens, key, compressed, known=frozenset()):
+    from rustic_core_amd.chunker import ConfigFile
+    from rustic_core_amd.pack import PackSizer, group_blobs
+    # cuts and ids against the oracle
+    chunks = []
+    for i, (o, n) in enumerate(zip(offs, lens)):
+        exp = oracle.chunk_cuts(host[int(o):int(o) + n])
+        assert np.array_equal(res.cuts[i], exp), i
+        prev = 0
+        for c in exp:
+            chunks.append(host[int(o) + prev:int(o) + int(c)].tobytes())
+            prev = int(c)
+    assert len(chunks) == len(res.ids)
+    ids = [hashlib.sha256(c).digest() for c in chunks]
+    assert [bytes(x) for x in res.ids] == ids
+    # dedup: first occurrence in chunk order, not in the index
+    seen, exp_new = set(known), []
+    for bid in ids:
+        exp_new.append(bid not in seen)
+        seen.add(bid)
+    assert res.new.tolist() == exp_new
+    new_chunks = [c for c, f in zip(chunks, exp_new) if f]
+    # pack grouping as the packer's PackSizer would
+    ulens = [len(c) for c in new_chunks] if compressed else [0] * len(new_chunks)
+    grp = group_blobs([int(x) - 32 for x in res.blobs["len"]],
+                      PackSizer.from_config(ConfigFile.new(2, oracle.DEFAULT_POLY), 0, 0), ulens)
+    assert [(int(p["blob0"]), int(p["nblobs"])) for p in res.pack_table] == grp
+    # every pack parsed, every blob opened and decoded back to its chunk
+    k = 0
+    for j in range(len(res.pack_table)):
+        f = res.pack_file(j)
+        assert len(f) == int(res.pack_table[j]["size"])
+        parsed = oracle.parse_pack(key, f)
+        assert len(parsed) == int(res.pack_table[j]["nblobs"])
+        for tpe, off, ln, ulen, bid in parsed:
+            assert tpe == 0 and off == int(res.blob_offsets[k])
+            plain = oracle.open_(key, f[off:off + ln])
+            data = zr.decompress(plain) if compressed else plain
+            assert data == new_chunks[k], k
+            assert bytes(bid) == hashlib.sha256(data).digest()
+            assert ulen == (len(data) if compressed else 0)
+            k += 1
+    assert k == len(new_chunks)
+    return chunks, ids, new_chunks
+
+
+def test_ingest_v2_matches_oracle():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    key = bytes(range(64))
+    ing, res, host, offs, lens, _ = _ingest(2, key=key)
+    chunks, ids, new_chunks = _check_result(res, host, offs, lens, key, compressed=True)
+    assert len(new_chunks) < len(chunks)  # the repeated streams dedup
+    assert (np.asarray(res.chunk_lens) > ing.long_chunk).any()  # both id launches ran
+    # index packs (Indexer::add input) carry the blobs' locations
+    ips = res.index_packs()
+    assert sum(len(p.blobs) for p in ips) == len(new_chunks)
+    for p, row in zip(ips, res.pack_table):
+        assert p.pack_size() == int(row["size"])
+    # a second backup of the same bytes: everything is in the index
+    _, res2, _, _, _, _ = _ingest(2, indexed=set(ids), key=key)
+    assert not res2.new.any() and len(res2.pack_table) == 0
+    ing.close()
+
+
+def test_ingest_partly_indexed_and_v1():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    key = bytes(range(1, 65))
+    # ids of a different seed's first stream are "in the index" too: none match;
+    # half of this batch's own ids are known
+    _, res, host, offs, lens, _ = _ingest(2, key=key, seed=3)
+    ids = [bytes(x) for x in res.ids]
+    known = set(ids[::2])
+    _, res2, host2, offs2, lens2, _ = _ingest(2, indexed=set(known), key=key, seed=3)
+    _check_result(res2, host2, offs2, lens2, key, compressed=True, known=known)
+    # version 1: stored blobs, verified as stored bytes; verify off too
+    for ev in (None, False):
+        _, res3, host3, offs3, lens3, _ = _ingest(1, extra_verify=ev, key=key, seed=4)
+        _check_result(res3, host3, offs3, lens3, key, compressed=False)
+
+
+def test_pack_build_raw_matches_sealed_build(gpu_ctx):
+    """rcdc_pack_build_raw (add_raw: blobs sealed elsewhere) gives the same
+    pack bytes as rcdc_pack_build sealing them in place."""
+    import torch
+    from rustic_core_amd.crypto import Key, make_refs, sealed_layout
+    from rustic_core_amd.pack import build_packs, make_blobs, pack_layout
+    rng = np.random.default_rng(21)
+    key = rng.integers(0, 256, 64, dtype=np.uint8).tobytes()
+    lens = [0, 1, 15, 17, 1000, 65537, 3, 1 << 20, 2 * MiB + 5, 31]
+    datas = [rng.integers(0, 256, n, dtype=np.uint8).tobytes() for n in lens]
+    offs, o = [], 0
+    for d in datas:
+        o += int(rng.integers(0, 16))
+        offs.append(o)
+        o += len(d)
+    host = np.zeros(o + 64, np.uint8)
+    for a, d in zip(offs, datas):
+        host[a:a + len(d)] = np.frombuffer(d, np.uint8)
+    d_in = torch.from_numpy(host).to("cuda:0")
+    nonces = rng.integers(0, 256, (len(lens), 16), dtype=np.uint8)
+    ids = rng.integers(0, 256, (len(lens), 32), dtype=np.uint8)
+    ulen = [n + 7 if i % 3 == 0 else 0 for i, n in enumerate(lens)]
+    groups, hn = [(0, 4), (4, 5), (9, 1)], rng.integers(0, 256, (3, 16), dtype=np.uint8)
+    # in place
+    blobs = make_blobs(offs, lens, ids, nonces, uncompressed=ulen)
+    packs, total = pack_layout(blobs, groups, hn, align=3)
+    out1 = torch.zeros(total + 64, dtype=torch.uint8, device="cuda:0")
+    off1 = build_packs(gpu_ctx, key, d_in.data_ptr(), blobs, packs, out1.data_ptr(), total)
+    # sealed first (at odd staging offsets), then add_raw
+    s_offs, s_tot = sealed_layout(lens)
+    s_offs = s_offs + np.arange(len(lens), dtype=np.uint64) * 3
+    staging = torch.zeros(s_tot + 64 + 3 * len(lens), dtype=torch.uint8, device="cuda:0")
+    Key(key).seal_blobs(d_in.data_ptr(), make_refs(offs, lens, s_offs, nonces),
+                        staging.data_ptr(), None, gpu_ctx)
+    rblobs = make_blobs(s_offs, [n + 32 for n in lens], ids, np.zeros_like(nonces),
+                        uncompressed=ulen)
+    rpacks, rtotal = pack_layout(rblobs, groups, hn, align=3, raw=True)
+    assert rtotal == total
+    out2 = torch.full((total + 64,), 7, dtype=torch.uint8, device="cuda:0")
+    off2 = build_packs(gpu_ctx, key, staging.data_ptr(), rblobs, rpacks, out2.data_ptr(), total,
+                       raw=True)
+    torch.cuda.synchronize()
+    assert np.array_equal(off1, off2)
+    assert np.array_equal(packs["size"], rpacks["size"])
+    a, b = out1.cpu().numpy(), out2.cpu().numpy()
+    for p in packs:
+        s, n = int(p["out_off"]), int(p["size"])
+        assert np.array_equal(a[s:s + n], b[s:s + n])
