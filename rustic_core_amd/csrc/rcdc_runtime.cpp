@@ -72,6 +72,8 @@ hipError_t launch_zstd(const uint8_t *in, uint8_t *out, const ZstdBlob *blobs, u
                        uint64_t *seqbuf, uint32_t grid, uint2 *res, uint64_t *bpos,
                        uint64_t *out_lens, uint32_t *queue, hipStream_t stream);
 uint64_t zstd_check_scratch_bytes(uint32_t grid);
+hipError_t launch_plan_set_len(StreamDesc *sds, ScanItem *items, uint32_t nitems, uint64_t n,
+                               uint64_t nseg, hipStream_t stream);
 hipError_t launch_copy_ranges(const uint8_t *in, uint8_t *out, const void *units, uint32_t n,
                               uint32_t cus, hipStream_t stream);
 hipError_t launch_zstd_check(const uint8_t *frames, const uint8_t *data, const void *refs,
@@ -146,6 +148,9 @@ struct rcdc_plan {
     uint32_t seg_bytes = 0;
     uint32_t blocks = 0;
     uint64_t nseg = 0, ncuts = 0, scanned = 0;
+    // capacity plans (single-stream host passes): the scan runs the first
+    // run_items items (0: all) on run_blocks workgroups; set by plan_set_len
+    uint32_t run_items = 0, run_blocks = 0;
     std::vector<ScanItem> items;
     std::vector<StreamDesc> sds;
     std::vector<uint64_t> cut_base;
@@ -168,6 +173,7 @@ struct rcdc_plan {
              cap_counts = 0;
     // walk path (long streams, rcdc_walk.hip)
     bool no_walk = false;             // force the scan path (fallback re-runs)
+    bool no_pieces = false;           // one resolve unit per stream (capacity plans)
     std::vector<WalkUnit> wunits;
     std::vector<uint32_t> wstream_u0;  // unit0 of every walked stream
     std::vector<uint32_t> worder;      // walk queue order (big pieces first)
@@ -250,14 +256,16 @@ struct rcdc_plan {
 // (archiver.rs:195) run on separate streams without a context-wide lock.
 struct Lane {
     hipStream_t stream = nullptr;
-    hipEvent_t ev[2] = {nullptr, nullptr};
-    uint8_t *pinned[2] = {nullptr, nullptr};
+    hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+    uint8_t *pinned[4] = {nullptr, nullptr, nullptr, nullptr};
+    uint32_t nslots = 2;
     uint64_t stage = 0;  // bytes per staging slot
     uint8_t *d_arena = nullptr;
     uint64_t arena_cap = 0;
     rcdc_plan *plan = nullptr;
     std::vector<uint64_t> lay_offs, lay_lens;  // layout of the cached plan
     uint64_t lay_arena = 0;
+    bool lay_cap = false;  // a capacity plan (one stream, length set per pass)
 };
 
 struct rcdc_ctx {
@@ -328,6 +336,7 @@ struct rcdc_stream {
     // when valid, 0 otherwise)
     uint8_t *d_tail = nullptr;  // from the context's pool, ctx->max + 256 bytes
     uint64_t tail_len = 0;
+    hipEvent_t tail_ev = nullptr;  // the copy into d_tail (on the last pass's lane stream)
 };
 
 namespace {
@@ -444,7 +453,7 @@ void build_resolve_units(rcdc_plan *pl, uint64_t mn) {
         if (pl->walked[i]) continue;
         const StreamDesc &d = pl->sds[i];
         const uint64_t N = d.n;
-        const uint64_t Lp = piece_bytes(N, mn);
+        const uint64_t Lp = pl->no_pieces ? 0 : piece_bytes(N, mn);
         if (Lp == 0 || N <= 2 * Lp) {
             ResolveUnit u{};
             u.start = 0;
@@ -789,8 +798,9 @@ rcdc_status plan_run(rcdc_plan *pl, const void *d_arena, hipStream_t stream) {
         if (pl->res_pending[set]) HIP_TRY(hipStreamWaitEvent(stream, pl->ev_res[set], 0));
     }
     if (ev) HIP_TRY(hipEventRecord(ev[0], stream));
-    HIP_TRY(launch_scan(ctx->variant, (const uint8_t *)d_arena, pl->d_items, (uint32_t)pl->items.size(),
-                        ctx->d_tables, sp, sums, masks, pl->blocks, stream));
+    HIP_TRY(launch_scan(ctx->variant, (const uint8_t *)d_arena, pl->d_items,
+                        pl->run_items ? pl->run_items : (uint32_t)pl->items.size(), ctx->d_tables,
+                        sp, sums, masks, pl->run_items ? pl->run_blocks : pl->blocks, stream));
     const uint32_t cus = (uint32_t)std::max(ctx->num_cus, 1);
     static const bool dbg = getenv("RCDC_DEBUG_SYNC") != nullptr;  // stage-by-stage sync
     if (dbg) {
@@ -1067,7 +1077,7 @@ void lane_free(rcdc_ctx *ctx, Lane *L) {
     DeviceGuard g(ctx->device);
     if (L->stream) (void)hipStreamSynchronize(L->stream);
     plan_free(L->plan);
-    for (int k = 0; k < 2; k++) {
+    for (int k = 0; k < 4; k++) {
         if (L->ev[k]) (void)hipEventDestroy(L->ev[k]);
         if (L->pinned[k]) (void)hipHostFree(L->pinned[k]);
     }
@@ -1091,7 +1101,7 @@ rcdc_status lane_acquire(rcdc_ctx *ctx, Lane **out) {
     lk.unlock();
     DeviceGuard g(ctx->device);
     hipError_t e = hipStreamCreateWithFlags(&L->stream, hipStreamNonBlocking);
-    for (int k = 0; k < 2 && e == hipSuccess; k++)
+    for (int k = 0; k < 4 && e == hipSuccess; k++)
         e = hipEventCreateWithFlags(&L->ev[k], hipEventDisableTiming);
     if (e != hipSuccess) {
         std::lock_guard<std::mutex> lk2(ctx->pool_mu);
@@ -1110,7 +1120,55 @@ void lane_release(rcdc_ctx *ctx, Lane *L) {
     ctx->pool_cv.notify_one();
 }
 
-constexpr uint64_t kStageBytes = 16ull << 20;  // per pinned staging slot
+// pinned staging per lane: 4 slots of 4 MiB (a 16-24 MiB stream pass's host
+// copies run ahead of its own DMA; 2 x 16 MiB: 40-46 GiB/s, 4 x 4 MiB:
+// 46.5-47.5 GiB/s through rcdc_stream_feed, tools/gpu_abi.sh)
+constexpr uint64_t kStageBytes = 4ull << 20;
+
+// RCDC_STAGE_MIB / RCDC_STAGE_SLOTS: staging slot size and count per lane
+// (A/B runs; smaller slots overlap a pass's host copy with its own DMA, more
+// slots let the copies run further ahead of the DMA)
+static uint64_t stage_bytes() {
+    static const uint64_t b = getenv("RCDC_STAGE_MIB")
+                                  ? std::max<uint64_t>((uint64_t)atoll(getenv("RCDC_STAGE_MIB")), 1) << 20
+                                  : kStageBytes;
+    return b;
+}
+
+static uint32_t stage_slots() {
+    static const uint32_t k = getenv("RCDC_STAGE_SLOTS")
+                                  ? std::min<uint32_t>(std::max(atoi(getenv("RCDC_STAGE_SLOTS")), 2), 4)
+                                  : 4u;
+    return k;
+}
+
+// Capacity class of a single-stream host pass: a lane's plan is built for
+// the class and reused for every length in it (the stream path's passes are
+// 16 MiB plus a tail of up to max bytes: a plan per exact length rebuilt it
+// on almost every pass).  Up to 64 MiB, built without walk pieces or
+// resolver pieces (one resolve wave per pass: a few tens of hops).
+static uint64_t cap_class(const rcdc_ctx *ctx, uint64_t n) {
+    const uint64_t c = round_up(std::max<uint64_t>(n, 1), 8ull << 20);
+    (void)ctx;
+    return c <= (64ull << 20) ? c : 0;
+}
+
+// The plan (built for a capacity of one stream) set to length n: the
+// stream's descriptor and the first items' end position on the device
+// (values as kernel arguments: nothing to copy), and the items the scan runs.
+static rcdc_status plan_set_len(rcdc_plan *pl, uint64_t n, hipStream_t st) {
+    const StreamDesc &d = pl->sds[0];
+    const uint64_t pos_lo = pl->ctx->min + kWindow;
+    uint64_t nseg = 0;
+    if (n > pos_lo && d.nseg) nseg = std::min<uint64_t>(d.nseg, (n - d.pos0 + pl->seg_bytes - 1) / pl->seg_bytes);
+    const uint32_t nit = (uint32_t)((nseg + 63) / 64);
+    pl->run_items = nit ? nit : 1;  // (an all-masked item when there is nothing to scan)
+    const uint32_t waves = pl->run_items;
+    pl->run_blocks = std::min<uint32_t>((waves + 15) / 16, (uint32_t)std::max(pl->ctx->num_cus, 1));
+    HIP_TRY(launch_plan_set_len(pl->d_sds, pl->d_items, nit ? nit : (uint32_t)std::min<size_t>(1, pl->items.size()),
+                                n, nseg, st));
+    return RCDC_OK;
+}
 
 // Host-path phase timing (RCDC_HOST_PROFILE=1: summary on stderr when the
 // context is destroyed): staging copies, waits for a staging slot, plan
@@ -1144,7 +1202,7 @@ struct HostPiece {
 rcdc_status run_host_pieces(rcdc_ctx *ctx, Lane *L, const std::vector<uint64_t> &lens,
                             const std::vector<HostPiece> &pieces, uint64_t *cuts, uint64_t cap,
                             uint64_t *counts, const uint8_t *d_prefix = nullptr,
-                            uint64_t prefix_len = 0) {
+                            uint64_t prefix_len = 0, hipEvent_t prefix_ready = nullptr) {
     const uint32_t n = (uint32_t)lens.size();
     std::vector<uint64_t> offs(n);
     uint64_t total = 0;
@@ -1153,25 +1211,34 @@ rcdc_status run_host_pieces(rcdc_ctx *ctx, Lane *L, const std::vector<uint64_t> 
         total = round_up(total + lens[i], 256);
     }
     const uint64_t arena_len = total + 256;
+    // one stream short of pieces and walk: a plan per capacity class, set
+    // to this pass's length on the device; otherwise a plan per exact layout
+    static const bool capacity = !getenv("RCDC_EXACT_PLANS");
+    const uint64_t cap1 = (capacity && n == 1) ? cap_class(ctx, lens[0]) : 0;
+    std::vector<uint64_t> klens = cap1 ? std::vector<uint64_t>{cap1} : lens;
+    const uint64_t karena = cap1 ? round_up(cap1, 256) + 256 : arena_len;
     DeviceGuard g(ctx->device);
     rcdc_status st;
-    if ((st = ensure_dev(&L->d_arena, &L->arena_cap, arena_len))) return st;
+    if ((st = ensure_dev(&L->d_arena, &L->arena_cap, std::max(arena_len, karena)))) return st;
     if (!L->pinned[0]) {
-        L->stage = kStageBytes;
-        for (int k = 0; k < 2; k++)
+        L->stage = stage_bytes();
+        L->nslots = stage_slots();
+        for (uint32_t k = 0; k < L->nslots; k++)
             HIP_TRY(hipHostMalloc((void **)&L->pinned[k], L->stage, hipHostMallocDefault));
     }
     uint64_t t_copy = 0, t_wait = 0, t0 = g_hprof_on ? now_ns() : 0;
-    if (prefix_len)
+    if (prefix_len) {
+        if (prefix_ready) HIP_TRY(hipStreamWaitEvent(L->stream, prefix_ready, 0));
         HIP_TRY(hipMemcpyAsync(L->d_arena, d_prefix, prefix_len, hipMemcpyDeviceToDevice,
                                L->stream));
+    }
     // staged copies: block k of the arena goes through slot k & 1
     size_t pi = 0;  // first piece that may overlap the block
     uint64_t k = 0;
     for (uint64_t p = prefix_len; p < total; p += L->stage, k++) {
         const uint64_t e = std::min(p + L->stage, total);
-        const int slot = (int)(k & 1);
-        if (k >= 2) {
+        const int slot = (int)(k % L->nslots);
+        if (k >= L->nslots) {
             const uint64_t w0 = g_hprof_on ? now_ns() : 0;
             HIP_TRY(hipEventSynchronize(L->ev[slot]));  // its previous DMA is done
             if (g_hprof_on) t_wait += now_ns() - w0;
@@ -1188,17 +1255,36 @@ rcdc_status run_host_pieces(rcdc_ctx *ctx, Lane *L, const std::vector<uint64_t> 
         HIP_TRY(hipEventRecord(L->ev[slot], L->stream));
     }
     const uint64_t b0 = g_hprof_on ? now_ns() : 0;
-    if (!L->plan || L->lay_offs != offs || L->lay_lens != lens || L->lay_arena != arena_len) {
+    // a lane's capacity plan serves any single-stream pass it covers (the
+    // scan runs only the items the pass needs)
+    const bool covers = cap1 && L->plan && L->lay_cap && L->lay_offs == offs &&
+                        L->lay_lens.size() == 1 && L->lay_lens[0] >= lens[0];
+    if (covers) klens = L->lay_lens;
+    if (!covers &&
+        (!L->plan || L->lay_offs != offs || L->lay_lens != klens || L->lay_arena != karena)) {
         if (!L->plan) L->plan = new rcdc_plan();
-        if ((st = plan_build(ctx, L->plan, offs.data(), lens.data(), n, arena_len, L->stream))) {
+        L->plan->no_walk = L->plan->no_pieces = cap1 != 0;
+        if ((st = plan_build(ctx, L->plan, offs.data(), klens.data(), n, karena, L->stream))) {
             L->lay_offs.clear();
             return st;
         }
+        L->plan->run_items = 0;
+        if (cap1 && (!L->plan->wunits.empty() || !L->plan->stitches.empty())) {
+            // not the shape a length can be set on: exact plans from here
+            L->plan->no_walk = L->plan->no_pieces = false;
+            if ((st = plan_build(ctx, L->plan, offs.data(), lens.data(), n, arena_len, L->stream))) {
+                L->lay_offs.clear();
+                return st;
+            }
+            klens = lens;
+        }
         L->lay_offs = offs;
-        L->lay_lens = lens;
-        L->lay_arena = arena_len;
+        L->lay_lens = klens;
+        L->lay_cap = cap1 && klens[0] == cap1;
+        L->lay_arena = L->lay_cap ? karena : arena_len;
         if (g_hprof_on) g_hprof.builds++;
     }
+    if (cap1 && L->lay_cap && (st = plan_set_len(L->plan, lens[0], L->stream))) return st;
     const uint64_t r0 = g_hprof_on ? now_ns() : 0;
     if ((st = plan_run(L->plan, L->d_arena, L->stream))) return st;
     st = plan_results(L->plan, cuts, cap, counts);
@@ -2343,6 +2429,10 @@ rcdc_status rcdc_stream_open(rcdc_ctx *ctx, rcdc_stream **out) {
 }
 
 void rcdc_stream_close(rcdc_stream *st) {
+    if (st && st->tail_ev) {  // the last tail copy is done before d_tail is reused
+        (void)hipEventSynchronize(st->tail_ev);
+        (void)hipEventDestroy(st->tail_ev);
+    }
     if (st && st->d_tail) {  // back to the context's pool
         std::lock_guard<std::mutex> lk(st->ctx->tail_mu);
         st->ctx->tail_pool.push_back(st->d_tail);
@@ -2385,7 +2475,8 @@ static rcdc_status stream_pass(rcdc_stream *st, const uint8_t *data, uint64_t le
     if (s2) return s2;
     st->tail_len = 0;
     s2 = run_host_pieces(ctx, L, lens, pieces, tmp.data(), tmp.size(), &cnt,
-                         dev_tail ? st->d_tail : nullptr, dev_tail ? P : 0);
+                         dev_tail ? st->d_tail : nullptr, dev_tail ? P : 0,
+                         dev_tail ? st->tail_ev : nullptr);
     uint64_t keep = cnt;
     if (!s2 && !is_final && cnt && tmp[cnt - 1] == N) keep = cnt - 1;
     const uint64_t consumed = keep ? tmp[keep - 1] : 0;
@@ -2406,10 +2497,15 @@ static rcdc_status stream_pass(rcdc_stream *st, const uint8_t *data, uint64_t le
                 st->d_tail = nullptr;
             }
         }
-        if (st->d_tail && N - consumed <= ctx->max + 256 &&
+        // asynchronous: the next pass (any lane) waits on tail_ev before
+        // it reads d_tail; the lane's next user queues behind the copy on
+        // the same stream before it overwrites the arena
+        if (!st->tail_ev && hipEventCreateWithFlags(&st->tail_ev, hipEventDisableTiming) != hipSuccess)
+            st->tail_ev = nullptr;
+        if (st->d_tail && st->tail_ev && N - consumed <= ctx->max + 256 &&
             hipMemcpyAsync(st->d_tail, L->d_arena + consumed, N - consumed,
                            hipMemcpyDeviceToDevice, L->stream) == hipSuccess &&
-            hipStreamSynchronize(L->stream) == hipSuccess)
+            hipEventRecord(st->tail_ev, L->stream) == hipSuccess)
             st->tail_len = N - consumed;
         s2 = RCDC_OK;  // without a device tail the next pass sends the host copy
     }

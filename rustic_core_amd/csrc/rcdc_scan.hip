@@ -129,3 +129,27 @@ hipError_t launch_scan(int code, const uint8_t *arena, const ScanItem *items, ui
 }
 
 }  // namespace rcdc
+
+// A capacity plan's stream set to length n (rcdc_runtime.cpp plan_set_len):
+// the descriptor's length and segment count, and the end position of the
+// items the scan runs.
+__global__ void rcdc_plan_set_len_kernel(StreamDesc *sds, ScanItem *items, uint32_t nitems,
+                                         uint64_t n, uint64_t nseg) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i == 0) {
+        sds[0].n = n;
+        sds[0].nseg = nseg;
+    }
+    if (i < nitems) items[i].hi = n;
+}
+
+namespace rcdc {
+
+hipError_t launch_plan_set_len(StreamDesc *sds, ScanItem *items, uint32_t nitems, uint64_t n,
+                               uint64_t nseg, hipStream_t stream) {
+    hipLaunchKernelGGL(rcdc_plan_set_len_kernel, dim3((nitems + 255) / 256 + 1), dim3(256), 0,
+                       stream, sds, items, nitems, n, nseg);
+    return hipGetLastError();
+}
+
+}  // namespace rcdc
