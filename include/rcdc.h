@@ -367,14 +367,17 @@ typedef struct {
 uint64_t rcdc_zstd_bound(uint64_t len);
 
 /* Compress n blobs (refs is a HOST array).  level: zstd's range
- * [-131072, 22] (0 = zstd's default, rustic's choice for version 2);
- * out-of-range -> InvalidInput.  On return (synchronous) out_lens[i] (host)
- * holds blob i's frame length.  Calls on one context take turns.  The
- * context keeps its scratch after the first call: up to 4 GiB of per-block
- * slots (batches of more than 32768 blocks run in windows) and 1 GiB of
- * per-wave sequence buffers, freed by rcdc_ctx_destroy.  Tuning (process
- * environment): RCDC_ZSTD_HLOG=12 (more hash buckets: better ratio on
- * structured data, fewer waves), RCDC_ZSTD_KEY=6 (6-byte minimum match).   */
+ * [-131072, 22] (0 = zstd's default, level 3: rustic's choice for version 2);
+ * out-of-range -> InvalidInput.  The level picks the parse: <= 1 keys
+ * positions on 6 bytes (6-byte minimum match, fastest), 2-3 on 4 bytes,
+ * >= 4 also doubles the hash table to 2^12 positions (better ratio on
+ * structured data, half the waves per CU).  On return (synchronous)
+ * out_lens[i] (host) holds blob i's frame length.  Calls on one context take
+ * turns.  The context keeps its scratch after the first call: up to 4 GiB of
+ * per-block slots (batches of more than 32768 blocks run in windows) and
+ * 1 GiB of per-wave sequence buffers, freed by rcdc_ctx_destroy.  A/B
+ * overrides (process environment): RCDC_ZSTD_HLOG (11 / 12), RCDC_ZSTD_KEY
+ * (4 / 6).                                                                  */
 rcdc_status rcdc_zstd_compress(rcdc_ctx *ctx, int level, const void *d_in,
                                const rcdc_zstd_ref *refs, uint32_t n, void *d_out,
                                uint64_t *out_lens, void *hip_stream);

@@ -65,13 +65,18 @@ hipError_t launch_aead(bool open, const uint8_t *in, uint8_t *out, const AeadBlo
                        uint32_t nblobs, const AeadUnit *units, uint32_t nunits,
                        const uint32_t *unit0, const AeadKeyDev *key, uint32_t *partials,
                        uint32_t *status, uint32_t cus, hipStream_t stream);
-uint32_t zstd_block_grid(uint32_t cus);
+uint32_t zstd_block_grid(uint32_t cus, int level);
 void zstd_prof_dump();
 hipError_t launch_zstd(const uint8_t *in, uint8_t *out, const ZstdBlob *blobs, uint32_t nblobs,
                        const ZstdBlk *blks, uint32_t nblk, const ZstdTables *tabs, uint8_t *slots,
                        uint64_t *seqbuf, uint32_t grid, uint2 *res, uint64_t *bpos,
-                       uint64_t *out_lens, uint32_t *queue, hipStream_t stream);
+                       uint64_t *out_lens, uint32_t *queue, int level, hipStream_t stream);
 uint64_t zstd_check_scratch_bytes(uint32_t grid);
+uint64_t zstd_blkdesc_bytes();
+hipError_t launch_zstd_check_blocks(const uint8_t *frames, const uint8_t *data, const void *refs,
+                                    const uint64_t *blk0, uint32_t n, void *blks, uint64_t nblk,
+                                    uint8_t *scratch, uint32_t grid, uint32_t *status,
+                                    uint32_t *ctr, hipStream_t stream);
 hipError_t launch_plan_set_len(StreamDesc *sds, ScanItem *items, uint32_t nitems, uint64_t n,
                                uint64_t nseg, hipStream_t stream);
 hipError_t launch_copy_ranges(const uint8_t *in, uint8_t *out, const void *units, uint32_t n,
@@ -319,6 +324,9 @@ struct rcdc_ctx {
     uint32_t *d_zck_order = nullptr, *d_zck_status = nullptr;
     uint8_t *d_zck_scratch = nullptr;
     uint64_t cap_zck_refs = 0, cap_zck_order = 0, cap_zck_status = 0, cap_zck_scratch = 0;
+    uint64_t *d_zck_blk0 = nullptr;  // block-parallel pass: per-frame block slots
+    uint8_t *d_zck_blks = nullptr;
+    uint64_t cap_zck_blk0 = 0, cap_zck_blks = 0;
     // pack files from sealed blobs (rcdc_pack_build_raw): copy units
     uint64_t *d_copy_units = nullptr;
     uint64_t cap_copy_units = 0;
@@ -1476,6 +1484,8 @@ void rcdc_ctx_destroy(rcdc_ctx *c) {
         (void)hipFree(c->d_zck_order);
         (void)hipFree(c->d_zck_status);
         (void)hipFree(c->d_zck_scratch);
+        (void)hipFree(c->d_zck_blk0);
+        (void)hipFree(c->d_zck_blks);
         (void)hipFree(c->d_copy_units);
         if (c->stream) (void)hipStreamDestroy(c->stream);
     }
@@ -2296,7 +2306,7 @@ rcdc_status zstd_compress(rcdc_ctx *ctx, int level, const void *d_in, const rcdc
         HIP_TRY(hipMemcpy(ctx->d_zstd_tabs, &zstd_tables(), sizeof(ZstdTables),
                           hipMemcpyHostToDevice));
     }
-    const uint32_t grid = zstd_block_grid((uint32_t)std::max(ctx->num_cus, 1));
+    const uint32_t grid = zstd_block_grid((uint32_t)std::max(ctx->num_cus, 1), level);
     if ((rs = ensure_dev(&ctx->d_zstd_seq, &ctx->cap_zstd_seq, (uint64_t)grid * kZstdMaxSeq)))
         return rs;
     const uint64_t nbl = blks.size(), nbo = blobs.size();
@@ -2319,7 +2329,7 @@ rcdc_status zstd_compress(rcdc_ctx *ctx, int level, const void *d_in, const rcdc
                             (uint32_t)w.nblob, ctx->d_zstd_blks + w.blk0, (uint32_t)w.nblk,
                             ctx->d_zstd_tabs, ctx->d_zstd_slots, ctx->d_zstd_seq, grid,
                             ctx->d_zstd_res + w.blk0, ctx->d_zstd_bpos + w.blk0,
-                            ctx->d_zstd_lens + w.blob0, ctx->d_zstd_queue + 128 * k, st));
+                            ctx->d_zstd_lens + w.blob0, ctx->d_zstd_queue + 128 * k, level, st));
     }
     HIP_TRY(hipMemcpyAsync(out_lens, ctx->d_zstd_lens, nbo * 8, hipMemcpyDeviceToHost, st));
     // the host descriptors die with this call
@@ -2329,41 +2339,68 @@ rcdc_status zstd_compress(rcdc_ctx *ctx, int level, const void *d_in, const rcdc
     return null_leave(ctx, hip_stream, st);
 }
 
-// Frame checks: one wave per frame, longest frames first (a frame's blocks
-// are read in order, so the longest frame bounds the launch).
+// Frame checks.  Compressed frames: the block-parallel pass (a wave per
+// block at the position it has when the frame's blocks are 128 KiB), then
+// the frames it could not settle checked in order, a wave per frame, longest
+// first.  Stored bytes: a wave per blob.
 rcdc_status zstd_check(rcdc_ctx *ctx, const void *d_frames, const void *d_data,
                        const rcdc_zstd_check_ref *refs, uint32_t n, uint32_t flags,
                        uint32_t *status, void *hip_stream) {
     if (!valid_ctx(ctx) || (n && (!refs || !d_frames || !d_data || !status)))
         return fail(RCDC_ERR_INVALID_INPUT, "null argument");
     if (!n) return RCDC_OK;
-    std::vector<uint32_t> order(n);
-    for (uint32_t i = 0; i < n; i++) order[i] = i;
-    std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) {
-        return refs[a].frame_len > refs[b].frame_len;
-    });
+    const bool stored = (flags & RCDC_CHECK_STORED) != 0;
+    static const bool blockpar = !(getenv("RCDC_CHECK_BLOCKS") && atoi(getenv("RCDC_CHECK_BLOCKS")) == 0);
     std::lock_guard<std::mutex> lk(ctx->zck_mu);
     DeviceGuard g(ctx->device);
     hipStream_t st;
     rcdc_status rs;
     if ((rs = null_enter(ctx, hip_stream, &st))) return rs;
-    const uint32_t grid = (uint32_t)std::max(ctx->num_cus, 1) * 8u;
+    // 12 waves per CU (the block kernel's registers allow 3 per SIMD)
+    const uint32_t grid = (uint32_t)std::max(ctx->num_cus, 1) * 12u;
     if ((rs = ensure_dev(&ctx->d_zck_refs, &ctx->cap_zck_refs, 4ull * n))) return rs;
     if ((rs = ensure_dev(&ctx->d_zck_order, &ctx->cap_zck_order, (uint64_t)n + 16))) return rs;
     if ((rs = ensure_dev(&ctx->d_zck_status, &ctx->cap_zck_status, n))) return rs;
     if ((rs = ensure_dev(&ctx->d_zck_scratch, &ctx->cap_zck_scratch, zstd_check_scratch_bytes(grid))))
         return rs;
-    // the queue counter sits after the order array
-    uint32_t *ctr = ctx->d_zck_order + n;
-    HIP_TRY(hipMemsetAsync(ctr, 0, 4, st));
+    uint32_t *ctr = ctx->d_zck_order + n;  // the queue counter sits after the order array
     HIP_TRY(hipMemcpyAsync(ctx->d_zck_refs, refs, sizeof(rcdc_zstd_check_ref) * n,
                            hipMemcpyHostToDevice, st));
-    HIP_TRY(hipMemcpyAsync(ctx->d_zck_order, order.data(), 4ull * n, hipMemcpyHostToDevice, st));
-    HIP_TRY(launch_zstd_check((const uint8_t *)d_frames, (const uint8_t *)d_data, ctx->d_zck_refs,
-                              ctx->d_zck_order, n, (flags & RCDC_CHECK_STORED) != 0,
-                              ctx->d_zck_scratch, grid, ctx->d_zck_status, ctr, st));
-    HIP_TRY(hipMemcpyAsync(status, ctx->d_zck_status, 4ull * n, hipMemcpyDeviceToHost, st));
-    HIP_TRY(hipStreamSynchronize(st));
+    std::vector<uint32_t> order;
+    if (!stored && blockpar) {
+        std::vector<uint64_t> blk0(n + 1, 0);
+        for (uint32_t i = 0; i < n; i++)
+            blk0[i + 1] = blk0[i] + std::max<uint64_t>((refs[i].data_len + kZstdBlock - 1) / kZstdBlock, 1);
+        const uint64_t nblk = blk0[n];
+        if ((rs = ensure_dev(&ctx->d_zck_blk0, &ctx->cap_zck_blk0, n + 1ull))) return rs;
+        if ((rs = ensure_dev(&ctx->d_zck_blks, &ctx->cap_zck_blks, nblk * zstd_blkdesc_bytes())))
+            return rs;
+        HIP_TRY(hipMemcpyAsync(ctx->d_zck_blk0, blk0.data(), 8ull * (n + 1), hipMemcpyHostToDevice, st));
+        HIP_TRY(hipMemsetAsync(ctr, 0, 4, st));
+        HIP_TRY(launch_zstd_check_blocks((const uint8_t *)d_frames, (const uint8_t *)d_data,
+                                         ctx->d_zck_refs, ctx->d_zck_blk0, n, ctx->d_zck_blks, nblk,
+                                         ctx->d_zck_scratch, grid, ctx->d_zck_status, ctr, st));
+        HIP_TRY(hipMemcpyAsync(status, ctx->d_zck_status, 4ull * n, hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipStreamSynchronize(st));
+        for (uint32_t i = 0; i < n; i++)
+            if (status[i] == 3u) order.push_back(i);
+    } else {
+        order.resize(n);
+        for (uint32_t i = 0; i < n; i++) order[i] = i;
+    }
+    if (!order.empty()) {
+        std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) {
+            return refs[a].frame_len > refs[b].frame_len;
+        });
+        HIP_TRY(hipMemsetAsync(ctr, 0, 4, st));
+        HIP_TRY(hipMemcpyAsync(ctx->d_zck_order, order.data(), 4ull * order.size(),
+                               hipMemcpyHostToDevice, st));
+        HIP_TRY(launch_zstd_check((const uint8_t *)d_frames, (const uint8_t *)d_data, ctx->d_zck_refs,
+                                  ctx->d_zck_order, (uint32_t)order.size(), stored,
+                                  ctx->d_zck_scratch, grid, ctx->d_zck_status, ctr, st));
+        HIP_TRY(hipMemcpyAsync(status, ctx->d_zck_status, 4ull * n, hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipStreamSynchronize(st));
+    }
     return null_leave(ctx, hip_stream, st);
 }
 

@@ -1589,37 +1589,49 @@ void zstd_prof_dump() {
     (void)hipMemcpyToSymbol(HIP_SYMBOL(g_zstd_prof), h, sizeof h);
 }
 
-// RCDC_ZSTD_HLOG: 11 (default; 8 KiB table, 16 waves per CU) or 12 (16 KiB,
-// 8 waves per CU: more buckets, better ratio on text, fewer waves)
-// RCDC_ZSTD_KEY: key bytes / minimum match, 4 or 6 (default below)
-// | 0x100: repeat codes on (RCDC_ZSTD_REP=0 turns them off, for A/B runs)
-static uint32_t zstd_key() {
-    static const uint32_t k = getenv("RCDC_ZSTD_KEY") ? (uint32_t)atoi(getenv("RCDC_ZSTD_KEY")) : 4u;
+// The parse strategy of a zstd level (decrypt.rs:494 passes the repository's
+// level; 0 is zstd's default, level 3).  Like zstd's own fast levels the
+// lowest ones key positions on 6 bytes (fewer, longer matches: faster, a
+// little larger on text); the default keys on 4 bytes; from level 4 up the
+// hash table doubles to 2^12 positions (better ratio on structured data, half
+// the waves per CU).  RCDC_ZSTD_KEY (4 or 6) and RCDC_ZSTD_HLOG (11 or 12)
+// override for A/B runs; RCDC_ZSTD_REP=0 turns repeat codes off.
+struct ZstdStrategy {
+    int hlog;
+    uint32_t key;  // key bytes | 0x100: repeat codes on
+};
+
+static ZstdStrategy zstd_strategy(int level) {
+    static const int ek = getenv("RCDC_ZSTD_KEY") ? atoi(getenv("RCDC_ZSTD_KEY")) : 0;
+    static const int eh = getenv("RCDC_ZSTD_HLOG") ? atoi(getenv("RCDC_ZSTD_HLOG")) : 0;
     static const bool rep = !(getenv("RCDC_ZSTD_REP") && atoi(getenv("RCDC_ZSTD_REP")) == 0);
-    return (k == 6 ? 6u : 4u) | (rep ? 0x100u : 0u);
+    if (level == 0) level = 3;  // ZSTD_CLEVEL_DEFAULT
+    ZstdStrategy z{level >= 4 ? 12 : 11, level <= 1 ? 6u : 4u};
+    if (ek == 4 || ek == 6) z.key = (uint32_t)ek;
+    if (eh == 11 || eh == 12) z.hlog = eh;
+    if (rep) z.key |= 0x100u;
+    return z;
 }
 
-static int zstd_hlog() {
-    static const int h = getenv("RCDC_ZSTD_HLOG") ? atoi(getenv("RCDC_ZSTD_HLOG")) : 11;
-    return h == 11 ? 11 : 12;
+uint32_t zstd_block_grid(uint32_t cus, int level) {
+    return cus * (zstd_strategy(level).hlog == 11 ? 16u : 8u);
 }
-
-uint32_t zstd_block_grid(uint32_t cus) { return cus * (zstd_hlog() == 11 ? 16u : 8u); }
 
 hipError_t launch_zstd(const uint8_t *in, uint8_t *out, const ZstdBlob *blobs, uint32_t nblobs,
                        const ZstdBlk *blks, uint32_t nblk, const ZstdTables *tabs, uint8_t *slots,
                        uint64_t *seqbuf, uint32_t grid, uint2 *res, uint64_t *bpos,
-                       uint64_t *out_lens, uint32_t *queue, hipStream_t stream) {
+                       uint64_t *out_lens, uint32_t *queue, int level, hipStream_t stream) {
     if (nblobs == 0) return hipSuccess;
+    const ZstdStrategy z = zstd_strategy(level);
     static const uint32_t dbg = getenv("RCDC_ZSTD_DBG") ? (uint32_t)atoi(getenv("RCDC_ZSTD_DBG")) : 0u;
     const uint32_t g = nblk < grid ? nblk : grid;
     if (g) {
-        if (zstd_hlog() == 11)
+        if (z.hlog == 11)
             hipLaunchKernelGGL(rcdc_zstd_block_kernel<11>, dim3(g), dim3(64), 0, stream, in, blobs,
-                               blks, nblk, tabs, slots, seqbuf, res, dbg, zstd_key(), queue);
+                               blks, nblk, tabs, slots, seqbuf, res, dbg, z.key, queue);
         else
             hipLaunchKernelGGL(rcdc_zstd_block_kernel<12>, dim3(g), dim3(64), 0, stream, in, blobs,
-                               blks, nblk, tabs, slots, seqbuf, res, dbg, zstd_key(), queue);
+                               blks, nblk, tabs, slots, seqbuf, res, dbg, z.key, queue);
     }
     hipLaunchKernelGGL(rcdc_zstd_frame_kernel, dim3((nblobs + 255) / 256), dim3(256), 0, stream,
                        blobs, nblobs, res, bpos, out, out_lens);

@@ -36,6 +36,7 @@ using namespace rcdc;
 namespace {
 
 constexpr uint32_t kCkOk = 0, kCkMismatch = 1, kCkCorrupt = 2;
+constexpr uint32_t kCkSeq = 3;  // block-parallel pass: re-check the frame in order
 constexpr uint32_t kBlockMax = 128u << 10;
 
 // Predefined distributions (RFC 8878 3.1.1.3.2.2) and code -> (baseline,
@@ -269,9 +270,11 @@ struct Dec {
     uint64_t dlen;
     uint64_t out;         // bytes decoded (= compared) so far
     uint32_t rep[3];
+    uint32_t rep_unk;     // bit i: rep[i] unknown (a block checked out of order)
     uint32_t huf_log;     // 0: no Huffman table yet
     uint32_t al_ll, al_ml, al_of;  // 255: no table yet
     uint32_t bad;         // status
+    bool block_mode;      // earlier blocks' state unknown: using it -> kCkSeq
 };
 
 // ---- comparisons (the whole wave) -----------------------------------------
@@ -525,7 +528,7 @@ __device__ void check_compressed(Dec &D, DecLds &L, const uint8_t *p, uint32_t b
             cs += tu;
             clen -= tu;
         } else if (D.huf_log == 0) {  // treeless: the previous block's table
-            D.bad = kCkCorrupt;
+            D.bad = D.block_mode ? kCkSeq : kCkCorrupt;
             return;
         }
         const uint32_t tl = D.huf_log;
@@ -606,7 +609,7 @@ __device__ void check_compressed(Dec &D, DecLds &L, const uint8_t *p, uint32_t b
                 al = a;
                 q += u;
             } else if (al == 255u) {  // repeat: needs an earlier table
-                D.bad = kCkCorrupt;
+                D.bad = D.block_mode ? kCkSeq : kCkCorrupt;
                 return;
             }
         }
@@ -616,6 +619,8 @@ __device__ void check_compressed(Dec &D, DecLds &L, const uint8_t *p, uint32_t b
         uint32_t sof = (uint32_t)brev_bits(r, D.al_of);
         uint32_t sml = (uint32_t)brev_bits(r, D.al_ml);
         uint32_t r0 = D.rep[0], r1 = D.rep[1], r2 = D.rep[2];
+        bool u0 = D.rep_unk & 1u, u1 = (D.rep_unk >> 1) & 1u, u2 = (D.rep_unk >> 2) & 1u;
+        bool unk_used = false;
         for (uint32_t s0 = 0; s0 < nseq; s0 += 64) {
             const uint32_t nb = min(64u, nseq - s0);
             uint32_t myll = 0, myml = 0, myoff = 0;
@@ -633,24 +638,39 @@ __device__ void check_compressed(Dec &D, DecLds &L, const uint8_t *p, uint32_t b
                     r2 = r1;
                     r1 = r0;
                     r0 = off;
+                    u2 = u1;
+                    u1 = u0;
+                    u0 = false;
                 } else {
                     const uint32_t idx = (uint32_t)ofv - 1u + (ll == 0 ? 1u : 0u);
                     if (idx == 0) {
                         off = r0;
+                        unk_used |= u0;
                     } else if (idx == 1) {
                         off = r1;
+                        unk_used |= u1;
                         r1 = r0;
+                        u1 = u0;
                         r0 = off;
+                        u0 = false;
                     } else if (idx == 2) {
                         off = r2;
+                        unk_used |= u2;
                         r2 = r1;
+                        u2 = u1;
                         r1 = r0;
+                        u1 = u0;
                         r0 = off;
+                        u0 = false;
                     } else {
                         off = r0 - 1u;
+                        unk_used |= u0;
                         r2 = r1;
+                        u2 = u1;
                         r1 = r0;
+                        u1 = u0;
                         r0 = off;
+                        u0 = false;
                     }
                 }
                 if (off == 0) err = true;
@@ -665,6 +685,7 @@ __device__ void check_compressed(Dec &D, DecLds &L, const uint8_t *p, uint32_t b
                     myoff = off;
                 }
             }
+            if (unk_used) { D.bad = kCkSeq; return; }  // (block mode only)
             if (err || r.pos < 0) { D.bad = kCkCorrupt; return; }
             // place the batch: exclusive prefix sums of ll and ll + ml
             uint64_t incl_l = myll, incl_o = (uint64_t)myll + myml;
@@ -712,6 +733,7 @@ __device__ void check_compressed(Dec &D, DecLds &L, const uint8_t *p, uint32_t b
         D.rep[0] = r0;
         D.rep[1] = r1;
         D.rep[2] = r2;
+        D.rep_unk = (u0 ? 1u : 0u) | (u1 ? 2u : 0u) | (u2 ? 4u : 0u);
     } else if (q != end) {
         D.bad = kCkCorrupt;
         return;
@@ -759,9 +781,11 @@ __device__ uint32_t check_frame(const uint8_t *f, uint64_t flen, const uint8_t *
     D.rep[0] = 1;
     D.rep[1] = 4;
     D.rep[2] = 8;
+    D.rep_unk = 0;
     D.huf_log = 0;
     D.al_ll = D.al_ml = D.al_of = 255u;
     D.bad = kCkOk;
+    D.block_mode = false;
     for (;;) {
         if (q + 3 > end) return kCkCorrupt;
         const uint32_t bh = q[0] | (q[1] << 8) | ((uint32_t)q[2] << 16);
@@ -822,9 +846,134 @@ __global__ __launch_bounds__(64) void rcdc_zstd_check_kernel(
     }
 }
 
+// ---- block-parallel pass -----------------------------------------------------
+// A thread per frame walks the frame header and block headers and gives each
+// block the output position it has when every block but the last decodes to
+// Block_Maximum_Size (128 KiB: how zstd encoders cut their input, this one
+// included).  A wave per block then checks it at that position; what it
+// cannot settle alone -- a repeat offset, Huffman table or FSE table from an
+// earlier block, a block of another size, any failure -- marks the frame
+// kCkSeq, and those frames are checked again in order (rcdc_zstd_check_kernel).
+
+struct BlkDesc {       // 32 B
+    uint64_t content;  // block content: offset in the frames buffer
+    uint64_t out;      // output position in the frame
+    uint32_t frame;
+    uint32_t size;     // Block_Size field
+    uint32_t flags;    // type | first << 2 | used << 3
+    uint32_t out_len;  // expected decoded bytes
+};
+
+__global__ __launch_bounds__(256) void rcdc_zstd_blocks_kernel(
+    const uint8_t *__restrict__ frames, const ulonglong4 *__restrict__ refs,
+    const uint64_t *__restrict__ blk0, uint32_t n, BlkDesc *__restrict__ blks,
+    uint32_t *__restrict__ status) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const ulonglong4 r = refs[i];
+    const uint8_t *f = frames + r.x, *end = f + r.y;
+    const uint64_t b0 = blk0[i], cap = blk0[i + 1] - b0, dlen = r.w;
+    for (uint64_t k = 0; k < cap; k++) blks[b0 + k].flags = 0;
+    uint32_t st = kCkOk;
+    do {
+        if (r.y < 6) { st = kCkCorrupt; break; }
+        const uint32_t magic = f[0] | (f[1] << 8) | (f[2] << 16) | ((uint32_t)f[3] << 24);
+        const uint32_t fhd = f[4];
+        if (magic != 0xFD2FB528u || (fhd & 8u)) { st = kCkCorrupt; break; }
+        const uint32_t fcs_flag = fhd >> 6, single = (fhd >> 5) & 1u, cksum = (fhd >> 2) & 1u,
+                       did_flag = fhd & 3u;
+        const uint8_t *q = f + 5 + (single ? 0 : 1);
+        const uint32_t did_len = did_flag == 0 ? 0 : did_flag == 1 ? 1 : did_flag == 2 ? 2 : 4;
+        const uint32_t fcs_len = fcs_flag == 0 ? (single ? 1 : 0) : fcs_flag == 1 ? 2 : fcs_flag == 2 ? 4 : 8;
+        if (q + did_len + fcs_len > end) { st = kCkCorrupt; break; }
+        uint32_t did = 0;
+        for (uint32_t j = 0; j < did_len; j++) did |= (uint32_t)q[j] << (8 * j);
+        if (did) { st = kCkCorrupt; break; }
+        q += did_len;
+        uint64_t fcs = 0;
+        for (uint32_t j = 0; j < fcs_len; j++) fcs |= (uint64_t)q[j] << (8 * j);
+        if (fcs_len == 2) fcs += 256;
+        q += fcs_len;
+        if (fcs_len && fcs != dlen) { st = kCkMismatch; break; }
+        uint64_t k = 0;
+        for (;;) {
+            if (q + 3 > end) { st = kCkCorrupt; break; }
+            const uint32_t bh = q[0] | (q[1] << 8) | ((uint32_t)q[2] << 16);
+            q += 3;
+            const uint32_t last = bh & 1u, btype = (bh >> 1) & 3u, bsize = bh >> 3;
+            const uint64_t csz = btype == 1 ? 1u : bsize;
+            if (btype == 3 || bsize > kBlockMax || q + csz > end) { st = kCkCorrupt; break; }
+            const uint64_t pos = k * kBlockMax;
+            const uint64_t want = last ? (dlen >= pos ? dlen - pos : ~0ull) : kBlockMax;
+            if (k >= cap || want > kBlockMax || (btype < 2 && bsize != want)) { st = kCkSeq; break; }
+            BlkDesc d;
+            d.content = r.x + (uint64_t)(q - f);
+            d.out = pos;
+            d.frame = i;
+            d.size = bsize;
+            d.flags = btype | (k == 0 ? 4u : 0u) | 8u;
+            d.out_len = (uint32_t)want;
+            blks[b0 + k] = d;
+            q += csz;
+            k++;
+            if (last) break;
+        }
+        if (st) break;
+        if (cksum) q += 4;
+        if (q != end) st = kCkCorrupt;
+    } while (false);
+    status[i] = st;
+}
+
+__global__ __launch_bounds__(64) void rcdc_zstd_block_check_kernel(
+    const uint8_t *__restrict__ frames, const uint8_t *__restrict__ data,
+    const ulonglong4 *__restrict__ refs, const BlkDesc *__restrict__ blks, uint64_t nblk,
+    uint8_t *scratch, uint32_t *status, uint32_t *ctr) {
+    __shared__ DecLds L;
+    const uint32_t lane = threadIdx.x;
+    uint8_t *scr = scratch + (uint64_t)blockIdx.x * (kBlockMax + 64);
+    for (;;) {
+        uint32_t k = 0;
+        if (lane == 0) k = atomicAdd(ctr, 1u);
+        k = __builtin_amdgcn_readfirstlane(__shfl(k, 0));
+        if (k >= nblk) break;
+        const BlkDesc b = blks[k];
+        if (!(b.flags & 8u)) continue;  // an unused slot
+        if (__builtin_amdgcn_readfirstlane(((volatile uint32_t *)status)[b.frame]) != kCkOk) continue;
+        const ulonglong4 r = refs[b.frame];
+        const uint8_t *dat = data + r.z;
+        const uint32_t btype = b.flags & 3u;
+        uint32_t st = kCkOk;
+        if (btype == 0) {
+            st = wave_cmp(dat + b.out, frames + b.content, 0, 0, b.out_len, lane) ? kCkOk : kCkSeq;
+        } else if (btype == 1) {
+            st = wave_cmp(dat + b.out, nullptr, frames[b.content], 1, b.out_len, lane) ? kCkOk : kCkSeq;
+        } else {
+            Dec D;
+            D.data = dat;
+            D.dlen = b.out + b.out_len;
+            D.out = b.out;
+            D.rep[0] = 1;
+            D.rep[1] = 4;
+            D.rep[2] = 8;
+            D.rep_unk = (b.flags & 4u) ? 0u : 7u;
+            D.huf_log = 0;
+            D.al_ll = D.al_ml = D.al_of = 255u;
+            D.bad = kCkOk;
+            D.block_mode = true;
+            check_compressed(D, L, frames + b.content, b.size, scr, lane);
+            st = (D.bad || D.out != D.dlen) ? kCkSeq : kCkOk;
+        }
+        if (st != kCkOk && lane == 0) atomicMax(&status[b.frame], kCkSeq);
+        __syncthreads();  // LDS tables are rebuilt by the next block
+    }
+}
+
 namespace rcdc {
 
 uint64_t zstd_check_scratch_bytes(uint32_t grid) { return (uint64_t)grid * (kBlockMax + 64); }
+
+uint64_t zstd_blkdesc_bytes() { return sizeof(BlkDesc); }
 
 hipError_t launch_zstd_check(const uint8_t *frames, const uint8_t *data, const void *refs,
                              const uint32_t *order, uint32_t n, bool stored, uint8_t *scratch,
@@ -833,6 +982,22 @@ hipError_t launch_zstd_check(const uint8_t *frames, const uint8_t *data, const v
     const uint32_t g = n < grid ? n : grid;
     hipLaunchKernelGGL(rcdc_zstd_check_kernel, dim3(g), dim3(64), 0, stream, frames, data,
                        (const ulonglong4 *)refs, order, n, stored ? 1u : 0u, scratch, status, ctr);
+    return hipGetLastError();
+}
+
+// the block-parallel pass: header walk, then a wave per block
+hipError_t launch_zstd_check_blocks(const uint8_t *frames, const uint8_t *data, const void *refs,
+                                    const uint64_t *blk0, uint32_t n, void *blks, uint64_t nblk,
+                                    uint8_t *scratch, uint32_t grid, uint32_t *status,
+                                    uint32_t *ctr, hipStream_t stream) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(rcdc_zstd_blocks_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, frames,
+                       (const ulonglong4 *)refs, blk0, n, (BlkDesc *)blks, status);
+    const uint32_t g = nblk < grid ? (uint32_t)nblk : grid;
+    if (g)
+        hipLaunchKernelGGL(rcdc_zstd_block_check_kernel, dim3(g), dim3(64), 0, stream, frames, data,
+                           (const ulonglong4 *)refs, (const BlkDesc *)blks, nblk, scratch, status,
+                           ctr);
     return hipGetLastError();
 }
 

@@ -156,12 +156,31 @@ def test_block_types(gpu_ctx):
     assert all(t == 0 for t, _, _ in br) and len(br) == 8 and br[-1][2]
 
 
+def _csv(rng, n):
+    vocab = _text(rng, 4000).split(b" ")
+    k = n // 24 + 2
+    a, b, v = rng.integers(0, len(vocab), k), rng.integers(0, len(vocab), k), rng.integers(0, 10 ** 6, k)
+    return b"".join(b"%08d,%s,%d,%s\n" % (i, vocab[a[i]], v[i], vocab[b[i]]) for i in range(k))[:n]
+
+
 def test_levels(gpu_ctx):
+    """The level picks the parse (rcdc_zstd.hip zstd_strategy): 6-byte keys
+    at levels <= 1, 4-byte keys at 2-3 (0 = zstd's default, 3), a 2^12-entry
+    table from 4 up.  Every level's frames decode; the levels differ and the
+    higher ones are not larger on structured rows."""
     from rustic_core_amd.errors import RusticError
     rng = np.random.default_rng(2)
-    d = [_text(rng, 300000)]
-    for lv in (-131072, -5, 0, 1, 3, 22):
-        _check(_compress(gpu_ctx, d, level=lv), d)
+    d = [_text(rng, 300000), _csv(rng, 400000)]
+    sizes = {}
+    for lv in (-131072, -5, 0, 1, 3, 4, 9, 22):
+        fr = _compress(gpu_ctx, d, level=lv)
+        _check(fr, d)
+        sizes[lv] = [len(f) for f in fr]
+    print("frame bytes by level (text, csv):", sizes)
+    assert sizes[0] == sizes[3]                      # 0 is the default level, 3
+    assert sizes[-5] == sizes[1] != sizes[3]         # fast levels: another parse
+    assert sizes[4] == sizes[9] == sizes[22] != sizes[3]
+    assert sizes[9][1] <= sizes[3][1]                # bigger table: not larger on rows
     for lv in (23, -131073):
         with pytest.raises(RusticError):
             _compress(gpu_ctx, d, level=lv)

@@ -170,6 +170,25 @@ def test_corrupted_frames_agree_with_libzstd(gpu_ctx, source):
     assert sum(exp) < len(exp) // 2  # the corruptions mostly break the frames
 
 
+def test_odd_block_sizes(gpu_ctx):
+    """Frames whose blocks are not 128 KiB (legal, no encoder here writes
+    them): the block-parallel pass cannot place them and hands them to the
+    in-order pass, which accepts the good ones and rejects the bad."""
+    import sys
+    sys.path.insert(0, __file__.rsplit("/", 1)[0])
+    from zstd_model import frame
+    rng = np.random.default_rng(31)
+    d = rng.integers(0, 256, 1000 + 131072 + 500, dtype=np.uint8).tobytes()
+    f1 = frame([(0, d[:1000], 1000), (0, d[1000:132072], 131072), (0, d[132072:], 500)], len(d))
+    z = bytes(70000) + d[:5]
+    f2 = frame([(1, bytes([0]), 70000), (0, d[:5], 5)], len(z))
+    assert zr.decompress(f1) == d and zr.decompress(f2) == z
+    bad = bytearray(d)
+    bad[131500] ^= 1
+    st = _check(gpu_ctx, [f1, f2, f1, f2], [d, z, bytes(bad), z[:-1] + b"?"])
+    assert st.tolist() == [0, 0, 1, 1]
+
+
 def test_stored_mode(gpu_ctx):
     rng = np.random.default_rng(5)
     datas = [_data(rng, n, "random") for n in (0, 3, 4096, 100003)]

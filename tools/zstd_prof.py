@@ -19,6 +19,9 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--gib", type=float, default=8)
 ap.add_argument("--reps", type=int, default=3)
 ap.add_argument("--kinds", default="random,zeros,mixed,text,csv,code")
+ap.add_argument("--levels", default="0", help="comma-separated zstd levels")
+ap.add_argument("--check", action="store_true", help="also decode every frame on the device "
+                "(rcdc_zstd_check) and time it")
 args = ap.parse_args()
 dev = torch.device("cuda:0")
 n = int(args.gib * (1 << 30))
@@ -67,16 +70,17 @@ def fill(kind):
 
 
 for kind in args.kinds.split(","):
-    fill(kind)
+  fill(kind)
+  for level in [int(x) for x in args.levels.split(",")]:
     torch.cuda.synchronize()
     st = torch.cuda.current_stream().cuda_stream
     for _ in range(3):  # warm-up (the first kind otherwise runs at a lower clock)
-        ln = compress_blobs(ctx, arena.data_ptr(), refs, frames.data_ptr(), 0, st)
+        ln = compress_blobs(ctx, arena.data_ptr(), refs, frames.data_ptr(), level, st)
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
     e0.record()
     for _ in range(args.reps):
-        ln = compress_blobs(ctx, arena.data_ptr(), refs, frames.data_ptr(), 0, st)
+        ln = compress_blobs(ctx, arena.data_ptr(), refs, frames.data_ptr(), level, st)
     e1.record()
     torch.cuda.synchronize()
     ms = e0.elapsed_time(e1) / args.reps
@@ -86,9 +90,17 @@ for kind in args.kinds.split(","):
         d = arena[int(offs[i]):int(offs[i]) + lens[i]].cpu().numpy().tobytes()
         f = frames[int(f_offs[i]):int(f_offs[i]) + int(ln[i])].cpu().numpy().tobytes()
         bad += zr.decompress(f) != d
+    chk = ""
+    if args.check:
+        from rustic_core_amd.compress import check_frames
+        t1 = time.perf_counter()
+        cs = check_frames(ctx, frames.data_ptr(), f_offs, ln, arena.data_ptr(), offs, lens, st)
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t1
+        chk = f", device check {n / dt / 2**30:.1f} GiB/s ({int((cs != 0).sum())} bad)"
     piece = arena[:16 << 20].cpu().numpy().tobytes()
     ref = sum(len(zr.compress(piece[o:o + (1 << 20)], 3)) for o in range(0, len(piece), 1 << 20))
-    print(f"{kind:7s} {len(lens)} blobs {n / 2**30:.1f} GiB: {ms:.2f} ms (wall {wall:.2f}) "
-          f"= {n / (ms / 1e3) / 2**30:.1f} GiB/s, ratio {int(ln.sum()) / n:.4f}, "
-          f"libzstd-3 ratio on 16 x 1 MiB {ref / len(piece):.4f}, decode mismatches {bad}",
+    print(f"{kind:7s} level {level:3d} {len(lens)} blobs {n / 2**30:.1f} GiB: {ms:.2f} ms "
+          f"(wall {wall:.2f}) = {n / (ms / 1e3) / 2**30:.1f} GiB/s, ratio {int(ln.sum()) / n:.4f}, "
+          f"libzstd-3 ratio on 16 x 1 MiB {ref / len(piece):.4f}, decode mismatches {bad}{chk}",
           flush=True)
