@@ -146,6 +146,66 @@ __device__ __forceinline__ uint64_t brev_bits(BRev &r, uint32_t n) {
     return v;
 }
 
+// The same bitstream read through a 64-bit window that slides down 32 bits
+// at a time, with the next three dwords already in flight: a refill never
+// waits on memory (the serial FSE and Huffman decodes stalled ~500 cycles on
+// each refill otherwise).  Reads are at most 32 bits.  Invariant: the
+// window holds bits [B, B + 64) and B <= pos (pos - B < 64).
+struct BRevQ {
+    const uint8_t *base;
+    int64_t len;
+    int64_t pos;
+    int64_t B;
+    uint64_t acc;
+    uint32_t q0, q1, q2;  // dwords of bits [B-32, B), [B-64, B-32), [B-96, B-64)
+};
+
+// 4 bytes at base + byte (any alignment), bytes outside [0, len) as 0
+__device__ __forceinline__ uint32_t brq_ld4(const uint8_t *base, int64_t len, int64_t byte) {
+    if (byte >= 0 && byte + 4 <= len) return ld4u(base + byte);
+    uint32_t v = 0;
+    for (int i = 0; i < 4; i++)
+        if (byte + i >= 0 && byte + i < len) v |= (uint32_t)base[byte + i] << (8 * i);
+    return v;
+}
+
+__device__ bool brq_init(BRevQ &r, const uint8_t *p, int64_t len) {
+    r.base = p;
+    r.len = len;
+    if (len <= 0) return false;
+    const uint32_t last = p[len - 1];
+    if (last == 0) return false;
+    r.pos = 8 * (len - 1) + (int64_t)highbit32(last);
+    r.B = ((r.pos >> 5) << 5) - 32;  // arithmetic shifts: floor
+    const int64_t by = r.B >> 3;
+    r.acc = (uint64_t)brq_ld4(p, len, by) | (uint64_t)brq_ld4(p, len, by + 4) << 32;
+    r.q0 = brq_ld4(p, len, by - 4);
+    r.q1 = brq_ld4(p, len, by - 8);
+    r.q2 = brq_ld4(p, len, by - 12);
+    return true;
+}
+
+__device__ __forceinline__ void brq_slide(BRevQ &r) {
+    r.acc = (r.acc << 32) | r.q0;
+    r.B -= 32;
+    r.q0 = r.q1;
+    r.q1 = r.q2;
+    r.q2 = brq_ld4(r.base, r.len, (r.B >> 3) - 12);
+}
+
+__device__ __forceinline__ uint32_t brq_peek(BRevQ &r, uint32_t n) {
+    if (n == 0) return 0;
+    const int64_t lo = r.pos - (int64_t)n;
+    if (lo < r.B) brq_slide(r);
+    return (uint32_t)((r.acc >> (uint32_t)(lo - r.B)) & ((1ull << n) - 1ull));
+}
+
+__device__ __forceinline__ uint32_t brq_bits(BRevQ &r, uint32_t n) {
+    const uint32_t v = brq_peek(r, n);
+    r.pos -= n;
+    return v;
+}
+
 // FSE_readNCount: a table description at p (at most `avail` bytes);
 // returns its byte length, or -1.  norm[0..*nsym) and *al are set.
 __device__ int read_ncount(const uint8_t *p, int64_t avail, uint32_t max_sym, uint32_t max_al,
@@ -427,13 +487,13 @@ __device__ uint32_t build_huf(DecLds &L, uint32_t nw, uint32_t lane) {
 // One Huffman stream [p, p+len) -> n symbols at out (one lane).
 __device__ bool huf_stream(const DecLds &L, uint32_t tl, const uint8_t *p, int64_t len,
                            uint8_t *out, uint32_t n) {
-    BRev r;
-    if (n == 0) return len == 0 || (brev_init(r, p, len) && r.pos == 0);
-    if (!brev_init(r, p, len)) return false;
+    BRevQ r;
+    if (n == 0) return len == 0 || (brq_init(r, p, len) && r.pos == 0);
+    if (!brq_init(r, p, len)) return false;
     uint32_t i = 0;
     // four symbols per dword store once aligned
     while (i < n && ((uintptr_t)(out + i) & 3u)) {
-        const HufD e = L.huf[brev_peek(r, tl)];
+        const HufD e = L.huf[brq_peek(r, tl)];
         out[i++] = e.sym;
         r.pos -= e.nb;
     }
@@ -441,14 +501,14 @@ __device__ bool huf_stream(const DecLds &L, uint32_t tl, const uint8_t *p, int64
         uint32_t v = 0;
 #pragma unroll
         for (int k = 0; k < 4; k++) {
-            const HufD e = L.huf[brev_peek(r, tl)];
+            const HufD e = L.huf[brq_peek(r, tl)];
             v |= (uint32_t)e.sym << (8 * k);
             r.pos -= e.nb;
         }
         *reinterpret_cast<uint32_t *>(out + i) = v;
     }
     for (; i < n; i++) {
-        const HufD e = L.huf[brev_peek(r, tl)];
+        const HufD e = L.huf[brq_peek(r, tl)];
         out[i] = e.sym;
         r.pos -= e.nb;
     }
@@ -613,11 +673,11 @@ __device__ void check_compressed(Dec &D, DecLds &L, const uint8_t *p, uint32_t b
                 return;
             }
         }
-        BRev r;
-        if (!brev_init(r, q, end - q)) { D.bad = kCkCorrupt; return; }
-        uint32_t sll = (uint32_t)brev_bits(r, D.al_ll);
-        uint32_t sof = (uint32_t)brev_bits(r, D.al_of);
-        uint32_t sml = (uint32_t)brev_bits(r, D.al_ml);
+        BRevQ r;
+        if (!brq_init(r, q, end - q)) { D.bad = kCkCorrupt; return; }
+        uint32_t sll = brq_bits(r, D.al_ll);
+        uint32_t sof = brq_bits(r, D.al_of);
+        uint32_t sml = brq_bits(r, D.al_ml);
         uint32_t r0 = D.rep[0], r1 = D.rep[1], r2 = D.rep[2];
         bool u0 = D.rep_unk & 1u, u1 = (D.rep_unk >> 1) & 1u, u2 = (D.rep_unk >> 2) & 1u;
         bool unk_used = false;
@@ -629,9 +689,9 @@ __device__ void check_compressed(Dec &D, DecLds &L, const uint8_t *p, uint32_t b
                 const FseD eo = L.of[sof], el = L.ll[sll], em = L.ml[sml];
                 const uint32_t ofc = eo.sym, llc = el.sym, mlc = em.sym;
                 if (ofc > 31 || llc > 35 || mlc > 52) err = true;
-                const uint64_t ofv = (1ull << ofc) + brev_bits(r, ofc);
-                const uint32_t ml = kMLBase[mlc] + (uint32_t)brev_bits(r, kMLBits[mlc]);
-                const uint32_t ll = kLLBase[llc] + (uint32_t)brev_bits(r, kLLBits[llc]);
+                const uint64_t ofv = (1ull << ofc) + brq_bits(r, ofc);
+                const uint32_t ml = kMLBase[mlc] + brq_bits(r, kMLBits[mlc]);
+                const uint32_t ll = kLLBase[llc] + brq_bits(r, kLLBits[llc]);
                 uint32_t off;
                 if (ofv > 3) {
                     off = (uint32_t)(ofv - 3);
@@ -675,9 +735,9 @@ __device__ void check_compressed(Dec &D, DecLds &L, const uint8_t *p, uint32_t b
                 }
                 if (off == 0) err = true;
                 if (s0 + j + 1 < nseq) {
-                    sll = el.next + (uint32_t)brev_bits(r, el.nb);
-                    sml = em.next + (uint32_t)brev_bits(r, em.nb);
-                    sof = eo.next + (uint32_t)brev_bits(r, eo.nb);
+                    sll = el.next + brq_bits(r, el.nb);
+                    sml = em.next + brq_bits(r, em.nb);
+                    sof = eo.next + brq_bits(r, eo.nb);
                 }
                 if (lane == j) {
                     myll = ll;

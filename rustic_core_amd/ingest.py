@@ -308,8 +308,7 @@ class DeviceIngest:
                                    packs.data_ptr(), total, sp, raw=True) if nb else \
             np.zeros(0, np.uint32)
         s_proc.synchronize()
-        for i in nidx:
-            self.indexed.add(bytes(ids[i]))
+        self.indexed.update(map(bytes, ids[nidx]))
         ms["pack"] = (time.perf_counter() - t3) * 1e3
         ms["total"] = (time.perf_counter() - t0) * 1e3
         del st_long, st_short

@@ -92,18 +92,24 @@ def group_blobs(lens: Sequence[int], sizer: PackSizer,
     reaches pack_size(); take_data (:749-758) adds the closed pack's
     PackHeaderRef::pack_size to the sizer.  (MAX_AGE, a wall-clock rule, is
     not modelled.)  The last pack holds the rest (finalize)."""
-    packs, b0, size, count, hdr = [], 0, 0, 0, 0
-    for i, n in enumerate(lens):
-        size += int(n) + 32
-        count += 1
-        hdr += header_entry_len(uncompressed[i] if uncompressed is not None else 0)
-        if count >= MAX_COUNT or size >= sizer.pack_size():
-            packs.append((b0, count))
-            sizer.add_size(size + hdr + 32 + 4)
-            b0, size, count, hdr = i + 1, 0, 0, 0
-    if count:
-        packs.append((b0, count))
-        sizer.add_size(size + hdr + 32 + 4)
+    # a pack at a time (pack_size() only changes when a pack closes): its
+    # last blob is the first whose running sealed size reaches pack_size(),
+    # or the MAX_COUNT-th (numpy over prefix sums, not a Python loop per blob)
+    n_all = len(lens)
+    sealed = np.asarray(lens, np.int64) + 32
+    hdr_b = np.full(n_all, 37, np.int64)
+    if uncompressed is not None:
+        hdr_b = np.where(np.asarray(uncompressed, np.int64) > 0, 41, 37)
+    cum = np.concatenate([np.zeros(1, np.int64), np.cumsum(sealed)])
+    cumh = np.concatenate([np.zeros(1, np.int64), np.cumsum(hdr_b)])
+    packs, b0 = [], 0
+    while b0 < n_all:
+        limit = cum[b0] + sizer.pack_size()
+        i = int(np.searchsorted(cum, limit, side="left"))  # cum[i] >= limit: blobs b0..i-1
+        e = min(max(i, b0 + 1), b0 + MAX_COUNT, n_all)       # one past the pack's last blob
+        packs.append((b0, e - b0))
+        sizer.add_size(int(cum[e] - cum[b0] + cumh[e] - cumh[b0]) + 32 + 4)
+        b0 = e
     return packs
 
 
@@ -127,11 +133,12 @@ def pack_layout(blobs: np.ndarray, groups: Sequence[Tuple[int, int]], header_non
     buffer (each pack `align`-aligned); returns (packs, total bytes).
     ``raw``: blobs["len"] are sealed lengths already (build_packs raw)."""
     packs = np.zeros(len(groups), PACK)
+    per = blobs["len"].astype(np.int64) + (0 if raw else 32) + \
+        np.where(blobs["uncompressed_len"] > 0, 41, 37)
+    cum = np.concatenate([np.zeros(1, np.int64), np.cumsum(per)])
     o = 0
     for k, (b0, n) in enumerate(groups):
-        sel = blobs[b0:b0 + n]
-        size = int(np.sum(sel["len"].astype(np.int64) + (0 if raw else 32)))
-        size += int(np.sum(np.where(sel["uncompressed_len"] > 0, 41, 37))) + 32 + 4
+        size = int(cum[b0 + n] - cum[b0]) + 32 + 4
         packs[k]["out_off"] = o
         packs[k]["blob0"] = b0
         packs[k]["nblobs"] = n
