@@ -1073,18 +1073,6 @@ namespace {
 
 typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));
 
-__device__ __forceinline__ u32x4v ld16u(const uint8_t *p) {
-    const uint32_t b = (uint32_t)(uintptr_t)p & 3u, sh = b * 8u;
-    const uint32_t *w = (const uint32_t *)(p - b);
-    const uint32_t w0 = w[0], w1 = w[1], w2 = w[2], w3 = w[3];
-    const uint32_t w4 = w[b ? 4 : 3];
-    u32x4v v;
-    v.x = __builtin_amdgcn_alignbit(w1, w0, sh);
-    v.y = __builtin_amdgcn_alignbit(w2, w1, sh);
-    v.z = __builtin_amdgcn_alignbit(w3, w2, sh);
-    v.w = __builtin_amdgcn_alignbit(w4, w3, sh);
-    return v;
-}
 
 }  // namespace
 
@@ -1092,7 +1080,7 @@ __global__ __launch_bounds__(256) void rcdc_copy_ranges_kernel(const uint8_t *__
                                                                uint8_t *__restrict__ out,
                                                                const ulonglong4 *__restrict__ units,
                                                                uint32_t n) {
-    const uint32_t t = threadIdx.x;
+    const uint32_t t = threadIdx.x, ln = t & 63u;
     for (uint32_t k = blockIdx.x; k < n; k += gridDim.x) {
         const ulonglong4 u = units[k];  // src, dst, len
         const uint8_t *s = in + u.x;
@@ -1102,18 +1090,73 @@ __global__ __launch_bounds__(256) void rcdc_copy_ranges_kernel(const uint8_t *__
         if (head > len) head = (uint32_t)len;
         if (t < head) d[t] = s[t];
         const uint64_t body = (len - head) / 16;
-        const uint8_t *sb = s + head;
         u32x4v *db = reinterpret_cast<u32x4v *>(d + head);
-        uint64_t i = t;
-        for (; i + 768 < body; i += 1024) {
-            const u32x4v v0 = ld16u(sb + 16 * i), v1 = ld16u(sb + 16 * (i + 256)),
-                        v2 = ld16u(sb + 16 * (i + 512)), v3 = ld16u(sb + 16 * (i + 768));
-            __builtin_nontemporal_store(v0, db + i);
-            __builtin_nontemporal_store(v1, db + i + 256);
-            __builtin_nontemporal_store(v2, db + i + 512);
-            __builtin_nontemporal_store(v3, db + i + 768);
+        // 16-aligned source loads; output chunk i takes aligned chunks i and
+        // i + 1 (the neighbour lane's, lane 63 loads its own) funnelled by
+        // the unit-uniform byte shift (the zstd copy kernel's scheme)
+        const uint8_t *sb = s + head;
+        const uint32_t sh = (uint32_t)(uintptr_t)sb & 15u, kk = sh >> 2, rr = (sh & 3u) * 8u;
+        const u32x4v *s16 = reinterpret_cast<const u32x4v *>(sb - sh);
+        auto funnel = [&](u32x4v A, u32x4v B) {
+            uint32_t x0, x1, x2, x3, x4;
+            if (kk == 0) {
+                x0 = A.x; x1 = A.y; x2 = A.z; x3 = A.w; x4 = B.x;
+            } else if (kk == 1) {
+                x0 = A.y; x1 = A.z; x2 = A.w; x3 = B.x; x4 = B.y;
+            } else if (kk == 2) {
+                x0 = A.z; x1 = A.w; x2 = B.x; x3 = B.y; x4 = B.z;
+            } else {
+                x0 = A.w; x1 = B.x; x2 = B.y; x3 = B.z; x4 = B.w;
+            }
+            u32x4v v;
+            v.x = __builtin_amdgcn_alignbit(x1, x0, rr);
+            v.y = __builtin_amdgcn_alignbit(x2, x1, rr);
+            v.z = __builtin_amdgcn_alignbit(x3, x2, rr);
+            v.w = __builtin_amdgcn_alignbit(x4, x3, rr);
+            return v;
+        };
+        auto nbr = [&](u32x4v A) {
+            u32x4v B;
+            B.x = __shfl_down(A.x, 1);
+            B.y = __shfl_down(A.y, 1);
+            B.z = __shfl_down(A.z, 1);
+            B.w = __shfl_down(A.w, 1);
+            return B;
+        };
+        uint64_t i0 = 0;
+        for (; i0 + 1024 <= body; i0 += 1024) {
+            u32x4v A[4], E[4];
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                A[q] = __builtin_nontemporal_load(s16 + i0 + 256 * q + t);
+                E[q] = A[q];
+                if (sh && ln == 63u) E[q] = __builtin_nontemporal_load(s16 + i0 + 256 * q + t + 1);
+            }
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                u32x4v v = A[q];
+                if (sh) {
+                    u32x4v B = nbr(A[q]);
+                    if (ln == 63u) B = E[q];
+                    v = funnel(A[q], B);
+                }
+                __builtin_nontemporal_store(v, db + i0 + 256 * q + t);
+            }
         }
-        for (; i < body; i += 256) __builtin_nontemporal_store(ld16u(sb + 16 * i), db + i);
+        for (uint64_t i = i0 + t; i0 < body; i0 += 256, i += 256) {
+            // every lane of the wave runs the shuffle; lanes past the body
+            // load nothing and store nothing
+            const bool on = i < body;
+            u32x4v A = {0u, 0u, 0u, 0u};
+            if (on) A = __builtin_nontemporal_load(s16 + i);
+            u32x4v v = A;
+            if (sh) {
+                u32x4v B = nbr(A);
+                if (on && (ln == 63u || i + 1 >= body)) B = __builtin_nontemporal_load(s16 + i + 1);
+                v = funnel(A, B);
+            }
+            if (on) __builtin_nontemporal_store(v, db + i);
+        }
         const uint64_t done = head + 16 * body;
         if (t < len - done) d[done + t] = s[done + t];
     }

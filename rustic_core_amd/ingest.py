@@ -55,6 +55,24 @@ def _void32(ids: np.ndarray) -> np.ndarray:
     return np.ascontiguousarray(ids).view(np.dtype((np.void, 32))).ravel()
 
 
+def first_occurrences(ids: np.ndarray, order: np.ndarray, known) -> np.ndarray:
+    """The chunks among `order` (indices in chunk order) that the packer
+    would add (packer.rs:304-315): the first occurrence of each id, unless
+    the index already has it (`known`, a set of 32-byte ids)."""
+    out = np.zeros(len(ids), bool)
+    order = np.sort(np.asarray(order, np.int64))
+    if not len(order):
+        return out
+    _, fi = np.unique(_void32(ids[order]), return_index=True)
+    cand = order[fi]
+    out[cand] = True
+    if known:
+        for i in cand:
+            if bytes(ids[i]) in known:
+                out[i] = False
+    return out
+
+
 def _slots(lens, extra: int = 48, align: int = 16):
     """Offsets of slots of (len + extra) bytes, each `align`-aligned."""
     lens = np.asarray(lens, np.int64)
@@ -250,16 +268,7 @@ class DeviceIngest:
         if len(sidx):
             ids[sidx] = sout[:len(sidx)].cpu().numpy()
         known = self.indexed
-        first = np.zeros(n, bool)
-        order_s = np.sort(sidx)
-        if len(order_s):
-            _, fi = np.unique(_void32(ids[order_s]), return_index=True)
-            cand = order_s[fi]
-            first[cand] = True
-            if known:
-                for i in cand:
-                    if bytes(ids[i]) in known:
-                        first[i] = False
+        first = first_occurrences(ids, sidx, known)
         snew = np.nonzero(first & ~is_long)[0]
         t2 = time.perf_counter()
         st_short = None
@@ -284,14 +293,7 @@ class DeviceIngest:
         ms["long_ids_ready"] = (time.perf_counter() - t0) * 1e3
         if len(lidx_q):
             ids[lidx_q] = lout[:len(lidx_q)].cpu().numpy()
-        new = np.zeros(n, bool)
-        if n:
-            _, fi = np.unique(_void32(ids), return_index=True)
-            new[fi] = True
-            if known:
-                for i in fi:
-                    if bytes(ids[i]) in known:
-                        new[i] = False
+        new = first_occurrences(ids, np.arange(n), known)
         assert done[new].all(), "a new blob was not processed"
         nidx = np.nonzero(new)[0]
         t3 = time.perf_counter()
