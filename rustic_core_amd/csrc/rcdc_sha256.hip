@@ -307,6 +307,12 @@ __device__ __forceinline__ uint64_t wave_max_u64(uint64_t x) {
 __device__ __forceinline__ void sha256_split(const uint8_t *__restrict__ arena, ChunkLoc c,
                                              uint32_t *__restrict__ out) {
     __shared__ uint4 kw[2][16][64];  // [slot][t / 4][lane]: 32 KiB
+    // issue priority over other kernels' waves on the same SIMD: a chunk's
+    // chain is latency-bound, and next to compress / seal kernels (the
+    // device ingest runs them under the ids) it otherwise gets a share of
+    // the SIMD's issue slots (waves of this kernel stay equal among
+    // themselves)
+    __builtin_amdgcn_s_setprio(2);
     const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const uint32_t k = (uint32_t)(c.p & 3);
     const uint32_t *q0 = (const uint32_t *)(arena + (c.p - k));
