@@ -25,8 +25,19 @@ __device__ __forceinline__ uint32_t in_vgpr(uint32_t x) {
     return r;
 }
 
+// The tables always live in LDS: address them there even where the pointer
+// reaches the code as a generic one (a non-inlined round, rcdc_walk.hip), so
+// the lookups are ds_read_b64 and not flat loads.
+typedef const __attribute__((address_space(3))) uint8_t lds_u8;
+typedef const __attribute__((address_space(3))) unsigned long long lds_u64;
+
 __device__ __forceinline__ uint2 lds_u2(const uint8_t *tab, uint32_t byte_addr) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    const unsigned long long v = *reinterpret_cast<lds_u64 *>((lds_u8 *)tab + byte_addr);
+    return make_uint2((uint32_t)v, (uint32_t)(v >> 32));
+#else  // (host pass: never called)
     return *reinterpret_cast<const uint2 *>(tab + byte_addr);
+#endif
 }
 
 struct Unit {

@@ -163,6 +163,8 @@ __device__ __forceinline__ void stats_flush(BlockStats &S, unsigned long long *g
     if (threadIdx.x < kWalkStats && S.v[threadIdx.x]) atomicAdd(&g[threadIdx.x], S.v[threadIdx.x]);
 }
 
+struct GapQueue;
+
 // A walker over one stream: one wave (LANES = 64) or one workgroup of 1024.
 struct Walk {
     const uint8_t *arena;
@@ -178,6 +180,12 @@ struct Walk {
     // and the bytes its rounds hashed (LANES x (S + 64) per round)
     uint32_t rounds, zones;
     uint64_t lbytes;
+    // walk kernel: the workgroup's round ring (nullptr elsewhere); a walker
+    // posts rounds ahead of its search there while waves of its workgroup
+    // are idle (the walk's tail), `wv` is its wave index
+    GapQueue *Q;
+    uint32_t wv, help;  // help: most rounds a walker posts at once
+    uint64_t hrounds, hbytes;  // rounds this wave ran for others (ring jobs), bytes
 };
 
 // Segment of a round that starts at A and only needs positions below end:
@@ -248,6 +256,126 @@ __device__ uint64_t round_first(const Walk &W, uint64_t A, uint64_t q, uint64_t 
     return best;
 }
 
+// ---- gap rounds shared inside a check workgroup ----------------------------
+// The chain phase lasts as long as its slowest boundary, and the slow ones
+// hash unsearched gaps (up to min + 64 bytes: 8 sequential 64-lane rounds).
+// A wave with a gap of >= 2 rounds posts them as jobs in an LDS ring; every
+// wave of the workgroup that waits -- for its own jobs, or because no
+// boundaries are left -- pops and runs jobs, so in the tail up to 8 waves
+// hash one gap.  No barriers: LDS atomics, per-slot ready flags, s_sleep.
+// Termination: a waiting wave runs jobs itself (its own included), so every
+// posted job is run; idle waves leave when no wave is active and the ring is
+// empty.
+constexpr uint32_t kGapSlots = 256;  // >= 16 walkers x 15 posted rounds (check: 8 x 16)
+constexpr uint32_t kChkWaves = 8;
+constexpr uint32_t kGapReq = 16;     // requesting waves (walk: 16, check: 8)
+struct GapQueue {
+    uint32_t head, tail, active, idle;  // idle: walk waves that found no piece left
+    uint32_t ready[kGapSlots];
+    uint32_t req[kGapSlots];
+    uint64_t A[kGapSlots], lo[kGapSlots], hi[kGapSlots], off[kGapSlots];
+    unsigned long long hit[kGapReq];  // per requesting wave: min over its rounds
+    uint32_t left[kGapReq];           // its rounds not yet run
+};
+
+__device__ __forceinline__ uint32_t lds_load(const uint32_t *p) {
+    return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+__device__ __forceinline__ void lds_store(uint32_t *p, uint32_t v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+// Pop one job (wave-uniform): its ring slot, or kGapSlots if the ring is empty.
+__device__ uint32_t gap_pop(GapQueue &Q, uint32_t lane) {
+    uint32_t got = 0xFFFFFFFFu;
+    if (lane == 0) {
+        uint32_t h = lds_load(&Q.head);
+        while (h < lds_load(&Q.tail)) {
+            const uint32_t prev = atomicCAS(&Q.head, h, h + 1);
+            if (prev == h) {
+                got = h;
+                break;
+            }
+            h = prev;
+        }
+    }
+    got = __builtin_amdgcn_readfirstlane(got);
+    if (got == 0xFFFFFFFFu) return kGapSlots;
+    const uint32_t sl = got % kGapSlots, lap = got / kGapSlots + 1;
+    // ready[sl] holds the lap of the job it carries (0: empty), so a job of
+    // an earlier lap not yet copied out is never taken for this one
+    while (__builtin_amdgcn_readfirstlane(lds_load(&Q.ready[sl])) != lap) __builtin_amdgcn_s_sleep(1);
+    return sl;
+}
+
+// Run the job in slot sl: one 64-lane round, its first hit into hit[req].
+template <int TSH, bool SMALL>
+__device__ void gap_run(GapQueue &Q, Walk &W, uint32_t sl, uint64_t &rounds, uint64_t &lbytes) {
+    const uint64_t A = Q.A[sl], lo = Q.lo[sl], hi = Q.hi[sl];
+    const uint64_t off = Q.off[sl], own_off = W.off;
+    const uint32_t r = Q.req[sl];
+    wave_sync();
+    if (W.lane == 0) lds_store(&Q.ready[sl], 0);  // fields copied: the slot is free
+    // a hit the requester already has before this round makes it moot
+    if (readlane64(__hip_atomic_load(&Q.hit[r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP), 0) <= A) {
+        if (W.lane == 0) atomicSub(&Q.left[r], 1u);
+        return;
+    }
+    const uint32_t S = round_seg<64>(W.S, A, hi);
+    W.off = off;  // (the requester's stream)
+    const uint64_t h = round_first<64, TSH, SMALL>(W, A, lo, hi, S);
+    W.off = own_off;
+    rounds++;
+    lbytes += 64ull * (S + 64);
+    if (W.lane == 0) {
+        if (h != kNoCut) atomicMin(&Q.hit[r], (unsigned long long)h);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        atomicSub(&Q.left[r], 1u);
+    }
+}
+
+// The walk's tail: while waves of the workgroup have no piece left, a
+// walker posts up to kHelpMax rounds after its round A to the ring, hashes
+// A itself and then waits for the idle waves to run the posted ones (it runs
+// none itself: one copy of the round loop per wave role keeps the walk
+// kernel spill-free).  Rounds past a hit are wasted, but only on waves that
+// would idle.
+constexpr uint32_t kHelpMax = 15;  // x 16 walkers <= kGapSlots; WalkParams.helpers caps it
+
+__device__ void walk_post(Walk &W, uint64_t A, uint64_t q, uint64_t end, uint32_t K) {
+    GapQueue &Q = *W.Q;
+    const uint64_t step = 64ull * W.S;
+    uint32_t t = 0;
+    if (W.lane == 0) {
+        Q.hit[W.wv] = kNoCut;
+        lds_store(&Q.left[W.wv], K);
+        t = atomicAdd(&Q.tail, K);
+        for (uint32_t r = 0; r < K; r++) {
+            const uint32_t sl = (t + r) % kGapSlots, lap = (t + r) / kGapSlots + 1;
+            while (lds_load(&Q.ready[sl]) != 0) __builtin_amdgcn_s_sleep(1);
+            Q.A[sl] = A + (r + 1) * step;
+            Q.lo[sl] = q;
+            Q.hi[sl] = end;
+            Q.off[sl] = W.off;
+            Q.req[sl] = W.wv;
+            lds_store(&Q.ready[sl], lap);
+        }
+    }
+    wave_sync();
+}
+
+// The first hit over the walker's own round (own) and its posted ones.
+__device__ uint64_t walk_wait(Walk &W, uint64_t own) {
+    GapQueue &Q = *W.Q;
+    if (W.lane == 0 && own != kNoCut) atomicMin(&Q.hit[W.wv], (unsigned long long)own);
+    while (__builtin_amdgcn_readfirstlane(lds_load(&Q.left[W.wv])) != 0) __builtin_amdgcn_s_sleep(2);
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    uint64_t h = 0;
+    if (W.lane == 0) h = Q.hit[W.wv];
+    return readlane64(h, 0);
+}
+
 // The end of the chunk starting at pos (rabin.rs:110-191), or kOpen if no
 // cut was found below stop_scan (the search stopped there).  *kind: what the
 // walker verified (rcdc_internal.h kKind*); *zero: all-zero prefill cut.
@@ -294,15 +422,29 @@ __device__ uint64_t walk_next(Walk &W, uint64_t pos, uint64_t stop_scan, uint64_
     const uint64_t end = min(limit, stop_scan);
     uint64_t A = ((W.off + q - 1) & ~63ull) - W.off;  // A + 1 <= q: q is tested
     while (A < end) {
+        uint32_t K = 0;  // rounds posted for idle waves (the walk kernel's tail)
+        if constexpr (LANES == 64) {
+            if (W.Q) {
+                const uint32_t idle = __builtin_amdgcn_readfirstlane(lds_load(&W.Q->idle));
+                if (idle) {
+                    const uint64_t step = 64ull * W.S, R = (end - A + step - 1) / step;
+                    K = (uint32_t)min((uint64_t)min(min(idle, kHelpMax), W.help), R - 1);
+                    if (K) walk_post(W, A, q, end, K);
+                }
+            }
+        }
         const uint32_t S = round_seg<LANES>(W.S, A, end);
         W.rounds++;
         W.lbytes += (uint64_t)LANES * (S + 64);
-        const uint64_t p = round_first<LANES, TSH, SMALL>(W, A, q, end, S);
+        uint64_t p = round_first<LANES, TSH, SMALL>(W, A, q, end, S);
+        if constexpr (LANES == 64) {
+            if (K) p = walk_wait(W, p);
+        }
         if (p != kNoCut) {
             *kind = kKindHit;
             return p;
         }
-        A += (uint64_t)LANES * W.S;
+        A += (uint64_t)LANES * W.S * (K + 1);
     }
     if (end == limit) {
         *kind = limit == W.N ? kKindEof : kKindMax;
@@ -347,8 +489,15 @@ __global__ __launch_bounds__(1024, 1) void rcdc_walk_kernel(
     __shared__ __attribute__((aligned(16))) uint8_t s_tab[kLdsBytes];
     __shared__ __attribute__((aligned(16))) uint8_t s_win[16][128];
     __shared__ BlockStats s_st;
+    __shared__ GapQueue s_q;
     stats_init(s_st);
-    fill_tables(s_tab, gtab, prm.idx_shift, threadIdx.x, 1024);
+    if (threadIdx.x == 0) {
+        s_q.head = s_q.tail = 0;
+        s_q.active = 16;
+        s_q.idle = 0;
+    }
+    for (uint32_t i = threadIdx.x; i < kGapSlots; i += blockDim.x) s_q.ready[i] = 0;
+    fill_tables(s_tab, gtab, prm.idx_shift, threadIdx.x, 1024);  // (ends with a barrier)
     const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
     Walk W;
     W.arena = arena;
@@ -365,12 +514,32 @@ __global__ __launch_bounds__(1024, 1) void rcdc_walk_kernel(
     W.lane = lane;
     W.wave = 0;  // a wave walker: lane t of the round is t
     W.tid = lane;
+    W.Q = prm.helpers ? &s_q : nullptr;
+    W.wv = wave;
+    W.help = prm.helpers;
+    W.hrounds = W.hbytes = 0;
+    // per-run unit state after the status words: the start each piece's
+    // chain was walked from, and (run-on) the claim epoch of each unit
+    uint64_t *pstart = pstatus + prm.nunits;
+    unsigned long long *claim = reinterpret_cast<unsigned long long *>(pstatus + 2ull * prm.nunits);
+    uint32_t u = 0;
+    uint64_t start = 0;
+    bool cont = false;  // u was claimed by running on from the previous piece
     for (;;) {
-        uint32_t q = 0;
-        if (lane == 0) q = atomicAdd(&ctr[0], 1u);
-        q = __builtin_amdgcn_readfirstlane(q);
-        if (q >= prm.nunits) break;
-        const uint32_t u = __builtin_amdgcn_readfirstlane(prm.order[q]);
+        if (!cont) {
+            uint32_t q = 0;
+            if (lane == 0) q = atomicAdd(&ctr[0], 1u);
+            q = __builtin_amdgcn_readfirstlane(q);
+            if (q >= prm.nunits) break;
+            u = __builtin_amdgcn_readfirstlane(prm.order[q]);
+            if (prm.runon) {  // a piece another walker ran on into is taken
+                uint32_t got = 0;
+                if (lane == 0) got = atomicMax(&claim[u], (unsigned long long)prm.epoch) < prm.epoch;
+                if (!__builtin_amdgcn_readfirstlane(got)) continue;
+            }
+            start = units[u].start;
+        }
+        cont = false;
         const uint64_t t0 = prm.trace ? (uint64_t)wall_clock64() : 0;
         W.rounds = W.zones = 0;
         W.lbytes = 0;
@@ -381,7 +550,7 @@ __global__ __launch_bounds__(1024, 1) void rcdc_walk_kernel(
         const uint8_t *s = arena + d.off;
         uint64_t *out = piece_cuts + U.out_base;
         const uint64_t stop_scan = U.stop < d.n ? U.stop + W.mn + 64 : ~0ull;
-        uint64_t pos = U.start, n = 0;
+        uint64_t pos = start, n = 0;
         bool open = false;
         while (pos < d.n) {
             uint64_t kind;
@@ -409,7 +578,32 @@ __global__ __launch_bounds__(1024, 1) void rcdc_walk_kernel(
             }
             if (pos >= U.stop) break;
         }
+        // run on: the chain ended at its first cut pos >= stop; the pieces
+        // up to the one holding pos are taken in order while nobody has
+        // them.  Those its last chunk spans are skipped (chain start pos, no
+        // cuts: no merge ever lands in them, and their boundaries are off
+        // the assembled chain); the one holding pos is walked from pos (its
+        // boundary merges at once: its chain starts on this one's).
+        uint32_t nxt = u + 1;
+        if (prm.runon && !open && pos >= U.stop && pos < d.n) {
+            const uint32_t uend = U.unit0 + U.npieces;
+            for (; nxt < uend; nxt++) {
+                uint32_t got = 0;
+                if (lane == 0)
+                    got = atomicMax(&claim[nxt], (unsigned long long)prm.epoch) < prm.epoch;
+                if (!__builtin_amdgcn_readfirstlane(got)) break;
+                if (pos < units[nxt].stop) {
+                    cont = true;
+                    break;
+                }
+                if (lane == 0) {
+                    pstart[nxt] = pos;
+                    pstatus[nxt] = 0;
+                }
+            }
+        }
         if (lane == 0) {
+            pstart[u] = start;
             pstatus[u] = min(n, (uint64_t)U.out_cap) | (open ? kOpenFlag : 0ull) |
                          (n > U.out_cap ? (kOpenFlag << 1) : 0ull);
             stats_add(s_st, kWalkStatRounds, W.rounds);
@@ -424,6 +618,32 @@ __global__ __launch_bounds__(1024, 1) void rcdc_walk_kernel(
                 tr[3] = n;
             }
         }
+        if (cont) {
+            u = nxt;
+            start = pos;
+        }
+    }
+    // no piece left: hash other walkers' rounds until every walker of the
+    // workgroup is done and the ring is empty
+    if (lane == 0) {
+        atomicAdd(&s_q.idle, 1u);
+        atomicSub(&s_q.active, 1u);
+    }
+    for (;;) {
+        const uint32_t sl = gap_pop(s_q, lane);
+        if (sl < kGapSlots) {
+            gap_run<TSH, SMALL>(s_q, W, sl, W.hrounds, W.hbytes);
+            continue;
+        }
+        const uint32_t act = __builtin_amdgcn_readfirstlane(lds_load(&s_q.active));
+        const uint32_t hd = __builtin_amdgcn_readfirstlane(lds_load(&s_q.head));
+        const uint32_t tl = __builtin_amdgcn_readfirstlane(lds_load(&s_q.tail));
+        if (act == 0 && hd == tl) break;
+        __builtin_amdgcn_s_sleep(2);
+    }
+    if (lane == 0) {
+        stats_add(s_st, kWalkStatRounds, W.hrounds);
+        stats_add(s_st, kWalkStatBytes, W.hbytes);
     }
     stats_flush(s_st, prm.stats);
 }
@@ -456,14 +676,18 @@ struct PieceView {
     bool open, full;  // full: the list holds every cut the walker found
 };
 
+// The piece's chain starts at the start its walker used (pstatus[nunits +
+// uk]): the unit's own start, or -- a piece its walker ran on into -- the
+// previous piece's last cut.
 __device__ __forceinline__ PieceView piece_view(const WalkUnit *units, const uint64_t *pstatus,
-                                                const uint64_t *piece_cuts, uint32_t uk) {
+                                                const uint64_t *piece_cuts, uint32_t uk,
+                                                uint32_t nunits) {
     const WalkUnit Uk = units[uk];
     const uint64_t st = pstatus[uk];
     PieceView V;
     V.L = piece_cuts + Uk.out_base;
     V.n = st & 0xFFFFFFFFu;
-    V.start = Uk.start;
+    V.start = pstatus[nunits + uk];
     V.stop = Uk.stop;
     V.open = (st & kOpenFlag) != 0;
     V.full = (st & (kOpenFlag << 1)) == 0;
@@ -540,6 +764,7 @@ struct CheckCtx {
     const uint64_t *pstatus, *piece_cuts;
     WalkUnit U;   // the boundary's unit (piece j)
     uint32_t u;   // its index
+    uint32_t nunits;
     uint64_t N, mn, mx;
     uint64_t Lp, Ls;  // piece sizes (piece_at)
     uint64_t budget;  // bytes this boundary may still hash
@@ -572,79 +797,6 @@ __device__ __forceinline__ uint32_t piece_of(const CheckCtx &C, uint64_t p) {
     return piece_at(C.U, C.Lp, C.Ls, p);
 }
 
-// ---- gap rounds shared inside a check workgroup ----------------------------
-// The chain phase lasts as long as its slowest boundary, and the slow ones
-// hash unsearched gaps (up to min + 64 bytes: 8 sequential 64-lane rounds).
-// A wave with a gap of >= 2 rounds posts them as jobs in an LDS ring; every
-// wave of the workgroup that waits -- for its own jobs, or because no
-// boundaries are left -- pops and runs jobs, so in the tail up to 8 waves
-// hash one gap.  No barriers: LDS atomics, per-slot ready flags, s_sleep.
-// Termination: a waiting wave runs jobs itself (its own included), so every
-// posted job is run; idle waves leave when no wave is active and the ring is
-// empty.
-constexpr uint32_t kGapSlots = 128;  // >= 8 waves x 9 outstanding rounds
-constexpr uint32_t kChkWaves = 8;
-struct GapQueue {
-    uint32_t head, tail, active, pad;
-    uint32_t ready[kGapSlots];
-    uint32_t req[kGapSlots];
-    uint64_t A[kGapSlots], lo[kGapSlots], hi[kGapSlots], off[kGapSlots];
-    unsigned long long hit[kChkWaves];  // per requesting wave: min over its rounds
-    uint32_t left[kChkWaves];           // its rounds not yet run
-};
-
-__device__ __forceinline__ uint32_t lds_load(const uint32_t *p) {
-    return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-
-__device__ __forceinline__ void lds_store(uint32_t *p, uint32_t v) {
-    __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-
-// Pop one job (wave-uniform): its ring slot, or kGapSlots if the ring is empty.
-__device__ uint32_t gap_pop(GapQueue &Q, uint32_t lane) {
-    uint32_t got = 0xFFFFFFFFu;
-    if (lane == 0) {
-        uint32_t h = lds_load(&Q.head);
-        while (h < lds_load(&Q.tail)) {
-            const uint32_t prev = atomicCAS(&Q.head, h, h + 1);
-            if (prev == h) {
-                got = h;
-                break;
-            }
-            h = prev;
-        }
-    }
-    got = __builtin_amdgcn_readfirstlane(got);
-    if (got == 0xFFFFFFFFu) return kGapSlots;
-    const uint32_t sl = got % kGapSlots, lap = got / kGapSlots + 1;
-    // ready[sl] holds the lap of the job it carries (0: empty), so a job of
-    // an earlier lap not yet copied out is never taken for this one
-    while (__builtin_amdgcn_readfirstlane(lds_load(&Q.ready[sl])) != lap) __builtin_amdgcn_s_sleep(1);
-    return sl;
-}
-
-// Run the job in slot sl: one 64-lane round, its first hit into hit[req].
-template <int TSH, bool SMALL>
-__device__ void gap_run(GapQueue &Q, const Walk &W, uint32_t sl, uint64_t *rounds,
-                        uint64_t *lbytes) {
-    Walk H = W;
-    const uint64_t A = Q.A[sl], lo = Q.lo[sl], hi = Q.hi[sl];
-    H.off = Q.off[sl];
-    const uint32_t r = Q.req[sl];
-    wave_sync();
-    if (W.lane == 0) lds_store(&Q.ready[sl], 0);  // fields copied: the slot is free
-    const uint32_t S = round_seg<64>(W.S, A, hi);
-    const uint64_t h = round_first<64, TSH, SMALL>(H, A, lo, hi, S);
-    (*rounds)++;
-    *lbytes += 64ull * (S + 64);
-    if (W.lane == 0) {
-        if (h != kNoCut) atomicMin(&Q.hit[r], (unsigned long long)h);
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-        atomicSub(&Q.left[r], 1u);
-    }
-}
-
 // First pure-window hit in [lo, lim) of the stream, or lim if none;
 // kNoCut if the hashing budget ran out.
 template <int TSH, bool SMALL>
@@ -662,7 +814,8 @@ __device__ uint64_t check_first_hit(Walk &W, CheckCtx &C, uint64_t lo, uint64_t 
         uint64_t gap_end = lim;
         for (int back = 0; back < 2 && !known; back++) {
             if (back == 1 && k == 0) break;
-            const PieceView V = piece_view(C.units, C.pstatus, C.piece_cuts, C.U.unit0 + k - back);
+            const PieceView V =
+                piece_view(C.units, C.pstatus, C.piece_cuts, C.U.unit0 + k - back, C.nunits);
             uint64_t vend, vkind, nxt;
             if (cover(V, p, C.mn, &vend, &vkind, &nxt)) {
                 if (vkind == kKindHit) return min(vend, lim);
@@ -681,7 +834,7 @@ __device__ uint64_t check_first_hit(Walk &W, CheckCtx &C, uint64_t lo, uint64_t 
         uint64_t A = ((W.off + p - 1) & ~63ull) - W.off;
         const uint64_t step = 64ull * W.S;
         const uint64_t R = (gap_end - A + step - 1) / step;
-        if (Q && R >= 2 && R <= kGapSlots / kChkWaves) {  // (ring capacity: 8 waves x 16)
+        if (Q && R >= 2 && R <= 16) {  // (ring capacity: 8 waves x 16)
             // post the R rounds, then run jobs until ours are done
             uint32_t t = 0;
             if (W.lane == 0) {
@@ -705,7 +858,7 @@ __device__ uint64_t check_first_hit(Walk &W, CheckCtx &C, uint64_t lo, uint64_t 
             wave_sync();
             while (__builtin_amdgcn_readfirstlane(lds_load(&Q->left[wave])) != 0) {
                 const uint32_t sl = gap_pop(*Q, W.lane);
-                if (sl < kGapSlots) gap_run<TSH, SMALL>(*Q, W, sl, shared_rounds, shared_lbytes);
+                if (sl < kGapSlots) gap_run<TSH, SMALL>(*Q, W, sl, *shared_rounds, *shared_lbytes);
                 else __builtin_amdgcn_s_sleep(2);
             }
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
@@ -736,7 +889,7 @@ __device__ __forceinline__ bool merged_at(const CheckCtx &C, uint64_t c, uint32_
         if (back == 1 && k == 0) break;
         const uint32_t uk = C.U.unit0 + k - back;
         if (uk < C.u) break;
-        const PieceView V = piece_view(C.units, C.pstatus, C.piece_cuts, uk);
+        const PieceView V = piece_view(C.units, C.pstatus, C.piece_cuts, uk, C.nunits);
         if (back == 0 && c == V.start) {
             *mu = uk;
             *idx = -1;
@@ -790,6 +943,9 @@ __global__ __launch_bounds__(kChkThreads, 1) void rcdc_walk_check_kernel(
     W.lane = lane;
     W.wave = 0;
     W.tid = lane;
+    W.Q = nullptr;
+    W.wv = wave;
+    W.hrounds = W.hbytes = 0;
     const ModRepl mod{s_tab, W.k.lwm};
     const uint64_t mn = prm.min_size, mx = prm.max_size;
     for (;;) {
@@ -813,6 +969,7 @@ __global__ __launch_bounds__(kChkThreads, 1) void rcdc_walk_check_kernel(
         C.piece_cuts = piece_cuts;
         C.U = U;
         C.u = u;
+        C.nunits = prm.nunits;
         C.N = N;
         C.mn = mn;
         C.mx = mx;
@@ -829,7 +986,7 @@ __global__ __launch_bounds__(kChkThreads, 1) void rcdc_walk_check_kernel(
         uint64_t *hops = s_hops[wave];
         // exact state at the previous piece's end: closed at c, or open from c
         // ([c+min+64, a_j+min+64) hit-free, no zone cut in c's zone)
-        const PieceView Vp = piece_view(units, pstatus, piece_cuts, u - 1);
+        const PieceView Vp = piece_view(units, pstatus, piece_cuts, u - 1, prm.nunits);
         uint64_t c;
         bool pending = false;
         if (Vp.open) {
@@ -963,7 +1120,7 @@ __global__ __launch_bounds__(kChkThreads, 1) void rcdc_walk_check_kernel(
     for (;;) {
         const uint32_t sl = gap_pop(s_q, lane);
         if (sl < kGapSlots) {
-            gap_run<TSH, SMALL>(s_q, W, sl, &shared_rounds, &shared_lbytes);
+            gap_run<TSH, SMALL>(s_q, W, sl, shared_rounds, shared_lbytes);
             continue;
         }
         const uint32_t act = __builtin_amdgcn_readfirstlane(lds_load(&s_q.active));
@@ -1014,6 +1171,9 @@ __global__ __launch_bounds__(1024, 1) void rcdc_walk_fixup_kernel(
     W.lane = lane;
     W.wave = wave;
     W.tid = threadIdx.x;
+    W.Q = nullptr;
+    W.wv = wave;
+    W.hrounds = W.hbytes = 0;
     for (uint32_t idx = blockIdx.x; idx < nfix; idx += gridDim.x) {
         const uint32_t u = fixlist[idx];
         const WalkUnit U = units[u];
@@ -1052,7 +1212,7 @@ __global__ __launch_bounds__(1024, 1) void rcdc_walk_fixup_kernel(
                             const uint32_t uk = U.unit0 + (uint32_t)(k - back);
                             if (uk < u) break;  // never before the boundary's own piece
                             const WalkUnit Uk = units[uk];
-                            if (back == 0 && cut == Uk.start) {
+                            if (back == 0 && cut == pstatus[prm.nunits + uk]) {
                                 mu = uk;
                                 at = -1;
                             } else {
@@ -1318,6 +1478,51 @@ __global__ __launch_bounds__(256) void rcdc_walk_cost_kernel(
     }
 }
 
+// Run-on queue order.  Walkers that start far apart in cost (not bytes)
+// finish their stretches at about the same time, and a walker that runs out
+// of work should take a piece halfway into the largest stretch nobody has
+// reached.  Both come from one key per piece: with the cost of piece j
+// c_j = 1 + 4 x (its sampled non-zero words, 0..64) and its stream's running
+// cost [a, b) = [c_0 + .. + c_{j-1}, a + c_j), key = the highest k such that
+// [a, b) holds a multiple of 2^k (a = 0: 63).  Sorted by descending key,
+// the queue hands out every stream's first piece, then the pieces holding
+// multiples of the largest powers of two, so streams get early pieces in
+// proportion to their cost and each later piece halves a stretch.  One
+// workgroup per stream (the keys then go through rcdc_walk_sort_kernel).
+__global__ __launch_bounds__(256) void rcdc_walk_level_kernel(const WalkUnit *__restrict__ units,
+                                                              WalkParams prm, uint8_t *key) {
+    __shared__ uint64_t s_w[4];
+    const uint32_t u0 = prm.su0[blockIdx.x];
+    const uint32_t P = units[u0].npieces;
+    const uint32_t t = threadIdx.x, lane = t & 63u, wave = t >> 6;
+    uint64_t carry = 0;
+    for (uint32_t c0 = 0; c0 < P; c0 += 256) {
+        const uint32_t j = c0 + t;
+        uint64_t c = 0;
+        if (j < P) {
+            const uint32_t k = key[u0 + j];  // cost kernel: class (+65 for big pieces)
+            c = 1u + 4u * (k >= 65u ? k - 65u : k);
+        }
+        uint64_t v = c;  // inclusive scan: wave, then the 4 wave totals
+        for (uint32_t o = 1; o < 64; o <<= 1) {
+            const uint64_t x = __shfl_up(v, o, 64);
+            if (lane >= o) v += x;
+        }
+        if (lane == 63) s_w[wave] = v;
+        __syncthreads();
+        uint64_t before = carry;
+        for (uint32_t w = 0; w < wave; w++) before += s_w[w];
+        const uint64_t total = s_w[0] + s_w[1] + s_w[2] + s_w[3];
+        __syncthreads();
+        if (j < P) {
+            const uint64_t b = before + v, a = b - c;
+            const uint32_t lvl = a == 0 ? 63u : 63u - (uint32_t)__builtin_clzll((a - 1) ^ (b - 1));
+            key[u0 + j] = (uint8_t)lvl;
+        }
+        carry += total;
+    }
+}
+
 // One workgroup: counting sort of the queue by key, descending.
 __global__ __launch_bounds__(1024) void rcdc_walk_sort_kernel(WalkParams prm,
                                                               const uint8_t *__restrict__ key) {
@@ -1356,6 +1561,9 @@ hipError_t launch_walk(const uint8_t *arena, const StreamDesc *sds, const WalkUn
         const uint32_t cb = std::min<uint32_t>((prm.nunits + 3) / 4, 4096);
         hipLaunchKernelGGL(rcdc_walk_cost_kernel, dim3(cb), dim3(256), 0, stream, arena, sds, units,
                            prm, key);
+        if (prm.runon && prm.su0)  // keys by unit (order_in is the unit order)
+            hipLaunchKernelGGL(rcdc_walk_level_kernel, dim3(prm.nwstreams), dim3(256), 0, stream,
+                               units, prm, key);
         hipLaunchKernelGGL(rcdc_walk_sort_kernel, dim3(1), dim3(1024), 0, stream, prm,
                            (const uint8_t *)key);
     }
