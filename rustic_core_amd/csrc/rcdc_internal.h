@@ -125,7 +125,7 @@ struct WalkParams {
     uint32_t nunits;
     uint32_t fix_cap;      // fixup cut slots per boundary
     uint32_t fix_seg;      // S for the fixup walker (latency-bound: smaller rounds)
-    uint32_t epoch;        // run-on claims: this run's epoch (> every earlier run's)
+    uint32_t pad;
     // kWalkStat* counters (always on: one atomic per piece / fixup boundary)
     unsigned long long *stats;
     // optional per-piece trace (nullptr = off): kTraceWords u64 per unit
@@ -137,15 +137,9 @@ struct WalkParams {
     const uint32_t *order_in;
     uint32_t *order_out;
     uint32_t nbig_units;   // order_in[0, nbig_units) are big pieces
-    uint32_t runon;        // a walker runs on into the next piece while nobody has it
+    uint32_t helpers;      // idle walk waves hash rounds ahead for the busy ones
     uint64_t chk_budget;   // bytes of gap hashing a boundary check may do before
                            // it hands the boundary to the fixup kernel
-    // run-on with cost ordering: the queue goes by the coarsest cost
-    // quantile each piece holds (rcdc_walk_level_kernel, one workgroup per
-    // walked stream: unit0 of each in su0)
-    const uint32_t *su0;
-    uint32_t nwstreams;
-    uint32_t helpers;      // idle walk waves hash up to this many rounds ahead of a busy one
 };
 
 // WalkParams.stats slots

@@ -184,8 +184,6 @@ struct rcdc_plan {
     std::vector<uint32_t> worder;      // walk queue order (big pieces first)
     uint32_t nsmall_units = 0;         // the split pieces at worder's end
     bool walk_many = false;            // pieces outnumber 2x the wave slots
-    bool walk_runon = false;           // walkers run on into the next piece
-    uint32_t wepoch = 0;               // run-on claim epoch of the last run
     uint64_t walk_small = 0;           // Ls of the split pieces
     std::vector<uint8_t> walked;       // per stream: on the walk path
     uint64_t nwpiece_cuts = 0;
@@ -524,34 +522,6 @@ static uint64_t walk_piece_bytes(const uint64_t *lens, uint32_t n, uint64_t mn, 
     return lp;
 }
 
-// Queue order for run-on walking: the walkers' first pieces spread evenly
-// over every stream, later ones split the stretches nobody has reached yet.
-// A stream's pieces go in bit-reversed index order (0, P/2, P/4, 3P/4, ...),
-// and the streams' lists are merged by the fraction of their list each entry
-// sits at, so long streams get proportionally many early entries.
-static void runon_order(rcdc_plan *pl) {
-    std::vector<std::pair<double, uint32_t>> key;
-    key.reserve(pl->wunits.size());
-    for (size_t i = 0; i < pl->wstream_u0.size(); i++) {
-        const uint32_t u0 = pl->wstream_u0[i];
-        const uint32_t P = pl->wunits[u0].npieces;
-        uint32_t bits = 0;
-        while ((1u << bits) < P) bits++;
-        uint32_t rank = 0;
-        for (uint32_t x = 0; x < (1u << bits); x++) {
-            uint32_t r = 0;
-            for (uint32_t b = 0; b < bits; b++) r |= ((x >> b) & 1u) << (bits - 1 - b);
-            if (r >= P) continue;
-            key.emplace_back((double)rank++ / P, u0 + r);
-        }
-    }
-    std::stable_sort(key.begin(), key.end(),
-                     [](const auto &a, const auto &b) { return a.first < b.first; });
-    pl->worder.clear();
-    for (const auto &k : key) pl->worder.push_back(k.second);
-    pl->nsmall_units = 0;
-}
-
 // up: the stream the work lists are uploaded on (nullptr: synchronous copies).
 // Uploads from the plan's own host vectors, which stay unchanged until the
 // next build of this plan (after its previous run has been waited for).
@@ -640,14 +610,7 @@ rcdc_status plan_build(rcdc_ctx *ctx, rcdc_plan *pl, const uint64_t *offs, const
             if (pl->walked[i]) big_total += std::max<uint64_t>(lens[i] / Lp, 1);
         const uint64_t slots = (uint64_t)std::max(ctx->num_cus, 1) * 16;
         pl->walk_many = big_total >= 2 * slots;
-        // run-on walking (RCDC_WALK_RUNON=1; off by default): a walker that
-        // closes its piece goes on into the next one unless another walker
-        // has it, so only the pieces taken from the queue start on an
-        // assumed cut.  It hashes ~2 % fewer bytes on C3 but leaves a longer
-        // tail (10.4 -> 11.5 ms at 4 MiB pieces)
-        pl->walk_runon = false;
-        if (const char *e = getenv("RCDC_WALK_RUNON")) pl->walk_runon = atoi(e) != 0;
-        uint64_t split_pct = pl->walk_many && !pl->walk_runon ? 20 : 0;
+        uint64_t split_pct = pl->walk_many ? 20 : 0;
         if (const char *e = getenv("RCDC_WALK_SPLIT")) split_pct = std::min<uint64_t>(atoll(e), 100);
         const uint64_t Ls = Lp ? std::max<uint64_t>(Lp / 4 / ctx->min, 1) * ctx->min : 0;
         pl->walk_small = Ls;
@@ -691,7 +654,6 @@ rcdc_status plan_build(rcdc_ctx *ctx, rcdc_plan *pl, const uint64_t *offs, const
         }
         pl->worder.insert(pl->worder.end(), small.begin(), small.end());
         pl->nsmall_units = (uint32_t)small.size();
-        if (pl->walk_runon) runon_order(pl);  // (the cost-ordered queue replaces it per run)
     }
     WalkParams &wp = pl->wprm;
     wp = WalkParams{};
@@ -708,10 +670,9 @@ rcdc_status plan_build(rcdc_ctx *ctx, rcdc_plan *pl, const uint64_t *offs, const
     wp.idx_shift = (uint32_t)(ctx->deg - 32);
     wp.shift = (uint32_t)(ctx->deg - 8);
     wp.nunits = (uint32_t)pl->wunits.size();
-    wp.runon = pl->walk_runon ? 1u : 0u;
     // the walk's tail: waves without a piece hash rounds for the busy ones
-    wp.helpers = 7;
-    if (const char *e = getenv("RCDC_WALK_HELP")) wp.helpers = (uint32_t)std::min(std::max(atoi(e), 0), 15);
+    wp.helpers = 1;
+    if (const char *e = getenv("RCDC_WALK_HELP")) wp.helpers = atoi(e) != 0;
     // a fixup walks until it meets a piece's chain: a few chunks, longer only
     // through phase-shifted zero runs (min-sized chunks); more -> host redo
     wp.fix_cap = (uint32_t)(4 * (Lp ? Lp : 1) / ctx->min + ctx->max / ctx->min + 64);
@@ -757,17 +718,9 @@ rcdc_status plan_build(rcdc_ctx *ctx, rcdc_plan *pl, const uint64_t *offs, const
         pl->wprm.order_in = cost ? pl->d_worder : nullptr;
         pl->wprm.order_out = cost ? pl->d_worder + nw : nullptr;
         pl->wprm.nbig_units = (uint32_t)(nw - pl->nsmall_units);
-        if (cost && pl->walk_runon) {
-            // run-on + cost: the level kernel keys pieces by unit, so the
-            // queue's input order is the unit order
-            for (uint32_t u = 0; u < (uint32_t)nw; u++) pl->worder[u] = u;
-            pl->wprm.su0 = pl->d_wsu0;
-            pl->wprm.nwstreams = (uint32_t)pl->wstream_u0.size();
-        }
         HIP_TRY(upload(pl->d_worder, pl->worder.data(), nw * sizeof(uint32_t)));
         if ((st = ensure_dev(&pl->d_wpiece, &pl->cap_wpiece, pl->nwpiece_cuts))) return st;
-        // per unit: status, the start its chain was walked from, run-on claim
-        if ((st = ensure_dev(&pl->d_pstatus, &pl->cap_pstatus, 3 * nw))) return st;
+        if ((st = ensure_dev(&pl->d_pstatus, &pl->cap_pstatus, nw))) return st;
         if ((st = ensure_dev(&pl->d_bres, &pl->cap_bres, nw))) return st;
         if ((st = ensure_dev(&pl->d_ctr, &pl->cap_ctr, 4))) return st;
         if ((st = ensure_dev(&pl->d_fixlist, &pl->cap_fixlist, nw))) return st;
@@ -782,12 +735,7 @@ rcdc_status plan_build(rcdc_ctx *ctx, rcdc_plan *pl, const uint64_t *offs, const
             pl->wprm.trace = pl->d_wtrace;
         }
         HIP_TRY(upload(pl->d_wunits, pl->wunits.data(), nw * sizeof(WalkUnit)));
-        // run-on claims hold epochs of earlier runs: start from none
-        HIP_TRY(up ? hipMemsetAsync(pl->d_pstatus + 2 * nw, 0, nw * 8, up)
-                   : hipMemset(pl->d_pstatus + 2 * nw, 0, nw * 8));
-        if (pl->d_pstatus2 && pl->cap_pstatus2 >= 3 * nw)
-            HIP_TRY(up ? hipMemsetAsync(pl->d_pstatus2 + 2 * nw, 0, nw * 8, up)
-                       : hipMemset(pl->d_pstatus2 + 2 * nw, 0, nw * 8));
+
         HIP_TRY(upload(pl->d_wsu0, pl->wstream_u0.data(),
                           pl->wstream_u0.size() * sizeof(uint32_t)));
     }
@@ -833,7 +781,6 @@ rcdc_status plan_run(rcdc_plan *pl, const void *d_arena, hipStream_t stream) {
     uint64_t *masks = set ? pl->d_masks2 : pl->d_masks;
     // this run's walk buffers and parameters
     WalkParams wprm = pl->wprm;
-    wprm.epoch = ++pl->wepoch;
     uint64_t *wpiece = pl->d_wpiece, *pstatus = pl->d_pstatus, *fixcuts = pl->d_fixcuts;
     BoundRes *bres = pl->d_bres;
     uint32_t *ctr = pl->d_ctr, *fixlist = pl->d_fixlist;
@@ -1622,8 +1569,7 @@ rcdc_status rcdc_plan_set_pipeline(rcdc_plan *plan, int enable) {
         return st;
     if (const uint64_t nw = plan->wunits.size()) {
         if ((st = ensure_dev(&plan->d_wpiece2, &plan->cap_wpiece2, plan->nwpiece_cuts))) return st;
-        if ((st = ensure_dev(&plan->d_pstatus2, &plan->cap_pstatus2, 3 * nw))) return st;
-        HIP_TRY(hipMemset(plan->d_pstatus2 + 2 * nw, 0, nw * 8));  // run-on claims
+        if ((st = ensure_dev(&plan->d_pstatus2, &plan->cap_pstatus2, nw))) return st;
         if ((st = ensure_dev(&plan->d_bres2, &plan->cap_bres2, nw))) return st;
         if ((st = ensure_dev(&plan->d_ctr2, &plan->cap_ctr2, 4))) return st;
         if ((st = ensure_dev(&plan->d_fixlist2, &plan->cap_fixlist2, nw))) return st;

@@ -47,7 +47,11 @@ using namespace rcdc;
 
 namespace {
 
-constexpr int kWR = 3, kWG = 16;   // ring of 3 register units, groups of 16 (scan default)
+#ifndef RCDC_WPAIR
+#define RCDC_WPAIR 0
+#endif
+constexpr int kWR = RCDC_WPAIR ? 4 : 3, kWG = RCDC_WPAIR ? 116 : 16;  // ring of register units, groups of 16
+constexpr bool kWPair = RCDC_WPAIR != 0;  // refill a 128-B line (two units) per lane
 constexpr uint64_t kNoCut = ~0ull;
 constexpr uint64_t kOpen = ~0ull - 1;
 constexpr uint32_t kNoUnit = 0xFFFFFFFFu;
@@ -184,8 +188,6 @@ struct Walk {
     // posts rounds ahead of its search there while waves of its workgroup
     // are idle (the walk's tail), `wv` is its wave index
     GapQueue *Q;
-    uint32_t wv, help;  // help: most rounds a walker posts at once
-    uint64_t hrounds, hbytes;  // rounds this wave ran for others (ring jobs), bytes
 };
 
 // Segment of a round that starts at A and only needs positions below end:
@@ -199,6 +201,15 @@ __device__ __forceinline__ uint32_t round_seg(uint32_t S, uint64_t A, uint64_t e
     if (span >= (uint64_t)LANES * S) return S;
     const uint64_t per = (span + LANES - 1) / LANES;
     return (uint32_t)max((per + 63) / 64 * 64, (uint64_t)64);
+}
+
+// Start A of the first round that tests position q (A + 1 <= q, A >= q -
+// 128), placed so that the lanes' reads (from off + A - 64 + t * S, S a
+// multiple of 128) start on 128-byte lines: with 64-byte-aligned starts
+// every lane's first line is fetched for half its bytes (PMC: the scan
+// kernel read 1.16 x its bytes that way, 1.03 x from 128-byte lines).
+__device__ __forceinline__ uint64_t round_base(uint64_t off, uint64_t q) {
+    return (((off + q - 1 - 64) & ~127ull) + 64) - off;
 }
 
 // First pure-window candidate p in [q, end) among the positions of one round
@@ -229,7 +240,7 @@ __device__ uint64_t round_first(const Walk &W, uint64_t A, uint64_t q, uint64_t 
             (uint32_t)(rest < 0xFFFFFFFFull ? rest : 0xFFFFFFFFull));
         const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
             (void *)(W.arena + wbase), (short)0, (int)rec, 0x00020000);
-        const Chain c = scan_segment<kWR, false, TSH, SMALL, kWG>(rsrc, W.lane * S, S / kUnit,
+        const Chain c = scan_segment<kWR, kWPair, TSH, SMALL, kWG>(rsrc, W.lane * S, S / kUnit,
                                                                    rlo, rhi, W.tab, W.k, valid,
                                                                    W.lane);
         const uint64_t hits = __builtin_amdgcn_ballot_w64(c.first != kNone) & valid;
@@ -341,15 +352,16 @@ __device__ void gap_run(GapQueue &Q, Walk &W, uint32_t sl, uint64_t &rounds, uin
 // none itself: one copy of the round loop per wave role keeps the walk
 // kernel spill-free).  Rounds past a hit are wasted, but only on waves that
 // would idle.
-constexpr uint32_t kHelpMax = 15;  // x 16 walkers <= kGapSlots; WalkParams.helpers caps it
+constexpr uint32_t kHelpMax = 7;  // x 16 walkers <= kGapSlots
 
 __device__ void walk_post(Walk &W, uint64_t A, uint64_t q, uint64_t end, uint32_t K) {
     GapQueue &Q = *W.Q;
+    const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint64_t step = 64ull * W.S;
     uint32_t t = 0;
     if (W.lane == 0) {
-        Q.hit[W.wv] = kNoCut;
-        lds_store(&Q.left[W.wv], K);
+        Q.hit[wv] = kNoCut;
+        lds_store(&Q.left[wv], K);
         t = atomicAdd(&Q.tail, K);
         for (uint32_t r = 0; r < K; r++) {
             const uint32_t sl = (t + r) % kGapSlots, lap = (t + r) / kGapSlots + 1;
@@ -358,7 +370,7 @@ __device__ void walk_post(Walk &W, uint64_t A, uint64_t q, uint64_t end, uint32_
             Q.lo[sl] = q;
             Q.hi[sl] = end;
             Q.off[sl] = W.off;
-            Q.req[sl] = W.wv;
+            Q.req[sl] = wv;
             lds_store(&Q.ready[sl], lap);
         }
     }
@@ -368,11 +380,12 @@ __device__ void walk_post(Walk &W, uint64_t A, uint64_t q, uint64_t end, uint32_
 // The first hit over the walker's own round (own) and its posted ones.
 __device__ uint64_t walk_wait(Walk &W, uint64_t own) {
     GapQueue &Q = *W.Q;
-    if (W.lane == 0 && own != kNoCut) atomicMin(&Q.hit[W.wv], (unsigned long long)own);
-    while (__builtin_amdgcn_readfirstlane(lds_load(&Q.left[W.wv])) != 0) __builtin_amdgcn_s_sleep(2);
+    const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    if (W.lane == 0 && own != kNoCut) atomicMin(&Q.hit[wv], (unsigned long long)own);
+    while (__builtin_amdgcn_readfirstlane(lds_load(&Q.left[wv])) != 0) __builtin_amdgcn_s_sleep(2);
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
     uint64_t h = 0;
-    if (W.lane == 0) h = Q.hit[W.wv];
+    if (W.lane == 0) h = Q.hit[wv];
     return readlane64(h, 0);
 }
 
@@ -420,7 +433,7 @@ __device__ uint64_t walk_next(Walk &W, uint64_t pos, uint64_t stop_scan, uint64_
     }
     const uint64_t q = z + 64;
     const uint64_t end = min(limit, stop_scan);
-    uint64_t A = ((W.off + q - 1) & ~63ull) - W.off;  // A + 1 <= q: q is tested
+    uint64_t A = round_base(W.off, q);
     while (A < end) {
         uint32_t K = 0;  // rounds posted for idle waves (the walk kernel's tail)
         if constexpr (LANES == 64) {
@@ -428,7 +441,7 @@ __device__ uint64_t walk_next(Walk &W, uint64_t pos, uint64_t stop_scan, uint64_
                 const uint32_t idle = __builtin_amdgcn_readfirstlane(lds_load(&W.Q->idle));
                 if (idle) {
                     const uint64_t step = 64ull * W.S, R = (end - A + step - 1) / step;
-                    K = (uint32_t)min((uint64_t)min(min(idle, kHelpMax), W.help), R - 1);
+                    K = (uint32_t)min((uint64_t)min(idle, kHelpMax), R - 1);
                     if (K) walk_post(W, A, q, end, K);
                 }
             }
@@ -515,31 +528,13 @@ __global__ __launch_bounds__(1024, 1) void rcdc_walk_kernel(
     W.wave = 0;  // a wave walker: lane t of the round is t
     W.tid = lane;
     W.Q = prm.helpers ? &s_q : nullptr;
-    W.wv = wave;
-    W.help = prm.helpers;
-    W.hrounds = W.hbytes = 0;
-    // per-run unit state after the status words: the start each piece's
-    // chain was walked from, and (run-on) the claim epoch of each unit
-    uint64_t *pstart = pstatus + prm.nunits;
-    unsigned long long *claim = reinterpret_cast<unsigned long long *>(pstatus + 2ull * prm.nunits);
-    uint32_t u = 0;
-    uint64_t start = 0;
-    bool cont = false;  // u was claimed by running on from the previous piece
+    uint64_t help_rounds = 0, help_bytes = 0;  // rounds this wave ran for others
     for (;;) {
-        if (!cont) {
-            uint32_t q = 0;
-            if (lane == 0) q = atomicAdd(&ctr[0], 1u);
-            q = __builtin_amdgcn_readfirstlane(q);
-            if (q >= prm.nunits) break;
-            u = __builtin_amdgcn_readfirstlane(prm.order[q]);
-            if (prm.runon) {  // a piece another walker ran on into is taken
-                uint32_t got = 0;
-                if (lane == 0) got = atomicMax(&claim[u], (unsigned long long)prm.epoch) < prm.epoch;
-                if (!__builtin_amdgcn_readfirstlane(got)) continue;
-            }
-            start = units[u].start;
-        }
-        cont = false;
+        uint32_t q = 0;
+        if (lane == 0) q = atomicAdd(&ctr[0], 1u);
+        q = __builtin_amdgcn_readfirstlane(q);
+        if (q >= prm.nunits) break;
+        const uint32_t u = __builtin_amdgcn_readfirstlane(prm.order[q]);
         const uint64_t t0 = prm.trace ? (uint64_t)wall_clock64() : 0;
         W.rounds = W.zones = 0;
         W.lbytes = 0;
@@ -550,7 +545,7 @@ __global__ __launch_bounds__(1024, 1) void rcdc_walk_kernel(
         const uint8_t *s = arena + d.off;
         uint64_t *out = piece_cuts + U.out_base;
         const uint64_t stop_scan = U.stop < d.n ? U.stop + W.mn + 64 : ~0ull;
-        uint64_t pos = start, n = 0;
+        uint64_t pos = U.start, n = 0;
         bool open = false;
         while (pos < d.n) {
             uint64_t kind;
@@ -578,32 +573,7 @@ __global__ __launch_bounds__(1024, 1) void rcdc_walk_kernel(
             }
             if (pos >= U.stop) break;
         }
-        // run on: the chain ended at its first cut pos >= stop; the pieces
-        // up to the one holding pos are taken in order while nobody has
-        // them.  Those its last chunk spans are skipped (chain start pos, no
-        // cuts: no merge ever lands in them, and their boundaries are off
-        // the assembled chain); the one holding pos is walked from pos (its
-        // boundary merges at once: its chain starts on this one's).
-        uint32_t nxt = u + 1;
-        if (prm.runon && !open && pos >= U.stop && pos < d.n) {
-            const uint32_t uend = U.unit0 + U.npieces;
-            for (; nxt < uend; nxt++) {
-                uint32_t got = 0;
-                if (lane == 0)
-                    got = atomicMax(&claim[nxt], (unsigned long long)prm.epoch) < prm.epoch;
-                if (!__builtin_amdgcn_readfirstlane(got)) break;
-                if (pos < units[nxt].stop) {
-                    cont = true;
-                    break;
-                }
-                if (lane == 0) {
-                    pstart[nxt] = pos;
-                    pstatus[nxt] = 0;
-                }
-            }
-        }
         if (lane == 0) {
-            pstart[u] = start;
             pstatus[u] = min(n, (uint64_t)U.out_cap) | (open ? kOpenFlag : 0ull) |
                          (n > U.out_cap ? (kOpenFlag << 1) : 0ull);
             stats_add(s_st, kWalkStatRounds, W.rounds);
@@ -618,10 +588,6 @@ __global__ __launch_bounds__(1024, 1) void rcdc_walk_kernel(
                 tr[3] = n;
             }
         }
-        if (cont) {
-            u = nxt;
-            start = pos;
-        }
     }
     // no piece left: hash other walkers' rounds until every walker of the
     // workgroup is done and the ring is empty
@@ -632,7 +598,7 @@ __global__ __launch_bounds__(1024, 1) void rcdc_walk_kernel(
     for (;;) {
         const uint32_t sl = gap_pop(s_q, lane);
         if (sl < kGapSlots) {
-            gap_run<TSH, SMALL>(s_q, W, sl, W.hrounds, W.hbytes);
+            gap_run<TSH, SMALL>(s_q, W, sl, help_rounds, help_bytes);
             continue;
         }
         const uint32_t act = __builtin_amdgcn_readfirstlane(lds_load(&s_q.active));
@@ -642,8 +608,8 @@ __global__ __launch_bounds__(1024, 1) void rcdc_walk_kernel(
         __builtin_amdgcn_s_sleep(2);
     }
     if (lane == 0) {
-        stats_add(s_st, kWalkStatRounds, W.hrounds);
-        stats_add(s_st, kWalkStatBytes, W.hbytes);
+        stats_add(s_st, kWalkStatRounds, help_rounds);
+        stats_add(s_st, kWalkStatBytes, help_bytes);
     }
     stats_flush(s_st, prm.stats);
 }
@@ -676,18 +642,14 @@ struct PieceView {
     bool open, full;  // full: the list holds every cut the walker found
 };
 
-// The piece's chain starts at the start its walker used (pstatus[nunits +
-// uk]): the unit's own start, or -- a piece its walker ran on into -- the
-// previous piece's last cut.
 __device__ __forceinline__ PieceView piece_view(const WalkUnit *units, const uint64_t *pstatus,
-                                                const uint64_t *piece_cuts, uint32_t uk,
-                                                uint32_t nunits) {
+                                                const uint64_t *piece_cuts, uint32_t uk) {
     const WalkUnit Uk = units[uk];
     const uint64_t st = pstatus[uk];
     PieceView V;
     V.L = piece_cuts + Uk.out_base;
     V.n = st & 0xFFFFFFFFu;
-    V.start = pstatus[nunits + uk];
+    V.start = Uk.start;
     V.stop = Uk.stop;
     V.open = (st & kOpenFlag) != 0;
     V.full = (st & (kOpenFlag << 1)) == 0;
@@ -764,7 +726,6 @@ struct CheckCtx {
     const uint64_t *pstatus, *piece_cuts;
     WalkUnit U;   // the boundary's unit (piece j)
     uint32_t u;   // its index
-    uint32_t nunits;
     uint64_t N, mn, mx;
     uint64_t Lp, Ls;  // piece sizes (piece_at)
     uint64_t budget;  // bytes this boundary may still hash
@@ -814,8 +775,7 @@ __device__ uint64_t check_first_hit(Walk &W, CheckCtx &C, uint64_t lo, uint64_t 
         uint64_t gap_end = lim;
         for (int back = 0; back < 2 && !known; back++) {
             if (back == 1 && k == 0) break;
-            const PieceView V =
-                piece_view(C.units, C.pstatus, C.piece_cuts, C.U.unit0 + k - back, C.nunits);
+            const PieceView V = piece_view(C.units, C.pstatus, C.piece_cuts, C.U.unit0 + k - back);
             uint64_t vend, vkind, nxt;
             if (cover(V, p, C.mn, &vend, &vkind, &nxt)) {
                 if (vkind == kKindHit) return min(vend, lim);
@@ -831,7 +791,7 @@ __device__ uint64_t check_first_hit(Walk &W, CheckCtx &C, uint64_t lo, uint64_t 
         // hash [p, gap_end): nobody searched it
         if (gap_end - p > C.budget) return kNoCut;
         C.budget -= gap_end - p;
-        uint64_t A = ((W.off + p - 1) & ~63ull) - W.off;
+        uint64_t A = round_base(W.off, p);
         const uint64_t step = 64ull * W.S;
         const uint64_t R = (gap_end - A + step - 1) / step;
         if (Q && R >= 2 && R <= 16) {  // (ring capacity: 8 waves x 16)
@@ -889,7 +849,7 @@ __device__ __forceinline__ bool merged_at(const CheckCtx &C, uint64_t c, uint32_
         if (back == 1 && k == 0) break;
         const uint32_t uk = C.U.unit0 + k - back;
         if (uk < C.u) break;
-        const PieceView V = piece_view(C.units, C.pstatus, C.piece_cuts, uk, C.nunits);
+        const PieceView V = piece_view(C.units, C.pstatus, C.piece_cuts, uk);
         if (back == 0 && c == V.start) {
             *mu = uk;
             *idx = -1;
@@ -944,8 +904,6 @@ __global__ __launch_bounds__(kChkThreads, 1) void rcdc_walk_check_kernel(
     W.wave = 0;
     W.tid = lane;
     W.Q = nullptr;
-    W.wv = wave;
-    W.hrounds = W.hbytes = 0;
     const ModRepl mod{s_tab, W.k.lwm};
     const uint64_t mn = prm.min_size, mx = prm.max_size;
     for (;;) {
@@ -969,7 +927,6 @@ __global__ __launch_bounds__(kChkThreads, 1) void rcdc_walk_check_kernel(
         C.piece_cuts = piece_cuts;
         C.U = U;
         C.u = u;
-        C.nunits = prm.nunits;
         C.N = N;
         C.mn = mn;
         C.mx = mx;
@@ -986,7 +943,7 @@ __global__ __launch_bounds__(kChkThreads, 1) void rcdc_walk_check_kernel(
         uint64_t *hops = s_hops[wave];
         // exact state at the previous piece's end: closed at c, or open from c
         // ([c+min+64, a_j+min+64) hit-free, no zone cut in c's zone)
-        const PieceView Vp = piece_view(units, pstatus, piece_cuts, u - 1, prm.nunits);
+        const PieceView Vp = piece_view(units, pstatus, piece_cuts, u - 1);
         uint64_t c;
         bool pending = false;
         if (Vp.open) {
@@ -1172,8 +1129,6 @@ __global__ __launch_bounds__(1024, 1) void rcdc_walk_fixup_kernel(
     W.wave = wave;
     W.tid = threadIdx.x;
     W.Q = nullptr;
-    W.wv = wave;
-    W.hrounds = W.hbytes = 0;
     for (uint32_t idx = blockIdx.x; idx < nfix; idx += gridDim.x) {
         const uint32_t u = fixlist[idx];
         const WalkUnit U = units[u];
@@ -1212,7 +1167,7 @@ __global__ __launch_bounds__(1024, 1) void rcdc_walk_fixup_kernel(
                             const uint32_t uk = U.unit0 + (uint32_t)(k - back);
                             if (uk < u) break;  // never before the boundary's own piece
                             const WalkUnit Uk = units[uk];
-                            if (back == 0 && cut == pstatus[prm.nunits + uk]) {
+                            if (back == 0 && cut == Uk.start) {
                                 mu = uk;
                                 at = -1;
                             } else {
@@ -1478,51 +1433,6 @@ __global__ __launch_bounds__(256) void rcdc_walk_cost_kernel(
     }
 }
 
-// Run-on queue order.  Walkers that start far apart in cost (not bytes)
-// finish their stretches at about the same time, and a walker that runs out
-// of work should take a piece halfway into the largest stretch nobody has
-// reached.  Both come from one key per piece: with the cost of piece j
-// c_j = 1 + 4 x (its sampled non-zero words, 0..64) and its stream's running
-// cost [a, b) = [c_0 + .. + c_{j-1}, a + c_j), key = the highest k such that
-// [a, b) holds a multiple of 2^k (a = 0: 63).  Sorted by descending key,
-// the queue hands out every stream's first piece, then the pieces holding
-// multiples of the largest powers of two, so streams get early pieces in
-// proportion to their cost and each later piece halves a stretch.  One
-// workgroup per stream (the keys then go through rcdc_walk_sort_kernel).
-__global__ __launch_bounds__(256) void rcdc_walk_level_kernel(const WalkUnit *__restrict__ units,
-                                                              WalkParams prm, uint8_t *key) {
-    __shared__ uint64_t s_w[4];
-    const uint32_t u0 = prm.su0[blockIdx.x];
-    const uint32_t P = units[u0].npieces;
-    const uint32_t t = threadIdx.x, lane = t & 63u, wave = t >> 6;
-    uint64_t carry = 0;
-    for (uint32_t c0 = 0; c0 < P; c0 += 256) {
-        const uint32_t j = c0 + t;
-        uint64_t c = 0;
-        if (j < P) {
-            const uint32_t k = key[u0 + j];  // cost kernel: class (+65 for big pieces)
-            c = 1u + 4u * (k >= 65u ? k - 65u : k);
-        }
-        uint64_t v = c;  // inclusive scan: wave, then the 4 wave totals
-        for (uint32_t o = 1; o < 64; o <<= 1) {
-            const uint64_t x = __shfl_up(v, o, 64);
-            if (lane >= o) v += x;
-        }
-        if (lane == 63) s_w[wave] = v;
-        __syncthreads();
-        uint64_t before = carry;
-        for (uint32_t w = 0; w < wave; w++) before += s_w[w];
-        const uint64_t total = s_w[0] + s_w[1] + s_w[2] + s_w[3];
-        __syncthreads();
-        if (j < P) {
-            const uint64_t b = before + v, a = b - c;
-            const uint32_t lvl = a == 0 ? 63u : 63u - (uint32_t)__builtin_clzll((a - 1) ^ (b - 1));
-            key[u0 + j] = (uint8_t)lvl;
-        }
-        carry += total;
-    }
-}
-
 // One workgroup: counting sort of the queue by key, descending.
 __global__ __launch_bounds__(1024) void rcdc_walk_sort_kernel(WalkParams prm,
                                                               const uint8_t *__restrict__ key) {
@@ -1561,9 +1471,6 @@ hipError_t launch_walk(const uint8_t *arena, const StreamDesc *sds, const WalkUn
         const uint32_t cb = std::min<uint32_t>((prm.nunits + 3) / 4, 4096);
         hipLaunchKernelGGL(rcdc_walk_cost_kernel, dim3(cb), dim3(256), 0, stream, arena, sds, units,
                            prm, key);
-        if (prm.runon && prm.su0)  // keys by unit (order_in is the unit order)
-            hipLaunchKernelGGL(rcdc_walk_level_kernel, dim3(prm.nwstreams), dim3(256), 0, stream,
-                               units, prm, key);
         hipLaunchKernelGGL(rcdc_walk_sort_kernel, dim3(1), dim3(1024), 0, stream, prm,
                            (const uint8_t *)key);
     }

@@ -17,13 +17,11 @@ KiB = 1 << 10
 MiB = 1 << 20
 
 
-@pytest.fixture(params=["runon0", "runon1"])
+@pytest.fixture(params=["help1", "help0"])
 def walk_env(request, monkeypatch, gpu_ctx):
-    """Walk-path overrides; every walk test runs with pieces taken only from
-    the queue (runon0) and with walkers running on into the next piece while
-    nobody has it (runon1: a piece's chain may start at the previous piece's
-    last cut)."""
-    monkeypatch.setenv("RCDC_WALK_RUNON", request.param[-1])
+    """Walk-path overrides; every walk test runs with the tail helpers (idle
+    waves hash rounds posted by busy walkers, the default) and without."""
+    monkeypatch.setenv("RCDC_WALK_HELP", request.param[-1])
 
     def set_(piece, min_pieces=1, fixcap=None):
         monkeypatch.setenv("RCDC_WALK_PIECE", str(piece))
