@@ -716,9 +716,13 @@ def main():
         # assemble, resolve) overlap run k + 1's hashing kernels
         plan.set_pipeline(True)
         pipelined = True
-    stream = torch.cuda.current_stream(dev)
+    # a stream of the job's own: given the legacy default stream (handle 0)
+    # every rcdc call is ordered with it through two events (rcdc.h), ~20 us
+    # of cross-queue latency per C2 step
+    stream = torch.cuda.Stream(dev)
     sptr = stream.cuda_stream
     ptr = arena.data_ptr()
+    torch.cuda.synchronize(dev)  # the workload was built on the default stream
 
     step = lambda: plan.run(ptr, sptr)  # noqa: E731
     if args.workload == "C5":

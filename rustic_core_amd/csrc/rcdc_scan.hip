@@ -117,6 +117,7 @@ hipError_t launch_scan(int code, const uint8_t *arena, const ScanItem *items, ui
     switch (code) {
         case 30: return launch4<3, false, 1024, 16>(arena, items, nitems, gtab, prm, sums, item_masks, blocks, stream);
         case 3116: return launch4<3, false, 1024, 116>(arena, items, nitems, gtab, prm, sums, item_masks, blocks, stream);
+        case 4116: return launch4<4, true, 1024, 116>(arena, items, nitems, gtab, prm, sums, item_masks, blocks, stream);
         case 930: return launch4<3, false, 1024, 16, false>(arena, items, nitems, gtab, prm, sums, item_masks, blocks, stream);
         case 50: return launch4<5, false, 1024, 16>(arena, items, nitems, gtab, prm, sums, item_masks, blocks, stream);
         case 150: return launch4<5, false, 1024, 8>(arena, items, nitems, gtab, prm, sums, item_masks, blocks, stream);

@@ -47,11 +47,15 @@ using namespace rcdc;
 
 namespace {
 
-#ifndef RCDC_WPAIR
-#define RCDC_WPAIR 0
-#endif
-constexpr int kWR = RCDC_WPAIR ? 4 : 3, kWG = RCDC_WPAIR ? 116 : 16;  // ring of register units, groups of 16
-constexpr bool kWPair = RCDC_WPAIR != 0;  // refill a 128-B line (two units) per lane
+// Round loop shape: a ring of 4 register units refilled a 128-byte line (two
+// units) per lane at a time, and groups of 16 positions that keep no
+// fingerprints (a flagged lane re-rolls its group, P ~ 2^-12): refilled one
+// 64-byte unit at a time the line's second half was often evicted from L2
+// before its load (PMC: 1.37 x the lane bytes fetched, now 1.02 x; walk
+// 9.83 -> 9.55 ms on C3).  Keeping the 16 fingerprints would not fit the
+// 4-unit ring in 128 VGPRs.
+constexpr int kWR = 4, kWG = 116;
+constexpr bool kWPair = true;
 constexpr uint64_t kNoCut = ~0ull;
 constexpr uint64_t kOpen = ~0ull - 1;
 constexpr uint32_t kNoUnit = 0xFFFFFFFFu;
