@@ -716,10 +716,13 @@ def main():
         # assemble, resolve) overlap run k + 1's hashing kernels
         plan.set_pipeline(True)
         pipelined = True
-    # a stream of the job's own: given the legacy default stream (handle 0)
-    # every rcdc call is ordered with it through two events (rcdc.h), ~20 us
-    # of cross-queue latency per C2 step
-    stream = torch.cuda.Stream(dev)
+    # Unpipelined plans (C2, C5) run on a stream of the job's own: given the
+    # legacy default stream (handle 0) every rcdc call is ordered with it
+    # through two events (rcdc.h), ~20 us of cross-queue latency per C2 step.
+    # A pipelined plan already spreads a run over its own streams; a fifth
+    # stream would share one of HIP's 4 hardware queues with them and
+    # serialise run k's chain with run k + 1's walk (C3: 9.6 -> 14 ms).
+    stream = torch.cuda.current_stream(dev) if pipelined else torch.cuda.Stream(dev)
     sptr = stream.cuda_stream
     ptr = arena.data_ptr()
     torch.cuda.synchronize(dev)  # the workload was built on the default stream
