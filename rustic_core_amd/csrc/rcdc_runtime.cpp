@@ -41,7 +41,10 @@ hipError_t launch_resolve(const uint8_t *arena, const StreamDesc *sds, const Res
                           hipStream_t stream);
 hipError_t launch_walk(const uint8_t *arena, const StreamDesc *sds, const WalkUnit *units,
                        const WalkParams &prm, const uint64_t *gtab, uint64_t *piece_cuts,
-                       uint64_t *pstatus, uint32_t *ctr, uint32_t blocks, hipStream_t stream);
+                       uint64_t *pstatus, uint32_t *ctr, uint32_t blocks, hipStream_t stream,
+                       bool ordered);
+hipError_t launch_walk_order(const uint8_t *arena, const StreamDesc *sds, const WalkUnit *units,
+                             const WalkParams &prm, hipStream_t stream);
 hipError_t launch_walk_chain(const uint8_t *arena, const StreamDesc *sds, const WalkUnit *units,
                              const uint32_t *stream_unit0, uint32_t nstreams,
                              const WalkParams &prm, const uint64_t *gtab,
@@ -801,12 +804,20 @@ rcdc_status plan_run(rcdc_plan *pl, const void *d_arena, hipStream_t stream) {
         }
         (void)nw;
     }
+    bool ordered = false;  // the walk queue's order already enqueued
     if (pl->pipelined) {
         // hashing on this set's stream, after the caller's earlier work and
         // after the chain that last read this set (run k - 2)
         HIP_TRY(hipEventRecord(pl->ev_in[set], stream));
         stream = pl->hstream[set];
         HIP_TRY(hipStreamWaitEvent(stream, pl->ev_in[set], 0));
+        // the walk queue's cost order reads only the arena: it need not wait
+        // for the chain of run k - 2, and fills CUs the last walk frees
+        if (!pl->wunits.empty()) {
+            HIP_TRY(launch_walk_order((const uint8_t *)d_arena, pl->d_sds, pl->d_wunits, wprm,
+                                      stream));
+            ordered = true;
+        }
         if (pl->res_pending[set]) HIP_TRY(hipStreamWaitEvent(stream, pl->ev_res[set], 0));
     }
     if (ev) HIP_TRY(hipEventRecord(ev[0], stream));
@@ -821,7 +832,8 @@ rcdc_status plan_run(rcdc_plan *pl, const void *d_arena, hipStream_t stream) {
     }
     HIP_TRY(launch_walk((const uint8_t *)d_arena, pl->d_sds, pl->d_wunits, wprm, ctx->d_tables,
                         wpiece, pstatus, ctr,
-                        (uint32_t)std::min<uint64_t>(cus, (pl->wunits.size() + 15) / 16), stream));
+                        (uint32_t)std::min<uint64_t>(cus, (pl->wunits.size() + 15) / 16), stream,
+                        ordered));
     if (dbg) {
         HIP_TRY(hipStreamSynchronize(stream));
         uint32_t h[4] = {0, 0, 0, 0};

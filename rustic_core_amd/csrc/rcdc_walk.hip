@@ -282,7 +282,6 @@ __device__ uint64_t round_first(const Walk &W, uint64_t A, uint64_t q, uint64_t 
 // posted job is run; idle waves leave when no wave is active and the ring is
 // empty.
 constexpr uint32_t kGapSlots = 256;  // >= 16 walkers x 15 posted rounds (check: 8 x 16)
-constexpr uint32_t kChkWaves = 8;
 constexpr uint32_t kGapReq = 16;     // requesting waves (walk: 16, check: 8)
 struct GapQueue {
     uint32_t head, tail, active, idle;  // idle: walk waves that found no piece left
@@ -870,7 +869,10 @@ __device__ __forceinline__ bool merged_at(const CheckCtx &C, uint64_t c, uint32_
     return false;
 }
 
-constexpr int kChkThreads = 512;  // 8 waves: 256 VGPRs per lane, the gap search spill-free
+#ifndef RCDC_CHK_THREADS
+#define RCDC_CHK_THREADS 512
+#endif
+constexpr int kChkThreads = RCDC_CHK_THREADS;  // 8 waves: 256 VGPRs per lane, the gap search spill-free
 
 template <int TSH, bool SMALL>
 __global__ __launch_bounds__(kChkThreads, 1) void rcdc_walk_check_kernel(
@@ -1460,23 +1462,36 @@ __global__ __launch_bounds__(1024) void rcdc_walk_sort_kernel(WalkParams prm,
 
 namespace rcdc {
 
-// The hashing part: counters reset, the queue's cost order, the walk kernel.
+// The queue's cost order of a run (reads only the arena and the units;
+// writes order_out, which no chain kernel reads): a pipelined run enqueues it
+// before waiting for the chain that last used its buffer set.
+hipError_t launch_walk_order(const uint8_t *arena, const StreamDesc *sds, const WalkUnit *units,
+                             const WalkParams &prm, hipStream_t stream) {
+    if (prm.nunits == 0 || !prm.order_in || !prm.order_out) return hipSuccess;
+    // the key bytes follow order_out in the same buffer (plan_build)
+    uint8_t *key = reinterpret_cast<uint8_t *>(prm.order_out + prm.nunits);
+    const uint32_t cb = std::min<uint32_t>((prm.nunits + 3) / 4, 4096);
+    hipLaunchKernelGGL(rcdc_walk_cost_kernel, dim3(cb), dim3(256), 0, stream, arena, sds, units,
+                       prm, key);
+    hipLaunchKernelGGL(rcdc_walk_sort_kernel, dim3(1), dim3(1024), 0, stream, prm,
+                       (const uint8_t *)key);
+    return hipGetLastError();
+}
+
+// The hashing part: counters reset, the queue's cost order (unless already
+// enqueued: `ordered`), the walk kernel.
 hipError_t launch_walk(const uint8_t *arena, const StreamDesc *sds, const WalkUnit *units,
                        const WalkParams &prm, const uint64_t *gtab, uint64_t *piece_cuts,
-                       uint64_t *pstatus, uint32_t *ctr, uint32_t blocks, hipStream_t stream) {
+                       uint64_t *pstatus, uint32_t *ctr, uint32_t blocks, hipStream_t stream,
+                       bool ordered) {
     if (prm.nunits == 0) return hipSuccess;
     hipError_t e = hipMemsetAsync(ctr, 0, 4 * sizeof(uint32_t), stream);
     if (e == hipSuccess)
         e = hipMemsetAsync(prm.stats, 0, kWalkStats * sizeof(unsigned long long), stream);
     if (e != hipSuccess) return e;
-    if (prm.order_in && prm.order_out) {
-        // the key bytes follow order_out in the same buffer (plan_build)
-        uint8_t *key = reinterpret_cast<uint8_t *>(prm.order_out + prm.nunits);
-        const uint32_t cb = std::min<uint32_t>((prm.nunits + 3) / 4, 4096);
-        hipLaunchKernelGGL(rcdc_walk_cost_kernel, dim3(cb), dim3(256), 0, stream, arena, sds, units,
-                           prm, key);
-        hipLaunchKernelGGL(rcdc_walk_sort_kernel, dim3(1), dim3(1024), 0, stream, prm,
-                           (const uint8_t *)key);
+    if (!ordered) {
+        e = launch_walk_order(arena, sds, units, prm, stream);
+        if (e != hipSuccess) return e;
     }
     const bool small = prm.mask < 0xFFFFu;
 #define RCDC_WALK_LAUNCH(TSH, SM)                                                                  \
