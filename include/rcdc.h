@@ -173,13 +173,20 @@ rcdc_status rcdc_plan_device_results(rcdc_plan *plan, uint64_t *d_cuts,
                                      uint64_t *d_counts,
                                      const uint64_t **cut_base);
 
-/* Pipelined runs: with enable = 1, run k's resolve goes to a stream of the
- * plan's own (after run k's scan) and run k + 1's scan, on the caller's
- * stream, overlaps it; the per-segment summaries alternate between two
- * buffer sets.  rcdc_plan_results / rcdc_plan_hash wait for the resolve;
- * a caller that reuses the arena must synchronise the device (or call
- * rcdc_plan_results) first.  RCDC_ERR_UNSUPPORTED for plans with walked
- * (long) streams.  enable = 0 restores serial runs.                       */
+/* Pipelined runs: with enable = 1, run k's hashing kernels (scan, walk) go
+ * to hashing stream k % 2 of the plan's own (after the caller's earlier
+ * work) and its chain kernels (resolve; walk check / fixup / assemble) to a
+ * third stream, so run k's chain overlaps run k + 1's hashing; every
+ * per-run buffer the chain reads alternates between two sets, and run
+ * k + 2's hashing waits for run k's chain.  rcdc_plan_results /
+ * rcdc_plan_hash wait for the last chain; a caller that reuses the arena
+ * must synchronise the device (or call rcdc_plan_results) first.  The plan
+ * then uses three streams: HIP maps a process's streams onto
+ * GPU_MAX_HW_QUEUES hardware queues (4 by default), and kernels whose
+ * streams share a queue run in order, so a caller that adds streams of its
+ * own around a pipelined plan can serialise its chain with the next walk
+ * (bench.py runs pipelined plans on the default stream).  enable = 0
+ * restores serial runs.                                                    */
 rcdc_status rcdc_plan_set_pipeline(rcdc_plan *plan, int enable);
 
 /* Scan-kernel geometry chosen by the plan (for profiling / roofline). */
