@@ -282,7 +282,7 @@ __device__ uint64_t round_first(const Walk &W, uint64_t A, uint64_t q, uint64_t 
 // posted job is run; idle waves leave when no wave is active and the ring is
 // empty.
 constexpr uint32_t kGapSlots = 256;  // >= 16 walkers x 15 posted rounds (check: 8 x 16)
-constexpr uint32_t kGapReq = 16;     // requesting waves (walk: 16, check: 8)
+constexpr uint32_t kGapReq = 16;     // requesting waves (a workgroup of 1024)
 struct GapQueue {
     uint32_t head, tail, active, idle;  // idle: walk waves that found no piece left
     uint32_t ready[kGapSlots];
@@ -797,7 +797,7 @@ __device__ uint64_t check_first_hit(Walk &W, CheckCtx &C, uint64_t lo, uint64_t 
         uint64_t A = round_base(W.off, p);
         const uint64_t step = 64ull * W.S;
         const uint64_t R = (gap_end - A + step - 1) / step;
-        if (Q && R >= 2 && R <= 16) {  // (ring capacity: 8 waves x 16)
+        if (Q && R >= 2 && R <= 16) {  // (ring capacity: 16 waves x 16)
             // post the R rounds, then run jobs until ours are done
             uint32_t t = 0;
             if (W.lane == 0) {
@@ -869,10 +869,15 @@ __device__ __forceinline__ bool merged_at(const CheckCtx &C, uint64_t c, uint32_
     return false;
 }
 
+// 16 waves per workgroup: the check is latency bound and, pipelined, holds
+// a CU per workgroup beside the next walk, so more boundaries in flight per
+// CU free the CUs sooner (C3 step 9.33 -> 9.26 ms in an interleaved A/B),
+// although at 128 VGPRs the gap search spills (~280 B per lane); 512
+// threads (8 waves, 256 VGPRs) is spill-free.
 #ifndef RCDC_CHK_THREADS
-#define RCDC_CHK_THREADS 512
+#define RCDC_CHK_THREADS 1024
 #endif
-constexpr int kChkThreads = RCDC_CHK_THREADS;  // 8 waves: 256 VGPRs per lane, the gap search spill-free
+constexpr int kChkThreads = RCDC_CHK_THREADS;
 
 template <int TSH, bool SMALL>
 __global__ __launch_bounds__(kChkThreads, 1) void rcdc_walk_check_kernel(
