@@ -51,7 +51,8 @@ hipError_t launch_walk_chain(const uint8_t *arena, const StreamDesc *sds, const 
                              const uint64_t *piece_cuts, const uint64_t *pstatus, BoundRes *bres,
                              uint32_t *ctr, uint32_t *fixlist, uint64_t *fix_cuts,
                              FixRes *fixres, uint64_t *cuts, uint64_t *counts,
-                             uint32_t fix_blocks, uint32_t chk_cap, hipStream_t stream);
+                             uint32_t fix_blocks, uint32_t chk_cap, hipStream_t stream,
+                             bool wide);
 hipError_t launch_sha256_list(const uint8_t *arena, const ulonglong2 *refs, uint32_t n,
                               uint32_t *digests, hipStream_t stream);
 hipError_t launch_sha256_plan(const uint8_t *arena, const StreamDesc *sds, uint32_t nstreams,
@@ -867,7 +868,8 @@ rcdc_status plan_run(rcdc_plan *pl, const void *d_arena, hipStream_t stream) {
                               wpiece, pstatus, bres, ctr, fixlist,
                               fixcuts, fixres, pl->d_cuts, pl->d_counts,
                               pl->pipelined ? std::min<uint32_t>(cus, 32) : cus,
-                              pl->pipelined ? pl->chk_blocks_pipe : cus, stream));
+                              pl->pipelined ? pl->chk_blocks_pipe : cus, stream,
+                              pl->pipelined));
     if (ev) HIP_TRY(hipEventRecord(ev[2], stream));
     pl->last_set = set;
     if (pl->pipelined) {

@@ -869,34 +869,32 @@ __device__ __forceinline__ bool merged_at(const CheckCtx &C, uint64_t c, uint32_
     return false;
 }
 
-// 16 waves per workgroup: the check is latency bound and, pipelined, holds
-// a CU per workgroup beside the next walk, so more boundaries in flight per
-// CU free the CUs sooner (C3 step 9.33 -> 9.26 ms in an interleaved A/B),
-// although at 128 VGPRs the gap search spills (~280 B per lane); 512
-// threads (8 waves, 256 VGPRs) is spill-free.
-#ifndef RCDC_CHK_THREADS
-#define RCDC_CHK_THREADS 1024
-#endif
-constexpr int kChkThreads = RCDC_CHK_THREADS;
+// Workgroup size CT: 512 threads (8 waves, 256 VGPRs, spill-free) for
+// serial runs; 1024 (16 waves) beside the next walk of a pipelined plan:
+// the check is latency bound and there each workgroup holds a CU the walk
+// waits for, so more boundaries in flight per CU free it sooner (C3 step
+// 9.33 -> 9.26 ms in an interleaved A/B) although at 128 VGPRs the gap
+// search spills (~280 B per lane).  Serial C5 was slower with 1024
+// (chain 126 -> 154 us).
 
-template <int TSH, bool SMALL>
-__global__ __launch_bounds__(kChkThreads, 1) void rcdc_walk_check_kernel(
+template <int TSH, bool SMALL, int CT>
+__global__ __launch_bounds__(CT, 1) void rcdc_walk_check_kernel(
     const uint8_t *__restrict__ arena, const StreamDesc *__restrict__ sds,
     const WalkUnit *__restrict__ units, WalkParams prm, const uint64_t *__restrict__ gtab,
     const uint64_t *__restrict__ piece_cuts, const uint64_t *__restrict__ pstatus,
     BoundRes *__restrict__ bres, uint32_t *ctr, uint32_t *__restrict__ fixlist) {
     __shared__ __attribute__((aligned(16))) uint8_t s_tab[kLdsBytes];
-    __shared__ __attribute__((aligned(16))) uint8_t s_win[kChkThreads / 64][128];
-    __shared__ uint64_t s_hops[kChkThreads / 64][kMaxHops];  // the wave's hop entries
+    __shared__ __attribute__((aligned(16))) uint8_t s_win[CT / 64][128];
+    __shared__ uint64_t s_hops[CT / 64][kMaxHops];  // the wave's hop entries
     __shared__ BlockStats s_st;
     __shared__ GapQueue s_q;
     stats_init(s_st);
     if (threadIdx.x == 0) {
         s_q.head = s_q.tail = 0;
-        s_q.active = kChkThreads / 64;
+        s_q.active = CT / 64;
     }
     for (uint32_t i = threadIdx.x; i < kGapSlots; i += blockDim.x) s_q.ready[i] = 0;
-    fill_tables(s_tab, gtab, prm.idx_shift, threadIdx.x, kChkThreads);  // (ends with a barrier)
+    fill_tables(s_tab, gtab, prm.idx_shift, threadIdx.x, CT);  // (ends with a barrier)
     uint64_t shared_rounds = 0, shared_lbytes = 0;
     const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
     Walk W;
@@ -1516,19 +1514,22 @@ hipError_t launch_walk_chain(const uint8_t *arena, const StreamDesc *sds, const 
                              const uint64_t *piece_cuts, const uint64_t *pstatus, BoundRes *bres,
                              uint32_t *ctr, uint32_t *fixlist, uint64_t *fix_cuts,
                              FixRes *fixres, uint64_t *cuts, uint64_t *counts,
-                             uint32_t fix_blocks, uint32_t chk_cap, hipStream_t stream) {
+                             uint32_t fix_blocks, uint32_t chk_cap, hipStream_t stream,
+                             bool wide) {
     if (prm.nunits == 0) return hipSuccess;
     static const bool dbg = getenv("RCDC_DEBUG_SYNC") != nullptr;
     const bool small = prm.mask < 0xFFFFu;
     const uint32_t chk_blocks =
         std::max<uint32_t>(std::min<uint32_t>(std::min(fix_blocks, chk_cap), (prm.nunits + 7) / 8), 1);
-#define RCDC_CHK_LAUNCH(TSH, SM)                                                                   \
-    hipLaunchKernelGGL((rcdc_walk_check_kernel<TSH, SM>), dim3(chk_blocks), dim3(kChkThreads), 0,  \
+#define RCDC_CHK_LAUNCH(TSH, SM, CT)                                                               \
+    hipLaunchKernelGGL((rcdc_walk_check_kernel<TSH, SM, CT>), dim3(chk_blocks), dim3(CT), 0,      \
                        stream,                                                                     \
                        arena, sds, units, prm, gtab, piece_cuts, pstatus, bres, ctr, fixlist)
-    if (prm.idx_shift == 21 && !small) RCDC_CHK_LAUNCH(105, false);
-    else if (small) RCDC_CHK_LAUNCH(-1, true);
-    else RCDC_CHK_LAUNCH(-1, false);
+    // (the wide form only for the default degree: pipelined C3 / C4 plans)
+    if (prm.idx_shift == 21 && !small && wide) RCDC_CHK_LAUNCH(105, false, 1024);
+    else if (prm.idx_shift == 21 && !small) RCDC_CHK_LAUNCH(105, false, 512);
+    else if (small) RCDC_CHK_LAUNCH(-1, true, 512);
+    else RCDC_CHK_LAUNCH(-1, false, 512);
 #undef RCDC_CHK_LAUNCH
     if (dbg) {
         (void)hipStreamSynchronize(stream);
