@@ -276,12 +276,12 @@ __device__ uint64_t round_first(const Walk &W, uint64_t A, uint64_t q, uint64_t 
 // hash unsearched gaps (up to min + 64 bytes: 8 sequential 64-lane rounds).
 // A wave with a gap of >= 2 rounds posts them as jobs in an LDS ring; every
 // wave of the workgroup that waits -- for its own jobs, or because no
-// boundaries are left -- pops and runs jobs, so in the tail up to 8 waves
+// boundaries are left -- pops and runs jobs, so in the tail up to 16 waves
 // hash one gap.  No barriers: LDS atomics, per-slot ready flags, s_sleep.
 // Termination: a waiting wave runs jobs itself (its own included), so every
 // posted job is run; idle waves leave when no wave is active and the ring is
-// empty.
-constexpr uint32_t kGapSlots = 256;  // >= 16 walkers x 15 posted rounds (check: 8 x 16)
+// empty.  The walk kernel reuses the ring for its tail (walk_post below).
+constexpr uint32_t kGapSlots = 256;  // >= 16 check waves x 16 rounds (walk: 16 x kHelpMax)
 constexpr uint32_t kGapReq = 16;     // requesting waves (a workgroup of 1024)
 struct GapQueue {
     uint32_t head, tail, active, idle;  // idle: walk waves that found no piece left
