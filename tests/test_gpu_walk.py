@@ -284,3 +284,15 @@ def test_walk_pipelined_runs(walk_env, params, piece):
     plan.run(devs[0].data_ptr())
     assert all(np.array_equal(g, e) for g, e in zip(plan.results(), exp[0]))
     plan.close()
+
+
+def test_walk_helpers_many_rounds(walk_env, monkeypatch):
+    """Short rounds (RCDC_WALK_SEG=128: 8 KiB per 64-lane round, ~60 rounds
+    per chunk search) on few pieces: most waves of a workgroup idle from the
+    start, so busy walkers post kHelpMax rounds at a time to the workgroup's
+    ring and hits land in posted rounds as well as in the walker's own (help1);
+    help0 is the same walk without the ring."""
+    walk_env(4 * MiB)
+    monkeypatch.setenv("RCDC_WALK_SEG", "128")
+    _run(DEFAULT, [_rand(300, 40 * MiB + 777), _mixed(301, 40 * MiB, 64 * KiB, 4 * MiB,
+                                                      4 * KiB, 2 * MiB)])
