@@ -170,8 +170,8 @@ __device__ __forceinline__ void rescan_group(Chain &c, uint32_t h0, uint32_t h1,
 
 template <int TSH, bool SMALL, int G>
 __device__ __forceinline__ void scan_unit(Chain &c, const Unit &un, const Unit &uo,
-                                          const uint8_t *tab, const Consts &k, uint64_t valid,
-                                          uint32_t lane, uint32_t rb) {
+                                          const uint8_t *tab, const Consts &k, bool lv,
+                                          uint32_t rb) {
     if constexpr (G >= 100) {
         constexpr int GG = G - 100;
 #pragma unroll
@@ -185,11 +185,9 @@ __device__ __forceinline__ void scan_unit(Chain &c, const Unit &un, const Unit &
                 const uint16_t t = SMALL ? (uint16_t)(c.h0 & k.mask) : (uint16_t)c.h0;
                 acc = __builtin_elementwise_min(acc, t);
             }
-            const uint64_t flagged = __builtin_amdgcn_ballot_w64(acc == 0) & valid;
-            if (flagged) {
-                if ((flagged >> lane) & 1u)
-                    rescan_group<TSH, GG>(c, h0s, h1s, un, uo, tab, k, rb + g * GG, g);
-            }
+            // a divergent branch on the lane mask (exec-skip when no lane is
+            // flagged): the compare is the only VALU of the test
+            if (acc == 0 && lv) rescan_group<TSH, GG>(c, h0s, h1s, un, uo, tab, k, rb + g * GG, g);
         }
     } else {
 #pragma unroll
@@ -206,10 +204,7 @@ __device__ __forceinline__ void scan_unit(Chain &c, const Unit &un, const Unit &
         }
         // one ballot per group; the prefilter is necessary, not sufficient:
         // flagged lanes run the exact test
-        const uint64_t flagged = __builtin_amdgcn_ballot_w64(acc == 0) & valid;
-        if (flagged) {
-            if ((flagged >> lane) & 1u) record_group<G>(c, hk, k.mask, rb + g * G);
-        }
+        if (acc == 0 && lv) record_group<G>(c, hk, k.mask, rb + g * G);
     }
     }
 }
@@ -241,9 +236,8 @@ __device__ __forceinline__ void load_unit(Unit &u, __amdgpu_buffer_rsrc_t rsrc, 
 template <int R, bool PAIR, int TSH, bool SMALL, int G, int B>
 __device__ __forceinline__ bool ring_step(Chain &c, Unit (&u)[R], uint32_t &i, uint32_t nunits,
                                           __amdgpu_buffer_rsrc_t rsrc, uint32_t voff,
-                                          const uint8_t *tab, const Consts &k, uint64_t valid,
-                                          uint32_t lane) {
-    scan_unit<TSH, SMALL, G>(c, u[B], u[(B + R - 1) % R], tab, k, valid, lane, (i - 1) * 64u);
+                                          const uint8_t *tab, const Consts &k, bool lv) {
+    scan_unit<TSH, SMALL, G>(c, u[B], u[(B + R - 1) % R], tab, k, lv, (i - 1) * 64u);
     if constexpr (PAIR) {
         if ((B & 1) == 0) {  // i even (R even, so B = i % R has i's parity)
             const uint32_t nxt = i - 2 + R;  // units nxt, nxt + 1 -> buffers B-2, B-1
@@ -262,12 +256,11 @@ __device__ __forceinline__ bool ring_step(Chain &c, Unit (&u)[R], uint32_t &i, u
 template <int R, bool PAIR, int TSH, bool SMALL, int G, int B = 1>
 __device__ __forceinline__ bool ring_pass(Chain &c, Unit (&u)[R], uint32_t &i, uint32_t nunits,
                                           __amdgpu_buffer_rsrc_t rsrc, uint32_t voff,
-                                          const uint8_t *tab, const Consts &k, uint64_t valid,
-                                          uint32_t lane) {
-    if (!ring_step<R, PAIR, TSH, SMALL, G, B % R>(c, u, i, nunits, rsrc, voff, tab, k, valid, lane))
+                                          const uint8_t *tab, const Consts &k, bool lv) {
+    if (!ring_step<R, PAIR, TSH, SMALL, G, B % R>(c, u, i, nunits, rsrc, voff, tab, k, lv))
         return false;
     if constexpr (B < R) return ring_pass<R, PAIR, TSH, SMALL, G, B + 1>(c, u, i, nunits, rsrc,
-                                                                        voff, tab, k, valid, lane);
+                                                                        voff, tab, k, lv);
     else return true;
 }
 
@@ -290,8 +283,9 @@ __device__ __forceinline__ Chain scan_segment(__amdgpu_buffer_rsrc_t rsrc, uint3
     for (int j = 0; j < R; j++)
         if ((uint32_t)j <= nunits) load_unit(u[j], rsrc, voff + j * 64u);
     warm_unit<TSH>(c, u[0], tab, k);
+    const bool lv = (valid >> lane) & 1u;
     uint32_t i = 1;
-    while (ring_pass<R, PAIR, TSH, SMALL, G>(c, u, i, nunits, rsrc, voff, tab, k, valid, lane)) {
+    while (ring_pass<R, PAIR, TSH, SMALL, G>(c, u, i, nunits, rsrc, voff, tab, k, lv)) {
     }
     return c;
 }
