@@ -1,5 +1,5 @@
 set -o pipefail
-OUT=gpurun_out/r3fin
+OUT=gpurun_out/${1:-r3fin}
 mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
 python -c "import torch" || exit 1
