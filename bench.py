@@ -428,12 +428,27 @@ def run_c4(args, torch, dist, dev, rank, world, local):
     sptr = torch.cuda.current_stream(dev).cuda_stream
     scan_ms = resolve_ms = 0.0
     runs = 0
+    # One resident batch per rank (the 8-GPU share, ~60 GiB, fits one): the K
+    # passes run back to back like C3's steps, pipelined (rcdc_plan_set_pipeline:
+    # pass k's chain kernels and the tail of its walk overlap pass k + 1's walk)
+    # unless --no-pipeline.  Several batches: each is refilled (untimed) and
+    # timed on its own.
+    single = len(layouts) == 1
+    pipelined = (single and not args.no_pipeline
+                 and layouts[0][2].info().get("walk_pieces", 0) > 0)
     # warmup on the first batch
     if layouts:
         b, offs, plan = layouts[0]
         c4_fill(torch, arena, offs, b, sizes, dev)
-        for _ in range(args.warmup):
+        if pipelined:
+            plan.set_pipeline(True)
+        t_w = time.perf_counter()
+        nw = 0
+        while nw < args.warmup or (single and time.perf_counter() - t_w < args.prewarm):
             plan.run(arena.data_ptr(), sptr)
+            nw += 1
+            if nw % 8 == 0:
+                torch.cuda.synchronize(dev)
     torch.cuda.synchronize(dev)
     el = 0.0
     sample_cuts = {}
@@ -441,7 +456,35 @@ def run_c4(args, torch, dist, dev, rank, world, local):
     rng = np.random.default_rng(4001)
     sample = set(int(x) for x in rng.choice(args.c4_files, size=min(64, args.c4_files),
                                              replace=False))
-    for step in range(args.steps):
+    if single and layouts:
+        b, offs, plan = layouts[0]
+        plan.set_timing(True, every=args.time_every)
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            plan.run(arena.data_ptr(), sptr)
+        torch.cuda.synchronize(dev)
+        el = time.perf_counter() - t0
+        if world > 1:
+            dist.barrier()
+        plan.set_timing(False)
+        runs, scan_ms, resolve_ms = plan.kernel_times()
+        got = plan.results()
+        ref_hashed = ref_slide_bytes(got, MIN)
+        inf = plan.info()
+        if inf["walk_pieces"]:
+            wst = plan.walk_stats()
+            lane_hashed = wst["round_bytes"] + wst["zones"] * 4096
+            walked_batches = 1
+        else:
+            lane_hashed = inf["scanned_bytes"] + 64 * inf["segments"]
+        for i, f in enumerate(b):
+            if f in sample and not args.no_parity:
+                o = int(offs[i])
+                sample_cuts[f] = (got[i], arena[o:o + sizes[f]].cpu().numpy())
+    for step in range(args.steps if not single else 0):
         for b, offs, plan in layouts:
             if len(layouts) > 1 or step == 0:
                 c4_fill(torch, arena, offs, b, sizes, dev)  # outside the timed span
@@ -486,7 +529,8 @@ def run_c4(args, torch, dist, dev, rank, world, local):
     el_max = float(t.item())
     total = sum(sizes) * args.steps
     share = sum(sizes[f] for f in mine)
-    hash_s = max(scan_ms / 1e3 / max(args.steps, 1), 1e-9)  # hashing kernels per pass
+    passes = max(runs if single else args.steps, 1)  # timed passes behind scan_ms
+    hash_s = max(scan_ms / 1e3 / passes, 1e-9)  # hashing kernels per pass
     bad = 0
     for f, (cuts, host) in sample_cuts.items():
         from oracle import oracle
@@ -494,6 +538,9 @@ def run_c4(args, torch, dist, dev, rank, world, local):
     checked = torch.tensor([len(sample_cuts), bad], dtype=torch.int64, device=coll_device(dev))
     if world > 1:
         dist.all_reduce(checked)
+    c4_traffic = None
+    if walked_batches == len(layouts) and args.c4_files == 1024 and world == 1:
+        c4_traffic, pmc = pmc_traffic("C4", "rcdc_walk_kernel")
     if rank == 0:
         line = {
             "metric": METRIC, "value": round(total / el_max / GiB, 2), "unit": "GiB/s",
@@ -515,13 +562,16 @@ def run_c4(args, torch, dist, dev, rank, world, local):
                          "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(share / hash_s / 1e9 / HBM_PEAK_GBS, 4) if runs else None,
                          "basis": "input bytes of the rank's files per pass / hashing-kernel time",
-                         "traffic": None,
+                         "traffic": c4_traffic,
+                         "frac_fetch": (round(c4_traffic / hash_s / 1e9 / HBM_PEAK_GBS, 4)
+                                        if c4_traffic else None),
                          "ref_hashed_bytes_per_pass": ref_hashed,
                          "frac_ref_hashed": round(ref_hashed / hash_s / 1e9 / HBM_PEAK_GBS, 4),
                          "lane_hashed_bytes_per_pass": lane_hashed,
                          "frac_lane_hashed": round(lane_hashed / hash_s / 1e9 / HBM_PEAK_GBS, 4),
-                         "hash_ms_per_pass": round(scan_ms / max(args.steps, 1), 3),
-                         "chain_ms_per_pass": round(resolve_ms / max(args.steps, 1), 3)},
+                         "hash_ms_per_pass": round(scan_ms / passes, 3),
+                         "chain_ms_per_pass": round(resolve_ms / passes, 3),
+                         "timed_passes": passes, "pipelined": pipelined},
             "parity": {"files_checked": int(checked[0]), "mismatches": int(checked[1]),
                        "checker": "oracle/cdc_ref on a seeded sample of 64 files"},
         }
@@ -817,6 +867,9 @@ def main():
         "unit": "GB/s",
         "frac": round(achieved / HBM_PEAK_GBS, 4),
         "traffic": traffic,
+        # HBM bytes the PMC counters saw (FETCH_SIZE calibrated + WRITE_SIZE,
+        # profiles/pmc_<workload>.json) / kernel time: the physical fraction
+        "frac_fetch": round(traffic / scan_s / 1e9 / HBM_PEAK_GBS, 4) if traffic else None,
         "algorithmic_bytes_per_launch": in_bytes,
         "basis": "input bytes per launch (SURVEY.md 8(d)); the kernel skips what the reference "
                  "skips, so hashed-byte rates are reported beside it",
@@ -1161,12 +1214,14 @@ def ingest_measure(torch, arena, offs, lens, dev, args) -> dict:
     ing = DeviceIngest(cfg, Key(key), device=dev.index or 0)
     o, n = [int(x) for x in offs[:ns]], [int(x) for x in lens[:ns]]
     times, res = [], None
+    from rustic_core_amd.pack import PackSizer
     for r in range(4):
-        ing.indexed = set()
+        ing.indexed = set()  # each call: a fresh repository (empty index and sizer)
+        ing.sizer = PackSizer.from_config(cfg, 0, 0)
         del res
         torch.cuda.synchronize(dev)
         t0 = time.perf_counter()
-        res = ing.ingest(arena, o, n)
+        res = ing.ingest(arena, o, n, finalize=True)
         torch.cuda.synchronize(dev)
         if r:
             times.append((time.perf_counter() - t0, res.ms))

@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define RCDC_ABI_VERSION 2u
+#define RCDC_ABI_VERSION 3u
 
 /* Status codes map onto rustic_core ErrorKind (crates/core/src/error.rs:108-124). */
 typedef enum {
@@ -168,7 +168,13 @@ rcdc_status rcdc_plan_results(rcdc_plan *plan, uint64_t *cuts,
 /* Device-side view of the results: stream i's cuts are
  * d_cuts[cut_base[i] .. cut_base[i] + d_counts[i]).  Complete after
  * rcdc_plan_finish; before it, a stream whose walk needs host completion
- * reads d_counts[i] == UINT64_MAX (and its digests are not written).        */
+ * reads d_counts[i] == UINT64_MAX (and its digests are not written).
+ * Ordering: a serial run's last kernel is ordered before later work on the
+ * run's stream (for hip_stream = 0, before later work on the legacy default
+ * stream too).  A pipelined run (rcdc_plan_set_pipeline) ends on a stream
+ * of the plan's own and is NOT ordered before the caller's later work on any
+ * stream: call rcdc_plan_finish (or synchronise the device) before reading
+ * these buffers from device code.                                          */
 rcdc_status rcdc_plan_device_results(rcdc_plan *plan, uint64_t *d_cuts,
                                      uint64_t *d_counts,
                                      const uint64_t **cut_base);
@@ -353,6 +359,32 @@ rcdc_status rcdc_pack_build_raw(rcdc_ctx *ctx, const uint8_t *key, const void *d
                                 const rcdc_pack_blob *blobs, uint32_t nblobs, rcdc_pack *packs,
                                 uint32_t npacks, void *d_out, uint64_t out_len,
                                 uint32_t *blob_offsets, void *hip_stream);
+
+/* rcdc_pack_build_raw over blobs that lie in several device buffers (sealed
+ * in different passes, or carried over from an earlier call while their pack
+ * was still open, packer.rs:659-671): blob i's bytes are at
+ * d_ins[blobs[i].pad] + in_off; pad >= n_ins is InvalidInput.              */
+rcdc_status rcdc_pack_build_raw_multi(rcdc_ctx *ctx, const uint8_t *key,
+                                      const void *const *d_ins, uint32_t n_ins,
+                                      const rcdc_pack_blob *blobs, uint32_t nblobs,
+                                      rcdc_pack *packs, uint32_t npacks, void *d_out,
+                                      uint64_t out_len, uint32_t *blob_offsets,
+                                      void *hip_stream);
+
+/* Device byte ranges gathered into one buffer: bytes [in_off, in_off + len)
+ * of d_ins[src] go to out_off of d_out (any alignment).  refs is a HOST
+ * array.  Returns once the copy has run (it is ordered on hip_stream).  Used
+ * to keep an open pack's sealed blobs alive across ingest calls.           */
+typedef struct {
+    uint64_t in_off;
+    uint64_t out_off;
+    uint64_t len;
+    uint32_t src;
+    uint32_t pad;
+} rcdc_copy_ref; /* 32 B */
+rcdc_status rcdc_copy_ranges(rcdc_ctx *ctx, const void *const *d_ins, uint32_t n_ins,
+                             const rcdc_copy_ref *refs, uint32_t n, void *d_out,
+                             void *hip_stream);
 
 /* ---- blob compression: backend/decrypt.rs:478-506 (`encode_all(data,
  * level)` before `Key::encrypt_data` when the repository is version 2,

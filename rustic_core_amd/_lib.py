@@ -27,9 +27,9 @@ EXPORTS = (
     "rcdc_plan_finish", "rcdc_stream_queued", "rcdc_stream_batch_bytes",
     "rcdc_aead_seal", "rcdc_aead_open", "rcdc_pack_build",
     "rcdc_zstd_bound", "rcdc_zstd_compress", "rcdc_zstd_tables", "rcdc_zstd_tables_size",
-    "rcdc_zstd_check", "rcdc_pack_build_raw",
+    "rcdc_zstd_check", "rcdc_pack_build_raw", "rcdc_pack_build_raw_multi", "rcdc_copy_ranges",
 )
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 
 class RcdcLibraryError(RuntimeError):
@@ -158,6 +158,10 @@ def lib() -> ctypes.CDLL:
     L.rcdc_pack_build.argtypes = [vp, vp, vp, vp, u32, vp, u32, vp, u64, vp, vp]
     L.rcdc_pack_build_raw.restype = st
     L.rcdc_pack_build_raw.argtypes = [vp, vp, vp, vp, u32, vp, u32, vp, u64, vp, vp]
+    L.rcdc_pack_build_raw_multi.restype = st
+    L.rcdc_pack_build_raw_multi.argtypes = [vp, vp, vp, u32, vp, u32, vp, u32, vp, u64, vp, vp]
+    L.rcdc_copy_ranges.restype = st
+    L.rcdc_copy_ranges.argtypes = [vp, vp, u32, vp, u32, vp, vp]
     L.rcdc_zstd_bound.restype = u64
     L.rcdc_zstd_bound.argtypes = [u64]
     L.rcdc_zstd_compress.restype = st

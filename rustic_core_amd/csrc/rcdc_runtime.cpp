@@ -83,8 +83,8 @@ hipError_t launch_zstd_check_blocks(const uint8_t *frames, const uint8_t *data, 
                                     uint32_t *ctr, hipStream_t stream);
 hipError_t launch_plan_set_len(StreamDesc *sds, ScanItem *items, uint32_t nitems, uint64_t n,
                                uint64_t nseg, hipStream_t stream);
-hipError_t launch_copy_ranges(const uint8_t *in, uint8_t *out, const void *units, uint32_t n,
-                              uint32_t cus, hipStream_t stream);
+hipError_t launch_copy_ranges(uint8_t *out, const void *units, uint32_t n, uint32_t cus,
+                              hipStream_t stream);
 hipError_t launch_zstd_check(const uint8_t *frames, const uint8_t *data, const void *refs,
                              const uint32_t *order, uint32_t n, bool stored, uint8_t *scratch,
                              uint32_t grid,
@@ -2072,10 +2072,49 @@ static_assert(sizeof(rcdc_pack) == 48, "rcdc_pack is 48 B");
 // type, u32 length, [u32 raw length], id) and its u32 length.
 // raw (add_raw): the blobs at in_off are sealed already (len = sealed bytes,
 // >= 32); they are copied into place and only the headers are sealed.
+// Device range copies (units of {src, dst, len, source base address}, at
+// most 1 MiB each) into d_out on st.  The unit list lives in the context
+// until the copy has run: calls take turns under the AEAD lock.
+rcdc_status copy_units_run(rcdc_ctx *ctx, const std::vector<uint64_t> &copies, void *d_out,
+                           hipStream_t st) {
+    if (copies.empty()) return RCDC_OK;
+    std::lock_guard<std::mutex> lk(ctx->aead_mu);
+    if (ctx->aead_done) HIP_TRY(hipEventSynchronize(ctx->aead_done));
+    const uint64_t nu = copies.size() / 4;
+    rcdc_status rs;
+    if ((rs = ensure_dev(&ctx->d_copy_units, &ctx->cap_copy_units, copies.size()))) return rs;
+    HIP_TRY(hipMemcpyAsync(ctx->d_copy_units, copies.data(), copies.size() * 8,
+                           hipMemcpyHostToDevice, st));
+    HIP_TRY(launch_copy_ranges((uint8_t *)d_out, ctx->d_copy_units, (uint32_t)nu,
+                               (uint32_t)std::max(ctx->num_cus, 1), st));
+    // the host vector dies with the caller's call
+    HIP_TRY(hipStreamSynchronize(st));
+    return RCDC_OK;
+}
+
+void push_copy(std::vector<uint64_t> &copies, const void *src_base, uint64_t src, uint64_t dst,
+               uint64_t len) {
+    for (uint64_t c = 0; c < len; c += 1u << 20) {
+        copies.push_back(src + c);
+        copies.push_back(dst + c);
+        copies.push_back(std::min<uint64_t>(1u << 20, len - c));
+        copies.push_back((uint64_t)(uintptr_t)src_base);
+    }
+}
+
+// srcs (raw only, n_src > 0): blob i's bytes are at srcs[blobs[i].pad] +
+// in_off (rcdc_pack_build_raw_multi); otherwise at d_in + in_off.
 rcdc_status pack_build(rcdc_ctx *ctx, const uint8_t key[64], const void *d_in,
                        const rcdc_pack_blob *blobs, uint32_t nblobs, rcdc_pack *packs,
                        uint32_t npacks, void *d_out, uint64_t out_len, uint32_t *blob_offsets,
-                       void *hip_stream, bool raw = false) {
+                       void *hip_stream, bool raw = false, const void *const *srcs = nullptr,
+                       uint32_t n_src = 0) {
+    if (n_src) {
+        if (!srcs) return fail(RCDC_ERR_INVALID_INPUT, "null argument");
+        for (uint32_t j = 0; j < n_src; j++)
+            if (!srcs[j]) return fail(RCDC_ERR_INVALID_INPUT, "source %u is null", j);
+        d_in = srcs[0];
+    }
     if (!valid_ctx(ctx) || !key || (npacks && (!packs || !d_out)) || (nblobs && (!blobs || !d_in)))
         return fail(RCDC_ERR_INVALID_INPUT, "null argument");
     std::vector<AeadBatch> bt(2);
@@ -2101,12 +2140,9 @@ rcdc_status pack_build(rcdc_ctx *ctx, const uint8_t key[64], const void *d_in,
             const uint32_t sealed = raw ? b.len : b.len + 32u;
             if (blob_offsets) blob_offsets[i] = (uint32_t)off;
             if (raw) {
-                for (uint64_t c = 0; c < sealed; c += 1u << 20) {
-                    copies.push_back(b.in_off + c);
-                    copies.push_back(P.out_off + off + c);
-                    copies.push_back(std::min<uint64_t>(1u << 20, sealed - c));
-                    copies.push_back(0);
-                }
+                if (n_src && b.pad >= n_src)
+                    return fail(RCDC_ERR_INVALID_INPUT, "blob %u: source %u of %u", i, b.pad, n_src);
+                push_copy(copies, n_src ? srcs[b.pad] : d_in, b.in_off, P.out_off + off, sealed);
             } else {
                 AeadBlob a{};
                 a.in_off = b.in_off;
@@ -2144,20 +2180,7 @@ rcdc_status pack_build(rcdc_ctx *ctx, const uint8_t key[64], const void *d_in,
     DeviceGuard g(ctx->device);
     hipStream_t st;
     if ((rs = null_enter(ctx, hip_stream, &st))) return rs;
-    if (!copies.empty()) {
-        // the unit list lives in the context until the copy has run (the
-        // AEAD lock below orders calls on this context's scratch)
-        std::lock_guard<std::mutex> lk(ctx->aead_mu);
-        if (ctx->aead_done) HIP_TRY(hipEventSynchronize(ctx->aead_done));
-        const uint64_t nu = copies.size() / 4;
-        if ((rs = ensure_dev(&ctx->d_copy_units, &ctx->cap_copy_units, copies.size()))) return rs;
-        HIP_TRY(hipMemcpyAsync(ctx->d_copy_units, copies.data(), copies.size() * 8,
-                               hipMemcpyHostToDevice, st));
-        HIP_TRY(launch_copy_ranges((const uint8_t *)d_in, (uint8_t *)d_out, ctx->d_copy_units,
-                                   (uint32_t)nu, (uint32_t)std::max(ctx->num_cus, 1), st));
-        // the host vector dies with this call
-        HIP_TRY(hipStreamSynchronize(st));
-    }
+    if ((rs = copy_units_run(ctx, copies, d_out, st))) return rs;
     if ((rs = aead_launch(ctx, false, key, bt, (uint8_t *)d_out, st, &hdr, nullptr))) return rs;
     return null_leave(ctx, hip_stream, st);
 }
@@ -2459,6 +2482,37 @@ rcdc_status rcdc_pack_build_raw(rcdc_ctx *ctx, const uint8_t *key, const void *d
                                 uint32_t *blob_offsets, void *hip_stream) {
     return pack_build(ctx, key, d_in, blobs, nblobs, packs, npacks, d_out, out_len, blob_offsets,
                       hip_stream, true);
+}
+
+rcdc_status rcdc_pack_build_raw_multi(rcdc_ctx *ctx, const uint8_t *key,
+                                      const void *const *d_ins, uint32_t n_ins,
+                                      const rcdc_pack_blob *blobs, uint32_t nblobs,
+                                      rcdc_pack *packs, uint32_t npacks, void *d_out,
+                                      uint64_t out_len, uint32_t *blob_offsets, void *hip_stream) {
+    if (n_ins == 0) return fail(RCDC_ERR_INVALID_INPUT, "no input buffers");
+    return pack_build(ctx, key, nullptr, blobs, nblobs, packs, npacks, d_out, out_len,
+                      blob_offsets, hip_stream, true, d_ins, n_ins);
+}
+
+rcdc_status rcdc_copy_ranges(rcdc_ctx *ctx, const void *const *d_ins, uint32_t n_ins,
+                             const rcdc_copy_ref *refs, uint32_t n, void *d_out,
+                             void *hip_stream) {
+    if (!valid_ctx(ctx) || (n && (!refs || !d_out || !d_ins || !n_ins)))
+        return fail(RCDC_ERR_INVALID_INPUT, "null argument");
+    std::vector<uint64_t> copies;
+    copies.reserve(4 * (size_t)n);
+    for (uint32_t i = 0; i < n; i++) {
+        const rcdc_copy_ref &c = refs[i];
+        if (c.src >= n_ins || !d_ins[c.src])
+            return fail(RCDC_ERR_INVALID_INPUT, "copy %u: source %u of %u", i, c.src, n_ins);
+        push_copy(copies, d_ins[c.src], c.in_off, c.out_off, c.len);
+    }
+    DeviceGuard g(ctx->device);
+    hipStream_t st;
+    rcdc_status rs;
+    if ((rs = null_enter(ctx, hip_stream, &st))) return rs;
+    if ((rs = copy_units_run(ctx, copies, d_out, st))) return rs;
+    return null_leave(ctx, hip_stream, st);
 }
 
 uint64_t rcdc_zstd_bound(uint64_t len) { return len + 3 * zstd_blocks(len) + 9; }

@@ -1065,9 +1065,11 @@ hipError_t launch_zstd_check_blocks(const uint8_t *frames, const uint8_t *data, 
 
 // ---- range copies (pack files from blobs sealed elsewhere: packer.rs
 // add_raw, :615-655) -----------------------------------------------------------
-// Unit k copies len bytes from in + src to out + dst (any alignments): the
-// output's 16-aligned body in dwordx4 stores of bytes loaded at any alignment
-// (five dwords + v_alignbit), the ragged head and tail byte by byte.
+// Unit k = {src, dst, len, base} copies len bytes from the device address
+// base + src to out + dst (any alignments; base is the unit's own source
+// buffer, so one launch gathers from several allocations): the output's
+// 16-aligned body in dwordx4 stores of bytes loaded at any alignment (the
+// neighbour lane's chunk + v_alignbit), the ragged head and tail byte by byte.
 
 namespace {
 
@@ -1076,14 +1078,13 @@ typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));
 
 }  // namespace
 
-__global__ __launch_bounds__(256) void rcdc_copy_ranges_kernel(const uint8_t *__restrict__ in,
-                                                               uint8_t *__restrict__ out,
+__global__ __launch_bounds__(256) void rcdc_copy_ranges_kernel(uint8_t *__restrict__ out,
                                                                const ulonglong4 *__restrict__ units,
                                                                uint32_t n) {
     const uint32_t t = threadIdx.x, ln = t & 63u;
     for (uint32_t k = blockIdx.x; k < n; k += gridDim.x) {
-        const ulonglong4 u = units[k];  // src, dst, len
-        const uint8_t *s = in + u.x;
+        const ulonglong4 u = units[k];  // src, dst, len, source base address
+        const uint8_t *s = reinterpret_cast<const uint8_t *>((uintptr_t)(u.w + u.x));
         uint8_t *d = out + u.y;
         const uint64_t len = u.z;
         uint32_t head = (uint32_t)((16u - ((uintptr_t)d & 15u)) & 15u);
@@ -1164,11 +1165,11 @@ __global__ __launch_bounds__(256) void rcdc_copy_ranges_kernel(const uint8_t *__
 
 namespace rcdc {
 
-hipError_t launch_copy_ranges(const uint8_t *in, uint8_t *out, const void *units, uint32_t n,
-                              uint32_t cus, hipStream_t stream) {
+hipError_t launch_copy_ranges(uint8_t *out, const void *units, uint32_t n, uint32_t cus,
+                              hipStream_t stream) {
     if (n == 0) return hipSuccess;
     const uint32_t g = n < cus * 8u ? n : cus * 8u;
-    hipLaunchKernelGGL(rcdc_copy_ranges_kernel, dim3(g), dim3(256), 0, stream, in, out,
+    hipLaunchKernelGGL(rcdc_copy_ranges_kernel, dim3(g), dim3(256), 0, stream, out,
                        (const ulonglong4 *)units, n);
     return hipGetLastError();
 }

@@ -48,7 +48,10 @@ from .device import DevicePlan, sha256_device
 from .errors import ErrorKind, RusticError
 from .compress import VERIFY_MESSAGE
 from .index import IndexPack, index_packs_from_build
-from .pack import PackSizer, build_packs, group_blobs, make_blobs, pack_layout
+from .pack import (PACK_BLOB, PackSizer, build_packs_multi, copy_ranges, group_blobs_open,
+                   make_blobs, pack_layout)
+
+_SRC_LONG, _SRC_SHORT, _SRC_CARRY = 0, 1, 2  # blobs["pad"]: the sealed blob's buffer
 
 
 def _void32(ids: np.ndarray) -> np.ndarray:
@@ -88,11 +91,14 @@ class IngestResult:
     """What one ``DeviceIngest.ingest`` call produced."""
     packs: object                 # uint8 CUDA tensor: the pack files back to back
     pack_table: np.ndarray        # PACK rows (out_off, blob0, nblobs, size, header_len)
-    blobs: np.ndarray             # PACK_BLOB rows of the new blobs, in pack order
-    blob_offsets: np.ndarray      # each new blob's offset in its pack
+    blobs: np.ndarray             # PACK_BLOB rows of the packed blobs, in pack order (the
+                                  # open pack's carried blobs first; in_off is relative to
+                                  # the sealed-blob buffer `pad`, dead after the call)
+    blob_offsets: np.ndarray      # each packed blob's offset in its pack
     cuts: list                    # per stream: its cut list
     ids: np.ndarray               # (chunks, 32): every chunk's id, in chunk order
-    new: np.ndarray               # bool per chunk: packed here (first occurrence, not indexed)
+    new: np.ndarray               # bool per chunk: added to the packer (first occurrence, not
+                                  # indexed) -- in a pack here or in the still open pack
     chunk_offs: np.ndarray        # arena offset of every chunk
     chunk_lens: np.ndarray
     ms: dict = field(default_factory=dict)
@@ -122,6 +128,31 @@ class IngestResult:
                                       time_ or rustic_time())
 
 
+@dataclass
+class _Pending:
+    """A batch between DeviceIngest.begin and .end."""
+    arena: object
+    ptr: int
+    t0: float
+    ms: dict
+    s_proc: object
+    groups: dict
+    cuts: list
+    c_offs: np.ndarray
+    c_lens: np.ndarray
+    is_long: np.ndarray
+    seal_off: np.ndarray
+    seal_len: np.ndarray
+    seal_src: np.ndarray
+    ulen: np.ndarray
+    done: np.ndarray
+    frames: object = None
+    st_long: object = None
+
+    def bound_bytes(self, sel) -> int:
+        return int((zstd_bounds(self.c_lens[sel]) + 64).sum()) + 64
+
+
 class DeviceIngest:
     """The backup data path for streams in HBM (see the module doc).
 
@@ -144,6 +175,10 @@ class DeviceIngest:
         self.indexed = indexed if indexed is not None else set()
         self._plan = None
         self._layout = None
+        # the open pack (blobs added, pack not yet saved): its sealed blobs in
+        # a device buffer of their own, PACK_BLOB rows with pad = _SRC_CARRY
+        self._carry = None
+        self._carry_blobs = np.zeros(0, PACK_BLOB)
 
     # ---- helpers ----------------------------------------------------------
     def _plan_for(self, offs, lens, arena_len):
@@ -195,9 +230,24 @@ class DeviceIngest:
                               f"{VERIFY_MESSAGE} (chunk at arena offset {int(c_offs[bad[0]])})")
 
     # ---- the batch ----------------------------------------------------------
-    def ingest(self, arena, offs, lens) -> IngestResult:
+    def ingest(self, arena, offs, lens, finalize: bool = False) -> IngestResult:
         """Back up the streams [offs[i], offs[i] + lens[i]) of `arena` (a
-        uint8 CUDA tensor, 256-byte aligned)."""
+        uint8 CUDA tensor, 256-byte aligned).  The packer stays open between
+        calls, as rustic's one Packer per backup (packer.rs:659-671): the
+        packs should_save closes are returned, the blobs of the still open
+        pack stay on the device for the next call (``finalize`` closes it
+        too, as ``finalize()`` does alone).  Work on `arena` is ordered after
+        the caller's current stream.  ``end(begin(...))``."""
+        return self.end(self.begin(arena, offs, lens), finalize)
+
+    def begin(self, arena, offs, lens) -> "_Pending":
+        """First half of ``ingest``: chunk, launch every chunk's blob id and
+        compress + seal + verify the long chunks speculatively.  The long ids
+        (the SHA-256 latency floor) are still running on return, so a caller
+        streaming batches runs ``begin(k + 1)`` before ``end(k)`` and the
+        floors of consecutive batches overlap (HostIngest).  Until ``end`` the
+        arena must stay unchanged; ``end`` calls must come in ``begin``
+        order (dedup and the open pack are sequential)."""
         import torch
         dev = arena.device
         t0 = time.perf_counter()
@@ -221,48 +271,64 @@ class DeviceIngest:
         ms["chunk"] = (time.perf_counter() - t0) * 1e3
         # 2. ids: short and long chunks on two streams, each longest first
         is_long = c_lens > self.long_chunk
-        ids_dev = torch.empty((max(n, 1), 32), dtype=torch.uint8, device=dev)
         groups = {}
         for name, mask, st in (("long", is_long, s_long), ("short", ~is_long, s_short)):
             idx = np.nonzero(mask)[0]
             idx = idx[np.argsort(-c_lens[idx].astype(np.int64), kind="stable")]
-            refs = torch.from_numpy(np.stack([c_offs[idx].astype(np.int64),
-                                              c_lens[idx].astype(np.int64)], 1)
-                                    if len(idx) else np.zeros((0, 2), np.int64)).to(dev)
             st.wait_stream(s_main)
-            out = torch.empty((max(len(idx), 1), 32), dtype=torch.uint8, device=dev)
+            with torch.cuda.stream(st):  # the buffers belong to the stream using them
+                refs = torch.from_numpy(np.stack([c_offs[idx].astype(np.int64),
+                                                  c_lens[idx].astype(np.int64)], 1)
+                                        if len(idx) else np.zeros((0, 2), np.int64)).to(dev)
+                out = torch.empty((max(len(idx), 1), 32), dtype=torch.uint8, device=dev)
             if len(idx):
                 sha256_device(self.ctx, arena, refs, out, st.cuda_stream)
             ev = torch.cuda.Event()
             ev.record(st)
             groups[name] = (idx, out, refs, ev)
         s_proc.wait_stream(s_main)
-        sp = s_proc.cuda_stream
-        seal_off = np.zeros(n, np.uint64)  # offsets relative to the long staging (mod 2^64)
-        seal_len = np.zeros(n, np.uint64)
-        ulen = np.zeros(n, np.uint64)
-        done = np.zeros(n, bool)
-
-        def bound_bytes(sel):
-            return int((zstd_bounds(c_lens[sel]) + 64).sum()) + 64
-
+        p = _Pending(arena=arena, ptr=ptr, t0=t0, ms=ms, s_proc=s_proc, groups=groups, cuts=cuts,
+                     c_offs=c_offs, c_lens=c_lens, is_long=is_long,
+                     seal_off=np.zeros(n, np.uint64), seal_len=np.zeros(n, np.uint64),
+                     seal_src=np.zeros(n, np.uint32), ulen=np.zeros(n, np.uint64),
+                     done=np.zeros(n, bool))
         # 3a. long chunks, speculatively (before their ids); frames are dead
-        # once sealed, so the verify opens into them
+        # once sealed, so the verify opens into them.  Every buffer the
+        # kernels on s_proc use is allocated on s_proc (the caching allocator
+        # then never hands its memory to another stream while they run).
+        # Sealed blobs: source 0 = the long staging, 1 = the short staging,
+        # 2 = the open pack carried over from the last call (_SRC_*).
         t1 = time.perf_counter()
         lidx = np.sort(groups["long"][0])
-        frames = torch.empty(bound_bytes(lidx), dtype=torch.uint8, device=dev)
-        st_long = torch.empty(bound_bytes(lidx), dtype=torch.uint8, device=dev)
-        base = st_long.data_ptr()
+        with torch.cuda.stream(s_proc):
+            p.frames = torch.empty(p.bound_bytes(lidx), dtype=torch.uint8, device=dev)
+            p.st_long = torch.empty(p.bound_bytes(lidx), dtype=torch.uint8, device=dev)
         if len(lidx):
-            so, sl, ul, _ = self._process(torch, ptr, lidx, c_offs, c_lens, frames, st_long, 0, sp)
-            seal_off[lidx], seal_len[lidx], ulen[lidx] = so, sl, ul
-            done[lidx] = True
+            sp = s_proc.cuda_stream
+            so, sl, ul, _ = self._process(torch, ptr, lidx, c_offs, c_lens, p.frames, p.st_long, 0,
+                                          sp)
+            p.seal_off[lidx], p.seal_len[lidx], p.ulen[lidx] = so, sl, ul
+            p.seal_src[lidx] = _SRC_LONG
+            p.done[lidx] = True
             if self.extra_verify:
-                self._verify(torch, st_long, so, sl, ptr, c_offs[lidx], c_lens[lidx], frames, sp)
+                self._verify(torch, p.st_long, so, sl, ptr, c_offs[lidx], c_lens[lidx], p.frames,
+                             sp)
         ms["long_speculative"] = (time.perf_counter() - t1) * 1e3
+        return p
+
+    def end(self, p: "_Pending", finalize: bool = False) -> IngestResult:
+        """Second half of ``ingest`` (see ``begin``): dedup the short chunks
+        on their ids and process the first occurrences, wait for the long
+        ids, dedup the whole batch in chunk order and pack."""
+        import torch
+        dev = p.arena.device
+        ms, t0, ptr = p.ms, p.t0, p.ptr
+        s_proc, sp = p.s_proc, p.s_proc.cuda_stream
+        c_offs, c_lens, is_long = p.c_offs, p.c_lens, p.is_long
+        n = len(c_lens)
         # 3b. short chunks: ids, dedup, first occurrences only
         ids = np.zeros((n, 32), np.uint8)
-        sidx, sout, _, sev = groups["short"]
+        sidx, sout, _, sev = p.groups["short"]
         sev.synchronize()
         ms["short_ids_ready"] = (time.perf_counter() - t0) * 1e3
         if len(sidx):
@@ -272,51 +338,306 @@ class DeviceIngest:
         snew = np.nonzero(first & ~is_long)[0]
         t2 = time.perf_counter()
         st_short = None
+        frames = p.frames
+        p.frames = None
         if len(snew):
-            need = bound_bytes(snew)
-            if frames.numel() < need:
-                del frames
-                frames = torch.empty(need, dtype=torch.uint8, device=dev)
-            st_short = torch.empty(need, dtype=torch.uint8, device=dev)
+            need = p.bound_bytes(snew)
+            with torch.cuda.stream(s_proc):
+                if frames.numel() < need:
+                    del frames
+                    frames = torch.empty(need, dtype=torch.uint8, device=dev)
+                st_short = torch.empty(need, dtype=torch.uint8, device=dev)
             so, sl, ul, _ = self._process(torch, ptr, snew, c_offs, c_lens, frames, st_short, 0, sp)
             if self.extra_verify:
                 self._verify(torch, st_short, so, sl, ptr, c_offs[snew], c_lens[snew], frames, sp)
-            # relative to the long staging's base (64-bit wrap-around offsets)
-            rel = np.uint64((st_short.data_ptr() - base) % (1 << 64))
-            seal_off[snew], seal_len[snew], ulen[snew] = so + rel, sl, ul
-            done[snew] = True
+            p.seal_off[snew], p.seal_len[snew], p.ulen[snew] = so, sl, ul
+            p.seal_src[snew] = _SRC_SHORT
+            p.done[snew] = True
         ms["short_new"] = (time.perf_counter() - t2) * 1e3
         del frames
         # 4. long ids, final dedup over the whole batch in chunk order
-        lidx_q, lout, _, lev = groups["long"]
+        lidx_q, lout, _, lev = p.groups["long"]
         lev.synchronize()
         ms["long_ids_ready"] = (time.perf_counter() - t0) * 1e3
         if len(lidx_q):
             ids[lidx_q] = lout[:len(lidx_q)].cpu().numpy()
         new = first_occurrences(ids, np.arange(n), known)
-        assert done[new].all(), "a new blob was not processed"
+        assert p.done[new].all(), "a new blob was not processed"
         nidx = np.nonzero(new)[0]
+        self.indexed.update(map(bytes, ids[nidx]))
         t3 = time.perf_counter()
         nb = len(nidx)
-        blobs = make_blobs(seal_off[nidx], seal_len[nidx], ids[nidx], np.zeros((nb, 16), np.uint8),
-                           uncompressed=ulen[nidx])
-        grp = group_blobs([int(x) - 32 for x in seal_len[nidx]], self.sizer,
-                          [int(x) for x in ulen[nidx]])
-        hn = np.frombuffer(os.urandom(16 * len(grp)), np.uint8).reshape(len(grp), 16) if grp else \
-            np.zeros((0, 16), np.uint8)
-        packs_t, total = pack_layout(blobs, grp, hn, raw=True)
-        packs = torch.empty(max(total, 1) + 64, dtype=torch.uint8, device=dev)
-        offs_in_pack = build_packs(self.ctx, self.key._key, base, blobs, packs_t,
-                                   packs.data_ptr(), total, sp, raw=True) if nb else \
-            np.zeros(0, np.uint32)
-        s_proc.synchronize()
-        self.indexed.update(map(bytes, ids[nidx]))
+        blobs_new = make_blobs(p.seal_off[nidx], p.seal_len[nidx], ids[nidx],
+                               np.zeros((nb, 16), np.uint8), uncompressed=p.ulen[nidx])
+        blobs_new["pad"] = p.seal_src[nidx]
+        st_long = p.st_long
+        srcs = [st_long.data_ptr(), (st_short if st_short is not None else st_long).data_ptr(),
+                self._carry.data_ptr() if self._carry is not None else st_long.data_ptr()]
+        res = self._pack(torch, np.concatenate([self._carry_blobs, blobs_new]), srcs, finalize, sp,
+                         s_proc, dev)
         ms["pack"] = (time.perf_counter() - t3) * 1e3
         ms["total"] = (time.perf_counter() - t0) * 1e3
+        p.st_long = None
         del st_long, st_short
-        return IngestResult(packs, packs_t, blobs, offs_in_pack, cuts, ids, new, c_offs, c_lens, ms)
+        packs, packs_t, blobs, offs_in_pack = res
+        return IngestResult(packs, packs_t, blobs, offs_in_pack, p.cuts, ids, new, c_offs, c_lens,
+                            ms)
+
+    def finalize(self) -> IngestResult:
+        """Close the open pack (Packer::finalize, packer.rs:385-398): its
+        blobs, carried from earlier calls, become the last pack."""
+        import torch
+        dev = torch.device("cuda", self.device)
+        s_proc = torch.cuda.Stream(dev)
+        s_proc.wait_stream(torch.cuda.current_stream(dev))
+        srcs = [self._carry.data_ptr()] * 3 if self._carry is not None else [0, 0, 0]
+        t0 = time.perf_counter()
+        packs, packs_t, blobs, offs_in_pack = self._pack(torch, self._carry_blobs, srcs, True,
+                                                         s_proc.cuda_stream, s_proc, dev)
+        z = np.zeros(0, np.uint64)
+        return IngestResult(packs, packs_t, blobs, offs_in_pack, [], np.zeros((0, 32), np.uint8),
+                            np.zeros(0, bool), z, z, {"pack": (time.perf_counter() - t0) * 1e3})
+
+    @property
+    def open_blobs(self) -> int:
+        """Blobs of the open pack (added, not yet in a pack file)."""
+        return len(self._carry_blobs)
+
+    def _pack(self, torch, blobs, srcs, finalize, sp, s_proc, dev):
+        """Group `blobs` (the open pack's first, then this call's new ones, in
+        chunk order) as the packer does, build the packs should_save closes
+        (rcdc_pack_build_raw_multi over the sealed blobs' buffers) and move the
+        open pack's blobs into a new carry buffer (rcdc_copy_ranges)."""
+        grp, open_from = group_blobs_open([int(x) - 32 for x in blobs["len"]], self.sizer,
+                                          [int(x) for x in blobs["uncompressed_len"]], finalize)
+        closed = blobs[:open_from]
+        hn = np.frombuffer(os.urandom(16 * len(grp)), np.uint8).reshape(len(grp), 16) if grp else \
+            np.zeros((0, 16), np.uint8)
+        packs_t, total = pack_layout(closed, grp, hn, raw=True)
+        with torch.cuda.stream(s_proc):
+            packs = torch.empty(max(total, 1) + 64, dtype=torch.uint8, device=dev)
+        offs_in_pack = build_packs_multi(self.ctx, self.key._key, srcs, closed, packs_t,
+                                         packs.data_ptr(), total, sp) if len(grp) else \
+            np.zeros(0, np.uint32)
+        rest = blobs[open_from:].copy()
+        carry = None
+        if len(rest):
+            lens = rest["len"].astype(np.uint64)
+            dst = np.zeros(len(rest), np.uint64)
+            dst[1:] = np.cumsum((lens + 15) // 16 * 16)[:-1]
+            with torch.cuda.stream(s_proc):
+                carry = torch.empty(int(dst[-1] + lens[-1]) + 64, dtype=torch.uint8, device=dev)
+            copy_ranges(self.ctx, srcs, rest["pad"], rest["in_off"], lens, dst, carry.data_ptr(),
+                        sp)
+            rest["in_off"] = dst
+            rest["pad"] = _SRC_CARRY
+        s_proc.synchronize()
+        self._carry, self._carry_blobs = carry, rest
+        return packs, packs_t, closed, offs_in_pack
 
     def close(self):
         if self._plan is not None:
             self._plan.close()
             self._plan = None
+
+
+# ---- files in host memory -> packs and pack ids in host memory -------------
+@dataclass
+class HostIngestResult:
+    """What ``HostIngest.run`` produced: every pack file in host memory (one
+    pinned buffer, packs back to back), their ids, and per batch the device
+    results (cuts, chunk ids, dedup decisions)."""
+    packs_host: object            # uint8 CPU tensor (pinned): pack files back to back
+    pack_offs: np.ndarray         # each pack's offset in packs_host
+    pack_sizes: np.ndarray
+    pack_ids: List[bytes]         # SHA-256 of each pack file (packer.rs:832-834)
+    batches: List[IngestResult]   # per batch (their .packs device tensors dropped)
+    batch_files: List[List[int]]  # the files of each batch
+    seconds: float                # wall time: first H2D issued .. last pack id computed
+    h2d_bytes: int
+    d2h_bytes: int
+    ms: dict = field(default_factory=dict)
+
+    def pack_file(self, k: int) -> bytes:
+        o = int(self.pack_offs[k])
+        return self.packs_host[o:o + int(self.pack_sizes[k])].numpy().tobytes()
+
+
+def plan_batches(sizes, first: int, middle: int, last: int) -> List[List[int]]:
+    """Whole files in order into batches of about ``first`` bytes, then
+    ``middle``, and a final one of about ``last``: a small first batch starts
+    the device early, a small last one shortens the drain (its ids, packs,
+    copy back and pack ids follow the last H2D)."""
+    total = int(sum(sizes))
+    rest = total - first - last
+    m = max(-(-rest // middle), 0)
+    targets = [first] + [-(-rest // m)] * m + [last] if m else [first, last]
+    ends = np.cumsum(targets)  # a batch closes where the running total would pass its end
+    out, cur, acc, t = [], [], 0, 0
+    for i, n in enumerate(sizes):
+        if cur and t < len(ends) - 1 and acc + n > ends[t]:
+            out.append(cur)
+            cur, t = [], t + 1
+        cur.append(i)
+        acc += int(n)
+    if cur:
+        out.append(cur)
+    return out
+
+
+class HostIngest:
+    """The backup data path from files in host memory to pack files and pack
+    ids in host memory, on one GPU.
+
+    Reference: ``FileArchiver::backup_reader`` reads each file and chunks it
+    (archiver/file_archiver.rs:144-160), ``Packer`` packs the new blobs
+    (blob/packer.rs:260-275, 615-735), hashes each finished pack file for its
+    id (``hash_reader``, packer.rs:832-834) and hands it to the backend.
+
+    Pipeline over batches of whole files (``plan_batches``), three device
+    arena slots:
+      - H2D of batch k + 2 (one copy stream) while the device works on k, k + 1;
+      - ``DeviceIngest.begin(k)`` (chunk, launch ids, long chunks
+        speculatively) before ``end(k - 1)`` (dedup, short chunks, packs), so
+        the SHA-256 latency floors of consecutive batches overlap;
+      - D2H of each batch's packs (a second copy stream, the other PCIe
+        direction) into one pinned host buffer;
+      - pack ids on ``hash_threads`` host threads (hashlib: OpenSSL SHA-256,
+        the GIL released), each pack as soon as its batch's copy is done.
+    The packer stays open across batches (one pack sequence, as one Packer
+    per backup) and the last batch finalizes it."""
+
+    def __init__(self, config: ConfigFile, key: Key, device: int = 0,
+                 indexed: Optional[set] = None, extra_verify: Optional[bool] = None,
+                 hash_threads: Optional[int] = None, first_batch: int = 4 << 30,
+                 batch: int = 16 << 30, last_batch: int = 4 << 30,
+                 pack_ratio: float = 0.8):
+        self.ingest = DeviceIngest(config, key, device, indexed, extra_verify)
+        self.device = device
+        if hash_threads is None:
+            try:
+                hash_threads = max(len(os.sched_getaffinity(0)) - 2, 1)
+            except AttributeError:  # pragma: no cover
+                hash_threads = 8
+            omp = os.environ.get("OMP_NUM_THREADS", "")
+            if omp.isdigit() and int(omp) > 0:
+                hash_threads = min(hash_threads, max(int(omp) - 2, 1))
+        self.hash_threads = int(hash_threads)
+        self.first_batch, self.batch, self.last_batch = int(first_batch), int(batch), int(last_batch)
+        self.pack_ratio = float(pack_ratio)  # initial pinned pack buffer / input bytes
+
+    def run(self, files) -> HostIngestResult:
+        """`files`: 1-D uint8 CPU tensors (pinned for full-rate copies)."""
+        import hashlib
+        import threading
+        from concurrent.futures import ThreadPoolExecutor
+
+        import torch
+        from .device import pack_offsets
+        dev = torch.device("cuda", self.device)
+        sizes = [int(f.numel()) for f in files]
+        batches = plan_batches(sizes, self.first_batch, self.batch, self.last_batch)
+        layouts = [pack_offsets([sizes[i] for i in b]) for b in batches]
+        slot_len = max(a for _, a in layouts)
+        arenas = [torch.empty(slot_len, dtype=torch.uint8, device=dev)
+                  for _ in range(min(3, len(batches)))]
+        total_in = sum(sizes)
+        host = torch.empty(int(total_in * self.pack_ratio) + (64 << 20), dtype=torch.uint8,
+                           pin_memory=True)
+        s_h2d, s_d2h = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
+        ev_h2d = [None] * len(batches)
+        pool = ThreadPoolExecutor(max_workers=self.hash_threads)
+        lock = threading.Lock()
+        ids_out, offs_out, sizes_out, futs, keep = [], [], [], [], []
+        state = {"host_off": 0, "d2h": 0, "host": host}
+        ms = {"begin": 0.0, "end": 0.0, "handoff": 0.0}
+
+        def h2d(k):
+            offs, _ = layouts[k]
+            a = arenas[k % len(arenas)]
+            with torch.cuda.stream(s_h2d):
+                for i, o in zip(batches[k], offs):
+                    a[int(o):int(o) + sizes[i]].copy_(files[i], non_blocking=True)
+                ev_h2d[k] = torch.cuda.Event()
+                ev_h2d[k].record(s_h2d)
+
+        def hash_pack(buf, o, n, slot):
+            d = hashlib.sha256(memoryview(buf[o:o + n].numpy())).digest()
+            with lock:
+                ids_out[slot] = d
+
+        def handoff(res):
+            # the packs of one batch: D2H into the pinned buffer, then hashed
+            t = time.perf_counter()
+            total = res.pack_bytes
+            if total:
+                o0 = state["host_off"]
+                if o0 + total > state["host"].numel():  # (rare) a larger buffer
+                    s_d2h.synchronize()
+                    big = torch.empty(int((o0 + total) * 1.25), dtype=torch.uint8,
+                                      pin_memory=True)
+                    big[:o0].copy_(state["host"][:o0])
+                    state["host"] = big
+                buf = state["host"]
+                with torch.cuda.stream(s_d2h):
+                    s_d2h.wait_stream(torch.cuda.current_stream(dev))
+                    buf[o0:o0 + total].copy_(res.packs[:total], non_blocking=True)
+                    ev = torch.cuda.Event()
+                    ev.record(s_d2h)
+                keep.append((res.packs, ev))
+                state["host_off"] = o0 + total
+                state["d2h"] += total
+                rows = [(o0 + int(p["out_off"]), int(p["size"])) for p in res.pack_table]
+                base = len(ids_out)
+                ids_out.extend([None] * len(rows))
+                for o, n in rows:
+                    offs_out.append(o)
+                    sizes_out.append(n)
+
+                def job(ev=ev, rows=rows, base=base, buf=buf):
+                    ev.synchronize()
+                    return [pool.submit(hash_pack, buf, o, n, base + j)
+                            for j, (o, n) in enumerate(rows)]
+                futs.append(pool.submit(job))
+            res.packs = None
+            ms["handoff"] += (time.perf_counter() - t) * 1e3
+
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for k in range(min(len(arenas), len(batches))):
+            h2d(k)
+        results, pending = [], None
+        for k in range(len(batches)):
+            torch.cuda.current_stream(dev).wait_event(ev_h2d[k])
+            offs, _ = layouts[k]
+            t = time.perf_counter()
+            p = self.ingest.begin(arenas[k % len(arenas)], offs, [sizes[i] for i in batches[k]])
+            ms["begin"] += (time.perf_counter() - t) * 1e3
+            if pending is not None:
+                t = time.perf_counter()
+                r = self.ingest.end(pending)
+                ms["end"] += (time.perf_counter() - t) * 1e3
+                handoff(r)
+                results.append(r)
+                # the slot of batch k - 1 is free: batch k + 2 goes there
+                if k + 2 < len(batches):
+                    h2d(k + 2)
+            pending = p
+        t = time.perf_counter()
+        r = self.ingest.end(pending, finalize=True)
+        ms["end"] += (time.perf_counter() - t) * 1e3
+        handoff(r)
+        results.append(r)
+        for f in futs:  # the per-batch waiters, then their pack jobs
+            for g in f.result():
+                g.result()
+        seconds = time.perf_counter() - t0
+        pool.shutdown()
+        keep.clear()
+        del arenas
+        return HostIngestResult(state["host"], np.asarray(offs_out, np.int64),
+                                np.asarray(sizes_out, np.int64), list(ids_out), results, batches,
+                                seconds, total_in, state["d2h"], ms)
+
+    def close(self):
+        self.ingest.close()

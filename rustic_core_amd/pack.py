@@ -92,6 +92,18 @@ def group_blobs(lens: Sequence[int], sizer: PackSizer,
     reaches pack_size(); take_data (:749-758) adds the closed pack's
     PackHeaderRef::pack_size to the sizer.  (MAX_AGE, a wall-clock rule, is
     not modelled.)  The last pack holds the rest (finalize)."""
+    return group_blobs_open(lens, sizer, uncompressed, finalize=True)[0]
+
+
+def group_blobs_open(lens: Sequence[int], sizer: PackSizer,
+                     uncompressed: Optional[Sequence[int]] = None,
+                     finalize: bool = False) -> Tuple[List[Tuple[int, int]], int]:
+    """group_blobs for a packer that stays open between calls (one Packer
+    for the whole backup, packer.rs:659-671 / 749-750): returns the packs
+    should_save closed and the index of the first blob of the still open
+    pack (len(lens) if none).  The open pack's size is NOT added to the sizer
+    (take_data has not run for it); with ``finalize`` it is closed too
+    (Packer::finalize)."""
     # a pack at a time (pack_size() only changes when a pack closes): its
     # last blob is the first whose running sealed size reaches pack_size(),
     # or the MAX_COUNT-th (numpy over prefix sums, not a Python loop per blob)
@@ -107,10 +119,13 @@ def group_blobs(lens: Sequence[int], sizer: PackSizer,
         limit = cum[b0] + sizer.pack_size()
         i = int(np.searchsorted(cum, limit, side="left"))  # cum[i] >= limit: blobs b0..i-1
         e = min(max(i, b0 + 1), b0 + MAX_COUNT, n_all)       # one past the pack's last blob
+        closed = cum[e] - cum[b0] >= sizer.pack_size() or e - b0 >= MAX_COUNT
+        if not closed and not finalize:
+            break  # should_save is false after the last blob: the pack stays open
         packs.append((b0, e - b0))
         sizer.add_size(int(cum[e] - cum[b0] + cumh[e] - cumh[b0]) + 32 + 4)
         b0 = e
-    return packs
+    return packs, b0
 
 
 def make_blobs(in_offs, lens, ids, nonces, types=None, uncompressed=None) -> np.ndarray:
@@ -166,6 +181,46 @@ def build_packs(ctx, key: bytes, d_in: int, blobs: np.ndarray, packs: np.ndarray
     if st:
         raise status_error(st, _lib.last_error())
     return offs[:len(blobs)]
+
+
+def build_packs_multi(ctx, key: bytes, d_ins: Sequence[int], blobs: np.ndarray,
+                      packs: np.ndarray, d_out: int, out_len: int,
+                      hip_stream: Optional[int] = None) -> np.ndarray:
+    """rcdc_pack_build_raw_multi: build_packs(raw=True) over sealed blobs in
+    several device buffers, blobs["pad"] selecting d_ins[pad]."""
+    blobs = np.ascontiguousarray(blobs, PACK_BLOB)
+    if not (packs.flags["C_CONTIGUOUS"] and packs.dtype == PACK):
+        raise TypeError("packs must be a C-contiguous PACK array (it receives the sizes)")
+    offs = np.zeros(max(len(blobs), 1), np.uint32)
+    kb = (ctypes.c_uint8 * 64).from_buffer_copy(bytes(key))
+    srcs = (ctypes.c_void_p * max(len(d_ins), 1))(*[int(p) for p in d_ins])
+    st = _lib.lib().rcdc_pack_build_raw_multi(
+        ctx.handle, kb, ctypes.cast(srcs, ctypes.c_void_p), len(d_ins), blobs.ctypes.data,
+        len(blobs), packs.ctypes.data, len(packs), ctypes.c_void_p(d_out), int(out_len),
+        offs.ctypes.data, ctypes.c_void_p(hip_stream or 0))
+    if st:
+        raise status_error(st, _lib.last_error())
+    return offs[:len(blobs)]
+
+
+COPY_REF = np.dtype([("in_off", "<u8"), ("out_off", "<u8"), ("len", "<u8"), ("src", "<u4"),
+                     ("pad", "<u4")])
+assert COPY_REF.itemsize == 32
+
+
+def copy_ranges(ctx, d_ins: Sequence[int], src, in_offs, lens, out_offs, d_out: int,
+                hip_stream: Optional[int] = None) -> None:
+    """rcdc_copy_ranges: bytes [in_off, +len) of d_ins[src] to out_off of d_out."""
+    n = len(lens)
+    refs = np.zeros(n, COPY_REF)
+    refs["in_off"], refs["out_off"], refs["len"] = in_offs, out_offs, lens
+    refs["src"] = src
+    srcs = (ctypes.c_void_p * max(len(d_ins), 1))(*[int(p) for p in d_ins])
+    st = _lib.lib().rcdc_copy_ranges(ctx.handle, ctypes.cast(srcs, ctypes.c_void_p), len(d_ins),
+                                     refs.ctypes.data, n, ctypes.c_void_p(d_out),
+                                     ctypes.c_void_p(hip_stream or 0))
+    if st:
+        raise status_error(st, _lib.last_error())
 
 
 def index_entries(blobs: np.ndarray, packs: np.ndarray, offsets: np.ndarray):

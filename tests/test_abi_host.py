@@ -29,7 +29,7 @@ def test_header_symbols_exported(rcdc_lib):
 
 
 def test_abi_version(rcdc_lib):
-    assert rcdc_lib.rcdc_abi_version() == 2
+    assert rcdc_lib.rcdc_abi_version() == 3
 
 
 @pytest.mark.parametrize("avg,mn,mx,status", [
@@ -168,3 +168,20 @@ def test_blob_id_entry_points_reject_null(rcdc_lib):
     assert L.rcdc_plan_hash_many(ctypes.cast(hs, ctypes.c_void_p), 9,
                                  ctypes.cast(ars, ctypes.c_void_p), None) == 2
     assert "8 plans" in _lib.last_error()
+
+
+def test_multi_source_entry_points_reject_bad_input(rcdc_lib):
+    """rcdc_pack_build_raw_multi / rcdc_copy_ranges (ABI 3): a null context,
+    no input buffers or a null source give RCDC_ERR_INVALID_INPUT before any
+    HIP call."""
+    from rustic_core_amd import _lib
+    L = _lib.lib()
+    key = (ctypes.c_uint8 * 64)()
+    assert L.rcdc_pack_build_raw_multi(None, key, None, 0, None, 0, None, 0, None, 0,
+                                       None, None) == 2
+    assert "no input buffers" in _lib.last_error()
+    srcs = (ctypes.c_void_p * 2)(None, None)
+    assert L.rcdc_pack_build_raw_multi(None, key, ctypes.cast(srcs, ctypes.c_void_p), 2, None,
+                                       0, None, 0, None, 0, None, None) == 2
+    assert "source 0 is null" in _lib.last_error()
+    assert L.rcdc_copy_ranges(None, None, 0, None, 0, None, None) == 2

@@ -71,7 +71,7 @@ def _ingest(version, indexed=None, extra_verify=None, key=bytes(range(64)), seed
     datas = _streams(seed)
     host, arena, offs, lens = _arena(datas)
     ing = DeviceIngest(cfg, Key(key), indexed=indexed, extra_verify=extra_verify)
-    res = ing.ingest(arena, offs, lens)
+    res = ing.ingest(arena, offs, lens, finalize=True)
     return ing, res, host, offs, lens, datas
 
 
@@ -207,3 +207,155 @@ def test_pack_build_raw_matches_sealed_build(gpu_ctx):
     for p in packs:
         s, n = int(p["out_off"]), int(p["size"])
         assert np.array_equal(a[s:s + n], b[s:s + n])
+
+
+def _packs_blobs(res, key, compressed):
+    """(header entries, decoded blob bytes) of every pack of `res`, parsed and
+    opened by the oracle."""
+    out = []
+    k = 0
+    for j in range(len(res.pack_table)):
+        f = res.pack_file(j)
+        assert len(f) == int(res.pack_table[j]["size"])
+        for tpe, off, ln, ulen, bid in oracle.parse_pack(key, f):
+            assert tpe == 0 and off == int(res.blob_offsets[k])
+            plain = oracle.open_(key, f[off:off + ln])
+            out.append((bytes(bid), zr.decompress(plain) if compressed else plain))
+            k += 1
+    return out
+
+
+def test_ingest_calls_keep_the_pack_open():
+    """One packer across calls (packer.rs:659-671, 749-750): three
+    ingest calls and finalize() close exactly the packs one pass over all new
+    blobs closes -- no undersized pack per call -- with the open pack's sealed
+    blobs carried on the device between calls (rcdc_copy_ranges) and built
+    from several buffers (rcdc_pack_build_raw_multi).  Chunks repeated across
+    calls are packed once."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from rustic_core_amd.chunker import ConfigFile
+    from rustic_core_amd.crypto import Key
+    from rustic_core_amd.ingest import DeviceIngest
+    from rustic_core_amd.pack import PackSizer, group_blobs
+    key = bytes(range(3, 67))
+    cfg = ConfigFile.new(2, oracle.DEFAULT_POLY)
+    datas = _streams(seed=9, n=8)
+    ing = DeviceIngest(cfg, Key(key))
+    ing.sizer = PackSizer.fixed(24 * MiB)  # several packs per call, one left open
+    results, all_chunks = [], []
+    for part in (datas[0:3], datas[3:6], datas[6:8]):
+        host, arena, offs, lens = _arena(part)
+        res = ing.ingest(arena, offs, lens)
+        results.append(res)
+        for i, (o, n) in enumerate(zip(offs, lens)):
+            exp = oracle.chunk_cuts(host[int(o):int(o) + n])
+            assert np.array_equal(res.cuts[i], exp)
+            prev = 0
+            for c in exp:
+                all_chunks.append(host[int(o) + prev:int(o) + int(c)].tobytes())
+                prev = int(c)
+        assert ing.open_blobs > 0
+    results.append(ing.finalize())
+    assert ing.open_blobs == 0
+    seen, new_chunks = set(), []
+    for c in all_chunks:
+        h = hashlib.sha256(c).digest()
+        if h not in seen:
+            seen.add(h)
+            new_chunks.append(c)
+    got = []
+    sizes = []
+    for r in results:
+        got += _packs_blobs(r, key, compressed=True)
+        sizes += [int(p["nblobs"]) for p in r.pack_table]
+    assert [d for _, d in got] == new_chunks
+    assert [b for b, _ in got] == [hashlib.sha256(c).digest() for c in new_chunks]
+    # the same grouping as one packer over every new blob (sealed sizes from
+    # the packs themselves)
+    sealed = np.concatenate([r.blobs["len"].astype(np.int64) for r in results])
+    ulens = np.concatenate([r.blobs["uncompressed_len"].astype(np.int64) for r in results])
+    one = group_blobs([int(x) - 32 for x in sealed], PackSizer.fixed(24 * MiB),
+                      [int(x) for x in ulens])
+    assert sizes == [n for _, n in one]
+    assert len(sizes) > len(results)  # packs closed by size inside calls
+
+
+def test_ingest_rejects_a_corrupted_blob(monkeypatch):
+    """extra_verify in the ingest path: a byte flipped in a sealed
+    blob between seal and verify -- in the long and in the short staging --
+    raises ErrorKind.Verification (backend/decrypt.rs:508-529, C003)."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from rustic_core_amd.chunker import ConfigFile
+    from rustic_core_amd.crypto import Key
+    from rustic_core_amd.errors import ErrorKind, RusticError
+    from rustic_core_amd.ingest import DeviceIngest
+    datas = _streams(seed=11, n=8)
+    host, arena, offs, lens = _arena(datas)
+    for which in (0, 1):  # 0: the first _process call (long chunks), 1: the second (short)
+        ing = DeviceIngest(ConfigFile.new(2, oracle.DEFAULT_POLY), Key(bytes(range(64))))
+        orig = ing._process
+        calls = [0]
+
+        def bad(torch_, arena_ptr, sel, c_offs, c_lens, frames, staging, s_off0, stream,
+                _orig=orig, _calls=calls, _which=which):
+            r = _orig(torch_, arena_ptr, sel, c_offs, c_lens, frames, staging, s_off0, stream)
+            if _calls[0] == _which:
+                so = int(r[0][len(r[0]) // 2])
+                with torch.cuda.stream(torch.cuda.ExternalStream(stream)):
+                    staging[so + 40] ^= 0x5A  # inside the ciphertext
+            _calls[0] += 1
+            return r
+        monkeypatch.setattr(ing, "_process", bad)
+        with pytest.raises(RusticError) as ei:
+            ing.ingest(arena, offs, lens, finalize=True)
+        assert ei.value.kind == ErrorKind.Verification
+        assert calls[0] > which
+
+
+def test_pack_build_raw_multi_matches_single_source(gpu_ctx):
+    """rcdc_pack_build_raw_multi over blobs split across two buffers (odd
+    offsets) gives the bytes rcdc_pack_build_raw gives from one buffer."""
+    import torch
+    from rustic_core_amd.pack import (build_packs, build_packs_multi, copy_ranges, make_blobs,
+                                      pack_layout)
+    rng = np.random.default_rng(5)
+    key = rng.integers(0, 256, 64, dtype=np.uint8).tobytes()
+    lens = [int(x) for x in rng.integers(32, 300_000, 12)] + [32, 33, (1 << 20) + 77]
+    n = len(lens)
+    offs = np.cumsum([0] + [x + 5 for x in lens[:-1]]).astype(np.uint64)
+    total_in = int(offs[-1]) + lens[-1] + 64
+    one = torch.from_numpy(rng.integers(0, 256, total_in, dtype=np.uint8)).to("cuda:0")
+    # the same bytes spread over two buffers: odd blobs in the second, shifted by 3
+    two = torch.zeros(total_in + 64, dtype=torch.uint8, device="cuda:0")
+    src = np.arange(n) % 2
+    offs2 = np.where(src == 1, offs + 3, offs).astype(np.uint64)
+    copy_ranges(gpu_ctx, [one.data_ptr()], np.zeros(n, np.uint32), offs[src == 1],
+                np.asarray(lens, np.uint64)[src == 1], offs2[src == 1], two.data_ptr())
+    ids = rng.integers(0, 256, (n, 32), dtype=np.uint8)
+    ulen = [x * 2 if i % 4 == 0 else 0 for i, x in enumerate(lens)]
+    groups, hn = [(0, 5), (5, 9), (14, 1)], rng.integers(0, 256, (3, 16), dtype=np.uint8)
+    b1 = make_blobs(offs, lens, ids, np.zeros((n, 16), np.uint8), uncompressed=ulen)
+    p1, total = pack_layout(b1, groups, hn, align=7, raw=True)
+    out1 = torch.zeros(total + 64, dtype=torch.uint8, device="cuda:0")
+    o1 = build_packs(gpu_ctx, key, one.data_ptr(), b1, p1, out1.data_ptr(), total, raw=True)
+    b2 = make_blobs(offs2, lens, ids, np.zeros((n, 16), np.uint8), uncompressed=ulen)
+    b2["pad"] = src
+    p2, _ = pack_layout(b2, groups, hn, align=7, raw=True)
+    out2 = torch.full((total + 64,), 9, dtype=torch.uint8, device="cuda:0")
+    o2 = build_packs_multi(gpu_ctx, key, [one.data_ptr(), two.data_ptr()], b2, p2,
+                           out2.data_ptr(), total)
+    torch.cuda.synchronize()
+    assert np.array_equal(o1, o2) and np.array_equal(p1["size"], p2["size"])
+    a, b = out1.cpu().numpy(), out2.cpu().numpy()
+    for p in p1:
+        s, m = int(p["out_off"]), int(p["size"])
+        assert np.array_equal(a[s:s + m], b[s:s + m])
+    b2["pad"][3] = 2  # no third buffer
+    from rustic_core_amd.errors import RusticError
+    with pytest.raises(RusticError):
+        build_packs_multi(gpu_ctx, key, [one.data_ptr(), two.data_ptr()], b2, p2,
+                          out2.data_ptr(), total)

@@ -83,3 +83,34 @@ def test_group_blobs():
     g = group_blobs([968] * 3, s)
     assert g == [(0, 1), (1, 2)]
     assert s.current_size == (1000 + 37 + 36) + (2000 + 2 * 37 + 36)
+
+
+def test_group_blobs_open_matches_one_packer():
+    """A packer that stays open between calls (packer.rs:659-671, 749-750)
+    closes the same packs as one pass over all blobs: feed the blob lengths
+    in several calls, carrying the open pack's blobs into the next call, and
+    finalize at the end (one undersized pack per call before)."""
+    import numpy as np
+    from rustic_core_amd.pack import MAX_COUNT, PackSizer, group_blobs, group_blobs_open
+    rng = np.random.default_rng(7)
+    lens = [int(x) for x in rng.integers(1, 9000, 3000)]
+    ulen = [int(x) if rng.random() < 0.5 else 0 for x in rng.integers(1, 20000, 3000)]
+    one = group_blobs(lens, PackSizer(50_000, 8, 400_000, 0, 30, 200), ulen)
+    sizer = PackSizer(50_000, 8, 400_000, 0, 30, 200)
+    got, carry = [], []  # carry: indices of the open pack's blobs
+    cuts = [0, 1, 17, 400, 401, 1500, 2999, 3000]
+    for a, b in zip(cuts[:-1], cuts[1:]):
+        idx = carry + list(range(a, b))
+        last = b == cuts[-1]
+        closed, open_from = group_blobs_open([lens[i] for i in idx], sizer,
+                                             [ulen[i] for i in idx], finalize=last)
+        got += [(idx[b0], n) for b0, n in closed]
+        carry = idx[open_from:]
+    assert not carry
+    assert got == one
+    assert sizer.current_size == PackSizer(50_000, 8, 400_000, 0, 30, 200).current_size + sum(
+        sum(lens[b0:b0 + n]) + 32 * n + sum(41 if ulen[i] else 37 for i in range(b0, b0 + n))
+        + 36 for b0, n in one)
+    # the count rule closes a pack without finalize
+    closed, open_from = group_blobs_open([1] * (MAX_COUNT + 5), PackSizer.fixed(1 << 30))
+    assert closed == [(0, MAX_COUNT)] and open_from == MAX_COUNT

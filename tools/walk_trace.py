@@ -1,7 +1,8 @@
 """Per-piece trace of rcdc_walk_kernel (RCDC_WALK_TRACE=1): where the walk's
 time goes on C3-shaped (mixed) and all-random 64 x 1 GiB batches.
 
-usage: python tools/walk_trace.py [mixed|random|both] [streams] [GiB per stream]
+usage: python tools/walk_trace.py [mixed|random|both|c4] [streams] [GiB per stream]
+(c4: bench.py's C4 files -- `streams` files, log-uniform 4-256 MiB, random bytes)
 Prints per batch: walk/chain time (HIP events), work counters, wave-slot
 utilisation (sum of piece durations / (4096 wave slots x makespan)), the
 active-piece timeline (how long fewer than 1024 / 256 pieces were in flight:
@@ -30,8 +31,16 @@ def run(kind, nstreams, sgib):
     dev = torch.device("cuda", 0)
     sb = int(sgib * GiB)
     lens = np.full(nstreams, sb, np.uint64)
+    if kind == "c4":  # bench.py C4: the first `nstreams` files, log-uniform 4-256 MiB
+        from bench import c4_fill, c4_files
+        sizes = c4_files(nstreams)
+        files = sorted(range(nstreams), key=lambda f: -sizes[f])
+        lens = np.array([sizes[f] for f in files], np.uint64)
     offs, alen = pack_offsets(lens)
-    if kind == "random":
+    if kind == "c4":
+        arena = torch.empty(alen, dtype=torch.uint8, device=dev)
+        c4_fill(torch, arena, offs, files, sizes, dev)
+    elif kind == "random":
         g = torch.Generator(device=dev)
         g.manual_seed(5)
         arena = torch.randint(0, 256, (alen,), dtype=torch.uint8, device=dev, generator=g)
