@@ -359,3 +359,59 @@ def test_pack_build_raw_multi_matches_single_source(gpu_ctx):
     with pytest.raises(RusticError):
         build_packs_multi(gpu_ctx, key, [one.data_ptr(), two.data_ptr()], b2, p2,
                           out2.data_ptr(), total)
+
+
+def test_host_ingest_files_to_packs_and_pack_ids():
+    """HostIngest: files in host memory -> pack files and
+    pack ids in host memory, in several pipelined batches (begin(k + 1)
+    before end(k), three arena slots, D2H + host hashing).  Every cut against
+    the oracle, every pack id against hashlib, every pack parsed and every
+    blob opened by the oracle and decoded by libzstd back to the new chunks
+    in order, and the pack grouping of one packer over all batches."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from rustic_core_amd.chunker import ConfigFile
+    from rustic_core_amd.crypto import Key
+    from rustic_core_amd.ingest import HostIngest
+    from rustic_core_amd.pack import PackSizer, group_blobs
+    key = bytes(range(5, 69))
+    datas = _streams(seed=13, n=8)
+    files = [torch.from_numpy(np.frombuffer(d, np.uint8).copy()).pin_memory() for d in datas]
+    hi = HostIngest(ConfigFile.new(2, oracle.DEFAULT_POLY), Key(key), hash_threads=4,
+                    first_batch=40 * MiB, batch=70 * MiB, last_batch=30 * MiB)
+    hi.ingest.sizer = PackSizer.fixed(16 * MiB)
+    res = hi.run(files)
+    assert len(res.batch_files) >= 3
+    assert res.h2d_bytes == sum(len(d) for d in datas)
+    chunks = []
+    for r, b in zip(res.batches, res.batch_files):
+        for i, got in zip(b, r.cuts):
+            exp = oracle.chunk_cuts(np.frombuffer(datas[i], np.uint8))
+            assert np.array_equal(got, exp)
+            prev = 0
+            for c in exp:
+                chunks.append(datas[i][prev:int(c)])
+                prev = int(c)
+    seen, new_chunks = set(), []
+    for c in chunks:
+        h = hashlib.sha256(c).digest()
+        if h not in seen:
+            seen.add(h)
+            new_chunks.append(c)
+    got, sealed, ulens = [], [], []
+    for k in range(len(res.pack_ids)):
+        f = res.pack_file(k)
+        assert hashlib.sha256(f).digest() == res.pack_ids[k]
+        for tpe, off, ln, ulen, bid in oracle.parse_pack(key, f):
+            data = zr.decompress(oracle.open_(key, f[off:off + ln]))
+            assert hashlib.sha256(data).digest() == bytes(bid) and ulen == len(data)
+            got.append(data)
+            sealed.append(ln)
+            ulens.append(ulen)
+    assert got == new_chunks
+    assert res.d2h_bytes == int(sum(res.pack_sizes))
+    one = group_blobs([x - 32 for x in sealed], PackSizer.fixed(16 * MiB), ulens)
+    sizes = [int(p["nblobs"]) for r in res.batches for p in r.pack_table]
+    assert sizes == [n for _, n in one]
+    hi.close()

@@ -56,3 +56,17 @@ def test_config_zstd_and_verify():
     assert ConfigFile.new(1, 0x3DA3358B4DC173).zstd() is None
     with pytest.raises(RusticError):
         ConfigFile.new(3, 0x3DA3358B4DC173).zstd()
+
+
+def test_plan_batches():
+    """HostIngest batches: whole files in order; a small first and last batch
+    around middle ones of about `middle` bytes."""
+    from rustic_core_amd.ingest import plan_batches
+    G = 1 << 30
+    b = plan_batches([G] * 96, 4 * G, 16 * G, 4 * G)
+    assert [len(x) for x in b][0] == 4 and [len(x) for x in b][-1] == 4
+    assert sum(b, []) == list(range(96))
+    assert all(len(x) <= 16 for x in b)
+    assert plan_batches([G] * 3, 4 * G, 16 * G, 4 * G) == [[0, 1, 2]]
+    b = plan_batches([5 << 20] * 7 + [300 << 20], 10 << 20, 20 << 20, 10 << 20)
+    assert sum(b, []) == list(range(8)) and b[-1] == [7]
