@@ -279,7 +279,7 @@ def test_ingest_calls_keep_the_pack_open():
     one = group_blobs([int(x) - 32 for x in sealed], PackSizer.fixed(24 * MiB),
                       [int(x) for x in ulens])
     assert sizes == [n for _, n in one]
-    assert len(sizes) > len(results)  # packs closed by size inside calls
+    assert sum(len(r.pack_table) for r in results[:-1]) >= 1  # closed inside a call
 
 
 def test_ingest_rejects_a_corrupted_blob(monkeypatch):

@@ -18,6 +18,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from oracle import oracle  # noqa: E402
 
 MIN, MAX = 512 << 10, 8 << 20
+SCHED = []  # per-lane segment of a search's first rounds (--sched), then --seg
 
 
 def mixed(seed, n):
@@ -96,10 +97,13 @@ def walk_piece(data, N, a, e, S, adaptive, hitpos):
         limit = min(s + MAX, N)
         end = min(limit, stop_scan)
         if c < end and c < limit:  # a hit inside the searched range
-            span = c - A  # positions A+1 .. c: the round holding c completes
-            step = 64 * S
-            r = (c - A - 1) // step + 1
-            b = r * 64 * (S + 64)
+            # rounds of SCHED[0], SCHED[1], ... then S bytes per lane
+            pos, b, r = A, 0, 0
+            while pos < c:
+                sg = SCHED[r] if r < len(SCHED) else S
+                pos += 64 * sg
+                b += 64 * (sg + 64)
+                r += 1
             lane += b
             ideal += c - q + 1
             waste_hit += b - (c - A) - r * 64 * 64
@@ -126,12 +130,16 @@ def main():
     ap.add_argument("--adaptive", action="store_true")
     ap.add_argument("--piece-mib", type=int, default=4)
     ap.add_argument("--split", type=int, default=20)
+    ap.add_argument("--random", action="store_true", help="uniform random bytes (C4's files)")
+    ap.add_argument("--sched", default="", help="comma list: segment of a search's first rounds")
     a = ap.parse_args()
+    SCHED[:] = [int(x) for x in a.sched.split(",") if x]
     tot = {"lane": 0, "ideal_search": 0, "zones": 0, "waste_hit": 0, "waste_open": 0,
            "ref_hashed": 0, "warm": 0, "pieces": 0, "open": 0, "true_lane": 0}
     for j in range(a.streams):
         N = a.mib << 20
-        data = mixed(3000 + j, N)
+        data = (np.random.default_rng(4000 + j).integers(0, 256, N, dtype=np.uint8)
+                if a.random else mixed(3000 + j, N))
         true = oracle.chunk_cuts(data).astype(np.int64)
         L = np.diff(np.concatenate([[0], true]))
         tot["ref_hashed"] += int(np.sum(L[L >= MIN] - MIN)) + 63 * int(np.count_nonzero(L >= MIN))
