@@ -333,7 +333,7 @@ def test_pack_build_raw_multi_matches_single_source(gpu_ctx):
     two = torch.zeros(total_in + 64, dtype=torch.uint8, device="cuda:0")
     src = np.arange(n) % 2
     offs2 = np.where(src == 1, offs + 3, offs).astype(np.uint64)
-    copy_ranges(gpu_ctx, [one.data_ptr()], np.zeros(n, np.uint32), offs[src == 1],
+    copy_ranges(gpu_ctx, [one.data_ptr()], np.zeros(int((src == 1).sum()), np.uint32), offs[src == 1],
                 np.asarray(lens, np.uint64)[src == 1], offs2[src == 1], two.data_ptr())
     ids = rng.integers(0, 256, (n, 32), dtype=np.uint8)
     ulen = [x * 2 if i % 4 == 0 else 0 for i, x in enumerate(lens)]
