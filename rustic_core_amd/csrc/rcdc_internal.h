@@ -137,7 +137,8 @@ struct WalkParams {
     const uint32_t *order_in;
     uint32_t *order_out;
     uint32_t nbig_units;   // order_in[0, nbig_units) are big pieces
-    uint32_t helpers;      // idle walk waves hash rounds ahead for the busy ones
+    uint32_t helpers;      // idle walk waves hash rounds ahead for the busy ones: at
+                           // most this many per round of the walker's own (0 = off)
     uint64_t chk_budget;   // bytes of gap hashing a boundary check may do before
                            // it hands the boundary to the fixup kernel
 };

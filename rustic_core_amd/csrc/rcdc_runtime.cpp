@@ -677,8 +677,10 @@ rcdc_status plan_build(rcdc_ctx *ctx, rcdc_plan *pl, const uint64_t *offs, const
     wp.shift = (uint32_t)(ctx->deg - 8);
     wp.nunits = (uint32_t)pl->wunits.size();
     // the walk's tail: waves without a piece hash rounds for the busy ones
-    wp.helpers = 1;
-    if (const char *e = getenv("RCDC_WALK_HELP")) wp.helpers = atoi(e) != 0;
+    // (up to wp.helpers rounds posted per round of the walker's own, <= 15)
+    wp.helpers = 7;
+    if (const char *e = getenv("RCDC_WALK_HELPMAX")) wp.helpers = (uint32_t)std::min(std::max(atoi(e), 1), 15);
+    if (const char *e = getenv("RCDC_WALK_HELP"); e && atoi(e) == 0) wp.helpers = 0;
     // a fixup walks until it meets a piece's chain: a few chunks, longer only
     // through phase-shifted zero runs (min-sized chunks); more -> host redo
     wp.fix_cap = (uint32_t)(4 * (Lp ? Lp : 1) / ctx->min + ctx->max / ctx->min + 64);

@@ -190,8 +190,9 @@ struct Walk {
     uint64_t lbytes;
     // walk kernel: the workgroup's round ring (nullptr elsewhere); a walker
     // posts rounds ahead of its search there while waves of its workgroup
-    // are idle (the walk's tail), `wv` is its wave index
+    // are idle (the walk's tail), at most help_max per round of its own
     GapQueue *Q;
+    uint32_t help_max;
 };
 
 // Segment of a round that starts at A and only needs positions below end:
@@ -355,7 +356,7 @@ __device__ void gap_run(GapQueue &Q, Walk &W, uint32_t sl, uint64_t &rounds, uin
 // none itself: one copy of the round loop per wave role keeps the walk
 // kernel spill-free).  Rounds past a hit are wasted, but only on waves that
 // would idle.
-constexpr uint32_t kHelpMax = 7;  // x 16 walkers <= kGapSlots
+constexpr uint32_t kHelpMax = 15;  // WalkParams.helpers <= kHelpMax; x 16 walkers <= kGapSlots
 
 __device__ void walk_post(Walk &W, uint64_t A, uint64_t q, uint64_t end, uint32_t K) {
     GapQueue &Q = *W.Q;
@@ -444,7 +445,7 @@ __device__ uint64_t walk_next(Walk &W, uint64_t pos, uint64_t stop_scan, uint64_
                 const uint32_t idle = __builtin_amdgcn_readfirstlane(lds_load(&W.Q->idle));
                 if (idle) {
                     const uint64_t step = 64ull * W.S, R = (end - A + step - 1) / step;
-                    K = (uint32_t)min((uint64_t)min(idle, kHelpMax), R - 1);
+                    K = (uint32_t)min((uint64_t)min(idle, W.help_max), R - 1);
                     if (K) walk_post(W, A, q, end, K);
                 }
             }
@@ -531,6 +532,7 @@ __global__ __launch_bounds__(1024, 1) void rcdc_walk_kernel(
     W.wave = 0;  // a wave walker: lane t of the round is t
     W.tid = lane;
     W.Q = prm.helpers ? &s_q : nullptr;
+    W.help_max = __builtin_amdgcn_readfirstlane(min(prm.helpers, kHelpMax));
     uint64_t help_rounds = 0, help_bytes = 0;  // rounds this wave ran for others
     for (;;) {
         uint32_t q = 0;
@@ -913,6 +915,7 @@ __global__ __launch_bounds__(CT, 1) void rcdc_walk_check_kernel(
     W.wave = 0;
     W.tid = lane;
     W.Q = nullptr;
+    W.help_max = 0;
     const ModRepl mod{s_tab, W.k.lwm};
     const uint64_t mn = prm.min_size, mx = prm.max_size;
     for (;;) {
@@ -1138,6 +1141,7 @@ __global__ __launch_bounds__(1024, 1) void rcdc_walk_fixup_kernel(
     W.wave = wave;
     W.tid = threadIdx.x;
     W.Q = nullptr;
+    W.help_max = 0;
     for (uint32_t idx = blockIdx.x; idx < nfix; idx += gridDim.x) {
         const uint32_t u = fixlist[idx];
         const WalkUnit U = units[u];

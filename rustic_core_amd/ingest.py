@@ -175,6 +175,12 @@ class DeviceIngest:
         self.indexed = indexed if indexed is not None else set()
         self._plan = None
         self._layout = None
+        # two sets of (short ids, long ids, processing) streams, alternating
+        # per begin(): a batch in flight next to the previous one gets its own
+        # queues (its long ids do not wait behind the previous batch's), and
+        # the caching allocator reuses each set's blocks (it pools per stream)
+        self._streams = None
+        self._nbegin = 0
         # the open pack (blobs added, pack not yet saved): its sealed blobs in
         # a device buffer of their own, PACK_BLOB rows with pad = _SRC_CARRY
         self._carry = None
@@ -240,7 +246,14 @@ class DeviceIngest:
         the caller's current stream.  ``end(begin(...))``."""
         return self.end(self.begin(arena, offs, lens), finalize)
 
-    def begin(self, arena, offs, lens) -> "_Pending":
+    def _stream_set(self, torch, dev):
+        if self._streams is None:
+            self._streams = [tuple(torch.cuda.Stream(dev) for _ in range(3)) for _ in range(2)]
+        st = self._streams[self._nbegin % 2]
+        self._nbegin += 1
+        return st
+
+    def begin(self, arena, offs, lens, plan: Optional[DevicePlan] = None) -> "_Pending":
         """First half of ``ingest``: chunk, launch every chunk's blob id and
         compress + seal + verify the long chunks speculatively.  The long ids
         (the SHA-256 latency floor) are still running on return, so a caller
@@ -253,10 +266,11 @@ class DeviceIngest:
         t0 = time.perf_counter()
         ms = {}
         s_main = torch.cuda.current_stream(dev)
-        s_short, s_long, s_proc = (torch.cuda.Stream(dev) for _ in range(3))
+        s_short, s_long, s_proc = self._stream_set(torch, dev)
         ptr = arena.data_ptr()
-        # 1. chunk
-        plan = self._plan_for(offs, lens, arena.numel())
+        # 1. chunk (a plan built for this layout beforehand, or the cached one)
+        if plan is None:
+            plan = self._plan_for(offs, lens, arena.numel())
         plan.run(ptr, s_main.cuda_stream)
         cuts = plan.results()
         c_offs, c_lens = [], []
@@ -550,7 +564,7 @@ class HostIngest:
         lock = threading.Lock()
         ids_out, offs_out, sizes_out, futs, keep = [], [], [], [], []
         state = {"host_off": 0, "d2h": 0, "host": host}
-        ms = {"begin": 0.0, "end": 0.0, "handoff": 0.0}
+        ms = {"begin": 0.0, "end": 0.0, "handoff": 0.0}  # host wall ms per step
 
         def h2d(k):
             offs, _ = layouts[k]
@@ -606,17 +620,26 @@ class HostIngest:
         t0 = time.perf_counter()
         for k in range(min(len(arenas), len(batches))):
             h2d(k)
+        # the batches' chunking plans (work lists and cut buffers: building one
+        # allocates device memory, so none is built inside the pipeline)
+        plans = [DevicePlan(self.ingest.ctx, offs, [sizes[i] for i in b], slot_len)
+                 for b, (offs, _) in zip(batches, layouts)]
+        ms["plans"] = (time.perf_counter() - t0) * 1e3
         results, pending = [], None
         for k in range(len(batches)):
             torch.cuda.current_stream(dev).wait_event(ev_h2d[k])
             offs, _ = layouts[k]
             t = time.perf_counter()
-            p = self.ingest.begin(arenas[k % len(arenas)], offs, [sizes[i] for i in batches[k]])
+            p = self.ingest.begin(arenas[k % len(arenas)], offs, [sizes[i] for i in batches[k]],
+                                  plan=plans[k])
             ms["begin"] += (time.perf_counter() - t) * 1e3
+            ms[f"begin{k}"] = (time.perf_counter() - t) * 1e3
             if pending is not None:
                 t = time.perf_counter()
                 r = self.ingest.end(pending)
                 ms["end"] += (time.perf_counter() - t) * 1e3
+                ms[f"end{k - 1}"] = (time.perf_counter() - t) * 1e3
+                ms[f"at{k - 1}"] = (time.perf_counter() - t0) * 1e3
                 handoff(r)
                 results.append(r)
                 # the slot of batch k - 1 is free: batch k + 2 goes there
@@ -628,11 +651,16 @@ class HostIngest:
         ms["end"] += (time.perf_counter() - t) * 1e3
         handoff(r)
         results.append(r)
+        ms["last_end"] = (time.perf_counter() - t0) * 1e3
         for f in futs:  # the per-batch waiters, then their pack jobs
             for g in f.result():
                 g.result()
         seconds = time.perf_counter() - t0
         pool.shutdown()
+        for pl in plans:
+            pl.close()
+        for r in results:  # per-phase times of each batch
+            ms.setdefault("batch_ms", []).append({k: round(v, 1) for k, v in r.ms.items()})
         keep.clear()
         del arenas
         return HostIngestResult(state["host"], np.asarray(offs_out, np.int64),

@@ -200,6 +200,7 @@ def main():
     ap.add_argument("--last-gib", type=float, default=4)
     ap.add_argument("--hash-threads", type=int, default=None)
     ap.add_argument("--open-packs", type=int, default=3)
+    ap.add_argument("--repeat", type=int, default=1, help="timed runs (fresh repository each)")
     ap.add_argument("--no-checks", action="store_true")
     ap.add_argument("--json", default=None)
     a = ap.parse_args()
@@ -213,9 +214,12 @@ def main():
     kw = dict(first_batch=int(a.first_gib * GiB), batch=int(a.batch_gib * GiB),
               last_batch=int(a.last_gib * GiB), hash_threads=a.hash_threads)
     # warm-up: contexts, plans, kernels, pinned pools (a small run, its own repository)
+    # (one batch as large as the run's largest, so the context's device
+    # scratch -- zstd, AEAD, frame check -- is sized before the timed run)
     w = HostIngest(cfg, Key(key), **kw)
-    w.first_batch = w.batch = w.last_batch = 2 * nbytes
-    w.run(files[:4])
+    nw = min(len(files), int(a.batch_gib * GiB) // nbytes + 1)
+    w.first_batch = w.batch = w.last_batch = nw * nbytes
+    w.run(files[:nw])
     w.close()
     del w
     torch.cuda.synchronize(dev)
@@ -248,7 +252,7 @@ def main():
         "frac_of_bound": round(bound_s / res.seconds, 3),
         "batches": [len(b) for b in res.batch_files],
         "hash_threads": hi.hash_threads,
-        "host_ms": {k: round(v, 1) for k, v in res.ms.items()},
+        "host_ms": {k: (round(v, 1) if isinstance(v, float) else v) for k, v in res.ms.items()},
         "packs": len(res.pack_ids),
         "data": f"{a.files} x {a.file_gib:g} GiB C3-style mixed streams (bench.py make_mixed, "
                 "seed 3000 + j) in pinned host memory; repository version 2 (zstd level 3), "
