@@ -14,6 +14,9 @@ fi
 if [ -n "$C4" ]; then
   NOTRACE=$NOTRACE bash tools/gpu_c4.sh $OUT/c4 $C4SWEEP || exit 1
 fi
+if [ -n "$C3SWEEP" ]; then
+  BENCH_ARGS="--no-ingest $C3ARGS" bash tools/gpu_sweep.sh $OUT/c3 $C3SWEEP || exit 1
+fi
 if [ -n "$ABI" ]; then
   timeout -k 10 300 ./tools/abi_e2e --threads 16 --files 64 --file-mib 256 --batch --mixed > gpurun_out/$OUT/abi_e2e.json 2> gpurun_out/$OUT/abi_e2e.err || { tail gpurun_out/$OUT/abi_e2e.err; exit 1; }
   cat gpurun_out/$OUT/abi_e2e.json
