@@ -519,7 +519,13 @@ class HostIngest:
       - pack ids on ``hash_threads`` host threads (hashlib: OpenSSL SHA-256,
         the GIL released), each pack as soon as its batch's copy is done.
     The packer stays open across batches (one pack sequence, as one Packer
-    per backup) and the last batch finalizes it."""
+    per backup) and the last batch finalizes it.
+
+    The process should give HIP more hardware queues than its default 4
+    (environment GPU_MAX_HW_QUEUES, e.g. 16, before the first HIP call): HIP
+    maps streams onto them round robin, and a kernel queued behind a
+    multi-GiB copy on a shared queue waits for that copy (the short ids of
+    one batch waited ~0.3 s behind the next batch's H2D with 4 queues)."""
 
     def __init__(self, config: ConfigFile, key: Key, device: int = 0,
                  indexed: Optional[set] = None, extra_verify: Optional[bool] = None,
@@ -618,13 +624,14 @@ class HostIngest:
 
         torch.cuda.synchronize(dev)
         t0 = time.perf_counter()
-        for k in range(min(len(arenas), len(batches))):
-            h2d(k)
-        # the batches' chunking plans (work lists and cut buffers: building one
-        # allocates device memory, so none is built inside the pipeline)
+        # the batches' chunking plans first (work lists and cut buffers:
+        # building one allocates device memory and uploads synchronously, so
+        # none is built inside the pipeline or behind the queued copies)
         plans = [DevicePlan(self.ingest.ctx, offs, [sizes[i] for i in b], slot_len)
                  for b, (offs, _) in zip(batches, layouts)]
         ms["plans"] = (time.perf_counter() - t0) * 1e3
+        for k in range(min(len(arenas), len(batches))):
+            h2d(k)
         results, pending = [], None
         for k in range(len(batches)):
             torch.cuda.current_stream(dev).wait_event(ev_h2d[k])

@@ -73,52 +73,52 @@ static double h2d_rate(bool pinned, uint64_t bytes) {
 }
 
 // The bound of the ABI paths under the same concurrency:
-// `threads` workers take the same files in the same `rd`-byte reads as the
-// stream workers and only copy them to the device, each on its own HIP
-// stream.  staged = false: hipMemcpyAsync straight from the pageable file
-// bytes (the runtime stages them); staged = true: what an rcdc lane does --
-// memcpy into one of two pinned slots, then an async DMA from it, the memcpy
-// of read k + 1 overlapping the DMA of read k.  Returns GiB/s.
-// mode 0: hipMemcpyAsync straight from the pageable file bytes; 1: staged
-// (memcpy into one of two pinned slots, then DMA, as an rcdc lane); 2: DMA
-// only, from pinned slots filled once (the link's own limit at this
-// concurrency, no host copy).
+// `threads` workers take the same files and only copy them to the device,
+// each on its own HIP stream.  mode 0: hipMemcpyAsync of each `rd`-byte read
+// straight from the pageable file bytes (the runtime stages them); 1: what an
+// rcdc lane does -- 4 MiB blocks memcpy'd into one of 4 pinned slots, then an
+// async DMA from it, the copies running ahead of the DMA (run_host_pieces,
+// kStageBytes / stage_slots); 2: the same DMA pattern from pinned slots
+// filled once (the link's own limit at this concurrency, no host copy).
+// Returns GiB/s.
 static double h2d_concurrent(const std::vector<uint8_t *> &data, uint64_t n, uint64_t rd,
                              int threads, int mode) {
-    const bool staged = mode >= 1;
+    constexpr int kSlots = 4;
+    const uint64_t blk = mode == 0 ? rd : (4ull << 20);
     std::atomic<int> next{0};
     std::atomic<int> bad{0};
     auto work = [&]() {
         hipStream_t s;
-        void *d[2] = {nullptr, nullptr};
-        void *h[2] = {nullptr, nullptr};
-        hipEvent_t ev[2];
+        void *d = nullptr;
+        void *h[kSlots] = {};
+        hipEvent_t ev[kSlots];
         if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) { bad++; return; }
-        for (int k = 0; k < 2; k++) {
-            if (hipMalloc(&d[k], rd) != hipSuccess) bad++;
-            if (staged && hipHostMalloc(&h[k], rd, hipHostMallocDefault) != hipSuccess) bad++;
+        if (hipMalloc(&d, n) != hipSuccess) bad++;
+        for (int k = 0; k < kSlots; k++) {
+            if (mode && hipHostMalloc(&h[k], blk, hipHostMallocDefault) != hipSuccess) bad++;
+            if (mode == 2 && h[k]) memset(h[k], 1, blk);
             (void)hipEventCreateWithFlags(&ev[k], hipEventDisableTiming);
         }
         uint64_t k = 0;
         for (;;) {
             const int f = next++;
             if (f >= (int)data.size() || bad) break;
-            for (uint64_t o = 0; o < n; o += rd, k++) {
-                const uint64_t len = std::min(rd, n - o);
-                const int b = (int)(k & 1);
-                if (staged) {
-                    (void)hipEventSynchronize(ev[b]);  // slot b's previous DMA is done
-                    if (mode == 1 || k < 2) memcpy(h[b], data[f] + o, len);
-                    (void)hipMemcpyAsync(d[b], h[b], len, hipMemcpyHostToDevice, s);
+            for (uint64_t o = 0; o < n; o += blk, k++) {
+                const uint64_t len = std::min(blk, n - o);
+                const int b = (int)(k % kSlots);
+                if (mode) {
+                    if (k >= (uint64_t)kSlots) (void)hipEventSynchronize(ev[b]);  // slot free
+                    if (mode == 1) memcpy(h[b], data[f] + o, len);
+                    (void)hipMemcpyAsync((uint8_t *)d + o, h[b], len, hipMemcpyHostToDevice, s);
                 } else {
-                    (void)hipMemcpyAsync(d[b], data[f] + o, len, hipMemcpyHostToDevice, s);
+                    (void)hipMemcpyAsync((uint8_t *)d + o, data[f] + o, len, hipMemcpyHostToDevice, s);
                 }
                 (void)hipEventRecord(ev[b], s);
             }
         }
         (void)hipStreamSynchronize(s);
-        for (int j = 0; j < 2; j++) {
-            (void)hipFree(d[j]);
+        (void)hipFree(d);
+        for (int j = 0; j < kSlots; j++) {
             if (h[j]) (void)hipHostFree(h[j]);
             (void)hipEventDestroy(ev[j]);
         }

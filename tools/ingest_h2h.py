@@ -30,7 +30,13 @@ import time
 from concurrent.futures import ThreadPoolExecutor
 
 import numpy as np
-import torch
+
+# more hardware queues than HIP's default 4 before anything initialises HIP:
+# the pipeline's copy streams must not share a queue with its kernels
+# (HostIngest docstring); GPU_MAX_HW_QUEUES=4 in the environment reproduces
+# the shared-queue stall
+os.environ.setdefault("GPU_MAX_HW_QUEUES", "16")
+import torch  # noqa: E402
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
@@ -252,6 +258,7 @@ def main():
         "frac_of_bound": round(bound_s / res.seconds, 3),
         "batches": [len(b) for b in res.batch_files],
         "hash_threads": hi.hash_threads,
+        "gpu_max_hw_queues": os.environ.get("GPU_MAX_HW_QUEUES"),
         "host_ms": {k: (round(v, 1) if isinstance(v, float) else v) for k, v in res.ms.items()},
         "packs": len(res.pack_ids),
         "data": f"{a.files} x {a.file_gib:g} GiB C3-style mixed streams (bench.py make_mixed, "
