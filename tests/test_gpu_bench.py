@@ -31,3 +31,38 @@ def test_bench_two_ranks_gloo(gpu_ctx):
     assert line["parity"]["mismatches"] == 0
     assert line["parity"]["streams_checked"] == 1024
     assert line["value"] > 0 and line["scaling"] == "weak"
+
+
+def _two_ranks(args):
+    env = dict(os.environ, RCDC_BENCH_BACKEND="gloo")
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2"] + args +
+                       ["--warmup", "1", "--prewarm", "0", "--no-cpu-baseline"],
+                       capture_output=True, text=True, timeout=600, env=env, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-3000:]
+    line = json.loads(lines[0])
+    assert line["n_gpus"] == 2 and line["value"] > 0
+    return line
+
+
+def test_bench_two_ranks_c4(gpu_ctx):
+    """C4 over two ranks: LPT shares of 256 files (~7.5
+    GiB per rank: walked), one resident batch per rank, pipelined passes, the
+    parity counts of the 64-file sample summed over the ranks (all_reduce) --
+    the path of the driver's 8-GPU C4 run."""
+    line = _two_ranks(["--workload", "C4", "--c4-files", "256", "--steps", "2"])
+    assert line["parity"]["files_checked"] == 64
+    assert line["parity"]["mismatches"] == 0
+    assert line["roofline"]["pipelined"] is True
+
+
+def test_bench_two_ranks_c5(gpu_ctx):
+    """C5 over two ranks: one 512 MiB zero stream sliced with max + 64 halos,
+    the cross-rank stitch (all_gather_object of cut lists) inside every
+    timed step; rank 0's cuts against the closed form and the oracle."""
+    line = _two_ranks(["--workload", "C5", "--stream-bytes", str(256 << 20), "--steps", "2"])
+    assert line["parity"]["mismatches"] == 0
+    assert line["parity"]["cuts"] >= (256 << 20) // (512 << 10) - 1
+    assert line["config"]["stream_bytes_total"] == 512 << 20

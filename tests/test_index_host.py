@@ -2,7 +2,7 @@
 indexer.rs:16-191 -- pinned to the reference's own index file (repo-mixed
 fixture, tests/golden/crypto_fixtures.json, decrypted with the oracle).
 
-The device builds the packs (test_gpu_index.py); here the host logic: JSON
+The device builds the packs (test_gpu_ingest.py, test_gpu_pack.py); here the host logic: JSON
 shape and field order (serde_json::to_vec of the structs), parse of the
 fixture, the IndexPack of the fixture pack from its pack-file index, the
 Indexer's save rule and dedup lookups."""
