@@ -21,7 +21,7 @@ summ $OUT/serial.json serial
 timeout -k 10 300 $B > $OUT/pipe.json 2> $OUT/pipe.err || { tail -20 $OUT/pipe.err; exit 1; }
 summ $OUT/pipe.json pipelined
 if [ -z "$NOTRACE" ]; then
-timeout -k 10 300 python -u tools/walk_trace.py c4 1024 > $OUT/trace.json 2> $OUT/trace.err || { tail -20 $OUT/trace.err; exit 1; }
+WALK_TRACE_NPZ=$OUT/trace timeout -k 10 300 python -u tools/walk_trace.py c4 1024 > $OUT/trace.json 2> $OUT/trace.err || { tail -20 $OUT/trace.err; exit 1; }
 cat $OUT/trace.json
 fi
 i=0

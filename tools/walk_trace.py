@@ -142,6 +142,9 @@ def run(kind, nstreams, sgib):
         "last_piece_start_us": float(a.max()),
     }
     print(json.dumps(out), flush=True)
+    if os.environ.get("WALK_TRACE_NPZ"):  # raw per-piece trace for offline analysis
+        np.savez_compressed(os.environ["WALK_TRACE_NPZ"] + f"_{kind}.npz", trace=tr, check=ct,
+                            lens=np.asarray(lens, np.uint64))
     plan.close()
     del arena
     torch.cuda.empty_cache()
