@@ -14,6 +14,9 @@ fi
 if [ -n "$C4" ]; then
   NOTRACE=$NOTRACE bash tools/gpu_c4.sh $OUT/c4 $C4SWEEP || exit 1
 fi
+if [ -n "$C4PMC" ]; then
+  bash tools/gpu_c4_pmc.sh $OUT/c4pmc || exit 1
+fi
 if [ -n "$C3SWEEP" ]; then
   BENCH_ARGS="--no-ingest $C3ARGS" bash tools/gpu_sweep.sh $OUT/c3 $C3SWEEP || exit 1
 fi

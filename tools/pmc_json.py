@@ -33,7 +33,7 @@ def main():
     r = line["roofline"]
     rd = fetch * 1024 / CAL
     wr = write * 1024
-    lane = r.get("lane_hashed_bytes_per_launch")
+    lane = r.get("lane_hashed_bytes_per_launch") or r.get("lane_hashed_bytes_per_pass")
     out = {
         "kernel": f"{kernel} ({wl})",
         "workload": line["config"]["workload"],
@@ -49,7 +49,8 @@ def main():
         "hbm_bytes_per_launch": int(rd + wr),
         "lane_hashed_bytes_per_launch": lane,
         "read_over_lane_bytes": round(rd / lane, 3) if lane else None,
-        "algorithmic_bytes_per_launch": r.get("algorithmic_bytes_per_launch"),
+        "algorithmic_bytes_per_launch": r.get("algorithmic_bytes_per_launch")
+        or line["config"].get("rank0_share_gib") and int(line["config"]["rank0_share_gib"] * 2**30),
     }
     json.dump(out, open(os.path.join("profiles", f"pmc_{wl}.json"), "w"), indent=1)
     print(json.dumps(out, indent=1))
