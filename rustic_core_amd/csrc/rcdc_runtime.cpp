@@ -609,9 +609,14 @@ rcdc_status plan_build(rcdc_ctx *ctx, rcdc_plan *pl, const uint64_t *offs, const
         // splitting pays only when a wave takes several pieces (the tail is
         // then the last pieces' length); with about one piece per wave slot
         // (C5: 3200 pieces, 4096 slots) it only adds boundaries
+        // a stream of N bytes has round(N / Lp) pieces of Lp, the last one
+        // running to N (0.5 - 1.5 Lp): with floor(N / Lp) a stream just under
+        // 3 Lp ended in a piece of ~2 Lp, the longest job of the queue (C4's
+        // 8-12 MiB files: 8 MiB pieces started last and set the makespan)
+        auto npieces = [Lp](uint64_t N) { return std::max<uint64_t>((N + Lp / 2) / Lp, 1); };
         uint64_t big_total = 0;
         for (uint32_t i = 0; i < n && Lp; i++)
-            if (pl->walked[i]) big_total += std::max<uint64_t>(lens[i] / Lp, 1);
+            if (pl->walked[i]) big_total += npieces(lens[i]);
         const uint64_t slots = (uint64_t)std::max(ctx->num_cus, 1) * 16;
         pl->walk_many = big_total >= 2 * slots;
         uint64_t split_pct = pl->walk_many ? 20 : 0;
@@ -622,7 +627,7 @@ rcdc_status plan_build(rcdc_ctx *ctx, rcdc_plan *pl, const uint64_t *offs, const
         for (uint32_t i = 0; i < n && Lp; i++) {
             if (!pl->walked[i]) continue;
             const uint64_t N = lens[i];
-            const uint64_t P = std::max<uint64_t>(N / Lp, 1);
+            const uint64_t P = npieces(N);
             const uint64_t nsplit = Ls < Lp ? (P * split_pct + 50) / 100 : 0;
             const uint32_t u0 = (uint32_t)pl->wunits.size();
             pl->wstream_u0.push_back(u0);

@@ -1419,15 +1419,15 @@ __global__ __launch_bounds__(kAsmB) void rcdc_walk_assemble_kernel(
 }
 
 // ---------------------------------------------------------------------------
-// Cost-ordered queue.  A piece's walk time is its hashed bytes, and on
-// mixed data most of the variation is how much of it is a zero run (64 B per
-// chunk) rather than random bytes.  One wave per piece samples 64 aligned
-// 8-byte words spread over the piece and counts the non-zero ones (0..64);
-// one workgroup then counting-sorts the queue by that class, big pieces
-// before small ones and heavier before lighter (longest-processing-time
-// first): the last pieces the waves take are the cheap ones.  Only the
-// schedule changes, never the cuts.
-constexpr int kCostKeys = 2 * 65;
+// Cost-ordered queue.  A piece's walk time is its hashed bytes: its length
+// times the share of it that is not zero runs (those cost 64 B per chunk).
+// One wave per piece samples 64 aligned 8-byte words spread over the piece
+// and counts the non-zero ones (0..64); the key is length x that share in
+// units of Lp / 48 (a full random piece of Lp: 48), and one workgroup
+// counting-sorts the queue by it, descending (longest-processing-time first:
+// the last pieces the waves take are the cheap ones; a stream's last piece,
+// up to 1.5 Lp, goes early).  Only the schedule changes, never the cuts.
+constexpr int kCostKeys = 128;
 
 __global__ __launch_bounds__(256) void rcdc_walk_cost_kernel(
     const uint8_t *__restrict__ arena, const StreamDesc *__restrict__ sds,
@@ -1442,7 +1442,9 @@ __global__ __launch_bounds__(256) void rcdc_walk_cost_kernel(
         const uint64_t a = (d.off + U.start + (len * lane) / 64u) & ~7ull;
         const uint64_t w = a + 8 <= d.off + d.n ? *reinterpret_cast<const uint64_t *>(arena + a) : 0;
         const uint32_t cls = (uint32_t)__builtin_popcountll(__ballot(w != 0));
-        if (lane == 0) key[q] = (uint8_t)((q < prm.nbig_units ? 65u : 0u) + cls);
+        const uint64_t quantum = max(prm.piece_bytes / 48, (uint64_t)1);
+        const uint64_t cost = len * cls / 64 / quantum;
+        if (lane == 0) key[q] = (uint8_t)min(cost, (uint64_t)(kCostKeys - 1));
     }
 }
 

@@ -33,9 +33,9 @@ import numpy as np
 
 # more hardware queues than HIP's default 4 before anything initialises HIP:
 # the pipeline's copy streams must not share a queue with its kernels
-# (HostIngest docstring); GPU_MAX_HW_QUEUES=4 in the environment reproduces
-# the shared-queue stall
-os.environ.setdefault("GPU_MAX_HW_QUEUES", "16")
+# (HostIngest docstring); --hw-queues=4 reproduces the shared-queue stall
+_q = [a.split("=", 1)[1] for a in sys.argv if a.startswith("--hw-queues=")]
+os.environ["GPU_MAX_HW_QUEUES"] = _q[0] if _q else "16"  # (the box exports 4)
 import torch  # noqa: E402
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -209,6 +209,8 @@ def main():
     ap.add_argument("--repeat", type=int, default=1, help="timed runs (fresh repository each)")
     ap.add_argument("--no-checks", action="store_true")
     ap.add_argument("--json", default=None)
+    ap.add_argument("--hw-queues", default="16", help="GPU_MAX_HW_QUEUES for this process "
+                    "(set before HIP initialises; --hw-queues=N form)")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     nbytes = int(a.file_gib * GiB)
