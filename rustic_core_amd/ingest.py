@@ -534,17 +534,18 @@ class HostIngest:
                  pack_ratio: float = 0.8):
         self.ingest = DeviceIngest(config, key, device, indexed, extra_verify)
         self.device = device
-        if hash_threads is None:
+        if hash_threads is None:  # the job's CPUs (the main thread mostly waits on the GPU)
             try:
-                hash_threads = max(len(os.sched_getaffinity(0)) - 2, 1)
+                hash_threads = len(os.sched_getaffinity(0))
             except AttributeError:  # pragma: no cover
                 hash_threads = 8
             omp = os.environ.get("OMP_NUM_THREADS", "")
             if omp.isdigit() and int(omp) > 0:
-                hash_threads = min(hash_threads, max(int(omp) - 2, 1))
+                hash_threads = min(hash_threads, int(omp))
         self.hash_threads = int(hash_threads)
         self.first_batch, self.batch, self.last_batch = int(first_batch), int(batch), int(last_batch)
         self.pack_ratio = float(pack_ratio)  # initial pinned pack buffer / input bytes
+        self.d2h_group = 512 << 20  # pack bytes per copy-back event
 
     def run(self, files) -> HostIngestResult:
         """`files`: 1-D uint8 CPU tensors (pinned for full-rate copies)."""
@@ -599,26 +600,39 @@ class HostIngest:
                     big[:o0].copy_(state["host"][:o0])
                     state["host"] = big
                 buf = state["host"]
-                with torch.cuda.stream(s_d2h):
-                    s_d2h.wait_stream(torch.cuda.current_stream(dev))
-                    buf[o0:o0 + total].copy_(res.packs[:total], non_blocking=True)
-                    ev = torch.cuda.Event()
-                    ev.record(s_d2h)
-                keep.append((res.packs, ev))
-                state["host_off"] = o0 + total
-                state["d2h"] += total
-                rows = [(o0 + int(p["out_off"]), int(p["size"])) for p in res.pack_table]
+                rows = [(int(p["out_off"]), int(p["size"])) for p in res.pack_table]
                 base = len(ids_out)
                 ids_out.extend([None] * len(rows))
                 for o, n in rows:
-                    offs_out.append(o)
+                    offs_out.append(o0 + o)
                     sizes_out.append(n)
+                # the copy back in groups of packs of >= d2h_group bytes, one
+                # event each: hashing starts with the first group, not after
+                # the whole batch
+                g0 = 0
+                with torch.cuda.stream(s_d2h):
+                    s_d2h.wait_stream(torch.cuda.current_stream(dev))
+                    while g0 < len(rows):
+                        g1, gb = g0, 0
+                        while g1 < len(rows) and (g1 == g0 or gb < self.d2h_group):
+                            gb += rows[g1][1]
+                            g1 += 1
+                        a, e = rows[g0][0], rows[g1 - 1][0] + rows[g1 - 1][1]
+                        buf[o0 + a:o0 + e].copy_(res.packs[a:e], non_blocking=True)
+                        ev = torch.cuda.Event()
+                        ev.record(s_d2h)
 
-                def job(ev=ev, rows=rows, base=base, buf=buf):
-                    ev.synchronize()
-                    return [pool.submit(hash_pack, buf, o, n, base + j)
-                            for j, (o, n) in enumerate(rows)]
-                futs.append(pool.submit(job))
+                        def job(ev=ev, grp=rows[g0:g1], j0=base + g0, buf=buf):
+                            ev.synchronize()
+                            return [pool.submit(hash_pack, buf, o0 + o, n, j0 + j)
+                                    for j, (o, n) in enumerate(grp)]
+                        futs.append(pool.submit(job))
+                        g0 = g1
+                    ev_all = torch.cuda.Event()
+                    ev_all.record(s_d2h)
+                keep.append((res.packs, ev_all))
+                state["host_off"] = o0 + total
+                state["d2h"] += total
             res.packs = None
             ms["handoff"] += (time.perf_counter() - t) * 1e3
 

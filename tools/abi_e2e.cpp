@@ -23,6 +23,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <functional>
 #include <string>
 #include <thread>
 #include <vector>
@@ -85,20 +86,28 @@ static double h2d_concurrent(const std::vector<uint8_t *> &data, uint64_t n, uin
                              int threads, int mode) {
     constexpr int kSlots = 4;
     const uint64_t blk = mode == 0 ? rd : (4ull << 20);
-    std::atomic<int> next{0};
-    std::atomic<int> bad{0};
-    auto work = [&]() {
-        hipStream_t s;
+    // per-thread streams, device buffers and pinned slots, allocated before
+    // the timed region (as a context's lanes are)
+    struct Res {
+        hipStream_t s = nullptr;
         void *d = nullptr;
         void *h[kSlots] = {};
-        hipEvent_t ev[kSlots];
-        if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) { bad++; return; }
-        if (hipMalloc(&d, n) != hipSuccess) bad++;
+        hipEvent_t ev[kSlots] = {};
+    };
+    std::vector<Res> res(threads);
+    int bad = 0;
+    for (auto &r : res) {
+        if (hipStreamCreateWithFlags(&r.s, hipStreamNonBlocking) != hipSuccess) bad++;
+        if (hipMalloc(&r.d, n) != hipSuccess) bad++;
         for (int k = 0; k < kSlots; k++) {
-            if (mode && hipHostMalloc(&h[k], blk, hipHostMallocDefault) != hipSuccess) bad++;
-            if (mode == 2 && h[k]) memset(h[k], 1, blk);
-            (void)hipEventCreateWithFlags(&ev[k], hipEventDisableTiming);
+            if (mode && hipHostMalloc(&r.h[k], blk, hipHostMallocDefault) != hipSuccess) bad++;
+            if (mode == 2 && r.h[k]) memset(r.h[k], 1, blk);
+            (void)hipEventCreateWithFlags(&r.ev[k], hipEventDisableTiming);
         }
+    }
+    (void)hipDeviceSynchronize();
+    std::atomic<int> next{0};
+    auto work = [&](Res &r) {
         uint64_t k = 0;
         for (;;) {
             const int f = next++;
@@ -107,28 +116,31 @@ static double h2d_concurrent(const std::vector<uint8_t *> &data, uint64_t n, uin
                 const uint64_t len = std::min(blk, n - o);
                 const int b = (int)(k % kSlots);
                 if (mode) {
-                    if (k >= (uint64_t)kSlots) (void)hipEventSynchronize(ev[b]);  // slot free
-                    if (mode == 1) memcpy(h[b], data[f] + o, len);
-                    (void)hipMemcpyAsync((uint8_t *)d + o, h[b], len, hipMemcpyHostToDevice, s);
+                    if (k >= (uint64_t)kSlots) (void)hipEventSynchronize(r.ev[b]);  // slot free
+                    if (mode == 1) memcpy(r.h[b], data[f] + o, len);
+                    (void)hipMemcpyAsync((uint8_t *)r.d + o, r.h[b], len, hipMemcpyHostToDevice, r.s);
                 } else {
-                    (void)hipMemcpyAsync((uint8_t *)d + o, data[f] + o, len, hipMemcpyHostToDevice, s);
+                    (void)hipMemcpyAsync((uint8_t *)r.d + o, data[f] + o, len, hipMemcpyHostToDevice,
+                                         r.s);
                 }
-                (void)hipEventRecord(ev[b], s);
+                (void)hipEventRecord(r.ev[b], r.s);
             }
         }
-        (void)hipStreamSynchronize(s);
-        (void)hipFree(d);
-        for (int j = 0; j < kSlots; j++) {
-            if (h[j]) (void)hipHostFree(h[j]);
-            (void)hipEventDestroy(ev[j]);
-        }
-        (void)hipStreamDestroy(s);
+        (void)hipStreamSynchronize(r.s);
     };
     const double t0 = now();
     std::vector<std::thread> th;
-    for (int t = 0; t < threads; t++) th.emplace_back(work);
+    for (int t = 0; t < threads; t++) th.emplace_back(work, std::ref(res[t]));
     for (auto &x : th) x.join();
     const double el = now() - t0;
+    for (auto &r : res) {
+        (void)hipFree(r.d);
+        for (int j = 0; j < kSlots; j++) {
+            if (r.h[j]) (void)hipHostFree(r.h[j]);
+            (void)hipEventDestroy(r.ev[j]);
+        }
+        (void)hipStreamDestroy(r.s);
+    }
     return bad ? -1.0 : (double)data.size() * n / el / (1ull << 30);
 }
 

@@ -1,0 +1,23 @@
+"""Host SHA-256 throughput (hashlib / OpenSSL) over pack-sized buffers with
+1..N threads: the pack-id budget of the host-to-host path (HostIngest hashes
+every pack file on host threads, packer.rs:832-834)."""
+import hashlib
+import json
+import os
+import sys
+import time
+from concurrent.futures import ThreadPoolExecutor
+
+import numpy as np
+
+n_buf, size = 64, 32 << 20
+bufs = [np.random.default_rng(i).integers(0, 256, size, dtype=np.uint8) for i in range(n_buf)]
+out = {"buffer_mib": size >> 20, "buffers": n_buf, "cpu_affinity": len(os.sched_getaffinity(0))}
+for t in [int(x) for x in (sys.argv[1:] or ["1", "8", "14", "16"])]:
+    with ThreadPoolExecutor(t) as pool:
+        list(pool.map(lambda b: hashlib.sha256(memoryview(b)).digest(), bufs[:t]))
+        t0 = time.perf_counter()
+        list(pool.map(lambda b: hashlib.sha256(memoryview(b)).digest(), bufs))
+        el = time.perf_counter() - t0
+    out[f"gbs_{t}_threads"] = round(n_buf * size / el / 1e9, 2)
+print(json.dumps(out))
