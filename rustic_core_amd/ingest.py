@@ -607,10 +607,17 @@ class HostIngest:
                 ev_h2d[k] = torch.cuda.Event()
                 ev_h2d[k].record(s_h2d)
 
+        hstat = {"busy_s": 0.0, "first": None, "last": 0.0}
+
         def hash_pack(buf, o, n, slot):
+            a = time.perf_counter()
             d = hashlib.sha256(memoryview(buf[o:o + n].numpy())).digest()
+            b = time.perf_counter()
             with lock:
                 ids_out[slot] = d
+                hstat["busy_s"] += b - a
+                hstat["first"] = a if hstat["first"] is None else min(hstat["first"], a)
+                hstat["last"] = max(hstat["last"], b)
 
         def handoff(res):
             # the packs of one batch: D2H into the pinned buffer, then hashed
@@ -731,6 +738,11 @@ class HostIngest:
         seconds = time.perf_counter() - t0
         pool.shutdown()
         id_pool.shutdown()
+        # pack-id hashing: thread-seconds spent, and its window
+        ms["hash_thread_s"] = round(hstat["busy_s"], 3)
+        if hstat["first"] is not None:
+            ms["hash_first_ms"] = (hstat["first"] - t0) * 1e3
+            ms["hash_last_ms"] = (hstat["last"] - t0) * 1e3
         for pl in plans:
             pl.close()
         for r in results:  # per-phase times of each batch

@@ -243,6 +243,14 @@ def main():
         chk = checks(res, files, key, a.open_packs, hi.hash_threads)
         chk["seconds"] = round(time.perf_counter() - t, 1)
         log(f"checks: {chk}")
+    # the host's pack-id budget on these very bytes: every pack hashed again
+    # with the run's thread count, nothing else running
+    t = time.perf_counter()
+    with ThreadPoolExecutor(hi.hash_threads) as pool:
+        list(pool.map(lambda k: hashlib.sha256(memoryview(res.packs_host[
+            int(res.pack_offs[k]):int(res.pack_offs[k]) + int(res.pack_sizes[k])].numpy())).digest(),
+            range(len(res.pack_sizes))))
+    rehash_s = time.perf_counter() - t
     bound = pcie_bound(files, res.batch_files, res.d2h_bytes, dev, res.packs_host)
     bound_s = bound["seconds_both"]
     line = {
@@ -258,6 +266,12 @@ def main():
                        "how": "the run's H2D copies (3 device slots, one stream) with its pack "
                               "bytes D2H on a second stream at the same time, no compute"},
         "frac_of_bound": round(bound_s / res.seconds, 3),
+        "pack_id_hashing": {"host_gbs_alone": round(res.d2h_bytes / rehash_s / 1e9, 2),
+                            "seconds_alone": round(rehash_s, 3),
+                            "thread_seconds_in_run": res.ms.get("hash_thread_s"),
+                            "note": "SHA-256 of every pack file (packer.rs:832-834) on the "
+                                    "job's host threads; hashing all packs alone takes "
+                                    "seconds_alone"},
         "batches": [len(b) for b in res.batch_files],
         "hash_threads": hi.hash_threads,
         "gpu_max_hw_queues": os.environ.get("GPU_MAX_HW_QUEUES"),
