@@ -551,8 +551,8 @@ class HostIngest:
 
     def __init__(self, config: ConfigFile, key: Key, device: int = 0,
                  indexed: Optional[set] = None, extra_verify: Optional[bool] = None,
-                 hash_threads: Optional[int] = None, first_batch: int = 4 << 30,
-                 batch: int = 16 << 30, last_batch: int = 4 << 30,
+                 hash_threads: Optional[int] = None, first_batch: int = 2 << 30,
+                 batch: int = 12 << 30, last_batch: int = 4 << 30,
                  pack_ratio: float = 0.8):
         self.ingest = DeviceIngest(config, key, device, indexed, extra_verify)
         self.device = device
@@ -568,9 +568,10 @@ class HostIngest:
         self.first_batch, self.batch, self.last_batch = int(first_batch), int(batch), int(last_batch)
         self.pack_ratio = float(pack_ratio)  # initial pinned pack buffer / input bytes
         self.d2h_group = 512 << 20  # pack bytes per copy-back event
-        # the last batch's long-chunk ids on host threads from the files (its
-        # device chains would follow the last copy: ~0.27 s per 8 MiB chunk)
-        self.host_last_ids = True
+        # the first and last batches' long-chunk ids on host threads from the
+        # files (their device chains are not hidden under other batches:
+        # ~0.27 s per 8 MiB chunk)
+        self.host_edge_ids = True
 
     def run(self, files) -> HostIngestResult:
         """`files`: 1-D uint8 CPU tensors (pinned for full-rate copies)."""
@@ -708,10 +709,13 @@ class HostIngest:
             torch.cuda.current_stream(dev).wait_event(ev_h2d[k])
             offs, _ = layouts[k]
             t = time.perf_counter()
-            last = k == len(batches) - 1
+            # the first and last batches' long-chunk ids on the host: the
+            # first batch's packs then reach the hash threads sooner (they are
+            # idle until then), the last one's follow the last copy at once
+            edge = (k == len(batches) - 1 or k == 0) and len(batches) > 1
             p = self.ingest.begin(arenas[k % len(arenas)], offs, [sizes[i] for i in batches[k]],
                                   plan=plans[k],
-                                  host_ids=host_ids_for(k) if last and self.host_last_ids else None)
+                                  host_ids=host_ids_for(k) if edge and self.host_edge_ids else None)
             ms["begin"] += (time.perf_counter() - t) * 1e3
             ms[f"begin{k}"] = (time.perf_counter() - t) * 1e3
             if pending is not None:
