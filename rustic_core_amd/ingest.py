@@ -498,13 +498,18 @@ class HostIngestResult:
 def plan_batches(sizes, first: int, middle: int, last: int,
                  taper: bool = True) -> List[List[int]]:
     """Whole files in order into batches of about ``first`` bytes, then
-    ``middle``, and a final one of about ``last`` (``taper``: preceded by one
-    of 2 x last): a small first batch starts the device early, small last ones
-    shorten the drain (their ids, packs, copy back and pack ids follow the
-    last H2D; the pack ids of a middle batch arriving last would hold the
-    host's hash threads ~0.25 s)."""
+    ``middle``, and a tail ending in one of about ``last`` (``taper``: a
+    halving tail middle/2, middle/4, ... down to ``last``): a small first
+    batch starts the device early, a shrinking tail shortens the drain (each
+    batch's packs reach the host hash threads about one batch after its copy;
+    the pack ids of a middle batch arriving last would hold them ~0.25 s)."""
     total = int(sum(sizes))
-    tail = [2 * last, last] if taper and total >= first + middle + 3 * last else [last]
+    tail = [last]
+    if taper:
+        b = middle // 2
+        while b > last and total >= first + middle + sum(tail) + b:
+            tail.insert(len(tail) - 1, b)
+            b //= 2
     rest = total - first - sum(tail)
     m = max(-(-rest // middle), 0)
     targets = [first] + [-(-rest // m)] * m + tail if m else [first] + tail
@@ -552,7 +557,7 @@ class HostIngest:
     def __init__(self, config: ConfigFile, key: Key, device: int = 0,
                  indexed: Optional[set] = None, extra_verify: Optional[bool] = None,
                  hash_threads: Optional[int] = None, first_batch: int = 2 << 30,
-                 batch: int = 12 << 30, last_batch: int = 4 << 30,
+                 batch: int = 12 << 30, last_batch: int = 1 << 30,
                  pack_ratio: float = 0.8):
         self.ingest = DeviceIngest(config, key, device, indexed, extra_verify)
         self.device = device
@@ -572,6 +577,7 @@ class HostIngest:
         # files (their device chains are not hidden under other batches:
         # ~0.27 s per 8 MiB chunk)
         self.host_edge_ids = True
+        self.host_tail_ids = 3  # the last batches whose long ids the host computes
 
     def run(self, files) -> HostIngestResult:
         """`files`: 1-D uint8 CPU tensors (pinned for full-rate copies)."""
@@ -712,7 +718,7 @@ class HostIngest:
             # the first and last batches' long-chunk ids on the host: the
             # first batch's packs then reach the hash threads sooner (they are
             # idle until then), the last one's follow the last copy at once
-            edge = (k == len(batches) - 1 or k == 0) and len(batches) > 1
+            edge = (k == 0 or k >= len(batches) - self.host_tail_ids) and len(batches) > 1
             p = self.ingest.begin(arenas[k % len(arenas)], offs, [sizes[i] for i in batches[k]],
                                   plan=plans[k],
                                   host_ids=host_ids_for(k) if edge and self.host_edge_ids else None)

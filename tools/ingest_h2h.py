@@ -203,7 +203,7 @@ def main():
     ap.add_argument("--file-gib", type=float, default=1.0)
     ap.add_argument("--first-gib", type=float, default=2)
     ap.add_argument("--batch-gib", type=float, default=12)
-    ap.add_argument("--last-gib", type=float, default=4)
+    ap.add_argument("--last-gib", type=float, default=1)
     ap.add_argument("--hash-threads", type=int, default=None)
     ap.add_argument("--open-packs", type=int, default=3)
     ap.add_argument("--repeat", type=int, default=1, help="timed runs (fresh repository each)")
