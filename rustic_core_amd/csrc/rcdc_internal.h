@@ -141,7 +141,31 @@ struct WalkParams {
                            // most this many per round of the walker's own (0 = off)
     uint64_t chk_budget;   // bytes of gap hashing a boundary check may do before
                            // it hands the boundary to the fixup kernel
+    // Seeded piece starts (this run's buffer set, 2 x nunits words): [0, nunits)
+    // a piece's end state when its walker finished, one word published by one
+    // atomic store (end_word: kEndOpen | epoch | the open chunk's start or its
+    // last cut; position kEndNone: list truncated), [nunits, 2 nunits) the
+    // chain start its walker used (kSeed* << 62 | position).  A walker whose
+    // previous piece is already done in this run (the word carries this run's
+    // epoch) continues that piece's chain instead of assuming a cut at its own
+    // start.  One word, so no fences: an acquire would invalidate the XCD's
+    // L2 under the other waves' streams.
+    uint64_t *wstate;
+    uint64_t epoch;        // this run's, 1 .. 2^21 - 1 (the buffers start zeroed)
+    uint32_t seed;         // seeding on
+    uint32_t pad2;
 };
+constexpr uint64_t kEndOpen = 1ull << 63;
+constexpr uint64_t kEndPos = (1ull << 42) - 1;  // position bits of an end word
+constexpr uint64_t kEndNone = kEndPos;          // position: no usable end state
+constexpr uint32_t kEpochShift = 42;            // epoch bits 42..62
+__host__ __device__ inline uint64_t end_word(bool open, uint64_t epoch, uint64_t pos) {
+    return (open ? kEndOpen : 0ull) | (epoch << kEpochShift) | (pos & kEndPos);
+}
+__host__ __device__ inline uint64_t end_epoch(uint64_t w) { return (w >> kEpochShift) & ((1ull << 21) - 1); }
+constexpr uint64_t kSeedNone = 0;    // speculative: a cut assumed at the piece start
+constexpr uint64_t kSeedClosed = 1;  // the chain starts at the previous piece's last cut
+constexpr uint64_t kSeedOpen = 2;    // the chain continues the previous piece's open chunk
 
 // WalkParams.stats slots
 constexpr int kWalkStatRounds = 0;     // walk kernel: 64-lane hashing rounds

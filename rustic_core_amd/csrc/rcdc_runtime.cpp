@@ -197,6 +197,9 @@ struct rcdc_plan {
     uint32_t *d_worder = nullptr;
     uint64_t *d_wpiece = nullptr;
     uint64_t *d_pstatus = nullptr;
+    uint64_t *d_wstate = nullptr, *d_wstate2 = nullptr;  // WalkParams.wstate of set 0 / 1
+    uint64_t cap_wstate = 0, cap_wstate2 = 0;
+    uint64_t walk_epoch = 0;  // runs of the walk kernel (WalkParams.epoch)
     BoundRes *d_bres = nullptr;
     uint32_t *d_ctr = nullptr;
     uint32_t *d_fixlist = nullptr;
@@ -691,6 +694,9 @@ rcdc_status plan_build(rcdc_ctx *ctx, rcdc_plan *pl, const uint64_t *offs, const
     wp.fix_cap = (uint32_t)(4 * (Lp ? Lp : 1) / ctx->min + ctx->max / ctx->min + 64);
     wp.fix_seg = 512;
     wp.chk_budget = 4 * ctx->max;  // gap hashing in the check kernel (64 lanes) before the fixup (1024)
+    // seeded piece starts (a walker continues its finished predecessor's chain)
+    wp.seed = 1;
+    if (const char *e = getenv("RCDC_WALK_SEED")) wp.seed = atoi(e) != 0;
     if (const char *e = getenv("RCDC_CHECK_BUDGET")) wp.chk_budget = strtoull(e, nullptr, 10);
     if (const char *e = getenv("RCDC_FIX_SEG")) wp.fix_seg = (uint32_t)std::max(atoi(e) / 128 * 128, 128);
     if (const char *e = getenv("RCDC_WALK_FIXCAP")) wp.fix_cap = (uint32_t)std::max(atoi(e), 1);  // tests
@@ -734,6 +740,15 @@ rcdc_status plan_build(rcdc_ctx *ctx, rcdc_plan *pl, const uint64_t *offs, const
         HIP_TRY(upload(pl->d_worder, pl->worder.data(), nw * sizeof(uint32_t)));
         if ((st = ensure_dev(&pl->d_wpiece, &pl->cap_wpiece, pl->nwpiece_cuts))) return st;
         if ((st = ensure_dev(&pl->d_pstatus, &pl->cap_pstatus, nw))) return st;
+        if ((st = ensure_dev(&pl->d_wstate, &pl->cap_wstate, 2 * nw))) return st;
+        // epoch 0 = no run (a rebuilt plan keeps counting its runs)
+        HIP_TRY(up ? hipMemsetAsync(pl->d_wstate, 0, 2 * nw * 8, up)
+                   : hipMemset(pl->d_wstate, 0, 2 * nw * 8));
+        if (pl->d_wstate2) {
+            if ((st = ensure_dev(&pl->d_wstate2, &pl->cap_wstate2, 2 * nw))) return st;
+            HIP_TRY(up ? hipMemsetAsync(pl->d_wstate2, 0, 2 * nw * 8, up)
+                       : hipMemset(pl->d_wstate2, 0, 2 * nw * 8));
+        }
         if ((st = ensure_dev(&pl->d_bres, &pl->cap_bres, nw))) return st;
         if ((st = ensure_dev(&pl->d_ctr, &pl->cap_ctr, 4))) return st;
         if ((st = ensure_dev(&pl->d_fixlist, &pl->cap_fixlist, nw))) return st;
@@ -795,6 +810,9 @@ rcdc_status plan_run(rcdc_plan *pl, const void *d_arena, hipStream_t stream) {
     // this run's walk buffers and parameters
     WalkParams wprm = pl->wprm;
     uint64_t *wpiece = pl->d_wpiece, *pstatus = pl->d_pstatus, *fixcuts = pl->d_fixcuts;
+    wprm.wstate = wprm.seed ? pl->d_wstate : nullptr;
+    pl->walk_epoch = pl->walk_epoch % ((1ull << 21) - 1) + 1;  // 1 .. 2^21 - 1
+    wprm.epoch = pl->walk_epoch;
     BoundRes *bres = pl->d_bres;
     uint32_t *ctr = pl->d_ctr, *fixlist = pl->d_fixlist;
     FixRes *fixres = pl->d_fixres;
@@ -802,6 +820,7 @@ rcdc_status plan_run(rcdc_plan *pl, const void *d_arena, hipStream_t stream) {
         const uint64_t nw = pl->wunits.size();
         wpiece = pl->d_wpiece2;
         pstatus = pl->d_pstatus2;
+        if (wprm.seed) wprm.wstate = pl->d_wstate2;
         fixcuts = pl->d_fixcuts2;
         bres = pl->d_bres2;
         ctr = pl->d_ctr2;
@@ -1074,6 +1093,8 @@ void plan_release(rcdc_plan *pl) {
     (void)hipFree(pl->d_masks2);
     (void)hipFree(pl->d_wpiece2);
     (void)hipFree(pl->d_pstatus2);
+    (void)hipFree(pl->d_wstate);
+    (void)hipFree(pl->d_wstate2);
     (void)hipFree(pl->d_fixcuts2);
     (void)hipFree(pl->d_bres2);
     (void)hipFree(pl->d_ctr2);
@@ -1593,6 +1614,8 @@ rcdc_status rcdc_plan_set_pipeline(rcdc_plan *plan, int enable) {
     if (const uint64_t nw = plan->wunits.size()) {
         if ((st = ensure_dev(&plan->d_wpiece2, &plan->cap_wpiece2, plan->nwpiece_cuts))) return st;
         if ((st = ensure_dev(&plan->d_pstatus2, &plan->cap_pstatus2, nw))) return st;
+        if ((st = ensure_dev(&plan->d_wstate2, &plan->cap_wstate2, 2 * nw))) return st;
+        HIP_TRY(hipMemset(plan->d_wstate2, 0, 2 * nw * 8));
         if ((st = ensure_dev(&plan->d_bres2, &plan->cap_bres2, nw))) return st;
         if ((st = ensure_dev(&plan->d_ctr2, &plan->cap_ctr2, 4))) return st;
         if ((st = ensure_dev(&plan->d_fixlist2, &plan->cap_fixlist2, nw))) return st;

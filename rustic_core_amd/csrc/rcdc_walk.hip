@@ -393,26 +393,37 @@ __device__ uint64_t walk_wait(Walk &W, uint64_t own) {
     return readlane64(h, 0);
 }
 
+template <int LANES, int TSH, bool SMALL>
+__device__ uint64_t walk_search(Walk &W, uint64_t q, uint64_t limit, uint64_t stop_scan,
+                                uint64_t *kind);
+
 // The end of the chunk starting at pos (rabin.rs:110-191), or kOpen if no
 // cut was found below stop_scan (the search stopped there).  *kind: what the
 // walker verified (rcdc_internal.h kKind*); *zero: all-zero prefill cut.
+// cont_q != 0: the chunk from pos was searched hit-free up to cont_q by
+// someone else (a seeded start continuing the previous piece's open chunk):
+// no zone, the search resumes at cont_q.  (One call site of walk_search per
+// kernel: a second inlined copy of the round loop spilled.)
 template <int LANES, int TSH, bool SMALL>
 __device__ uint64_t walk_next(Walk &W, uint64_t pos, uint64_t stop_scan, uint64_t *kind,
-                              bool *zero) {
+                              bool *zero, uint64_t cont_q = 0) {
     *zero = false;
-    if (W.N - pos <= W.mn) {  // rabin.rs:141-147: the rest is the last chunk
+    const uint64_t limit = min(pos + W.mx, W.N);  // rabin.rs:154 / EOF
+    if (!cont_q && W.N - pos <= W.mn) {  // rabin.rs:141-147: the rest is the last chunk
         *kind = kKindEof;
         return W.N;
     }
     const uint64_t z = pos + W.mn;
-    const uint64_t limit = min(pos + W.mx, W.N);  // rabin.rs:154 / EOF
-    uint64_t zc;
-    bool zz;
+    uint64_t zc = kNoCut;
+    bool zz = false;
     const ModRepl mod{W.tab, W.k.lwm};
-    W.zones++;
-    if constexpr (LANES == 64) {
+    if (cont_q) {
+        // (the search below resumes at cont_q)
+    } else if constexpr (LANES == 64) {
+        W.zones++;
         zc = zone_wave(W.arena + W.off, W.N, z, limit, W.mask, W.shift, mod, W.win, W.lane, &zz);
     } else {
+        W.zones++;
         if (W.wave == 0) {
             zc = zone_wave(W.arena + W.off, W.N, z, limit, W.mask, W.shift, mod, W.win, W.lane,
                            &zz);
@@ -431,11 +442,20 @@ __device__ uint64_t walk_next(Walk &W, uint64_t pos, uint64_t stop_scan, uint64_
         *zero = zz;
         return zc;
     }
-    if (limit <= z + 64) {
+    if (!cont_q && limit <= z + 64) {
         *kind = limit == W.N ? kKindEof : kKindMax;
         return limit;
     }
-    const uint64_t q = z + 64;
+    return walk_search<LANES, TSH, SMALL>(W, cont_q ? cont_q : z + 64, limit, stop_scan, kind);
+}
+
+// The pure-window search of a chunk (rabin.rs:153-188) from position q: its
+// first hit below min(limit, stop_scan), else limit (kind Max / Eof) if the
+// search reached it, else kOpen.  In rounds of LANES x S bytes; in the walk
+// kernel's tail, idle waves of the workgroup hash rounds ahead (walk_post).
+template <int LANES, int TSH, bool SMALL>
+__device__ uint64_t walk_search(Walk &W, uint64_t q, uint64_t limit, uint64_t stop_scan,
+                                uint64_t *kind) {
     const uint64_t end = min(limit, stop_scan);
     uint64_t A = round_base(W.off, q);
     while (A < end) {
@@ -552,10 +572,38 @@ __global__ __launch_bounds__(1024, 1) void rcdc_walk_kernel(
         const uint64_t stop_scan = U.stop < d.n ? U.stop + W.mn + 64 : ~0ull;
         uint64_t pos = U.start, n = 0;
         bool open = false;
-        while (pos < d.n) {
+        // Seeded start: if the previous piece of the stream has finished in
+        // this run, continue its chain (closed at its last cut, or inside its
+        // open chunk) instead of assuming a cut at U.start -- the chains then
+        // agree from here on and this piece hashes nothing the true chain
+        // skips (rcdc_internal.h WalkParams.wstate).
+        uint64_t seedw = kSeedNone << 62;  // (stored now: nothing live across the walk)
+        bool cont = false;
+        if (prm.seed && U.piece > 0) {
+            uint64_t pe = 0;
+            if (lane == 0)
+                pe = __hip_atomic_load(prm.wstate + (u - 1), __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+            pe = readlane64(pe, 0);
+            if (end_epoch(pe) == prm.epoch && (pe & kEndPos) != kEndNone) {
+                const uint64_t pp = pe & kEndPos;
+                if ((pe & kEndOpen) && pp < U.start) {
+                    cont = true;  // chunk [pp, ...) searched hit-free up to U.start + min + 64
+                    pos = pp;
+                    seedw = (kSeedOpen << 62) | pp;
+                } else if (!(pe & kEndOpen) && pp >= U.start && pp < U.stop) {
+                    pos = pp;
+                    seedw = (kSeedClosed << 62) | pp;
+                }
+            }
+        }
+        if (prm.wstate && lane == 0) prm.wstate[prm.nunits + u] = seedw;
+        while (pos < d.n && (n == 0 || pos < U.stop)) {
             uint64_t kind;
             bool zero;
-            const uint64_t c = walk_next<64, TSH, SMALL>(W, pos, stop_scan, &kind, &zero);
+            const uint64_t c = walk_next<64, TSH, SMALL>(W, pos, stop_scan, &kind, &zero,
+                                                         cont ? U.start + W.mn + 64 : 0);
+            cont = false;
             if (c == kOpen) {
                 open = true;
                 break;
@@ -581,6 +629,10 @@ __global__ __launch_bounds__(1024, 1) void rcdc_walk_kernel(
         if (lane == 0) {
             pstatus[u] = min(n, (uint64_t)U.out_cap) | (open ? kOpenFlag : 0ull) |
                          (n > U.out_cap ? (kOpenFlag << 1) : 0ull);
+            if (prm.wstate)
+                __hip_atomic_store(prm.wstate + u,
+                                   end_word(open, prm.epoch, n > U.out_cap ? kEndNone : pos),
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             stats_add(s_st, kWalkStatRounds, W.rounds);
             stats_add(s_st, kWalkStatZones, W.zones);
             stats_add(s_st, kWalkStatBytes, W.lbytes);
@@ -644,11 +696,17 @@ constexpr uint64_t kHopRun = 1;  // hop entry kind: cuts prev + min, prev + 2 mi
 struct PieceView {
     const uint64_t *L;
     uint64_t n, start, stop;
+    uint64_t cstart;  // the chain's first point (a cut; kNoCut: it continues an
+                      // open chunk of the previous piece, kSeedOpen)
+    uint64_t prev0;   // chunk 0 searched [prev0 + min + 64, L[0])
     bool open, full;  // full: the list holds every cut the walker found
 };
 
+// pseed: WalkParams.wstate + nunits (nullptr: no seeding, every chain starts
+// with a cut at its piece start).
 __device__ __forceinline__ PieceView piece_view(const WalkUnit *units, const uint64_t *pstatus,
-                                                const uint64_t *piece_cuts, uint32_t uk) {
+                                                const uint64_t *piece_cuts, uint32_t uk,
+                                                const uint64_t *pseed) {
     const WalkUnit Uk = units[uk];
     const uint64_t st = pstatus[uk];
     PieceView V;
@@ -658,6 +716,14 @@ __device__ __forceinline__ PieceView piece_view(const WalkUnit *units, const uin
     V.stop = Uk.stop;
     V.open = (st & kOpenFlag) != 0;
     V.full = (st & (kOpenFlag << 1)) == 0;
+    V.cstart = Uk.start;
+    V.prev0 = Uk.start;
+    if (pseed) {
+        const uint64_t sd = pseed[uk], kind = sd >> 62, pos = sd & kCutVal;
+        if (kind == kSeedClosed) V.cstart = V.prev0 = pos;
+        else if (kind == kSeedOpen) V.cstart = kNoCut;  // (prev0 = start: its first
+                                                        // search began at start + min + 64)
+    }
     return V;
 }
 
@@ -697,7 +763,7 @@ __device__ bool cover(const PieceView &V, uint64_t p, uint64_t mn, uint64_t *ven
     if (!V.full) return false;
     const uint64_t t = lower_cut_wave(V.L, V.n, p);
     if (t < V.n) {
-        const uint64_t prev = t ? (V.L[t - 1] & kCutVal) : V.start;
+        const uint64_t prev = t ? (V.L[t - 1] & kCutVal) : V.prev0;
         const uint64_t base = prev + mn + 64;
         const uint64_t kd = V.L[t] >> 62, v = V.L[t] & kCutVal;
         // chunk t searched [base, v) hit-free; v is a hit (Hit), untested
@@ -714,7 +780,7 @@ __device__ bool cover(const PieceView &V, uint64_t p, uint64_t mn, uint64_t *ven
         return false;
     }
     if (V.open) {
-        const uint64_t base = (V.n ? (V.L[V.n - 1] & kCutVal) : V.start) + mn + 64;
+        const uint64_t base = (V.n ? (V.L[V.n - 1] & kCutVal) : V.prev0) + mn + 64;
         const uint64_t oend = V.stop + mn + 64;
         if (base <= p && p < oend) {
             *vend = oend;
@@ -729,6 +795,7 @@ __device__ bool cover(const PieceView &V, uint64_t p, uint64_t mn, uint64_t *ven
 struct CheckCtx {
     const WalkUnit *units;
     const uint64_t *pstatus, *piece_cuts;
+    const uint64_t *pseed;  // nullptr: no seeded starts
     WalkUnit U;   // the boundary's unit (piece j)
     uint32_t u;   // its index
     uint64_t N, mn, mx;
@@ -780,7 +847,8 @@ __device__ uint64_t check_first_hit(Walk &W, CheckCtx &C, uint64_t lo, uint64_t 
         uint64_t gap_end = lim;
         for (int back = 0; back < 2 && !known; back++) {
             if (back == 1 && k == 0) break;
-            const PieceView V = piece_view(C.units, C.pstatus, C.piece_cuts, C.U.unit0 + k - back);
+            const PieceView V = piece_view(C.units, C.pstatus, C.piece_cuts, C.U.unit0 + k - back,
+                                           C.pseed);
             uint64_t vend, vkind, nxt;
             if (cover(V, p, C.mn, &vend, &vkind, &nxt)) {
                 if (vkind == kKindHit) return min(vend, lim);
@@ -854,8 +922,8 @@ __device__ __forceinline__ bool merged_at(const CheckCtx &C, uint64_t c, uint32_
         if (back == 1 && k == 0) break;
         const uint32_t uk = C.U.unit0 + k - back;
         if (uk < C.u) break;
-        const PieceView V = piece_view(C.units, C.pstatus, C.piece_cuts, uk);
-        if (back == 0 && c == V.start) {
+        const PieceView V = piece_view(C.units, C.pstatus, C.piece_cuts, uk, C.pseed);
+        if (back == 0 && c == V.cstart) {
             *mu = uk;
             *idx = -1;
             return true;
@@ -937,6 +1005,7 @@ __global__ __launch_bounds__(CT, 1) void rcdc_walk_check_kernel(
         C.units = units;
         C.pstatus = pstatus;
         C.piece_cuts = piece_cuts;
+        C.pseed = prm.wstate ? prm.wstate + prm.nunits : nullptr;
         C.U = U;
         C.u = u;
         C.N = N;
@@ -955,10 +1024,15 @@ __global__ __launch_bounds__(CT, 1) void rcdc_walk_check_kernel(
         uint64_t *hops = s_hops[wave];
         // exact state at the previous piece's end: closed at c, or open from c
         // ([c+min+64, a_j+min+64) hit-free, no zone cut in c's zone)
-        const PieceView Vp = piece_view(units, pstatus, piece_cuts, u - 1);
+        const PieceView Vp = piece_view(units, pstatus, piece_cuts, u - 1, C.pseed);
         uint64_t c;
         bool pending = false;
-        if (Vp.open) {
+        if (prm.wstate) {  // the end state the previous walker published
+            const uint64_t pe = prm.wstate[u - 1];
+            c = pe & kEndPos;
+            pending = (pe & kEndOpen) != 0;
+            if (c == kEndNone) c = Vp.n ? (Vp.L[Vp.n - 1] & kCutVal) : Vp.start;  // (!full below)
+        } else if (Vp.open) {
             c = Vp.n ? (Vp.L[Vp.n - 1] & kCutVal) : Vp.start;
             pending = true;
         } else {
@@ -1180,7 +1254,13 @@ __global__ __launch_bounds__(1024, 1) void rcdc_walk_fixup_kernel(
                             const uint32_t uk = U.unit0 + (uint32_t)(k - back);
                             if (uk < u) break;  // never before the boundary's own piece
                             const WalkUnit Uk = units[uk];
-                            if (back == 0 && cut == Uk.start) {
+                            uint64_t cst = Uk.start;  // the chain's first point (PieceView.cstart)
+                            if (prm.wstate) {
+                                const uint64_t sd = prm.wstate[prm.nunits + uk];
+                                if ((sd >> 62) == kSeedClosed) cst = sd & kCutVal;
+                                else if ((sd >> 62) == kSeedOpen) cst = kNoCut;
+                            }
+                            if (back == 0 && cut == cst) {
                                 mu = uk;
                                 at = -1;
                             } else {
@@ -1427,7 +1507,10 @@ __global__ __launch_bounds__(kAsmB) void rcdc_walk_assemble_kernel(
 // counting-sorts the queue by it, descending (longest-processing-time first:
 // the last pieces the waves take are the cheap ones; a stream's last piece,
 // up to 1.5 Lp, goes early).  Only the schedule changes, never the cuts.
-constexpr int kCostKeys = 128;
+// With seeded starts (WalkParams.seed) the key's low bit puts a stream's
+// even pieces before its odd ones of the same cost: an odd piece then mostly
+// starts after its predecessor has finished and continues its chain.
+constexpr int kCostKeys = 256;
 
 __global__ __launch_bounds__(256) void rcdc_walk_cost_kernel(
     const uint8_t *__restrict__ arena, const StreamDesc *__restrict__ sds,
@@ -1443,8 +1526,9 @@ __global__ __launch_bounds__(256) void rcdc_walk_cost_kernel(
         const uint64_t w = a + 8 <= d.off + d.n ? *reinterpret_cast<const uint64_t *>(arena + a) : 0;
         const uint32_t cls = (uint32_t)__builtin_popcountll(__ballot(w != 0));
         const uint64_t quantum = max(prm.piece_bytes / 48, (uint64_t)1);
-        const uint64_t cost = len * cls / 64 / quantum;
-        if (lane == 0) key[q] = (uint8_t)min(cost, (uint64_t)(kCostKeys - 1));
+        const uint64_t cost = min(len * cls / 64 / quantum, (uint64_t)(kCostKeys / 2 - 1));
+        const uint64_t even = prm.seed ? (uint64_t)((U.piece & 1u) == 0u) : 0u;
+        if (lane == 0) key[q] = (uint8_t)(cost * 2 + even);
     }
 }
 
