@@ -515,11 +515,15 @@ static uint64_t walk_piece_bytes(const uint64_t *lens, uint32_t n, uint64_t mn, 
     if (const char *e = getenv("RCDC_WALK_PIECE")) lp_env = (uint64_t)atoll(e);
     if (const char *e = getenv("RCDC_WALK_MIN_PIECES")) min_pieces = (uint64_t)atoll(e);
     if (lp_env == 0) return 0;
-    const uint64_t lo = 4ull << 20, hi = 32ull << 20;
-    uint64_t total = 0;
+    // Floor 4 MiB for files averaging >= 256 MiB, 3 MiB below (round-4 sweep
+    // with seeded starts, profiles/r04/piece_sweep.txt: C4's 4-256 MiB files
+    // +1.8 % at 3 MiB, C3's 1 GiB files -1.5 %).
+    const uint64_t hi = 32ull << 20;
+    uint64_t total = 0, nbig = 0;
     for (uint32_t i = 0; i < n; i++)
-        if (lens[i] >= 2 * lo) total += lens[i];
-    uint64_t lp = lp_env != ~0ull ? lp_env : std::min(std::max(total / 16384, lo), hi);
+        if (lens[i] >= 6ull << 20) total += lens[i], nbig++;
+    const uint64_t lo = nbig && total / nbig >= 256ull << 20 ? 4ull << 20 : 3ull << 20;
+    uint64_t lp = lp_env != ~0ull ? lp_env : std::min(std::max(total / 32768, lo), hi);
     lp = std::max<uint64_t>(lp / mn, 1) * mn;
     (void)mx;
     uint64_t walkable = 0;

@@ -161,7 +161,7 @@ def test_walk_fixup_overflow_falls_back(walk_env):
 
 def test_walk_selected_by_default_for_large_batches():
     """Without overrides a plan over >= 1024 pieces' worth of long streams
-    walks (64 x 64 MiB = 1024 pieces of 4 MiB); parity on two of them."""
+    walks (64 x 64 MiB, 21 pieces of 3 MiB each); parity on two of them."""
     import torch
     from rustic_core_amd.chunker import Context
     from rustic_core_amd.device import DevicePlan, pack_offsets
@@ -173,9 +173,10 @@ def test_walk_selected_by_default_for_large_batches():
     g.manual_seed(90)
     arena = torch.randint(0, 256, (alen,), dtype=torch.uint8, device="cuda:0", generator=g)
     plan = DevicePlan(ctx, offs, lens, alen)
-    # 16 pieces of 4 MiB per stream; 1024 pieces are fewer than two per wave
-    # slot (256 CUs x 16 waves), so none is split (RCDC_WALK_SPLIT forces it)
-    assert plan.info()["walk_pieces"] == 1024
+    # files averaging < 256 MiB get 3 MiB pieces: (64 MiB + 1.5 MiB) // 3 MiB
+    # = 21 per stream; 1344 pieces are fewer than two per wave slot (256 CUs x
+    # 16 waves), so none is split (RCDC_WALK_SPLIT forces it)
+    assert plan.info()["walk_pieces"] == 64 * 21
     plan.run(arena.data_ptr())
     got = plan.results()
     plan.close()
