@@ -18,6 +18,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from oracle import oracle  # noqa: E402
 
 MIN, MAX = 512 << 10, 8 << 20
+LANES = [64]  # lanes per round (--lanes)
 SCHED = []  # per-lane segment of a search's first rounds (--sched), then --seg
 
 
@@ -60,15 +61,16 @@ def round_bytes(S, span, adaptive):
     """Lane-hashed bytes of the rounds that cover `span` positions from A
     (64 lanes x (S + 64)); adaptive: the last round shrinks its segment to
     the 64-byte units it needs."""
-    step = 64 * S
+    nl = LANES[0]
+    step = nl * S
     full, rest = divmod(span, step)
-    b = full * 64 * (S + 64)
+    b = full * nl * (S + 64)
     if rest:
         if adaptive:
             s2 = min(S, max(((rest + 63) // 64 + 63) // 64 * 64, 64))
-            b += 64 * (s2 + 64)
+            b += nl * (s2 + 64)
         else:
-            b += 64 * (S + 64)
+            b += nl * (S + 64)
     return b
 
 
@@ -101,12 +103,12 @@ def walk_piece(data, N, a, e, S, adaptive, hitpos):
             pos, b, r = A, 0, 0
             while pos < c:
                 sg = SCHED[r] if r < len(SCHED) else S
-                pos += 64 * sg
-                b += 64 * (sg + 64)
+                pos += LANES[0] * sg
+                b += LANES[0] * (sg + 64)
                 r += 1
             lane += b
             ideal += c - q + 1
-            waste_hit += b - (c - A) - r * 64 * 64
+            waste_hit += b - (c - A) - r * LANES[0] * 64
             s = c
         else:
             span = end - A
@@ -114,7 +116,8 @@ def walk_piece(data, N, a, e, S, adaptive, hitpos):
             lane += b
             ideal += end - q
             if end < limit:
-                waste_open += b - span - ((span + 64 * S - 1) // (64 * S)) * 64 * 64
+                nl = LANES[0]
+                waste_open += b - span - ((span + nl * S - 1) // (nl * S)) * nl * 64
                 return lane, ideal, zones, waste_hit, waste_open, True
             s = c
         if s >= e:
@@ -131,9 +134,11 @@ def main():
     ap.add_argument("--piece-mib", type=int, default=4)
     ap.add_argument("--split", type=int, default=20)
     ap.add_argument("--random", action="store_true", help="uniform random bytes (C4's files)")
+    ap.add_argument("--lanes", type=int, default=64, help="lanes per round (one chain)")
     ap.add_argument("--sched", default="", help="comma list: segment of a search's first rounds")
     a = ap.parse_args()
     SCHED[:] = [int(x) for x in a.sched.split(",") if x]
+    LANES[0] = a.lanes
     tot = {"lane": 0, "ideal_search": 0, "zones": 0, "waste_hit": 0, "waste_open": 0,
            "ref_hashed": 0, "warm": 0, "pieces": 0, "open": 0, "true_lane": 0}
     for j in range(a.streams):
