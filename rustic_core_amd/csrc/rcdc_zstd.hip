@@ -138,6 +138,27 @@ __device__ __forceinline__ uint32_t ztag(uint64_t k) {
 }
 constexpr uint32_t kZstdPosMask = (1u << 17) - 1u;
 
+// Narrow table (levels >= 3): 16-bit entries holding a position's low 16
+// bits, twice the buckets in the same LDS (zstd's level-3 tables are 2^16-2^17;
+// on structured data the history depth is what pays: CSV rows 0.29 -> 0.21 at
+// 2^11 -> 2^12 positions in tests/zstd_model.py).  A bucket names the latest
+// position below p with those low bits; candidates are verified on the bytes,
+// so an older position 64 KiB away only costs a lost candidate.  0xFFFF is
+// empty (a position with those low bits is lost).
+constexpr uint32_t kZstdNone16 = 0xFFFFu;
+__device__ __forceinline__ uint32_t narrow_cand(uint32_t e, uint32_t p) {
+    if (e == kZstdNone16) return kZstdNone;
+    const uint32_t c = (p & ~0xFFFFu) | e;
+    return c < p ? c : (c >= 0x10000u ? c - 0x10000u : kZstdNone);
+}
+
+// key flags (ZstdStrategy.key): key bytes | kZstdRep (repeat codes) |
+// kZstdRepCheck (every position also tries the last offset, zstd_fast's
+// repcode check: taken before a table match, and one position later wins
+// over a table match here)
+constexpr uint32_t kZstdRep = 0x100u, kZstdRepCheck = 0x200u, kZstdInsAll = 0x400u,
+                   kZstdRep1 = 0x800u, kZstdLazyRep = 0x1000u;
+
 // Equal bytes of a[0..) and b[0..), at most maxlen (wave-uniform result).
 // Lane l compares 16 bytes per round (1 KiB per wave round); the last,
 // partial groups go byte-safe.
@@ -1057,14 +1078,17 @@ __device__ bool wave_is_rle(const uint8_t *src, uint32_t n, const uint8_t *lim) 
 }  // namespace
 
 // res[b] = {type | rle byte << 8, content bytes}.  HL: hash table of 2^HL
-// positions (LDS 4 * 2^HL bytes per wave: more buckets, or more waves per CU)
-template <int HL>
-__global__ __launch_bounds__(64, HL == 11 ? 4 : 3) void rcdc_zstd_block_kernel(
+// positions (LDS 4 * 2^HL bytes per wave, 2 * 2^HL when NARROW: more buckets,
+// or more waves per CU)
+template <int HL, bool NARROW>
+__global__ __launch_bounds__(64, (NARROW ? HL - 1 : HL) == 11 ? 4 : 2) void rcdc_zstd_block_kernel(
     const uint8_t *__restrict__ in, const ZstdBlob *__restrict__ blobs,
     const ZstdBlk *__restrict__ blks, uint32_t nblk, const ZstdTables *__restrict__ tabs,
     uint8_t *__restrict__ slots, uint64_t *__restrict__ seqbuf, uint2 *__restrict__ res,
     uint32_t dbg, uint32_t key, uint32_t *__restrict__ queue) {
-    __shared__ uint32_t table[1 << HL];
+    __shared__ uint32_t table[NARROW ? 1 << (HL - 1) : 1 << HL];
+    uint16_t *const t16 = reinterpret_cast<uint16_t *>(table);
+    constexpr uint32_t kTabWords = NARROW ? 1u << (HL - 1) : 1u << HL;
     __shared__ ZstdTables T;
     const uint32_t lane = lane_id();
     for (uint32_t i = lane; i < sizeof(ZstdTables) / 4; i += 64)
@@ -1136,7 +1160,7 @@ __global__ __launch_bounds__(64, HL == 11 ? 4 : 3) void rcdc_zstd_block_kernel(
                     continue;
                 }
             }
-            for (uint32_t i = lane; i < (1u << HL); i += 64) table[i] = kZstdNone;
+            for (uint32_t i = lane; i < kTabWords; i += 64) table[i] = kZstdNone;
             __builtin_amdgcn_wave_barrier();
             const uint32_t ilimit = n - 8;  // last position a match may start at
             uint32_t base = 0;
@@ -1146,19 +1170,38 @@ __global__ __launch_bounds__(64, HL == 11 ? 4 : 3) void rcdc_zstd_block_kernel(
                 if (stride > kZstdMaxStride) stride = kZstdMaxStride;
                 const uint32_t p = base + lane * stride;
                 const bool act = p <= ilimit;
-                uint32_t w = 0, h = 0, tg = 0, c = kZstdNone;
+                uint32_t w = 0, wr = 0, wr1 = 0, wr2 = 0, h = 0, tg = 0, c = kZstdNone;
+                bool isrep = false, rc = false, rc1 = false, rc2 = false;
                 if (act) {
+                    // the last offsets' 4 bytes load with the position's own
+                    rc = (key & kZstdRepCheck) && rep0 != 0u && p >= rep0;
+                    rc1 = (key & kZstdRep1) && rep1 != 0u && p >= rep1;
+                    rc2 = (key & kZstdRep1) && rep2 != 0u && p >= rep2;
                     w = ld4(src + p);
+                    wr = ld4(src + (rc ? p - rep0 : p));
+                    wr1 = ld4(src + (rc1 ? p - rep1 : p));
+                    wr2 = ld4(src + (rc2 ? p - rep2 : p));
                     const uint64_t k6 = key48(w, (key & 0xFFu) == 6 ? ld4(src + p + 4) : 0u,
                                               key & 0xFFu);
                     h = zhash<HL>(k6);
-                    tg = ztag(k6);
-                    const uint32_t e = table[h];
-                    if (e != kZstdNone && (e >> 17) == tg) c = e & kZstdPosMask;
+                    if constexpr (!NARROW) {
+                        tg = ztag(k6);
+                        const uint32_t e = table[h];
+                        if (e != kZstdNone && (e >> 17) == tg) c = e & kZstdPosMask;
+                    }
                 }
-                __builtin_amdgcn_wave_barrier();
-                if (act) table[h] = p | tg << 17;
-                __builtin_amdgcn_wave_barrier();
+                if constexpr (NARROW)
+                    if (act) c = narrow_cand(t16[h], p);
+                if (rc && wr == w) {
+                    c = p - rep0;
+                    isrep = true;
+                } else if (rc1 && wr1 == w) {  // the step's matches may have moved them
+                    c = p - rep1;
+                    isrep = true;
+                } else if (rc2 && wr2 == w) {
+                    c = p - rep2;
+                    isrep = true;
+                }
                 // a candidate's 4 bytes are checked from memory, in the same
                 // round trip as its extension: every candidate lane extends
                 // its own match by up to 16 bytes each way (most matches end
@@ -1192,7 +1235,7 @@ __global__ __launch_bounds__(64, HL == 11 ? 4 : 3) void rcdc_zstd_block_kernel(
                         bl = last_eq16(ld16(src + p - 16), ld16(src + c - 16));
                         if (bl > limb) bl = limb;
                     }
-                    ok = wc == w && 4 + fl >= (key & 0xFFu);
+                    ok = wc == w && (isrep || 4 + fl >= (key & 0xFFu));  // last offset: 4 bytes
                     if (ok && c < 16)
                         while (bl < limb && src[p - 1 - bl] == src[c - 1 - bl]) bl++;
                 }
@@ -1205,13 +1248,21 @@ __global__ __launch_bounds__(64, HL == 11 ? 4 : 3) void rcdc_zstd_block_kernel(
                 uint32_t tgt = lane;
                 {
                     const uint32_t fn = __shfl_down(fl, 1);
+                    const bool rn = __shfl_down((uint32_t)isrep, 1) != 0u;
                     const bool okn = lane < 63 && ((m >> (lane + 1)) & 1ull);
-                    if (stride == 1 && ok && fl < 16 && okn && fn > fl + 1) tgt = lane + 1;
+                    // the next position's match wins if it reaches two bytes
+                    // further (kZstdLazyRep: or if it is a last offset and
+                    // this one is not; off: CSV rows 0.194 vs 0.196 but code
+                    // lines 0.125 vs 0.119, tools/zstd_wave_model.py)
+                    if (stride == 1 && ok && okn &&
+                        ((fl < 16 && fn > fl + 1) || ((key & kZstdLazyRep) && rn && !isrep)))
+                        tgt = lane + 1;
                 }
                 // the round's sequences stay in the picked lanes' registers
                 // and are stored together after the loop
                 uint32_t vll = 0, vml = 0, vof = 0;
                 uint64_t sel = 0;
+                bool covered = false;  // p strictly inside a selected match
                 while (m) {
                     const int j = (int)rdl(tgt, __builtin_ctzll(m));
                     const uint32_t f = rdl(fl, j);
@@ -1233,7 +1284,7 @@ __global__ __launch_bounds__(64, HL == 11 ? 4 : 3) void rcdc_zstd_block_kernel(
                     // earlier blocks are unknown here: 0), else offset + 3
                     const uint32_t off = pj - cj, ll = pj - anchor;
                     uint32_t ofv;
-                    if (!(key & 0x100u)) {  // RCDC_ZSTD_REP=0 (A/B): literal offsets only
+                    if (!(key & kZstdRep)) {  // RCDC_ZSTD_REP=0 (A/B): literal offsets only
                         ofv = off + 3;
                     } else if (ll) {
                         if (off == rep0) {
@@ -1281,9 +1332,19 @@ __global__ __launch_bounds__(64, HL == 11 ? 4 : 3) void rcdc_zstd_block_kernel(
                     vof = me ? ofv : vof;
                     sel |= 1ull << j;
                     matched += len;
+                    covered = covered || (p > pj && p < pj + len);
                     anchor = pj + len;
                     m &= __ballot(p >= anchor);
                 }
+                // the step's positions into the table, except those inside
+                // the matches just taken (a match's own position stays): as
+                // zstd's parsers, which skip them, the table then reaches
+                // further back (CSV rows 0.31 -> 0.24, code lines 0.136 -> 0.123)
+                if (act && (!covered || ((sel >> lane) & 1ull) || (key & kZstdInsAll))) {
+                    if constexpr (NARROW) t16[h] = (uint16_t)p;
+                    else table[h] = p | tg << 17;
+                }
+                wave_lds_sync();
                 if ((sel >> lane) & 1ull)
                     seqs[nseq + __popcll(sel & ((1ull << lane) - 1ull))] = seq_pack(vll, vml, vof);
                 nseq += __popcll(sel);
@@ -1598,23 +1659,37 @@ void zstd_prof_dump() {
 // override for A/B runs; RCDC_ZSTD_REP=0 turns repeat codes off.
 struct ZstdStrategy {
     int hlog;
-    uint32_t key;  // key bytes | 0x100: repeat codes on
+    bool narrow;   // 16-bit table entries (twice the buckets per LDS byte)
+    uint32_t key;  // key bytes | kZstdRep | kZstdRepCheck
 };
 
 static ZstdStrategy zstd_strategy(int level) {
     static const int ek = getenv("RCDC_ZSTD_KEY") ? atoi(getenv("RCDC_ZSTD_KEY")) : 0;
     static const int eh = getenv("RCDC_ZSTD_HLOG") ? atoi(getenv("RCDC_ZSTD_HLOG")) : 0;
     static const bool rep = !(getenv("RCDC_ZSTD_REP") && atoi(getenv("RCDC_ZSTD_REP")) == 0);
+    static const bool rchk =
+        !(getenv("RCDC_ZSTD_REPCHK") && atoi(getenv("RCDC_ZSTD_REPCHK")) == 0);
+    static const bool insall = getenv("RCDC_ZSTD_INSALL") && atoi(getenv("RCDC_ZSTD_INSALL")) == 1;
+    static const bool rep1 = !(getenv("RCDC_ZSTD_REP1") && atoi(getenv("RCDC_ZSTD_REP1")) == 0);
+    static const bool lazyrep = getenv("RCDC_ZSTD_LAZYREP") && atoi(getenv("RCDC_ZSTD_LAZYREP")) == 1;
     if (level == 0) level = 3;  // ZSTD_CLEVEL_DEFAULT
-    ZstdStrategy z{level >= 4 ? 12 : 11, level <= 1 ? 6u : 4u};
+    ZstdStrategy z{11, false, level <= 1 ? 6u : 4u};
+    if (level >= 3) z = ZstdStrategy{level >= 4 ? 13 : 12, true, 6u};
     if (ek == 4 || ek == 6) z.key = (uint32_t)ek;
-    if (eh == 11 || eh == 12) z.hlog = eh;
-    if (rep) z.key |= 0x100u;
+    if (eh == 11) z.hlog = 11, z.narrow = false;
+    if (eh == 12 || eh == 13) z.hlog = eh, z.narrow = true;
+    if (rep) z.key |= kZstdRep;
+    if (rep && rchk) z.key |= kZstdRepCheck;
+    if (insall) z.key |= kZstdInsAll;
+    if (rep && rchk && rep1) z.key |= kZstdRep1;
+    if (lazyrep) z.key |= kZstdLazyRep;
     return z;
 }
 
+// LDS per wave: 8 KiB table (16 waves per CU) or 16 KiB (8)
 uint32_t zstd_block_grid(uint32_t cus, int level) {
-    return cus * (zstd_strategy(level).hlog == 11 ? 16u : 8u);
+    const ZstdStrategy z = zstd_strategy(level);
+    return cus * ((z.narrow ? z.hlog - 1 : z.hlog) == 11 ? 16u : 8u);
 }
 
 hipError_t launch_zstd(const uint8_t *in, uint8_t *out, const ZstdBlob *blobs, uint32_t nblobs,
@@ -1626,12 +1701,11 @@ hipError_t launch_zstd(const uint8_t *in, uint8_t *out, const ZstdBlob *blobs, u
     static const uint32_t dbg = getenv("RCDC_ZSTD_DBG") ? (uint32_t)atoi(getenv("RCDC_ZSTD_DBG")) : 0u;
     const uint32_t g = nblk < grid ? nblk : grid;
     if (g) {
-        if (z.hlog == 11)
-            hipLaunchKernelGGL(rcdc_zstd_block_kernel<11>, dim3(g), dim3(64), 0, stream, in, blobs,
-                               blks, nblk, tabs, slots, seqbuf, res, dbg, z.key, queue);
-        else
-            hipLaunchKernelGGL(rcdc_zstd_block_kernel<12>, dim3(g), dim3(64), 0, stream, in, blobs,
-                               blks, nblk, tabs, slots, seqbuf, res, dbg, z.key, queue);
+        auto *k = !z.narrow      ? rcdc_zstd_block_kernel<11, false>
+                  : z.hlog == 12 ? rcdc_zstd_block_kernel<12, true>
+                                 : rcdc_zstd_block_kernel<13, true>;
+        hipLaunchKernelGGL(k, dim3(g), dim3(64), 0, stream, in, blobs, blks, nblk, tabs, slots,
+                           seqbuf, res, dbg, z.key, queue);
     }
     hipLaunchKernelGGL(rcdc_zstd_frame_kernel, dim3((nblobs + 255) / 256), dim3(256), 0, stream,
                        blobs, nblobs, res, bpos, out, out_lens);
