@@ -153,7 +153,7 @@ struct WalkParams {
     uint64_t *wstate;
     uint64_t epoch;        // this run's, 1 .. 2^21 - 1 (the buffers start zeroed)
     uint32_t seed;         // seeding on
-    uint32_t pad2;
+    uint32_t early;        // hit rounds stop early, the owed tails spread over the lanes
 };
 constexpr uint64_t kEndOpen = 1ull << 63;
 constexpr uint64_t kEndPos = (1ull << 42) - 1;  // position bits of an end word

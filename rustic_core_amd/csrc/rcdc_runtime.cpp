@@ -701,6 +701,9 @@ rcdc_status plan_build(rcdc_ctx *ctx, rcdc_plan *pl, const uint64_t *offs, const
     // seeded piece starts (a walker continues its finished predecessor's chain)
     wp.seed = 1;
     if (const char *e = getenv("RCDC_WALK_SEED")) wp.seed = atoi(e) != 0;
+    // a hit round stops early and spreads the lanes' owed tails (round_first)
+    wp.early = 1;
+    if (const char *e = getenv("RCDC_WALK_EARLY")) wp.early = atoi(e) != 0;
     if (const char *e = getenv("RCDC_CHECK_BUDGET")) wp.chk_budget = strtoull(e, nullptr, 10);
     if (const char *e = getenv("RCDC_FIX_SEG")) wp.fix_seg = (uint32_t)std::max(atoi(e) / 128 * 128, 128);
     if (const char *e = getenv("RCDC_WALK_FIXCAP")) wp.fix_cap = (uint32_t)std::max(atoi(e), 1);  // tests

@@ -290,6 +290,41 @@ __device__ __forceinline__ Chain scan_segment(__amdgpu_buffer_rsrc_t rsrc, uint3
     return c;
 }
 
+// scan_segment that stops early (the walk's hit rounds): after each ring pass,
+// when a lane below 32 has a hit and at least 4 units per lane are left, it
+// returns with *done = the units every lane tested (else nunits).  The lanes
+// before the first hit lane then owe the rest of their segments, which the
+// caller spreads over all 64 lanes (walk round_first).
+template <int R, bool PAIR, int TSH, bool SMALL, int G>
+__device__ __forceinline__ Chain scan_segment_early(__amdgpu_buffer_rsrc_t rsrc, uint32_t voff,
+                                                    uint32_t nunits, uint32_t rlo, uint32_t rhi,
+                                                    const uint8_t *tab, const Consts &k,
+                                                    uint64_t valid, uint32_t lane, uint32_t &done,
+                                                    bool may_stop) {
+    Chain c;
+    c.h0 = c.h1 = 0;
+    c.first = c.last = kNone;
+    c.count = 0;
+    c.rlo = rlo;
+    c.rhi = rhi;
+    Unit u[R];
+#pragma unroll
+    for (int j = 0; j < R; j++)
+        if ((uint32_t)j <= nunits) load_unit(u[j], rsrc, voff + j * 64u);
+    warm_unit<TSH>(c, u[0], tab, k);
+    const bool lv = (valid >> lane) & 1u;
+    uint32_t i = 1;
+    done = nunits;
+    while (ring_pass<R, PAIR, TSH, SMALL, G>(c, u, i, nunits, rsrc, voff, tab, k, lv)) {
+        const uint64_t hb = __builtin_amdgcn_ballot_w64(c.first != kNone) & valid;
+        if (may_stop && hb && __builtin_ctzll(hb) < 32 && nunits - (i - 1) >= 4) {
+            done = i - 1;
+            break;
+        }
+    }
+    return c;
+}
+
 // Kernel prologue: 32 lane-private copies of OM and MOD into LDS (entry e of
 // copy c at e * 256 + c * 8; MOD kTableBytes further).  OM[e] = OUT'[e]
 // reduced: the top byte of out << 8 sits at bits deg .. deg + 7 and MOD's

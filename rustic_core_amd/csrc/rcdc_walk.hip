@@ -193,6 +193,7 @@ struct Walk {
     // are idle (the walk's tail), at most help_max per round of its own
     GapQueue *Q;
     uint32_t help_max;
+    uint32_t early;  // walk rounds: WalkParams.early (0 elsewhere)
 };
 
 // Segment of a round that starts at A and only needs positions below end:
@@ -222,8 +223,15 @@ __device__ __forceinline__ uint64_t round_base(uint64_t off, uint64_t q) {
 // hashes bytes [A - 64 + t*S, A + (t+1)*S): after the 64-byte warm-up the
 // first slide gives the window of position A + t*S + 1, so lane t tests
 // [A + 1 + t*S, A + 1 + (t+1)*S) (the scan kernel's r = 0 <-> lane start + 65).
-template <int LANES, int TSH, bool SMALL>
-__device__ uint64_t round_first(const Walk &W, uint64_t A, uint64_t q, uint64_t end, uint32_t S) {
+//
+// EARLY (the walker's own rounds, W.early): a hit round stops once a lane L
+// below 32 has a hit (scan_segment_early); lanes 0 .. L-1 owe the rest of
+// their segments, [done, S) each, which all 64 lanes then hash in one shorter
+// round (64 / L lanes per owed tail).  The first hit there, else lane L's, is
+// the round's.  *lb: the bytes the lanes hashed.
+template <int LANES, int TSH, bool SMALL, bool EARLY = false>
+__device__ uint64_t round_first(const Walk &W, uint64_t A, uint64_t q, uint64_t end, uint32_t S,
+                               uint64_t *lb = nullptr) {
     const uint64_t P0 = A + 1 + (uint64_t)W.tid * S;
     // signed clamps: hipcc (ROCm 7.2) dropped the `end > P0 ?` guard of the
     // unsigned form in the workgroup instantiation (lanes past `end` then
@@ -245,6 +253,45 @@ __device__ uint64_t round_first(const Walk &W, uint64_t A, uint64_t q, uint64_t 
             (uint32_t)(rest < 0xFFFFFFFFull ? rest : 0xFFFFFFFFull));
         const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
             (void *)(W.arena + wbase), (short)0, (int)rec, 0x00020000);
+        if constexpr (EARLY && LANES == 64) {
+            // one scan_segment site, run twice at most: the round (stopping
+            // early only while W.early), then the owed tails
+            uint32_t voff = W.lane * S, nun = S / kUnit, lo = rlo, hi = rhi, done;
+            uint64_t vm = valid, pbase = P0;
+            bool again = W.early != 0;
+            for (;;) {
+                const Chain c = scan_segment_early<kWR, kWPair, TSH, SMALL, kWG>(
+                    rsrc, voff, nun, lo, hi, W.tab, W.k, vm, W.lane, done, again);
+                const uint64_t hits = __builtin_amdgcn_ballot_w64(c.first != kNone) & vm;
+                if (hits) best = readlane64(pbase + c.first, (uint32_t)__builtin_ctzll(hits));
+                if (!again || done == nun) break;  // the tails' round, or a full round
+                // stopped early (a lane L < 32 has a hit): lanes 0 .. L-1 owe
+                // [done units, S) of their segments
+                again = false;
+                const uint32_t L = (uint32_t)__builtin_ctzll(hits);
+                if (lb) *lb = 64ull * (done * 64u + 64u);
+                if (L == 0) break;
+                const uint32_t kk = 64u / L;  // >= 2 lanes per owed tail
+                const uint32_t t0 = done * 64u, rem = S - t0;
+                const uint32_t part = ((rem + kk - 1) / kk + 63u) / 64u * 64u;
+                const uint32_t i = W.lane / kk, j = W.lane % kk;
+                const uint32_t st = t0 + j * part;
+                const bool on = i < L && st < S;
+                const uint32_t len = on ? min(part, S - st) : 0u;
+                // the owed lane's range of counted positions, shifted to this part
+                const int32_t ilo = __shfl((int32_t)rlo, (int)min(i, 63u));
+                const int32_t ihi = __shfl((int32_t)rhi, (int)min(i, 63u));
+                lo = (uint32_t)min(max(ilo - (int32_t)st, 0), (int32_t)len);
+                hi = (uint32_t)min(max(ihi - (int32_t)st, 0), (int32_t)len);
+                vm = __builtin_amdgcn_ballot_w64(on && lo < hi);
+                if (!vm) break;
+                voff = i * S + st;
+                nun = part / kUnit;
+                pbase = A + 1 + (uint64_t)i * S + st;
+                if (lb) *lb += 64ull * (part + 64u);
+            }
+            return best;
+        }
         const Chain c = scan_segment<kWR, kWPair, TSH, SMALL, kWG>(rsrc, W.lane * S, S / kUnit,
                                                                    rlo, rhi, W.tab, W.k, valid,
                                                                    W.lane);
@@ -472,8 +519,9 @@ __device__ uint64_t walk_search(Walk &W, uint64_t q, uint64_t limit, uint64_t st
         }
         const uint32_t S = round_seg<LANES>(W.S, A, end);
         W.rounds++;
-        W.lbytes += (uint64_t)LANES * (S + 64);
-        uint64_t p = round_first<LANES, TSH, SMALL>(W, A, q, end, S);
+        uint64_t lb = (uint64_t)LANES * (S + 64);
+        uint64_t p = round_first<LANES, TSH, SMALL, true>(W, A, q, end, S, &lb);
+        W.lbytes += lb;
         if constexpr (LANES == 64) {
             if (K) p = walk_wait(W, p);
         }
@@ -553,6 +601,7 @@ __global__ __launch_bounds__(1024, 1) void rcdc_walk_kernel(
     W.tid = lane;
     W.Q = prm.helpers ? &s_q : nullptr;
     W.help_max = __builtin_amdgcn_readfirstlane(min(prm.helpers, kHelpMax));
+    W.early = prm.early;
     uint64_t help_rounds = 0, help_bytes = 0;  // rounds this wave ran for others
     for (;;) {
         uint32_t q = 0;
@@ -984,6 +1033,7 @@ __global__ __launch_bounds__(CT, 1) void rcdc_walk_check_kernel(
     W.tid = lane;
     W.Q = nullptr;
     W.help_max = 0;
+    W.early = 0;
     const ModRepl mod{s_tab, W.k.lwm};
     const uint64_t mn = prm.min_size, mx = prm.max_size;
     for (;;) {
@@ -1216,6 +1266,7 @@ __global__ __launch_bounds__(1024, 1) void rcdc_walk_fixup_kernel(
     W.tid = threadIdx.x;
     W.Q = nullptr;
     W.help_max = 0;
+    W.early = 0;
     for (uint32_t idx = blockIdx.x; idx < nfix; idx += gridDim.x) {
         const uint32_t u = fixlist[idx];
         const WalkUnit U = units[u];
