@@ -600,6 +600,9 @@ class HostIngest:
         s_h2d, s_d2h = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
         ev_h2d = [None] * len(batches)
         pool = ThreadPoolExecutor(max_workers=self.hash_threads)
+        # one thread waits for the copy-back events (in order) and hands each
+        # landed group to the hash threads: a hash thread never blocks on one
+        waiter = ThreadPoolExecutor(max_workers=1)
         lock = threading.Lock()
         ids_out, offs_out, sizes_out, futs, keep = [], [], [], [], []
         state = {"host_off": 0, "d2h": 0, "host": host}
@@ -665,7 +668,7 @@ class HostIngest:
                             ev.synchronize()
                             return [pool.submit(hash_pack, buf, o0 + o, n, j0 + j)
                                     for j, (o, n) in enumerate(grp)]
-                        futs.append(pool.submit(job))
+                        futs.append(waiter.submit(job))
                         g0 = g1
                     ev_all = torch.cuda.Event()
                     ev_all.record(s_d2h)
@@ -747,6 +750,7 @@ class HostIngest:
                 g.result()
         seconds = time.perf_counter() - t0
         pool.shutdown()
+        waiter.shutdown()
         id_pool.shutdown()
         # pack-id hashing: thread-seconds spent, and its window
         ms["hash_thread_s"] = round(hstat["busy_s"], 3)
