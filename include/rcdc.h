@@ -260,6 +260,14 @@ rcdc_status rcdc_sha256_chunks(rcdc_ctx *ctx, const void *d_arena,
                                const rcdc_chunk_ref *d_refs, uint32_t n,
                                uint8_t *d_digests, void *hip_stream);
 
+/* SHA-256 of n buffers in host memory (pack ids: blob/packer.rs:832-834
+ * `hash_reader` of each finished pack file), on the calling thread: 16
+ * messages side by side in the lanes of AVX-512 registers, a lane taking the
+ * next message when its own ends.  digests: 32 bytes per buffer.
+ * RCDC_ERR_UNSUPPORTED on a CPU without AVX-512F/BW (no digest written).   */
+rcdc_status rcdc_sha256_host(const void *const *ptrs, const uint64_t *lens, uint32_t n,
+                             uint8_t *digests);
+
 /* Fused blob ids of a plan: after rcdc_plan_run over d_arena (the same
  * pointer), enqueue the SHA-256 of every chunk it found, on the device
  * cut list (no host round trip).  Asynchronous.                           */

@@ -39,6 +39,9 @@ hipError_t launch_resolve(const uint8_t *arena, const StreamDesc *sds, const Res
                           const uint64_t *item_masks, uint64_t *cuts, uint64_t *counts,
                           uint64_t *piece_cuts, uint64_t *piece_counts, uint64_t *stats,
                           hipStream_t stream);
+bool host_sha_supported();
+void host_sha256_many(const uint8_t *const *ptrs, const uint64_t *lens, uint32_t n,
+                      uint8_t *digests);
 hipError_t launch_walk(const uint8_t *arena, const StreamDesc *sds, const WalkUnit *units,
                        const WalkParams &prm, const uint64_t *gtab, uint64_t *piece_cuts,
                        uint64_t *pstatus, uint32_t *ctr, uint32_t blocks, hipStream_t stream,
@@ -1752,6 +1755,16 @@ uint64_t rcdc_fixed_cuts(uint64_t n, uint64_t size, uint64_t *cuts, uint64_t cap
 }
 
 // ---- SHA-256 blob ids (crypto/hasher.rs:17-19, file_archiver.rs:151) -----
+
+rcdc_status rcdc_sha256_host(const void *const *ptrs, const uint64_t *lens, uint32_t n,
+                             uint8_t *digests) {
+    if (n && (!ptrs || !lens || !digests)) return fail(RCDC_ERR_INVALID_INPUT, "null argument");
+    for (uint32_t i = 0; i < n; i++)
+        if (!ptrs[i] && lens[i]) return fail(RCDC_ERR_INVALID_INPUT, "null buffer");
+    if (!host_sha_supported()) return fail(RCDC_ERR_UNSUPPORTED, "CPU without AVX-512F/BW");
+    host_sha256_many(reinterpret_cast<const uint8_t *const *>(ptrs), lens, n, digests);
+    return RCDC_OK;
+}
 
 rcdc_status rcdc_sha256_chunks(rcdc_ctx *ctx, const void *d_arena, const rcdc_chunk_ref *d_refs,
                                uint32_t n, uint8_t *d_digests, void *hip_stream) {

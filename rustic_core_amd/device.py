@@ -177,6 +177,27 @@ def hash_many(plans, d_arena_ptrs, hip_stream: Optional[int] = None) -> None:
         raise status_error(st, _lib.last_error())
 
 
+def sha256_host_supported() -> bool:
+    """rcdc_sha256_host runs on this CPU (AVX-512F/BW)."""
+    return _lib.lib().rcdc_sha256_host(None, None, 0, None) == 0
+
+
+def sha256_host(addrs, lens) -> list:
+    """SHA-256 of host buffers (addresses and lengths; pack files,
+    packer.rs:832-834) on the calling thread, 16 at a time in AVX-512 lanes
+    (rcdc_sha256_host; the GIL is released during the call).  Raises
+    RusticError (Unsupported) on a CPU without AVX-512F/BW."""
+    n = len(addrs)
+    ptrs = (ctypes.c_void_p * max(n, 1))(*[int(a) for a in addrs])
+    ls = (ctypes.c_uint64 * max(n, 1))(*[int(x) for x in lens])
+    out = ctypes.create_string_buffer(32 * max(n, 1))
+    st = _lib.lib().rcdc_sha256_host(ptrs, ls, n, out)
+    if st:
+        raise status_error(st, _lib.last_error())
+    raw = out.raw
+    return [raw[32 * i:32 * i + 32] for i in range(n)]
+
+
 def sha256_device(ctx: Context, arena_tensor, refs, out_tensor=None, stream=None):
     """SHA-256 of chunks ``refs`` (an ``(n, 2)`` int64 CUDA tensor of
     ``(offset, length)`` rows) of a device arena; returns an ``(n, 32)``

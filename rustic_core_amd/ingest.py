@@ -44,7 +44,7 @@ import numpy as np
 from .chunker import ConfigFile, Context
 from .compress import check_frames, compress_blobs, make_refs as zstd_refs, zstd_bounds
 from .crypto import Key, make_refs as aead_refs
-from .device import DevicePlan, sha256_device
+from .device import DevicePlan, sha256_device, sha256_host, sha256_host_supported
 from .errors import ErrorKind, RusticError
 from .compress import VERIFY_MESSAGE
 from .index import IndexPack, index_packs_from_build
@@ -578,6 +578,11 @@ class HostIngest:
         # ~0.27 s per 8 MiB chunk)
         self.host_edge_ids = True
         self.host_tail_ids = 3  # the last batches whose long ids the host computes
+        # pack ids of all but the last host_tail_ids batches 16 packs at a time
+        # in AVX-512 lanes (rcdc_sha256_host: ~2x a core's SHA extensions per
+        # core); the last batches' packs one per thread (hashlib), whose
+        # latency (~16 ms per 40 MB pack, not ~16x that) the run's end waits on
+        self.multi_buffer_ids = sha256_host_supported()
 
     def run(self, files) -> HostIngestResult:
         """`files`: 1-D uint8 CPU tensors (pinned for full-rate copies)."""
@@ -629,7 +634,19 @@ class HostIngest:
                 hstat["first"] = a if hstat["first"] is None else min(hstat["first"], a)
                 hstat["last"] = max(hstat["last"], b)
 
-        def handoff(res):
+        def hash_group(buf, grp, j0, base_addr):
+            # one call, up to 16 packs side by side (GIL released inside)
+            a = time.perf_counter()
+            ds = sha256_host([base_addr + o for o, _ in grp], [n for _, n in grp])
+            b = time.perf_counter()
+            with lock:
+                for j, d in enumerate(ds):
+                    ids_out[j0 + j] = d
+                hstat["busy_s"] += b - a
+                hstat["first"] = a if hstat["first"] is None else min(hstat["first"], a)
+                hstat["last"] = max(hstat["last"], b)
+
+        def handoff(res, k):
             # the packs of one batch: D2H into the pinned buffer, then hashed
             t = time.perf_counter()
             total = res.pack_bytes
@@ -652,11 +669,13 @@ class HostIngest:
                 # event each: hashing starts with the first group, not after
                 # the whole batch
                 g0 = 0
+                mb = self.multi_buffer_ids and k < len(batches) - self.host_tail_ids
                 with torch.cuda.stream(s_d2h):
                     s_d2h.wait_stream(torch.cuda.current_stream(dev))
                     while g0 < len(rows):
                         g1, gb = g0, 0
-                        while g1 < len(rows) and (g1 == g0 or gb < self.d2h_group):
+                        while g1 < len(rows) and (g1 == g0 or (g1 - g0 < 16 if mb else
+                                                               gb < self.d2h_group)):
                             gb += rows[g1][1]
                             g1 += 1
                         a, e = rows[g0][0], rows[g1 - 1][0] + rows[g1 - 1][1]
@@ -664,8 +683,11 @@ class HostIngest:
                         ev = torch.cuda.Event()
                         ev.record(s_d2h)
 
-                        def job(ev=ev, grp=rows[g0:g1], j0=base + g0, buf=buf):
+                        def job(ev=ev, grp=rows[g0:g1], j0=base + g0, buf=buf, mb=mb):
                             ev.synchronize()
+                            if mb:
+                                return [pool.submit(hash_group, buf, [(o0 + o, n) for o, n in grp],
+                                                    j0, buf.data_ptr())]
                             return [pool.submit(hash_pack, buf, o0 + o, n, j0 + j)
                                     for j, (o, n) in enumerate(grp)]
                         futs.append(waiter.submit(job))
@@ -733,7 +755,7 @@ class HostIngest:
                 ms["end"] += (time.perf_counter() - t) * 1e3
                 ms[f"end{k - 1}"] = (time.perf_counter() - t) * 1e3
                 ms[f"at{k - 1}"] = (time.perf_counter() - t0) * 1e3
-                handoff(r)
+                handoff(r, k - 1)
                 results.append(r)
                 # the slot of batch k - 1 is free: batch k + 2 goes there
                 if k + 2 < len(batches):
@@ -742,7 +764,7 @@ class HostIngest:
         t = time.perf_counter()
         r = self.ingest.end(pending, finalize=True)
         ms["end"] += (time.perf_counter() - t) * 1e3
-        handoff(r)
+        handoff(r, len(batches) - 1)
         results.append(r)
         ms["last_end"] = (time.perf_counter() - t0) * 1e3
         for f in futs:  # the per-batch waiters, then their pack jobs

@@ -1,0 +1,40 @@
+"""rcdc_sha256_host (include/rcdc.h): SHA-256 of many host buffers, 16 side
+by side in AVX-512 lanes -- HostIngest's pack ids (blob/packer.rs:832-834
+`hash_reader`).  Checked against hashlib on every padding case (lengths
+around the 55/56/64-byte block edges), empty messages, and more messages
+than lanes of unequal lengths (a lane takes the next message when its own
+ends).  CPU only."""
+import hashlib
+
+import numpy as np
+import pytest
+
+from rustic_core_amd.device import sha256_host, sha256_host_supported
+
+pytestmark = pytest.mark.skipif(not sha256_host_supported(), reason="CPU without AVX-512F/BW")
+
+
+def _check(lens, seed=0):
+    rng = np.random.default_rng(seed)
+    bufs = [rng.integers(0, 256, n, dtype=np.uint8) for n in lens]
+    got = sha256_host([b.ctypes.data for b in bufs], [b.size for b in bufs])
+    assert got == [hashlib.sha256(b.tobytes()).digest() for b in bufs]
+
+
+def test_block_edges():
+    _check(list(range(0, 200)))
+
+
+def test_more_messages_than_lanes():
+    rng = np.random.default_rng(7)
+    _check([int(x) for x in rng.integers(0, 70000, 53)] + [1 << 20, 3, 0, 64 * 1000 + 55], seed=1)
+
+
+def test_none():
+    assert sha256_host([], []) == []
+
+
+def test_bad_input():
+    from rustic_core_amd.errors import RusticError
+    with pytest.raises(RusticError):
+        sha256_host([0], [5])  # a null buffer with bytes

@@ -208,6 +208,8 @@ def main():
     ap.add_argument("--open-packs", type=int, default=3)
     ap.add_argument("--repeat", type=int, default=1, help="timed runs (fresh repository each)")
     ap.add_argument("--no-checks", action="store_true")
+    ap.add_argument("--no-multi-buffer", action="store_true",
+                    help="pack ids with hashlib only (no rcdc_sha256_host)")
     ap.add_argument("--json", default=None)
     ap.add_argument("--hw-queues", default="16", help="GPU_MAX_HW_QUEUES for this process "
                     "(set before HIP initialises; --hw-queues=N form)")
@@ -233,6 +235,8 @@ def main():
     torch.cuda.synchronize(dev)
     log("warm-up done")
     hi = HostIngest(cfg, Key(key), **kw)
+    if a.no_multi_buffer:
+        hi.multi_buffer_ids = False
     res = hi.run(files)
     total = sum(int(f.numel()) for f in files)
     log(f"run: {res.seconds:.3f} s, {total / res.seconds / GiB:.1f} GiB/s, "
@@ -274,6 +278,7 @@ def main():
                                     "seconds_alone"},
         "batches": [len(b) for b in res.batch_files],
         "hash_threads": hi.hash_threads,
+        "multi_buffer_ids": hi.multi_buffer_ids,
         "gpu_max_hw_queues": os.environ.get("GPU_MAX_HW_QUEUES"),
         "host_ms": {k: (round(v, 1) if isinstance(v, float) else v) for k, v in res.ms.items()},
         "packs": len(res.pack_ids),
@@ -282,8 +287,9 @@ def main():
                 "extra_verify on",
         "path": "rustic_core_amd.ingest.HostIngest: H2D (copy stream) -> DeviceIngest.begin "
                 "(chunk, ids, long chunks speculatively) / end (dedup, short chunks, packs; "
-                "packer open across batches) -> D2H (second copy stream) -> pack ids (hashlib "
-                "on host threads)",
+                "packer open across batches) -> D2H (second copy stream) -> pack ids on host "
+                "threads (rcdc_sha256_host, 16 packs per call in AVX-512 lanes; hashlib for "
+                "the last batches)",
     }
     if chk is not None:
         line["checks"] = chk
