@@ -578,11 +578,15 @@ class HostIngest:
         # ~0.27 s per 8 MiB chunk)
         self.host_edge_ids = True
         self.host_tail_ids = 3  # the last batches whose long ids the host computes
-        # pack ids of all but the last host_tail_ids batches 16 packs at a time
+        # pack ids of all but the last hashlib_tail batches 16 packs at a time
         # in AVX-512 lanes (rcdc_sha256_host: ~2x a core's SHA extensions per
         # core); the last batches' packs one per thread (hashlib), whose
         # latency (~16 ms per 40 MB pack, not ~16x that) the run's end waits on
         self.multi_buffer_ids = sha256_host_supported()
+        self.hashlib_tail = 2  # the last batches whose pack ids go one per thread
+        # batches before those hashed 8 packs per call (half the lanes, half the
+        # latency); 0: measured best (groups of 8 left a larger backlog)
+        self.mb_half_batches = 0
 
     def run(self, files) -> HostIngestResult:
         """`files`: 1-D uint8 CPU tensors (pinned for full-rate copies)."""
@@ -669,12 +673,13 @@ class HostIngest:
                 # event each: hashing starts with the first group, not after
                 # the whole batch
                 g0 = 0
-                mb = self.multi_buffer_ids and k < len(batches) - self.host_tail_ids
+                mb = self.multi_buffer_ids and k < len(batches) - self.hashlib_tail
+                mb_n = 8 if k >= len(batches) - self.hashlib_tail - self.mb_half_batches else 16
                 with torch.cuda.stream(s_d2h):
                     s_d2h.wait_stream(torch.cuda.current_stream(dev))
                     while g0 < len(rows):
                         g1, gb = g0, 0
-                        while g1 < len(rows) and (g1 == g0 or (g1 - g0 < 16 if mb else
+                        while g1 < len(rows) and (g1 == g0 or (g1 - g0 < mb_n if mb else
                                                                gb < self.d2h_group)):
                             gb += rows[g1][1]
                             g1 += 1

@@ -210,6 +210,10 @@ def main():
     ap.add_argument("--no-checks", action="store_true")
     ap.add_argument("--no-multi-buffer", action="store_true",
                     help="pack ids with hashlib only (no rcdc_sha256_host)")
+    ap.add_argument("--mb-half", type=int, default=None,
+                    help="HostIngest.mb_half_batches (batches hashed 8 packs per call)")
+    ap.add_argument("--hashlib-tail", type=int, default=None,
+                    help="HostIngest.hashlib_tail (last batches hashed one pack per thread)")
     ap.add_argument("--json", default=None)
     ap.add_argument("--hw-queues", default="16", help="GPU_MAX_HW_QUEUES for this process "
                     "(set before HIP initialises; --hw-queues=N form)")
@@ -237,6 +241,10 @@ def main():
     hi = HostIngest(cfg, Key(key), **kw)
     if a.no_multi_buffer:
         hi.multi_buffer_ids = False
+    if a.mb_half is not None:
+        hi.mb_half_batches = a.mb_half
+    if a.hashlib_tail is not None:
+        hi.hashlib_tail = a.hashlib_tail
     res = hi.run(files)
     total = sum(int(f.numel()) for f in files)
     log(f"run: {res.seconds:.3f} s, {total / res.seconds / GiB:.1f} GiB/s, "
