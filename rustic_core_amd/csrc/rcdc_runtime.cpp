@@ -228,6 +228,8 @@ struct rcdc_plan {
     // bound and each workgroup holds a whole CU (128 KiB of LDS tables), so
     // overlapped with the next walk it runs on few CUs (RCDC_CHK_BLOCKS)
     uint32_t chk_blocks_pipe = 64;
+    uint32_t fix_blocks_pipe = 64;  // chain workgroups beside the next walk (RCDC_CHAIN_BLOCKS;
+                                    // 64 vs 32: C3 -0.7 %, C4 +1.5 %, profiles/r04/chain_blocks.txt)
     uint32_t pp = 0;                  // buffer set of the next run
     uint32_t last_set = 0;            // buffer set of the last run
     uint4 *d_sums2 = nullptr;
@@ -905,7 +907,7 @@ rcdc_status plan_run(rcdc_plan *pl, const void *d_arena, hipStream_t stream) {
                               (uint32_t)pl->wstream_u0.size(), wprm, ctx->d_tables,
                               wpiece, pstatus, bres, ctr, fixlist,
                               fixcuts, fixres, pl->d_cuts, pl->d_counts,
-                              pl->pipelined ? std::min<uint32_t>(cus, 32) : cus,
+                              pl->pipelined ? std::min<uint32_t>(cus, pl->fix_blocks_pipe) : cus,
                               pl->pipelined ? pl->chk_blocks_pipe : cus, stream,
                               pl->pipelined));
     if (ev) HIP_TRY(hipEventRecord(ev[2], stream));
@@ -1674,6 +1676,7 @@ rcdc_status rcdc_plan_set_pipeline(rcdc_plan *plan, int enable) {
     }
     plan->pp = 0;
     if (const char *e = getenv("RCDC_CHK_BLOCKS")) plan->chk_blocks_pipe = (uint32_t)std::max(atoi(e), 1);
+    if (const char *e = getenv("RCDC_CHAIN_BLOCKS")) plan->fix_blocks_pipe = (uint32_t)std::max(atoi(e), 1);
     plan->pipelined = true;
     return RCDC_OK;
 }
