@@ -27,7 +27,7 @@ fi
 i=0
 for e in "$@"; do
   i=$((i+1))
-  timeout -k 10 300 env $e $B --no-parity > $OUT/sw$i.json 2> $OUT/sw$i.err || { tail -20 $OUT/sw$i.err; exit 1; }
+  timeout -k 10 300 env $(echo $e | tr , " ") $B --no-parity > $OUT/sw$i.json 2> $OUT/sw$i.err || { tail -20 $OUT/sw$i.err; exit 1; }
   summ $OUT/sw$i.json "$e"
 done
 echo done
