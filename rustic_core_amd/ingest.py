@@ -557,7 +557,7 @@ class HostIngest:
     def __init__(self, config: ConfigFile, key: Key, device: int = 0,
                  indexed: Optional[set] = None, extra_verify: Optional[bool] = None,
                  hash_threads: Optional[int] = None, first_batch: int = 2 << 30,
-                 batch: int = 12 << 30, last_batch: int = 1 << 30,
+                 batch: int = 8 << 30, last_batch: int = 1 << 30,
                  pack_ratio: float = 0.8):
         self.ingest = DeviceIngest(config, key, device, indexed, extra_verify)
         self.device = device

@@ -202,7 +202,7 @@ def main():
     ap.add_argument("--files", type=int, default=96)
     ap.add_argument("--file-gib", type=float, default=1.0)
     ap.add_argument("--first-gib", type=float, default=2)
-    ap.add_argument("--batch-gib", type=float, default=12)
+    ap.add_argument("--batch-gib", type=float, default=8)
     ap.add_argument("--last-gib", type=float, default=1)
     ap.add_argument("--hash-threads", type=int, default=None)
     ap.add_argument("--open-packs", type=int, default=3)
