@@ -125,7 +125,7 @@ struct WalkParams {
     uint32_t nunits;
     uint32_t fix_cap;      // fixup cut slots per boundary
     uint32_t fix_seg;      // S for the fixup walker (latency-bound: smaller rounds)
-    uint32_t pad;
+    uint32_t seed_classes; // queue classes by piece index mod K (seeded starts)
     // kWalkStat* counters (always on: one atomic per piece / fixup boundary)
     unsigned long long *stats;
     // optional per-piece trace (nullptr = off): kTraceWords u64 per unit

@@ -706,6 +706,14 @@ rcdc_status plan_build(rcdc_ctx *ctx, rcdc_plan *pl, const uint64_t *offs, const
     // seeded piece starts (a walker continues its finished predecessor's chain)
     wp.seed = 1;
     if (const char *e = getenv("RCDC_WALK_SEED")) wp.seed = atoi(e) != 0;
+    // queue classes by piece index mod K: even pieces before odd ones (K = 2)
+    // for streams of many pieces; thirds (K = 3) when streams average under
+    // 64 pieces (C4 share +1.2 %, lane/ref 1.110 -> 1.102; C3's 256-piece
+    // streams lose 0.3 % at K = 3, profiles/r04/seed_classes.txt)
+    const uint64_t nws = std::max<uint64_t>(pl->wstream_u0.size(), 1);
+    wp.seed_classes = pl->wunits.size() / nws < 64 ? 3 : 2;
+    // (RCDC_WALK_CLASSES: 1-8, experiments)
+    if (const char *e = getenv("RCDC_WALK_CLASSES")) wp.seed_classes = (uint32_t)std::min(std::max(atoi(e), 1), 8);
     // a hit round stops early and spreads the lanes' owed tails (round_first)
     wp.early = 1;
     if (const char *e = getenv("RCDC_WALK_EARLY")) wp.early = atoi(e) != 0;

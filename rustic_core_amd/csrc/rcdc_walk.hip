@@ -1577,9 +1577,13 @@ __global__ __launch_bounds__(256) void rcdc_walk_cost_kernel(
         const uint64_t w = a + 8 <= d.off + d.n ? *reinterpret_cast<const uint64_t *>(arena + a) : 0;
         const uint32_t cls = (uint32_t)__builtin_popcountll(__ballot(w != 0));
         const uint64_t quantum = max(prm.piece_bytes / 48, (uint64_t)1);
-        const uint64_t cost = min(len * cls / 64 / quantum, (uint64_t)(kCostKeys / 2 - 1));
-        const uint64_t even = prm.seed ? (uint64_t)((U.piece & 1u) == 0u) : 0u;
-        if (lane == 0) key[q] = (uint8_t)(cost * 2 + even);
+        // K classes by piece index: at equal cost, a stream's pieces 0, K,
+        // 2K, ... go first, then 1, K + 1, ... (each then mostly starts
+        // after its predecessor has finished and continues its chain)
+        const uint32_t K = prm.seed ? max(prm.seed_classes, 1u) : 1u;
+        const uint64_t cost = min(len * cls / 64 / quantum, (uint64_t)(kCostKeys / K - 1));
+        const uint64_t cl = K - 1u - U.piece % K;
+        if (lane == 0) key[q] = (uint8_t)(cost * K + cl);
     }
 }
 
