@@ -199,6 +199,22 @@ def test_walk_split_pieces(walk_env, monkeypatch, costsort):
                  np.concatenate([_rand(97, 999), np.zeros(3 * MiB, np.uint8), _rand(98, MiB)])])
 
 
+@pytest.mark.parametrize("early,classes", [("0", "2"), ("1", "1"), ("1", "3"), ("1", "4")])
+def test_walk_early_rounds_and_queue_classes(walk_env, monkeypatch, early, classes):
+    """Round-4 walk knobs on every data kind: hit rounds that stop early and
+    spread the owed segment tails (RCDC_WALK_EARLY), and the queue's classes
+    by piece index (RCDC_WALK_CLASSES), with the cost-ordered queue and
+    seeded starts on; the cuts stay the oracle's."""
+    walk_env(256 * KiB)
+    monkeypatch.setenv("RCDC_WALK_EARLY", early)
+    monkeypatch.setenv("RCDC_WALK_CLASSES", classes)
+    monkeypatch.setenv("RCDC_WALK_COSTSORT", "1")
+    _run(SMALL, [_rand(195, 9 * MiB + 7), np.zeros(3 * MiB, np.uint8),
+                 _mixed(196, 12 * MiB, 4 * KiB, 512 * KiB, 1 * KiB, 600 * KiB),
+                 np.concatenate([_rand(197, 4321), np.zeros(2 * MiB, np.uint8), _rand(198, 3 * MiB)]),
+                 _rand(199, 7 * MiB)])
+
+
 def test_walk_many_pieces_per_stream(walk_env):
     # > 1024 pieces per stream: the assembler follows the chain over several
     # node blocks, and the phase-shifted 40 MiB zero run's fixup merges more
