@@ -2,7 +2,8 @@
 # Round-4 PMC pass on the final tree: for C4 (1024-file share), C3 and C2 the
 # bench line, then FETCH_SIZE and WRITE_SIZE of the dominant kernel in
 # separate rocprofv3 passes (-> profiles/pmc_<W>.json via tools/pmc_json.py
-# gpurun_out/$1/<W> <W> <kernel> "<source>"); two SQ passes on C4.
+# gpurun_out/$1/<W> <W> <kernel> "<source>"); two SQ passes on C4 (C4SQ=C4) and
+# C3 (C3SQ=C3).
 # Output under gpurun_out/$1/<W>.
 set -o pipefail
 OUT=gpurun_out/${1:-r4pmc}
@@ -25,9 +26,12 @@ for W in ${WORKLOADS:-C4 C3 C2}; do
   done
   echo "$W pmc ok"
 done
-if [ -n "$C4SQ" ]; then
-  D=$OUT/C4
-  B="bench.py --workload C4 --c4-files 1024 --no-cpu-baseline"
+for SQW in $C4SQ $C3SQ; do
+  case $SQW in
+    C3) D=$OUT/C3; B="bench.py --no-cpu-baseline --no-ingest" ;;
+    *) D=$OUT/C4; B="bench.py --workload C4 --c4-files 1024 --no-cpu-baseline" ;;
+  esac
+  mkdir -p $D
   P1="SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_LDS SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS GRBM_GUI_ACTIVE"
   P2="SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS SQ_INSTS_BRANCH SQ_ACTIVE_INST_SCA SQ_WAIT_ANY SQ_ACTIVE_INST_ANY"
   for c in "$P1" "$P2"; do
@@ -44,6 +48,6 @@ for k,v in agg.items(): print(f"{k:28s} {sum(v)/len(v):16.6g} (n={len(v)})")
 PY
   done > $D/sq_summary.txt
   cat $D/sq_summary.txt
-fi
+done
 find $OUT -name "*counter_collection.csv" -size +20M -delete
 echo done
