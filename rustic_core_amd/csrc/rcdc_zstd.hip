@@ -122,7 +122,9 @@ __device__ __forceinline__ uint32_t ld4_lo(const uint8_t *p, const uint8_t *lo) 
 // matches cost more sequence bits than the literals they replace; 6-byte keys
 // pay only with enough buckets).
 __device__ __forceinline__ uint64_t key48(uint32_t w, uint32_t w2, uint32_t key) {
-    return key == 6 ? (uint64_t)w | (uint64_t)(w2 & 0xFFFFu) << 32 : (uint64_t)w;
+    return key == 6   ? (uint64_t)w | (uint64_t)(w2 & 0xFFFFu) << 32
+           : key == 5 ? (uint64_t)w | (uint64_t)(w2 & 0xFFu) << 32
+                      : (uint64_t)w;
 }
 
 template <int HL>
@@ -157,7 +159,7 @@ __device__ __forceinline__ uint32_t narrow_cand(uint32_t e, uint32_t p) {
 // repcode check: taken before a table match, and one position later wins
 // over a table match here)
 constexpr uint32_t kZstdRep = 0x100u, kZstdRepCheck = 0x200u, kZstdInsAll = 0x400u,
-                   kZstdRep1 = 0x800u, kZstdLazyRep = 0x1000u;
+                   kZstdRep1 = 0x800u, kZstdLazyRep = 0x1000u, kZstdAdaptKey = 0x2000u;
 
 // Equal bytes of a[0..) and b[0..), at most maxlen (wave-uniform result).
 // Lane l compares 16 bytes per round (1 KiB per wave round); the last,
@@ -1140,6 +1142,7 @@ __global__ __launch_bounds__(64, (NARROW ? HL - 1 : HL) == 11 ? 4 : 2) void rcdc
             // order-0 entropy of four 1 KiB windows spread over the block;
             // all near 8 bits per byte -> stored raw without a parse (the
             // plug-in estimate of random bytes over 4 KiB is ~7.95)
+            uint32_t keyb = key & 0xFFu;  // this block's key bytes
             if (n >= 8192) {
                 uint32_t *hs = table;
                 for (uint32_t i = lane; i < 256; i += 64) hs[i] = 0;
@@ -1158,6 +1161,18 @@ __global__ __launch_bounds__(64, (NARROW ? HL - 1 : HL) == 11 ? 4 : 2) void rcdc
                 if (hb > 7.9f * 4096.f) {
                     if (lane == 0) res[b] = make_uint2(kZstdTypeRaw, n);
                     continue;
+                }
+                // kZstdAdaptKey: 5-byte keys unless the sample is numeric
+                // (>= 10 % ASCII digits).  Rows of numbers repeat in 4-5
+                // byte pieces that cost more sequence bits than their
+                // literals; prose's one- and two-word matches pay from 5
+                // (tools/zstd_wave_model.py: text 0.384 -> 0.367, CSV rows
+                // and code lines unchanged at their 6-byte ratios)
+                if (key & kZstdAdaptKey) {
+                    const uint32_t dg = lane < 10 ? hs[48 + lane] : 0u;
+                    uint32_t sd = dg;
+                    for (int d = 32; d >= 1; d >>= 1) sd += __shfl_xor(sd, d);
+                    keyb = sd * 10u < 4096u ? 5u : 6u;
                 }
             }
             for (uint32_t i = lane; i < kTabWords; i += 64) table[i] = kZstdNone;
@@ -1181,8 +1196,7 @@ __global__ __launch_bounds__(64, (NARROW ? HL - 1 : HL) == 11 ? 4 : 2) void rcdc
                     wr = ld4(src + (rc ? p - rep0 : p));
                     wr1 = ld4(src + (rc1 ? p - rep1 : p));
                     wr2 = ld4(src + (rc2 ? p - rep2 : p));
-                    const uint64_t k6 = key48(w, (key & 0xFFu) == 6 ? ld4(src + p + 4) : 0u,
-                                              key & 0xFFu);
+                    const uint64_t k6 = key48(w, keyb > 4 ? ld4(src + p + 4) : 0u, keyb);
                     h = zhash<HL>(k6);
                     if constexpr (!NARROW) {
                         tg = ztag(k6);
@@ -1235,7 +1249,7 @@ __global__ __launch_bounds__(64, (NARROW ? HL - 1 : HL) == 11 ? 4 : 2) void rcdc
                         bl = last_eq16(ld16(src + p - 16), ld16(src + c - 16));
                         if (bl > limb) bl = limb;
                     }
-                    ok = wc == w && (isrep || 4 + fl >= (key & 0xFFu));  // last offset: 4 bytes
+                    ok = wc == w && (isrep || 4 + fl >= keyb);  // last offset: 4 bytes
                     if (ok && c < 16)
                         while (bl < limb && src[p - 1 - bl] == src[c - 1 - bl]) bl++;
                 }
@@ -1675,7 +1689,8 @@ static ZstdStrategy zstd_strategy(int level) {
     if (level == 0) level = 3;  // ZSTD_CLEVEL_DEFAULT
     ZstdStrategy z{11, false, level <= 1 ? 6u : 4u};
     if (level >= 3) z = ZstdStrategy{level >= 4 ? 13 : 12, true, 6u};
-    if (ek == 4 || ek == 6) z.key = (uint32_t)ek;
+    if (z.narrow) z.key |= kZstdAdaptKey;  // per-block 5 or 6 (RCDC_ZSTD_KEY fixes it)
+    if (ek == 4 || ek == 5 || ek == 6) z.key = (uint32_t)ek;
     if (eh == 11) z.hlog = 11, z.narrow = false;
     if (eh == 12 || eh == 13) z.hlog = eh, z.narrow = true;
     if (rep) z.key |= kZstdRep;

@@ -166,8 +166,8 @@ def _csv(rng, n):
 def test_levels(gpu_ctx):
     """The level picks the parse (rcdc_zstd.hip zstd_strategy): a 2^11-entry
     tagged table with 6-byte keys at levels <= 1 and 4-byte keys at 2; from 3
-    (0 = zstd's default) 6-byte keys in 16-bit tables of 2^12 entries, 2^13
-    from 4 up.  Every level's frames decode; the levels differ and the higher
+    (0 = zstd's default) 16-bit tables of 2^12 entries, 2^13 from 4 up, keyed
+    on 5 or 6 bytes per block.  Every level's frames decode; the levels differ and the higher
     ones are not larger on structured rows."""
     from rustic_core_amd.errors import RusticError
     rng = np.random.default_rng(2)
