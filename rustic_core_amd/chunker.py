@@ -21,6 +21,7 @@ import ctypes
 import enum
 import io
 import os
+import queue
 import threading
 from dataclasses import dataclass
 from typing import Iterator, Optional
@@ -302,6 +303,113 @@ def _read_into(reader, mv: memoryview) -> int:
         return n or 0
 
 
+# Read blocks: READ_SIZE bytearrays reused across iterators (a fresh 16 MiB
+# block costs its page faults on every file); a block takes further reads
+# while at least MIN_READ bytes of it are free.
+_POOL: collections.deque = collections.deque()
+_POOL_MAX = 8
+MIN_READ = 1 * MB
+# Blocks read and fed ahead of the consumer by the read-ahead thread.
+READ_AHEAD = 2
+
+
+def _block():
+    """(block, its address)."""
+    try:
+        return _POOL.pop()
+    except IndexError:
+        blk = bytearray(READ_SIZE)
+        return blk, ctypes.addressof((ctypes.c_char * READ_SIZE).from_buffer(blk))
+
+
+def _release(blk) -> None:
+    if len(_POOL) < _POOL_MAX:
+        _POOL.append(blk)
+
+
+# A chunk is a new bytes object filled by memmove, which runs without the GIL
+# (ctypes releases it around foreign calls), so the consumer's copies overlap
+# the read-ahead thread's reads and feeds instead of holding it off for a
+# switch interval at a time.  The object is written before anyone else sees it.
+_new_bytes = ctypes.pythonapi.PyBytes_FromStringAndSize
+_new_bytes.restype = ctypes.py_object
+_new_bytes.argtypes = (ctypes.c_void_p, ctypes.c_ssize_t)
+_BYTES_DATA = bytes.__basicsize__ - 1  # offset of PyBytesObject.ob_sval
+
+
+class _Source:
+    """The reading half of RabinChunkIter: reads the file into blocks and
+    feeds every piece to the device stream (rabin.rs:110-191's read loop).
+    Runs inline, or -- once a read has filled a whole block, i.e. the file is
+    large -- on one read-ahead thread that is then the only user of the reader
+    and the stream, so that reads and device passes overlap the consumer's
+    chunk copies."""
+
+    def __init__(self, ctx: Context, reader):
+        self.reader = reader
+        self.stream = _Stream(ctx)
+        self.blk = None
+        self.pos = 0
+        self.q = None
+        self.thread = None
+        self.stop = threading.Event()
+
+    def step(self):
+        """One read + feed -> (block, start, n, last use of block, cuts, eof)."""
+        if self.blk is None:
+            self.blk, self.pos = _block(), 0
+        blk, p = self.blk, self.pos
+        with memoryview(blk[0]) as mv:
+            n = _read_into(self.reader, mv[p:])
+            eof = not n
+            cuts = self.stream.feed(mv[p:p + n], eof)
+        self.pos = p + n
+        last = eof or READ_SIZE - self.pos < MIN_READ
+        if last:
+            self.blk = None
+        return blk, p, n, last, cuts, eof
+
+    def start(self) -> None:
+        self.q = queue.Queue(READ_AHEAD)
+        self.thread = threading.Thread(target=self._run, name="rcdc-read-ahead", daemon=True)
+        self.thread.start()
+
+    def _put(self, item) -> None:
+        while not self.stop.is_set():
+            try:
+                self.q.put(item, timeout=0.05)
+                return
+            except queue.Full:
+                continue
+
+    def _run(self) -> None:
+        try:
+            while not self.stop.is_set():
+                item = self.step()
+                self._put(item)
+                if item[5]:
+                    break
+        except Exception as e:  # delivered in order, after the cuts before it
+            self._put(e)
+        finally:
+            self.stream.close()
+
+    def next(self):
+        if self.q is None:
+            return self.step()
+        item = self.q.get()
+        if isinstance(item, Exception):
+            raise item
+        return item
+
+    def close(self) -> None:
+        self.stop.set()
+        if self.thread is None:
+            self.stream.close()
+        elif self.thread is not threading.current_thread():
+            self.thread.join()
+
+
 class RabinChunkIter:
     """rabin.rs ChunkIter with device-computed cut points.
 
@@ -312,13 +420,10 @@ class RabinChunkIter:
     def __init__(self, ctx: Context, reader, size_hint: int = 0):
         check_rabin_params(ctx.avg, ctx.min_size, ctx.max_size)
         self._ctx = ctx
-        self._reader = reader
         self.size_hint = size_hint  # capacity hint only; never affects cuts
-        self._stream = _Stream(ctx)
-        self._buf = bytearray()      # _buf[:_len] read, not yet compacted away
-        self._len = 0
-        self._off = 0                # _buf[_off:_len] not yet yielded
-        self._base = 0               # absolute offset of _buf[_off]
+        self._src = _Source(ctx, reader)
+        self._segs = collections.deque()  # [block, start, n, last]: read, not yet yielded
+        self._base = 0                    # absolute offset of the next chunk
         self._cuts = collections.deque()
         self._eof = False
         self._finished = False
@@ -328,23 +433,46 @@ class RabinChunkIter:
 
     def _fill(self) -> None:
         while not self._cuts and not self._eof:
-            # compact what was yielded once it dominates the buffer (amortised
-            # O(1) per byte instead of a memmove per chunk)
-            if self._off and self._off >= self._len // 2:
-                rem = self._len - self._off
-                self._buf[:rem] = self._buf[self._off:self._len]
-                self._off, self._len = 0, rem
-            if len(self._buf) < self._len + READ_SIZE:
-                self._buf.extend(bytes(self._len + READ_SIZE - len(self._buf)))
-            # the reader fills the buffer in place (one copy fewer than
-            # read() + append)
-            with memoryview(self._buf) as mv:
-                n = _read_into(self._reader, mv[self._len:self._len + READ_SIZE])
-                if not n:
-                    self._eof = True
-                cuts = self._stream.feed(mv[self._len:self._len + n], self._eof)
-            self._len += n
-            self._cuts.extend(int(c) for c in cuts)
+            blk, p, n, last, cuts, eof = self._src.next()
+            self._segs.append([blk, p, n, last])
+            self._cuts.extend(cuts.tolist())
+            self._eof = eof
+            if n == READ_SIZE and not eof and self._src.thread is None:
+                self._src.start()
+
+    def _finish(self) -> None:
+        self._finished = True
+        self._src.close()
+
+    def _take(self, k: int) -> bytes:
+        """The next k bytes of the read segments, releasing spent blocks."""
+        segs = self._segs
+        chunk = _new_bytes(None, k)
+        dst, rem = id(chunk) + _BYTES_DATA, k
+        for s in segs:  # usually one segment; a chunk may span reads and blocks
+            t = min(rem, s[2])
+            ctypes.memmove(dst, s[0][1] + s[1], t)
+            dst += t
+            rem -= t
+            if not rem:
+                break
+        if rem:
+            raise AssertionError("rcdc stream cut beyond the bytes fed")
+        rem = k
+        while segs:
+            s = segs[0]
+            t = min(rem, s[2])
+            s[1] += t
+            s[2] -= t
+            rem -= t
+            if s[2]:
+                break
+            segs.popleft()
+            if s[3]:
+                _release(s[0])
+            if not rem and (not segs or segs[0][2]):
+                break
+        return chunk
 
     def __next__(self) -> bytes:
         if self._finished:
@@ -352,20 +480,23 @@ class RabinChunkIter:
         try:
             self._fill()
         except RusticError:
-            self._finished = True
-            self._stream.close()
+            self._finish()
             raise
         if not self._cuts:
-            self._finished = True
-            self._stream.close()
+            self._finish()
             raise StopIteration
         end = self._cuts.popleft()
-        k = end - self._base
-        chunk = bytes(memoryview(self._buf)[self._off:self._off + k])
-        self._off += k
+        chunk = self._take(end - self._base)
         self._base = end
         self.size_hint = max(self.size_hint - len(chunk), 0)
         return chunk
+
+    def __del__(self):
+        src = getattr(self, "_src", None)
+        if src is not None and not self._finished:
+            src.stop.set()  # an abandoned iterator: the read-ahead thread ends
+            if src.thread is None:
+                src.stream.close()
 
 
 class FixedSizeChunkIter:

@@ -1,0 +1,117 @@
+"""Host side of RabinChunkIter (rabin.rs:110-191's read loop) without a GPU:
+the device stream is replaced by a stand-in that cuts every 700001 bytes and
+hands cuts out one piece late (as rcdc_stream_feed may), so the block reuse,
+the chunks that span reads and blocks, the read-ahead thread (started once a
+read fills a whole block) and the end of an abandoned iterator are checked
+against plain byte slicing.  The cut points themselves are the GPU tests'."""
+import gc
+import io
+import random
+
+import numpy as np
+import pytest
+
+from rustic_core_amd import chunker as C
+
+K = 700001
+
+
+class _FakeStream:
+    def __init__(self, ctx):
+        self.n, self.pending, self.closed = 0, [], False
+
+    def feed(self, data, fin):
+        a = self.n
+        self.n += len(data)
+        new = [c for c in range((a // K + 1) * K, self.n, K)]
+        out, self.pending = self.pending, new
+        if fin:
+            out = out + self.pending + ([self.n] if self.n else [])
+            self.pending = []
+        return np.array(out, np.uint64)
+
+    def close(self):
+        self.closed = True
+
+
+class _Ctx:
+    avg, min_size, max_size = 1 << 20, 512 << 10, 8 << 20
+
+
+class _Short(io.RawIOBase):
+    """readinto returns 1..k bytes per call."""
+
+    def __init__(self, data, k, seed):
+        self._b, self._k, self._r = io.BytesIO(data), k, random.Random(seed)
+
+    def readable(self):
+        return True
+
+    def readinto(self, mv):
+        b = self._b.read(min(len(mv), self._r.randint(1, self._k)))
+        mv[:len(b)] = b
+        return len(b)
+
+
+@pytest.fixture
+def fake(monkeypatch):
+    monkeypatch.setattr(C, "_Stream", _FakeStream)
+    monkeypatch.setattr(C, "check_rabin_params", lambda *a: None)
+
+
+@pytest.mark.parametrize("size", [0, 1, K, 3 << 20, 16 << 20, (16 << 20) + 3, 70 << 20])
+@pytest.mark.parametrize("kind", ["bytesio", "short", "buffered"])
+def test_chunks_are_the_bytes_between_cuts(fake, size, kind):
+    data = np.random.default_rng(size).integers(0, 256, size, dtype=np.uint8).tobytes()
+    reader = {"bytesio": lambda: io.BytesIO(data),
+              "short": lambda: _Short(data, 3 << 20, size),
+              "buffered": lambda: io.BufferedReader(io.BytesIO(data))}[kind]()
+    it = C.RabinChunkIter(_Ctx(), reader, size)
+    chunks = list(it)
+    assert b"".join(chunks) == data
+    want = list(range(K, size, K)) + ([size] if size else [])
+    assert np.cumsum([len(c) for c in chunks]).tolist() == want
+    assert it._src.stream.closed
+    assert (it._src.thread is not None) == (kind != "short" and size >= C.READ_SIZE)
+    assert list(it) == [] and it.size_hint == 0
+
+
+def test_abandoned_iterator_stops_read_ahead(fake):
+    it = C.RabinChunkIter(_Ctx(), io.BytesIO(bytes(80 << 20)))
+    next(it)
+    src = it._src
+    del it
+    gc.collect()
+    src.thread.join(5)
+    assert not src.thread.is_alive() and src.stream.closed
+
+
+def test_read_error_after_read_ahead(fake):
+    """An error on a later read reaches the consumer after every chunk cut
+    before it, then the iterator is finished (rabin.rs:131-138)."""
+    from rustic_core_amd.errors import ErrorKind, RusticError
+    data = bytes(40 << 20)
+
+    class _Fail(io.RawIOBase):
+        def __init__(self):
+            self._b, self._calls = io.BytesIO(data), 0
+
+        def readable(self):
+            return True
+
+        def readinto(self, mv):
+            self._calls += 1
+            if self._calls == 3:
+                raise OSError("injected")
+            b = self._b.read(len(mv))
+            mv[:len(b)] = b
+            return len(b)
+
+    it = C.RabinChunkIter(_Ctx(), _Fail())
+    got = []
+    with pytest.raises(RusticError) as e:
+        for c in it:
+            got.append(len(c))
+    assert e.value.kind == ErrorKind.InputOutput
+    assert sum(got) <= 32 << 20 and it._src.stream.closed
+    assert list(it) == []
