@@ -21,7 +21,6 @@ import ctypes
 import enum
 import io
 import os
-import queue
 import threading
 from dataclasses import dataclass
 from typing import Iterator, Optional
@@ -309,120 +308,38 @@ def _read_into(reader, mv: memoryview) -> int:
 _POOL: collections.deque = collections.deque()
 _POOL_MAX = 8
 MIN_READ = 1 * MB
-# Blocks read and fed ahead of the consumer by the read-ahead thread.
-READ_AHEAD = 2
 
 
-def _block():
-    """(block, its address)."""
+def _block() -> bytearray:
     try:
         return _POOL.pop()
     except IndexError:
-        blk = bytearray(READ_SIZE)
-        return blk, ctypes.addressof((ctypes.c_char * READ_SIZE).from_buffer(blk))
+        return bytearray(READ_SIZE)
 
 
-def _release(blk) -> None:
+def _release(blk: bytearray) -> None:
     if len(_POOL) < _POOL_MAX:
         _POOL.append(blk)
-
-
-# A chunk is a new bytes object filled by memmove, which runs without the GIL
-# (ctypes releases it around foreign calls), so the consumer's copies overlap
-# the read-ahead thread's reads and feeds instead of holding it off for a
-# switch interval at a time.  The object is written before anyone else sees it.
-_new_bytes = ctypes.pythonapi.PyBytes_FromStringAndSize
-_new_bytes.restype = ctypes.py_object
-_new_bytes.argtypes = (ctypes.c_void_p, ctypes.c_ssize_t)
-_BYTES_DATA = bytes.__basicsize__ - 1  # offset of PyBytesObject.ob_sval
-
-
-class _Source:
-    """The reading half of RabinChunkIter: reads the file into blocks and
-    feeds every piece to the device stream (rabin.rs:110-191's read loop).
-    Runs inline, or -- once a read has filled a whole block, i.e. the file is
-    large -- on one read-ahead thread that is then the only user of the reader
-    and the stream, so that reads and device passes overlap the consumer's
-    chunk copies."""
-
-    def __init__(self, ctx: Context, reader):
-        self.reader = reader
-        self.stream = _Stream(ctx)
-        self.blk = None
-        self.pos = 0
-        self.q = None
-        self.thread = None
-        self.stop = threading.Event()
-
-    def step(self):
-        """One read + feed -> (block, start, n, last use of block, cuts, eof)."""
-        if self.blk is None:
-            self.blk, self.pos = _block(), 0
-        blk, p = self.blk, self.pos
-        with memoryview(blk[0]) as mv:
-            n = _read_into(self.reader, mv[p:])
-            eof = not n
-            cuts = self.stream.feed(mv[p:p + n], eof)
-        self.pos = p + n
-        last = eof or READ_SIZE - self.pos < MIN_READ
-        if last:
-            self.blk = None
-        return blk, p, n, last, cuts, eof
-
-    def start(self) -> None:
-        self.q = queue.Queue(READ_AHEAD)
-        self.thread = threading.Thread(target=self._run, name="rcdc-read-ahead", daemon=True)
-        self.thread.start()
-
-    def _put(self, item) -> None:
-        while not self.stop.is_set():
-            try:
-                self.q.put(item, timeout=0.05)
-                return
-            except queue.Full:
-                continue
-
-    def _run(self) -> None:
-        try:
-            while not self.stop.is_set():
-                item = self.step()
-                self._put(item)
-                if item[5]:
-                    break
-        except Exception as e:  # delivered in order, after the cuts before it
-            self._put(e)
-        finally:
-            self.stream.close()
-
-    def next(self):
-        if self.q is None:
-            return self.step()
-        item = self.q.get()
-        if isinstance(item, Exception):
-            raise item
-        return item
-
-    def close(self) -> None:
-        self.stop.set()
-        if self.thread is None:
-            self.stream.close()
-        elif self.thread is not threading.current_thread():
-            self.thread.join()
 
 
 class RabinChunkIter:
     """rabin.rs ChunkIter with device-computed cut points.
 
     Yields ``bytes`` chunks; raises ``RusticError`` like the reference's
-    ``Some(Err(..))`` items (after which iteration stops).
+    ``Some(Err(..))`` items (after which iteration stops).  The reader fills
+    pooled blocks in place; every read is fed to the device stream as it
+    lands; a chunk is one copy out of the block(s) it lies in.
     """
 
     def __init__(self, ctx: Context, reader, size_hint: int = 0):
         check_rabin_params(ctx.avg, ctx.min_size, ctx.max_size)
         self._ctx = ctx
+        self._reader = reader
         self.size_hint = size_hint  # capacity hint only; never affects cuts
-        self._src = _Source(ctx, reader)
-        self._segs = collections.deque()  # [block, start, n, last]: read, not yet yielded
+        self._stream = _Stream(ctx)
+        self._blk = None                  # block taking the next read
+        self._pos = 0
+        self._segs = collections.deque()  # [block, start, n, last use]: read, not yet yielded
         self._base = 0                    # absolute offset of the next chunk
         self._cuts = collections.deque()
         self._eof = False
@@ -433,33 +350,39 @@ class RabinChunkIter:
 
     def _fill(self) -> None:
         while not self._cuts and not self._eof:
-            blk, p, n, last, cuts, eof = self._src.next()
+            if self._blk is None:
+                self._blk, self._pos = _block(), 0
+            blk, p = self._blk, self._pos
+            with memoryview(blk) as mv:
+                n = _read_into(self._reader, mv[p:])
+                self._eof = not n
+                cuts = self._stream.feed(mv[p:p + n], self._eof)
+            self._pos = p + n
+            last = self._eof or READ_SIZE - self._pos < MIN_READ
+            if last:
+                self._blk = None
             self._segs.append([blk, p, n, last])
             self._cuts.extend(cuts.tolist())
-            self._eof = eof
-            if n == READ_SIZE and not eof and self._src.thread is None:
-                self._src.start()
-
-    def _finish(self) -> None:
-        self._finished = True
-        self._src.close()
 
     def _take(self, k: int) -> bytes:
-        """The next k bytes of the read segments, releasing spent blocks."""
+        """The next k bytes read, releasing spent blocks."""
         segs = self._segs
-        chunk = _new_bytes(None, k)
-        dst, rem = id(chunk) + _BYTES_DATA, k
-        for s in segs:  # usually one segment; a chunk may span reads and blocks
-            t = min(rem, s[2])
-            ctypes.memmove(dst, s[0][1] + s[1], t)
-            dst += t
-            rem -= t
-            if not rem:
-                break
-        if rem:
-            raise AssertionError("rcdc stream cut beyond the bytes fed")
+        s = segs[0]
+        if k <= s[2]:
+            chunk = bytes(memoryview(s[0])[s[1]:s[1] + k])
+        else:  # the chunk spans reads or blocks
+            parts, rem = [], k
+            for s in segs:
+                t = min(rem, s[2])
+                parts.append(memoryview(s[0])[s[1]:s[1] + t])
+                rem -= t
+                if not rem:
+                    break
+            if rem:
+                raise AssertionError("rcdc stream cut beyond the bytes fed")
+            chunk = b"".join(parts)
         rem = k
-        while segs:
+        while segs and (rem or not segs[0][2]):
             s = segs[0]
             t = min(rem, s[2])
             s[1] += t
@@ -470,9 +393,11 @@ class RabinChunkIter:
             segs.popleft()
             if s[3]:
                 _release(s[0])
-            if not rem and (not segs or segs[0][2]):
-                break
         return chunk
+
+    def _finish(self) -> None:
+        self._finished = True
+        self._stream.close()
 
     def __next__(self) -> bytes:
         if self._finished:
@@ -490,13 +415,6 @@ class RabinChunkIter:
         self._base = end
         self.size_hint = max(self.size_hint - len(chunk), 0)
         return chunk
-
-    def __del__(self):
-        src = getattr(self, "_src", None)
-        if src is not None and not self._finished:
-            src.stop.set()  # an abandoned iterator: the read-ahead thread ends
-            if src.thread is None:
-                src.stream.close()
 
 
 class FixedSizeChunkIter:

@@ -1,9 +1,8 @@
 """Host side of RabinChunkIter (rabin.rs:110-191's read loop) without a GPU:
 the device stream is replaced by a stand-in that cuts every 700001 bytes and
 hands cuts out one piece late (as rcdc_stream_feed may), so the block reuse,
-the chunks that span reads and blocks, the read-ahead thread (started once a
-read fills a whole block) and the end of an abandoned iterator are checked
-against plain byte slicing.  The cut points themselves are the GPU tests'."""
+the chunks that span reads and blocks and the block reuse across iterators
+are checked against plain byte slicing.  The cut points themselves are the GPU tests'."""
 import gc
 import io
 import random
@@ -71,22 +70,22 @@ def test_chunks_are_the_bytes_between_cuts(fake, size, kind):
     assert b"".join(chunks) == data
     want = list(range(K, size, K)) + ([size] if size else [])
     assert np.cumsum([len(c) for c in chunks]).tolist() == want
-    assert it._src.stream.closed
-    assert (it._src.thread is not None) == (kind != "short" and size >= C.READ_SIZE)
+    assert it._stream.closed
     assert list(it) == [] and it.size_hint == 0
 
 
-def test_abandoned_iterator_stops_read_ahead(fake):
-    it = C.RabinChunkIter(_Ctx(), io.BytesIO(bytes(80 << 20)))
+def test_blocks_are_reused(fake):
+    """Spent blocks go back to the pool and the next file reads into them."""
+    C._POOL.clear()
+    list(C.RabinChunkIter(_Ctx(), io.BytesIO(bytes(40 << 20))))
+    pooled = {id(b) for b in C._POOL}
+    assert pooled
+    it = C.RabinChunkIter(_Ctx(), io.BytesIO(bytes(1 << 20)))
     next(it)
-    src = it._src
-    del it
-    gc.collect()
-    src.thread.join(5)
-    assert not src.thread.is_alive() and src.stream.closed
+    assert id(it._segs[0][0]) in pooled or not it._segs
 
 
-def test_read_error_after_read_ahead(fake):
+def test_read_error_after_earlier_reads(fake):
     """An error on a later read reaches the consumer after every chunk cut
     before it, then the iterator is finished (rabin.rs:131-138)."""
     from rustic_core_amd.errors import ErrorKind, RusticError
@@ -113,5 +112,5 @@ def test_read_error_after_read_ahead(fake):
         for c in it:
             got.append(len(c))
     assert e.value.kind == ErrorKind.InputOutput
-    assert sum(got) <= 32 << 20 and it._src.stream.closed
+    assert sum(got) <= 32 << 20 and it._stream.closed
     assert list(it) == []

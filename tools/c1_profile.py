@@ -1,9 +1,7 @@
 """Where C1's drop-in time goes (bench.py run_c1's file through
 ChunkIter.from_config): wall time split into the file reads (_read_into),
 the device feeds (_Stream.feed: H2D, chunking, cuts D2H) and the rest
-(chunk copies, Python).  With the read-ahead thread (chunker._Source) the
-reads and feeds overlap the consumer and their times include GIL waits, so
-"rest" is no longer a serial share.  Prints one JSON line.
+(chunk copies, Python).  Prints one JSON line.
 
   python tools/c1_profile.py [--mib 256] [--passes 5]
 """
