@@ -268,6 +268,15 @@ rcdc_status rcdc_sha256_chunks(rcdc_ctx *ctx, const void *d_arena,
 rcdc_status rcdc_sha256_host(const void *const *ptrs, const uint64_t *lens, uint32_t n,
                              uint8_t *digests);
 
+/* Page-locked host memory for read buffers.  Host-buffer calls
+ * (rcdc_stream_feed, rcdc_chunk_batch) whose pieces all lie in such memory
+ * copy them to the device by DMA straight from the caller's buffer, with no
+ * staging copy.  The reference reads into a Vec (rabin.rs:110-191); this is
+ * the buffer a caller's read loop would fill instead.  rcdc_host_free(NULL)
+ * is a no-op.                                                              */
+rcdc_status rcdc_host_alloc(uint64_t bytes, void **out);
+void rcdc_host_free(void *p);
+
 /* Fused blob ids of a plan: after rcdc_plan_run over d_arena (the same
  * pointer), enqueue the SHA-256 of every chunk it found, on the device
  * cut list (no host round trip).  Asynchronous.                           */

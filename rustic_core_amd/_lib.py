@@ -28,7 +28,7 @@ EXPORTS = (
     "rcdc_aead_seal", "rcdc_aead_open", "rcdc_pack_build",
     "rcdc_zstd_bound", "rcdc_zstd_compress", "rcdc_zstd_tables", "rcdc_zstd_tables_size",
     "rcdc_zstd_check", "rcdc_pack_build_raw", "rcdc_pack_build_raw_multi", "rcdc_copy_ranges",
-    "rcdc_sha256_host",
+    "rcdc_sha256_host", "rcdc_host_alloc", "rcdc_host_free",
 )
 ABI_VERSION = 3
 
@@ -165,6 +165,10 @@ def lib() -> ctypes.CDLL:
     L.rcdc_copy_ranges.argtypes = [vp, vp, u32, vp, u32, vp, vp]
     L.rcdc_sha256_host.restype = st
     L.rcdc_sha256_host.argtypes = [vp, vp, u32, vp]
+    L.rcdc_host_alloc.restype = st
+    L.rcdc_host_alloc.argtypes = [u64, vp]
+    L.rcdc_host_free.restype = None
+    L.rcdc_host_free.argtypes = [vp]
     L.rcdc_zstd_bound.restype = u64
     L.rcdc_zstd_bound.argtypes = [u64]
     L.rcdc_zstd_compress.restype = st

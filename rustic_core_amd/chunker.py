@@ -302,22 +302,51 @@ def _read_into(reader, mv: memoryview) -> int:
         return n or 0
 
 
-# Read blocks: READ_SIZE bytearrays reused across iterators (a fresh 16 MiB
-# block costs its page faults on every file); a block takes further reads
-# while at least MIN_READ bytes of it are free.
+# Read blocks: READ_SIZE buffers in page-locked memory (rcdc_host_alloc), so
+# that rcdc_stream_feed DMAs each read straight to the device instead of
+# copying it through its staging slots; reused across iterators (allocation
+# costs milliseconds).  A block takes further reads while at least MIN_READ
+# bytes of it are free.
 _POOL: collections.deque = collections.deque()
 _POOL_MAX = 8
 MIN_READ = 1 * MB
 
 
-def _block() -> bytearray:
+class _Block:
+    __slots__ = ("ptr", "mv", "_keep")
+
+    def __init__(self):
+        p = ctypes.c_void_p()
+        self.ptr = None
+        try:
+            if _lib.lib().rcdc_host_alloc(READ_SIZE, ctypes.byref(p)) == 0:
+                self.ptr = p.value
+        except Exception:  # no librcdc: the iterator's constructor raises anyway
+            pass
+        if self.ptr:
+            self._keep = None
+            self.mv = memoryview((ctypes.c_char * READ_SIZE).from_address(self.ptr)).cast("B")
+        else:  # page-locked memory refused: pageable (the feed stages it)
+            self._keep = bytearray(READ_SIZE)
+            self.mv = memoryview(self._keep)
+
+    def __del__(self):
+        if self.ptr:
+            try:
+                _lib.lib().rcdc_host_free(self.ptr)
+            except Exception:  # interpreter shutdown
+                pass
+            self.ptr = None
+
+
+def _block() -> _Block:
     try:
         return _POOL.pop()
     except IndexError:
-        return bytearray(READ_SIZE)
+        return _Block()
 
 
-def _release(blk: bytearray) -> None:
+def _release(blk: _Block) -> None:
     if len(_POOL) < _POOL_MAX:
         _POOL.append(blk)
 
@@ -327,8 +356,8 @@ class RabinChunkIter:
 
     Yields ``bytes`` chunks; raises ``RusticError`` like the reference's
     ``Some(Err(..))`` items (after which iteration stops).  The reader fills
-    pooled blocks in place; every read is fed to the device stream as it
-    lands; a chunk is one copy out of the block(s) it lies in.
+    pooled page-locked blocks in place; every read is fed to the device
+    stream as it lands; a chunk is one copy out of the block(s) it lies in.
     """
 
     def __init__(self, ctx: Context, reader, size_hint: int = 0):
@@ -353,10 +382,9 @@ class RabinChunkIter:
             if self._blk is None:
                 self._blk, self._pos = _block(), 0
             blk, p = self._blk, self._pos
-            with memoryview(blk) as mv:
-                n = _read_into(self._reader, mv[p:])
-                self._eof = not n
-                cuts = self._stream.feed(mv[p:p + n], self._eof)
+            n = _read_into(self._reader, blk.mv[p:])
+            self._eof = not n
+            cuts = self._stream.feed(blk.mv[p:p + n], self._eof)
             self._pos = p + n
             last = self._eof or READ_SIZE - self._pos < MIN_READ
             if last:
@@ -369,12 +397,12 @@ class RabinChunkIter:
         segs = self._segs
         s = segs[0]
         if k <= s[2]:
-            chunk = bytes(memoryview(s[0])[s[1]:s[1] + k])
+            chunk = bytes(s[0].mv[s[1]:s[1] + k])
         else:  # the chunk spans reads or blocks
             parts, rem = [], k
             for s in segs:
                 t = min(rem, s[2])
-                parts.append(memoryview(s[0])[s[1]:s[1] + t])
+                parts.append(s[0].mv[s[1]:s[1] + t])
                 rem -= t
                 if not rem:
                     break

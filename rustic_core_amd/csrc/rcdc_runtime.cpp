@@ -1261,6 +1261,18 @@ inline uint64_t now_ns() {
                std::chrono::steady_clock::now().time_since_epoch()).count();
 }
 
+// Whether a host address lies in page-locked memory HIP knows of (pageable
+// memory answers with an error or "unregistered"; the error is cleared so no
+// later launch check sees it).
+bool host_pinned(const void *p) {
+    hipPointerAttribute_t a{};
+    if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    return a.type == hipMemoryTypeHost;
+}
+
 // One piece of host memory at an arena offset.
 struct HostPiece {
     uint64_t off;
@@ -1308,10 +1320,21 @@ rcdc_status run_host_pieces(rcdc_ctx *ctx, Lane *L, const std::vector<uint64_t> 
         HIP_TRY(hipMemcpyAsync(L->d_arena, d_prefix, prefix_len, hipMemcpyDeviceToDevice,
                                L->stream));
     }
+    // every piece page-locked (rcdc_host_alloc): DMA straight from the
+    // caller's buffer; plan_results below waits for the pass, so the buffer
+    // is free again when this returns
+    static const bool direct_ok = !getenv("RCDC_NO_DIRECT_DMA");
+    bool direct = direct_ok && !pieces.empty();
+    for (size_t j = 0; direct && j < pieces.size(); j++)
+        direct = host_pinned(pieces[j].p) && host_pinned(pieces[j].p + pieces[j].n - 1);
+    if (direct)
+        for (const HostPiece &pc : pieces)
+            HIP_TRY(hipMemcpyAsync(L->d_arena + pc.off, pc.p, pc.n, hipMemcpyHostToDevice,
+                                   L->stream));
     // staged copies: block k of the arena goes through slot k & 1
     size_t pi = 0;  // first piece that may overlap the block
     uint64_t k = 0;
-    for (uint64_t p = prefix_len; p < total; p += L->stage, k++) {
+    for (uint64_t p = prefix_len; !direct && p < total; p += L->stage, k++) {
         const uint64_t e = std::min(p + L->stage, total);
         const int slot = (int)(k % L->nslots);
         if (k >= L->nslots) {
@@ -1763,6 +1786,17 @@ uint64_t rcdc_fixed_cuts(uint64_t n, uint64_t size, uint64_t *cuts, uint64_t cap
         s = e;
     }
     return k;
+}
+
+rcdc_status rcdc_host_alloc(uint64_t bytes, void **out) {
+    if (!out) return fail(RCDC_ERR_INVALID_INPUT, "null argument");
+    *out = nullptr;
+    HIP_TRY(hipHostMalloc(out, bytes ? bytes : 1, hipHostMallocDefault));
+    return RCDC_OK;
+}
+
+void rcdc_host_free(void *p) {
+    if (p) (void)hipHostFree(p);
 }
 
 // ---- SHA-256 blob ids (crypto/hasher.rs:17-19, file_archiver.rs:151) -----

@@ -215,3 +215,45 @@ def test_plan_finish_device_views_after_fallback(monkeypatch, gpu_ctx):
         assert bytes(digs[j]) == hashlib.sha256(a[prev:int(c)].tobytes()).digest(), j
         prev = int(c)
     plan.close()
+
+
+@pytest.mark.gpu
+def test_pinned_pieces_direct_dma(gpu_ctx, rcdc_lib):
+    """Pieces in rcdc_host_alloc memory go to the device by DMA straight from
+    the caller's buffer (no staging copy): stream feeds from one reused
+    page-locked buffer, mixed with pageable feeds, and a chunk_batch over
+    page-locked files give the oracle's cuts."""
+    import ctypes
+    from rustic_core_amd.chunker import _Stream
+    data = _mixed(11, 40 * MiB + 77)
+    want = oracle.chunk_cuts(data)
+    p = ctypes.c_void_p()
+    size = 9 * MiB
+    assert rcdc_lib.rcdc_host_alloc(size, ctypes.byref(p)) == 0
+    try:
+        pinned = np.ctypeslib.as_array((ctypes.c_uint8 * size).from_address(p.value))
+        st = _Stream(gpu_ctx)
+        rng = np.random.default_rng(5)
+        cuts, i = [], 0
+        while i < data.size:
+            k = int(rng.integers(1, size))
+            piece = data[i:i + k]
+            i += piece.size
+            if rng.integers(0, 4):  # mostly page-locked, sometimes pageable
+                pinned[:piece.size] = piece
+                cuts.extend(st.feed(pinned[:piece.size], i >= data.size).tolist())
+            else:
+                cuts.extend(st.feed(piece.tobytes(), i >= data.size).tolist())
+        st.close()
+        assert np.array_equal(np.array(cuts, np.uint64), want)
+        files = [oracle.stdrng_bytes(900 + j, (j + 1) * MiB + 3 * j) for j in range(3)]
+        offs = np.cumsum([0] + [f.size for f in files])
+        assert offs[-1] <= size
+        for f, o in zip(files, offs):
+            pinned[o:o + f.size] = f
+        got = gpu_ctx.chunk_batch([pinned[o:o + f.size] for f, o in zip(files, offs)])
+        for j, f in enumerate(files):
+            assert np.array_equal(got[j], oracle.chunk_cuts(f)), j
+    finally:
+        rcdc_lib.rcdc_host_free(p)
+    rcdc_lib.rcdc_host_free(None)
