@@ -17,6 +17,7 @@ constructor raises.
 from __future__ import annotations
 
 import collections
+import concurrent.futures
 import ctypes
 import enum
 import io
@@ -313,7 +314,7 @@ MIN_READ = 1 * MB
 
 
 class _Block:
-    __slots__ = ("ptr", "mv", "_keep")
+    __slots__ = ("ptr", "mv", "addr", "_keep")
 
     def __init__(self):
         p = ctypes.c_void_p()
@@ -329,6 +330,7 @@ class _Block:
         else:  # page-locked memory refused: pageable (the feed stages it)
             self._keep = bytearray(READ_SIZE)
             self.mv = memoryview(self._keep)
+        self.addr = ctypes.addressof(ctypes.c_char.from_buffer(self.mv))
 
     def __del__(self):
         if self.ptr:
@@ -337,6 +339,12 @@ class _Block:
             except Exception:  # interpreter shutdown
                 pass
             self.ptr = None
+
+
+_new_bytes = ctypes.pythonapi.PyBytes_FromStringAndSize
+_new_bytes.restype = ctypes.py_object
+_new_bytes.argtypes = (ctypes.c_void_p, ctypes.c_ssize_t)
+_BYTES_DATA = bytes.__basicsize__ - 1  # offset of PyBytesObject.ob_sval
 
 
 def _block() -> _Block:
@@ -349,6 +357,20 @@ def _block() -> _Block:
 def _release(blk: _Block) -> None:
     if len(_POOL) < _POOL_MAX:
         _POOL.append(blk)
+
+
+_readers = None
+_readers_lock = threading.Lock()
+
+
+def _reader_pool():
+    """Threads for the read-ahead of large files (one read in flight per
+    iterator)."""
+    global _readers
+    with _readers_lock:
+        if _readers is None:
+            _readers = concurrent.futures.ThreadPoolExecutor(16, thread_name_prefix="rcdc-read")
+        return _readers
 
 
 class RabinChunkIter:
@@ -373,6 +395,8 @@ class RabinChunkIter:
         self._cuts = collections.deque()
         self._eof = False
         self._finished = False
+        self._threaded = False
+        self._ahead = None                # the next read, running on a reader thread
 
     def __iter__(self) -> Iterator[bytes]:
         return self
@@ -382,43 +406,53 @@ class RabinChunkIter:
             if self._blk is None:
                 self._blk, self._pos = _block(), 0
             blk, p = self._blk, self._pos
-            n = _read_into(self._reader, blk.mv[p:])
+            if self._ahead is not None:  # the read started during the last feed
+                fut, self._ahead = self._ahead, None
+                n = fut.result()
+            else:
+                n = _read_into(self._reader, blk.mv[p:])
             self._eof = not n
-            cuts = self._stream.feed(blk.mv[p:p + n], self._eof)
             self._pos = p + n
             last = self._eof or READ_SIZE - self._pos < MIN_READ
             if last:
                 self._blk = None
+            # a large file (a read filled a whole block): the next read runs
+            # on a reader thread while this piece is fed and cut (both
+            # release the GIL); it fills bytes past everything fed
+            if n and (self._threaded or n == READ_SIZE) and os.environ.get("RCDC_READ_AHEAD", "1") != "0":
+                self._threaded = True
+                if self._blk is None:
+                    self._blk, self._pos = _block(), 0
+                self._ahead = _reader_pool().submit(_read_into, self._reader,
+                                                    self._blk.mv[self._pos:])
+            cuts = self._stream.feed(blk.mv[p:p + n], self._eof)
             self._segs.append([blk, p, n, last])
             self._cuts.extend(cuts.tolist())
 
     def _take(self, k: int) -> bytes:
-        """The next k bytes read, releasing spent blocks."""
+        """The next k bytes read, releasing spent blocks.  The chunk is a new
+        bytes object filled by memmove, which runs without the GIL (ctypes
+        releases it around foreign calls), so the copy does not hold off the
+        reader thread; the object is written before anyone else sees it."""
         segs = self._segs
-        s = segs[0]
-        if k <= s[2]:
-            chunk = bytes(s[0].mv[s[1]:s[1] + k])
-        else:  # the chunk spans reads or blocks
-            parts, rem = [], k
-            for s in segs:
-                t = min(rem, s[2])
-                parts.append(s[0].mv[s[1]:s[1] + t])
-                rem -= t
-                if not rem:
-                    break
-            if rem:
+        chunk = _new_bytes(None, k)
+        dst, rem = id(chunk) + _BYTES_DATA, k
+        while rem:  # usually one segment; a chunk may span reads and blocks
+            if not segs:
                 raise AssertionError("rcdc stream cut beyond the bytes fed")
-            chunk = b"".join(parts)
-        rem = k
-        while segs and (rem or not segs[0][2]):
             s = segs[0]
             t = min(rem, s[2])
+            ctypes.memmove(dst, s[0].addr + s[1], t)
+            dst += t
+            rem -= t
             s[1] += t
             s[2] -= t
-            rem -= t
-            if s[2]:
-                break
-            segs.popleft()
+            if not s[2]:
+                segs.popleft()
+                if s[3]:
+                    _release(s[0])
+        while segs and not segs[0][2]:  # the EOF read's empty segment
+            s = segs.popleft()
             if s[3]:
                 _release(s[0])
         return chunk
