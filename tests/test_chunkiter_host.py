@@ -58,9 +58,13 @@ def fake(monkeypatch):
     monkeypatch.setattr(C, "check_rabin_params", lambda *a: None)
 
 
+@pytest.mark.parametrize("ahead", ["1", "0"])
 @pytest.mark.parametrize("size", [0, 1, K, 3 << 20, 16 << 20, (16 << 20) + 3, 70 << 20])
 @pytest.mark.parametrize("kind", ["bytesio", "short", "buffered"])
-def test_chunks_are_the_bytes_between_cuts(fake, size, kind):
+def test_chunks_are_the_bytes_between_cuts(fake, monkeypatch, size, kind, ahead):
+    """Also with the read ahead (a reader thread once a read fills a whole
+    block) on and off (RCDC_READ_AHEAD)."""
+    monkeypatch.setenv("RCDC_READ_AHEAD", ahead)
     data = np.random.default_rng(size).integers(0, 256, size, dtype=np.uint8).tobytes()
     reader = {"bytesio": lambda: io.BytesIO(data),
               "short": lambda: _Short(data, 3 << 20, size),
@@ -71,6 +75,7 @@ def test_chunks_are_the_bytes_between_cuts(fake, size, kind):
     want = list(range(K, size, K)) + ([size] if size else [])
     assert np.cumsum([len(c) for c in chunks]).tolist() == want
     assert it._stream.closed
+    assert it._threaded == (ahead == "1" and kind != "short" and size >= C.READ_SIZE)
     assert list(it) == [] and it.size_hint == 0
 
 
