@@ -309,7 +309,8 @@ def _read_into(reader, mv: memoryview) -> int:
 # costs milliseconds).  A block takes further reads while at least MIN_READ
 # bytes of it are free.
 _POOL: collections.deque = collections.deque()
-_POOL_MAX = 8
+# (what concurrent iterators held at once is kept, up to this many blocks)
+_POOL_MAX = int(os.environ.get("RCDC_BLOCK_POOL", "32"))
 MIN_READ = 1 * MB
 
 
