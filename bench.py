@@ -17,7 +17,8 @@ Other SURVEY.md 8(d) configurations (--workload, not the driver's line):
       (each batch generated on device before its timed chunking).
   C5  one all-zero stream of 12.5 GiB per GPU (100 GiB at 8 GPUs) split
       across ranks (shard.slice_bounds, max + 64 B halos); a step includes
-      the cross-rank stitch (shard.chunk_long_stream_sharded).
+      the cross-rank stitch (shard.SlicedStream: one fixed-size all_gather of
+      crossing windows).
 
 Multi-GPU: one process per GPU (torchrun).  C2/C3: each rank chunks its own
 streams (independent files shard per GPU, no collective on the data path:
@@ -605,28 +606,38 @@ def run_c1(args, torch, dev, rank, world):
     from rustic_core_amd.chunker import Context
     from rustic_core_amd.device import DevicePlan, pack_offsets
     n = args.stream_bytes or (256 << 20)
-    data = stdrng_numpy(0x256, n)
-    fd, path = tempfile.mkstemp(prefix="rcdc_c1_", dir=os.environ.get("TMPDIR", "/tmp"))
-    with os.fdopen(fd, "wb") as f:
-        f.write(data.tobytes())
     cfg = ConfigFile.new(2, POLY)
-    try:
-        def one_pass():
-            out = []
-            with open(path, "rb") as f:
-                for c in ChunkIter.from_config(cfg, f, n):
-                    out.append(len(c))
-            return out
-        lens = one_pass()  # warm: context, lanes, plans, page cache
-        for _ in range(max(args.warmup - 1, 0)):
-            one_pass()
-        t0 = time.perf_counter()
-        for _ in range(args.steps):
-            lens = one_pass()
-        el = time.perf_counter() - t0
-    finally:
-        os.unlink(path)
-    cuts = np.cumsum(np.array(lens, dtype=np.uint64))
+
+    def drop_in(data):
+        """(GiB/s, cut offsets) of the drop-in path over `data` in a file."""
+        fd, path = tempfile.mkstemp(prefix="rcdc_c1_", dir=os.environ.get("TMPDIR", "/tmp"))
+        with os.fdopen(fd, "wb") as f:
+            f.write(data.tobytes())
+        try:
+            def one_pass():
+                out = []
+                with open(path, "rb") as f:
+                    for c in ChunkIter.from_config(cfg, f, n):
+                        out.append(len(c))
+                return out
+            lens = one_pass()  # warm: context, lanes, plans, page cache
+            for _ in range(max(args.warmup - 1, 0)):
+                one_pass()
+            t0 = time.perf_counter()
+            for _ in range(args.steps):
+                lens = one_pass()
+            el = time.perf_counter() - t0
+        finally:
+            os.unlink(path)
+        return el, np.cumsum(np.array(lens, dtype=np.uint64))
+
+    # BASELINE.json configs[0] names a /dev/urandom file: one is read here
+    # beside the reproducible StdRng(0x256) stand-in (SURVEY.md 8(d))
+    with open("/dev/urandom", "rb") as f:
+        udata = np.frombuffer(f.read(n), dtype=np.uint8)
+    el_u, cuts_u = drop_in(udata)
+    data = stdrng_numpy(0x256, n)
+    el, cuts = drop_in(data)
     # the same bytes device-resident
     ctx = Context.get(POLY, MIN, AVG, MAX, device=dev.index)
     offs, alen = pack_offsets([n])
@@ -657,6 +668,14 @@ def run_c1(args, torch, dev, rank, world):
                                 nthreads=1)
         reps += 1
     el_cpu = (time.perf_counter() - t2) / reps
+    want_u = oracle.chunk_cuts(udata)
+    t3 = time.perf_counter()
+    reps_u = 0
+    while time.perf_counter() - t3 < min(args.cpu_seconds, 3.0):
+        oracle.chunk_many_owned(udata, np.zeros(1, np.uint64), np.array([n], np.uint64),
+                                nthreads=1)
+        reps_u += 1
+    el_cpu_u = (time.perf_counter() - t3) / reps_u
     scan_s = scan_ms / max(runs, 1) / 1e3
     line = {
         "metric": METRIC, "value": round(n * args.steps / el / GiB, 3), "unit": "GiB/s",
@@ -686,6 +705,13 @@ def run_c1(args, torch, dev, rank, world):
                          "kind": "port", "sample": f"the whole {n >> 20} MiB file, {reps} passes, "
                          "cdc_ref reference-equivalent mode (owned chunks, 4 KiB reads)",
                          "cpu_model": _cpu_model()},
+        "urandom_file": {"gibs": round(n * args.steps / el_u / GiB, 3),
+                         "ms_per_pass": round(el_u / args.steps * 1e3, 3),
+                         "chunks": int(len(cuts_u)),
+                         "mismatches": int(not np.array_equal(cuts_u, want_u)),
+                         "cpu_gibs_1_thread": round(n / el_cpu_u / GiB, 3),
+                         "note": f"{n >> 20} MiB read from /dev/urandom into a file, then the same "
+                                 "drop-in path and checker (BASELINE.json configs[0] as stated)"},
     }
     print(json.dumps(line), flush=True)
 
@@ -778,18 +804,17 @@ def main():
     torch.cuda.synchronize(dev)  # the workload was built on the default stream
 
     step = lambda: plan.run(ptr, sptr)  # noqa: E731
+    sliced = None
     if args.workload == "C5":
-        from rustic_core_amd.shard import chunk_long_stream_sharded
-        a, b, e = desc["slice"]
-        total_c5 = desc["stream_bytes_total"]
-
-        from rustic_core_amd.shard import device_chunk_from
-        chunk_from = device_chunk_from(ctx, arena, a, b, e, total_c5, first_plan=plan,
-                                       stream=sptr)
-
-        def step():  # noqa: F811
-            plan.run(ptr, sptr)
-            return chunk_long_stream_sharded(total_c5, rank, world, MIN, MAX, chunk_from)
+        # one stream over the ranks: every step runs the slice's plan, then
+        # the stitch -- the crossing window of the device cut list
+        # (rcdc_plan_window), one fixed-size all_gather of the windows, the
+        # host walk over them; the cut lists stay on their ranks (at N = 1
+        # the chain from 0 is the truth and there is nothing to stitch)
+        from rustic_core_amd.shard import SlicedStream
+        sliced = SlicedStream(ctx, arena, plan, desc["stream_bytes_total"], rank, world, MIN, MAX,
+                              stream=sptr)
+        step = sliced.step  # noqa: F811
 
     # W warmup steps, then more untimed steps until the card has run the
     # workload for --prewarm seconds: the first ~20 ms of back-to-back C2
@@ -909,7 +934,8 @@ def main():
 
     out_extra = {}
     if rank == 0 and not args.no_parity:
-        out_extra["parity"] = parity_check(args, arena, offs, lens, plan, last, desc)
+        out_extra["parity"] = parity_check(args, arena, offs, lens, plan,
+                                           sliced.cuts(last) if sliced else last, desc)
     if rank == 0 and not args.no_cpu_baseline and world == 1:
         out_extra["cpu_baseline"] = cpu_baseline(arena, offs, lens, args.cpu_seconds)
     if args.sha256:
@@ -954,8 +980,8 @@ def main():
     if rank == 0:
         parallel = (f"per-stream sharding over {world} GPU(s), no collectives"
                     if args.workload != "C5" else
-                    f"one stream sliced over {world} GPU(s); one all_gather of cut lists "
-                    "per step for the cross-slice stitch")
+                    f"one stream sliced over {world} GPU(s); one fixed-size all_gather of "
+                    "crossing windows per step for the cross-slice stitch (N > 1)")
         data = desc.pop("data")
         desc.pop("slice", None)
         line = {

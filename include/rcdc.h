@@ -179,6 +179,18 @@ rcdc_status rcdc_plan_device_results(rcdc_plan *plan, uint64_t *d_cuts,
                                      uint64_t *d_counts,
                                      const uint64_t **cut_base);
 
+/* Crossing window of stream `stream` of the last run, for stitching one
+ * stream sliced over GPUs (each rank runs a plan over its slice
+ * plus a max + 64 byte halo).  Writes 3 + k words to the device buffer d_out
+ * (8-B aligned), asynchronously on hip_stream (0: the context's stream),
+ * ordered after the run: [0] the stream's cut count n, [1] j = the index of
+ * its first cut >= bound (n if none), [2] that cut (UINT64_MAX if none),
+ * [3 + t] cut t for t < k (UINT64_MAX for t >= n).  Cuts are relative to the
+ * stream's first byte.  n == UINT64_MAX: the stream needs rcdc_plan_finish
+ * (never seen outside forced tests); the caller then reads the host list.   */
+rcdc_status rcdc_plan_window(rcdc_plan *plan, uint32_t stream, uint64_t bound, uint32_t k,
+                             uint64_t *d_out, void *hip_stream);
+
 /* Pipelined runs: with enable = 1, run k's hashing kernels (scan, walk) go
  * to hashing stream k % 2 of the plan's own (after the caller's earlier
  * work) and its chain kernels (resolve; walk check / fixup / assemble) to a

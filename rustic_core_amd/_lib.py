@@ -28,7 +28,7 @@ EXPORTS = (
     "rcdc_aead_seal", "rcdc_aead_open", "rcdc_pack_build",
     "rcdc_zstd_bound", "rcdc_zstd_compress", "rcdc_zstd_tables", "rcdc_zstd_tables_size",
     "rcdc_zstd_check", "rcdc_pack_build_raw", "rcdc_pack_build_raw_multi", "rcdc_copy_ranges",
-    "rcdc_sha256_host", "rcdc_host_alloc", "rcdc_host_free",
+    "rcdc_sha256_host", "rcdc_host_alloc", "rcdc_host_free", "rcdc_plan_window",
 )
 ABI_VERSION = 3
 
@@ -179,6 +179,8 @@ def lib() -> ctypes.CDLL:
     L.rcdc_zstd_tables.argtypes = [vp]
     L.rcdc_zstd_tables_size.restype = u64
     L.rcdc_zstd_tables_size.argtypes = []
+    L.rcdc_plan_window.restype = st
+    L.rcdc_plan_window.argtypes = [vp, u32, u64, u32, vp, vp]
     L.rcdc_plan_device_digests.restype = st
     L.rcdc_plan_device_digests.argtypes = [vp, P(u64)]
     _lib = L

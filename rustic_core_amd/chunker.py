@@ -360,6 +360,39 @@ def _release(blk: _Block) -> None:
         _POOL.append(blk)
 
 
+# Live iterators: when the last one finishes, the pool keeps only
+# _POOL_IDLE blocks, so an idle process holds _POOL_IDLE x READ_SIZE of
+# page-locked memory (not _POOL_MAX x READ_SIZE).
+_POOL_IDLE = int(os.environ.get("RCDC_BLOCK_POOL_IDLE", "2"))
+_live = 0
+_live_lock = threading.Lock()
+
+
+def _iter_started() -> None:
+    global _live
+    with _live_lock:
+        _live += 1
+
+
+def _iter_done() -> None:
+    global _live
+    with _live_lock:
+        _live -= 1
+        if _live == 0:
+            while len(_POOL) > _POOL_IDLE:
+                try:
+                    _POOL.popleft()  # freed by _Block.__del__
+                except IndexError:
+                    break
+
+
+def _read_ahead(reader, blk: _Block, pos: int) -> int:
+    """The reader thread's read into blk from pos; the future holds `blk`
+    (through these arguments) until the read has returned, so the block
+    cannot be freed or handed to another iterator under it."""
+    return _read_into(reader, blk.mv[pos:])
+
+
 _readers = None
 _readers_lock = threading.Lock()
 
@@ -398,6 +431,7 @@ class RabinChunkIter:
         self._finished = False
         self._threaded = False
         self._ahead = None                # the next read, running on a reader thread
+        _iter_started()
 
     def __iter__(self) -> Iterator[bytes]:
         return self
@@ -424,8 +458,8 @@ class RabinChunkIter:
                 self._threaded = True
                 if self._blk is None:
                     self._blk, self._pos = _block(), 0
-                self._ahead = _reader_pool().submit(_read_into, self._reader,
-                                                    self._blk.mv[self._pos:])
+                self._ahead = _reader_pool().submit(_read_ahead, self._reader, self._blk,
+                                                    self._pos)
             cuts = self._stream.feed(blk.mv[p:p + n], self._eof)
             self._segs.append([blk, p, n, last])
             self._cuts.extend(cuts.tolist())
@@ -459,8 +493,32 @@ class RabinChunkIter:
         return chunk
 
     def _finish(self) -> None:
+        """End of iteration (EOF, an error, or the caller dropping the
+        iterator): wait for a read still running on a reader thread before
+        the blocks can go back to the pool, then close the device stream."""
+        if self._finished:
+            return
         self._finished = True
+        fut, self._ahead = self._ahead, None
+        if fut is not None:
+            try:
+                fut.result()
+            except Exception:  # the read's own error is moot now
+                pass
+        self._blk = None
+        self._segs.clear()
         self._stream.close()
+        _iter_done()
+
+    def close(self) -> None:
+        """Stop early (the caller breaks out of its loop)."""
+        self._finish()
+
+    def __del__(self):
+        try:
+            self._finish()
+        except Exception:  # interpreter shutdown
+            pass
 
     def __next__(self) -> bytes:
         if self._finished:

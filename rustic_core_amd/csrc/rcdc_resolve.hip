@@ -356,10 +356,54 @@ __global__ __launch_bounds__(64) void rcdc_stitch_kernel(
     }
 }
 
+// Crossing window of one stream's device cut list (rcdc_plan_window), for the
+// cross-rank stitch of one stream sliced over GPUs: out[0] = the
+// count n, out[1] = j, the index of the first cut >= bound (n if none),
+// out[2] = that cut (~0 if none), out[3 + t] = cut t for t < k (~0 past n).
+// The list is sorted, so exactly one index satisfies c[j] >= bound >
+// c[j - 1]; every thread tests a strided share and only that one writes.
+// n == ~0 (a walked stream that needs host completion) is passed through.
+__global__ __launch_bounds__(256) void rcdc_window_kernel(const uint64_t *__restrict__ cuts,
+                                                          const uint64_t *__restrict__ counts,
+                                                          uint32_t stream, uint64_t base,
+                                                          uint64_t bound, uint32_t k,
+                                                          uint64_t *__restrict__ out) {
+    const uint64_t n = counts[stream];
+    const uint64_t *c = cuts + base;
+    const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t nthr = gridDim.x * blockDim.x;
+    if (n == ~0ull) {
+        if (tid == 0) out[0] = n;
+        return;
+    }
+    if (tid == 0) {
+        out[0] = n;
+        if (n == 0 || c[n - 1] < bound) {  // no cut >= bound
+            out[1] = n;
+            out[2] = ~0ull;
+        }
+    }
+    for (uint32_t t = tid; t < k; t += nthr) out[3 + t] = t < n ? c[t] : ~0ull;
+    for (uint64_t i = tid; i < n; i += nthr) {
+        if (c[i] >= bound && (i == 0 || c[i - 1] < bound)) {
+            out[1] = i;
+            out[2] = c[i];
+        }
+    }
+}
+
 // ---------------------------------------------------------------------------
 // host-side launchers (called from rcdc_runtime.cpp)
 // ---------------------------------------------------------------------------
 namespace rcdc {
+
+hipError_t launch_window(const uint64_t *cuts, const uint64_t *counts, uint32_t stream,
+                         uint64_t base, uint64_t bound, uint32_t k, uint64_t *out,
+                         hipStream_t hs) {
+    hipLaunchKernelGGL(rcdc_window_kernel, dim3(32), dim3(256), 0, hs, cuts, counts, stream, base,
+                       bound, k, out);
+    return hipGetLastError();
+}
 
 hipError_t launch_resolve(const uint8_t *arena, const StreamDesc *sds, const ResolveUnit *units,
                           uint32_t nunits, const StitchDesc *stitches, uint32_t nstitch,

@@ -39,6 +39,9 @@ hipError_t launch_resolve(const uint8_t *arena, const StreamDesc *sds, const Res
                           const uint64_t *item_masks, uint64_t *cuts, uint64_t *counts,
                           uint64_t *piece_cuts, uint64_t *piece_counts, uint64_t *stats,
                           hipStream_t stream);
+hipError_t launch_window(const uint64_t *cuts, const uint64_t *counts, uint32_t stream,
+                         uint64_t base, uint64_t bound, uint32_t k, uint64_t *out,
+                         hipStream_t hs);
 bool host_sha_supported();
 void host_sha256_many(const uint8_t *const *ptrs, const uint64_t *lens, uint32_t n,
                       uint8_t *digests);
@@ -1315,6 +1318,17 @@ rcdc_status run_host_pieces(rcdc_ctx *ctx, Lane *L, const std::vector<uint64_t> 
             HIP_TRY(hipHostMalloc((void **)&L->pinned[k], L->stage, hipHostMallocDefault));
     }
     uint64_t t_copy = 0, t_wait = 0, t0 = g_hprof_on ? now_ns() : 0;
+    // From the first copy on, an early error return must not leave a DMA
+    // from the caller's buffer (direct) or the lane's slots (staged) in
+    // flight: the header promises the buffer is free on return, and the lane
+    // goes back to the pool.  Disarmed once plan_results has waited.
+    struct DrainOnError {
+        hipStream_t s;
+        bool armed = true;
+        ~DrainOnError() {
+            if (armed) (void)hipStreamSynchronize(s);
+        }
+    } drain{L->stream};
     if (prefix_len) {
         if (prefix_ready) HIP_TRY(hipStreamWaitEvent(L->stream, prefix_ready, 0));
         HIP_TRY(hipMemcpyAsync(L->d_arena, d_prefix, prefix_len, hipMemcpyDeviceToDevice,
@@ -1387,6 +1401,7 @@ rcdc_status run_host_pieces(rcdc_ctx *ctx, Lane *L, const std::vector<uint64_t> 
     const uint64_t r0 = g_hprof_on ? now_ns() : 0;
     if ((st = plan_run(L->plan, L->d_arena, L->stream))) return st;
     st = plan_results(L->plan, cuts, cap, counts);
+    drain.armed = st != RCDC_OK && st != RCDC_ERR_CAPACITY;  // capacity: the pass completed
     if (g_hprof_on) {
         const uint64_t t1 = now_ns();
         g_hprof.ns[0] += t_copy;
@@ -1633,6 +1648,24 @@ rcdc_status rcdc_plan_device_results(rcdc_plan *plan, uint64_t *d_cuts, uint64_t
     *d_counts = (uint64_t)(uintptr_t)plan->d_counts;
     *cut_base = plan->cut_base.data();
     return RCDC_OK;
+}
+
+rcdc_status rcdc_plan_window(rcdc_plan *plan, uint32_t stream, uint64_t bound, uint32_t k,
+                             uint64_t *d_out, void *hip_stream) {
+    if (!plan || !d_out) return fail(RCDC_ERR_INVALID_INPUT, "null argument");
+    if (stream >= plan->n)
+        return fail(RCDC_ERR_INVALID_INPUT, "stream %u of a %u-stream plan", stream, plan->n);
+    if (!plan->ran) return fail(RCDC_ERR_INVALID_INPUT, "plan has not been run");
+    if (((uintptr_t)d_out & 7u) != 0) return fail(RCDC_ERR_INVALID_INPUT, "d_out not 8-B aligned");
+    rcdc_ctx *ctx = plan->ctx;
+    DeviceGuard g(ctx->device);
+    hipStream_t st;
+    if (rcdc_status ns = null_enter(ctx, hip_stream, &st)) return ns;
+    // a pipelined run ends on the plan's chain stream: order after it
+    if (plan->pipelined) HIP_TRY(hipStreamWaitEvent(st, plan->done, 0));
+    HIP_TRY(launch_window(plan->d_cuts, plan->d_counts, stream, plan->cut_base[stream], bound, k,
+                          d_out, st));
+    return null_leave(ctx, hip_stream, st);
 }
 
 rcdc_status rcdc_plan_set_pipeline(rcdc_plan *plan, int enable) {

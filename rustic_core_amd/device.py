@@ -84,6 +84,17 @@ class DevicePlan:
             raise status_error(st, _lib.last_error())
         return dc.value, dn.value, np.ctypeslib.as_array(base, shape=(max(self.n, 1),))[:self.n]
 
+    def window(self, stream: int, bound: int, k: int, d_out_ptr: int,
+               hip_stream: Optional[int] = None) -> None:
+        """Enqueue the crossing window of ``stream``'s cut list into the device
+        buffer ``d_out_ptr`` (3 + k u64: count, index and value of the first
+        cut >= ``bound``, the first k cuts; ``rcdc_plan_window``)."""
+        st = _lib.lib().rcdc_plan_window(self._h, int(stream), int(bound), int(k),
+                                         ctypes.c_void_p(d_out_ptr),
+                                         ctypes.c_void_p(hip_stream or 0))
+        if st:
+            raise status_error(st, _lib.last_error())
+
     def hash(self, d_arena_ptr: int, hip_stream: Optional[int] = None) -> None:
         """Enqueue the SHA-256 blob id of every chunk of the last ``run``
         (``rcdc_plan_hash``; crypto/hasher.rs:17-19, file_archiver.rs:151)."""

@@ -396,7 +396,6 @@ class DeviceIngest:
         new = first_occurrences(ids, np.arange(n), known)
         assert p.done[new].all(), "a new blob was not processed"
         nidx = np.nonzero(new)[0]
-        self.indexed.update(map(bytes, ids[nidx]))
         t3 = time.perf_counter()
         nb = len(nidx)
         blobs_new = make_blobs(p.seal_off[nidx], p.seal_len[nidx], ids[nidx],
@@ -407,6 +406,9 @@ class DeviceIngest:
                 self._carry.data_ptr() if self._carry is not None else st_long.data_ptr()]
         res = self._pack(torch, np.concatenate([self._carry_blobs, blobs_new]), srcs, finalize, sp,
                          s_proc, dev)
+        # indexed only once packed (or carried in the open pack): a failed
+        # _pack must not make later calls dedup these blobs away
+        self.indexed.update(map(bytes, ids[nidx]))
         ms["pack"] = (time.perf_counter() - t3) * 1e3
         ms["total"] = (time.perf_counter() - t0) * 1e3
         p.st_long = None
@@ -705,91 +707,96 @@ class HostIngest:
             res.packs = None
             ms["handoff"] += (time.perf_counter() - t) * 1e3
 
-        torch.cuda.synchronize(dev)
-        t0 = time.perf_counter()
-        # the batches' chunking plans first (work lists and cut buffers:
-        # building one allocates device memory and uploads synchronously, so
-        # none is built inside the pipeline or behind the queued copies)
-        plans = [DevicePlan(self.ingest.ctx, offs, [sizes[i] for i in b], slot_len)
-                 for b, (offs, _) in zip(batches, layouts)]
-        ms["plans"] = (time.perf_counter() - t0) * 1e3
-        for k in range(min(len(arenas), len(batches))):
-            h2d(k)
-        results, pending = [], None
+        plans = []
         id_pool = ThreadPoolExecutor(max_workers=self.hash_threads)
+        try:
+            torch.cuda.synchronize(dev)
+            t0 = time.perf_counter()
+            # the batches' chunking plans first (work lists and cut buffers:
+            # building one allocates device memory and uploads synchronously, so
+            # none is built inside the pipeline or behind the queued copies)
+            plans += [DevicePlan(self.ingest.ctx, offs, [sizes[i] for i in b], slot_len)
+                     for b, (offs, _) in zip(batches, layouts)]
+            ms["plans"] = (time.perf_counter() - t0) * 1e3
+            for k in range(min(len(arenas), len(batches))):
+                h2d(k)
+            results, pending = [], None
 
-        def host_ids_for(k):
-            # the batch's long-chunk ids from the files in host memory
-            offs_k = np.asarray(layouts[k][0], np.uint64)
-            files_k = batches[k]
+            def host_ids_for(k):
+                # the batch's long-chunk ids from the files in host memory
+                offs_k = np.asarray(layouts[k][0], np.uint64)
+                files_k = batches[k]
 
-            def one(a, n):
-                j = int(np.searchsorted(offs_k, a, side="right")) - 1
-                o = int(a - offs_k[j])
-                f = files[files_k[j]]
-                return hashlib.sha256(memoryview(f[o:o + int(n)].numpy())).digest()
+                def one(a, n):
+                    j = int(np.searchsorted(offs_k, a, side="right")) - 1
+                    o = int(a - offs_k[j])
+                    f = files[files_k[j]]
+                    return hashlib.sha256(memoryview(f[o:o + int(n)].numpy())).digest()
 
-            def run(c_offs_sel, c_lens_sel):
-                futs_ = [id_pool.submit(one, int(a), int(n)) for a, n in zip(c_offs_sel, c_lens_sel)]
+                def run(c_offs_sel, c_lens_sel):
+                    futs_ = [id_pool.submit(one, int(a), int(n)) for a, n in zip(c_offs_sel, c_lens_sel)]
 
-                class _All:
-                    def result(self_):
-                        out = np.zeros((len(futs_), 32), np.uint8)
-                        for i, f_ in enumerate(futs_):
-                            out[i] = np.frombuffer(f_.result(), np.uint8)
-                        return out
-                return _All()
-            return run
+                    class _All:
+                        def result(self_):
+                            out = np.zeros((len(futs_), 32), np.uint8)
+                            for i, f_ in enumerate(futs_):
+                                out[i] = np.frombuffer(f_.result(), np.uint8)
+                            return out
+                    return _All()
+                return run
 
-        for k in range(len(batches)):
-            torch.cuda.current_stream(dev).wait_event(ev_h2d[k])
-            offs, _ = layouts[k]
-            t = time.perf_counter()
-            # the first and last batches' long-chunk ids on the host: the
-            # first batch's packs then reach the hash threads sooner (they are
-            # idle until then), the last one's follow the last copy at once
-            edge = (k == 0 or k >= len(batches) - self.host_tail_ids) and len(batches) > 1
-            p = self.ingest.begin(arenas[k % len(arenas)], offs, [sizes[i] for i in batches[k]],
-                                  plan=plans[k],
-                                  host_ids=host_ids_for(k) if edge and self.host_edge_ids else None)
-            ms["begin"] += (time.perf_counter() - t) * 1e3
-            ms[f"begin{k}"] = (time.perf_counter() - t) * 1e3
-            if pending is not None:
+            for k in range(len(batches)):
+                torch.cuda.current_stream(dev).wait_event(ev_h2d[k])
+                offs, _ = layouts[k]
                 t = time.perf_counter()
-                r = self.ingest.end(pending)
-                ms["end"] += (time.perf_counter() - t) * 1e3
-                ms[f"end{k - 1}"] = (time.perf_counter() - t) * 1e3
-                ms[f"at{k - 1}"] = (time.perf_counter() - t0) * 1e3
-                handoff(r, k - 1)
-                results.append(r)
-                # the slot of batch k - 1 is free: batch k + 2 goes there
-                if k + 2 < len(batches):
-                    h2d(k + 2)
-            pending = p
-        t = time.perf_counter()
-        r = self.ingest.end(pending, finalize=True)
-        ms["end"] += (time.perf_counter() - t) * 1e3
-        handoff(r, len(batches) - 1)
-        results.append(r)
-        ms["last_end"] = (time.perf_counter() - t0) * 1e3
-        for f in futs:  # the per-batch waiters, then their pack jobs
-            for g in f.result():
-                g.result()
-        seconds = time.perf_counter() - t0
-        pool.shutdown()
-        waiter.shutdown()
-        id_pool.shutdown()
-        # pack-id hashing: thread-seconds spent, and its window
-        ms["hash_thread_s"] = round(hstat["busy_s"], 3)
-        if hstat["first"] is not None:
-            ms["hash_first_ms"] = (hstat["first"] - t0) * 1e3
-            ms["hash_last_ms"] = (hstat["last"] - t0) * 1e3
-        for pl in plans:
-            pl.close()
-        for r in results:  # per-phase times of each batch
-            ms.setdefault("batch_ms", []).append({k: round(v, 1) for k, v in r.ms.items()})
-        keep.clear()
-        del arenas
+                # the first and last batches' long-chunk ids on the host: the
+                # first batch's packs then reach the hash threads sooner (they are
+                # idle until then), the last one's follow the last copy at once
+                edge = (k == 0 or k >= len(batches) - self.host_tail_ids) and len(batches) > 1
+                p = self.ingest.begin(arenas[k % len(arenas)], offs, [sizes[i] for i in batches[k]],
+                                      plan=plans[k],
+                                      host_ids=host_ids_for(k) if edge and self.host_edge_ids else None)
+                ms["begin"] += (time.perf_counter() - t) * 1e3
+                ms[f"begin{k}"] = (time.perf_counter() - t) * 1e3
+                if pending is not None:
+                    t = time.perf_counter()
+                    r = self.ingest.end(pending)
+                    ms["end"] += (time.perf_counter() - t) * 1e3
+                    ms[f"end{k - 1}"] = (time.perf_counter() - t) * 1e3
+                    ms[f"at{k - 1}"] = (time.perf_counter() - t0) * 1e3
+                    handoff(r, k - 1)
+                    results.append(r)
+                    # the slot of batch k - 1 is free: batch k + 2 goes there
+                    if k + 2 < len(batches):
+                        h2d(k + 2)
+                pending = p
+            t = time.perf_counter()
+            r = self.ingest.end(pending, finalize=True)
+            ms["end"] += (time.perf_counter() - t) * 1e3
+            handoff(r, len(batches) - 1)
+            results.append(r)
+            ms["last_end"] = (time.perf_counter() - t0) * 1e3
+            for f in futs:  # the per-batch waiters, then their pack jobs
+                for g in f.result():
+                    g.result()
+            seconds = time.perf_counter() - t0
+            # pack-id hashing: thread-seconds spent, and its window
+            ms["hash_thread_s"] = round(hstat["busy_s"], 3)
+            if hstat["first"] is not None:
+                ms["hash_first_ms"] = (hstat["first"] - t0) * 1e3
+                ms["hash_last_ms"] = (hstat["last"] - t0) * 1e3
+            for r in results:  # per-phase times of each batch
+                ms.setdefault("batch_ms", []).append({k: round(v, 1) for k, v in r.ms.items()})
+        finally:
+            # on any exit: the hash and wait threads stop, the plans' device
+            # buffers and the arena slots are released
+            waiter.shutdown()
+            pool.shutdown()
+            id_pool.shutdown()
+            for pl in plans:
+                pl.close()
+            keep.clear()
+            arenas.clear()
         return HostIngestResult(state["host"], np.asarray(offs_out, np.int64),
                                 np.asarray(sizes_out, np.int64), list(ids_out), results, batches,
                                 seconds, total_in, state["d2h"], ms)

@@ -109,31 +109,75 @@ def slice_bounds(total: int, world: int, min_size: int, max_size: int):
     return out
 
 
-def _stitch_lists(bounds, lists, total):
-    """Walk the ranks in order.  lists[r] = (entry, cuts): cuts of the chain
-    that starts at `entry` (absolute), ending with its first cut >= b_r (or
-    total).  Returns (true cut lists per rank, first rank that could not be
-    merged and the true entry it needs, or None)."""
-    true = []
+def window_len(min_size: int, max_size: int) -> int:
+    """Head cuts a crossing window carries: the true chain enters slice r at
+    x < a_r + max, and the chain from a_r has at most max / min cuts below
+    that (every chunk but the last is >= min)."""
+    return max_size // min_size + 2
+
+
+NONE = np.int64(-1)  # UINT64_MAX as the int64 the collectives move
+
+
+def host_window(cuts_rel, bound_rel: int, k: int) -> np.ndarray:
+    """The crossing window of a host cut list (relative to its chain start):
+    [n, j, c[j], c[0..k)] with j the first cut >= bound_rel -- the same words
+    rcdc_plan_window writes on the device (include/rcdc.h)."""
+    c = np.asarray(cuts_rel, dtype=np.int64)
+    n = len(c)
+    j = int(np.searchsorted(c, bound_rel))
+    out = np.full(3 + k, NONE, dtype=np.int64)
+    out[0], out[1] = n, j
+    if j < n:
+        out[2] = c[j]
+    m = min(k, n)
+    out[3:3 + m] = c[:m]
+    return out
+
+
+def stitch_windows(bounds, entries, wins, k: int):
+    """Walk the ranks in order over their crossing windows.  wins[r] is rank
+    r's window of the chain that starts at entries[r] (relative cuts, list
+    truncated after its first cut >= b_r).  Returns (per rank (i0, j): its
+    true cuts are list[i0 .. j], or None for none; first rank that could not
+    be merged and the true entry it needs, or None)."""
+    out = []
     x = 0  # true chain position entering slice r
     for r, (a, b, _) in enumerate(bounds):
-        entry, cuts = lists[r]
         if x >= b or a >= b:
-            true.append(np.zeros(0, np.uint64))
+            out.append(None)
             continue
-        cuts = np.asarray(cuts, dtype=np.uint64)
-        if x == entry:
-            keep = cuts
+        w = np.asarray(wins[r], dtype=np.int64)
+        n, j = int(w[0]), int(w[1])
+        if x == entries[r]:
+            i0 = 0
         else:
-            i = int(np.searchsorted(cuts, x))
-            if i < len(cuts) and int(cuts[i]) == x:
-                keep = cuts[i + 1:]
-            else:
-                return true, (r, x)
-        true.append(keep)
-        if len(keep):
-            x = int(keep[-1])
-    return true, None
+            head = w[3:3 + min(k, n)] + entries[r]
+            hit = np.flatnonzero(head == x)
+            if not len(hit):
+                return out, (r, x)
+            i0 = int(hit[0]) + 1
+        out.append((i0, j))
+        if j < n:
+            x = int(w[2]) + entries[r]
+    return out, None
+
+
+def _all_gather_windows(win, world: int, group=None):
+    """One fixed-size all_gather of every rank's window (3 + k words):
+    torch tensors on the device over RCCL, on the host over gloo."""
+    import torch
+    import torch.distributed as dist
+    if world == 1:
+        return [win.cpu().numpy() if hasattr(win, "cpu") else np.asarray(win)]
+    t = win if isinstance(win, torch.Tensor) else torch.from_numpy(np.ascontiguousarray(win))
+    if dist.get_backend(group) == "gloo" and t.is_cuda:
+        t = t.cpu()
+    elif dist.get_backend(group) != "gloo" and not t.is_cuda:
+        t = t.to(torch.device("cuda", torch.cuda.current_device()))
+    out = torch.empty(world * t.numel(), dtype=t.dtype, device=t.device)
+    dist.all_gather_into_tensor(out, t, group=group)
+    return list(out.cpu().numpy().reshape(world, -1))
 
 
 def chunk_long_stream_sharded(total: int, rank: int, world: int, min_size: int,
@@ -148,31 +192,112 @@ def chunk_long_stream_sharded(total: int, rank: int, world: int, min_size: int,
     because the halo covers s + max + 63).
 
     Every rank chunks its slice speculatively from a_r; one all_gather of
-    the cut lists lets every rank walk the chain in order; a rank whose list
-    does not contain the true entry cut re-chunks from that entry (another
-    round).  Returns this rank's true cuts (absolute; rank 0 starts at 0).
+    fixed-size crossing windows (window_len + 3 words per rank, never the
+    lists) lets every rank walk the chain in order; a rank whose window does
+    not contain the true entry cut re-chunks from that entry (another round;
+    every rank tracks the entries, so they are not exchanged).  Returns this
+    rank's true cuts (absolute; rank 0 starts at 0).
     """
     import torch.distributed as dist
     bounds = slice_bounds(total, world, min_size, max_size)
     a, b, _ = bounds[rank]
-    entry = a
+    k = window_len(min_size, max_size)
+    entries = [bb[0] for bb in bounds]
     mine = np.asarray(chunk_from(a), dtype=np.uint64) if a < b else np.zeros(0, np.uint64)
     distributed = world > 1 and dist.is_available() and dist.is_initialized()
     if world > 1 and not distributed:
         raise RuntimeError("chunk_long_stream_sharded: world > 1 needs torch.distributed")
     while True:
-        parts: list = [None] * world
-        if distributed:
-            dist.all_gather_object(parts, (entry, mine), group=group)
-        else:
-            parts[0] = (entry, mine)
-        true, todo = _stitch_lists(bounds, parts, total)
+        win = host_window(mine.astype(np.int64) - entries[rank], b - entries[rank], k)
+        wins = _all_gather_windows(win, world, group)
+        spans, todo = stitch_windows(bounds, entries, wins, k)
         if todo is None:
-            return true[rank]
+            sp = spans[rank]
+            return mine[sp[0]:sp[1] + 1] if sp is not None else np.zeros(0, np.uint64)
         r, x = todo
+        entries[r] = x
         if r == rank:
-            entry = x
             mine = np.asarray(chunk_from(x), dtype=np.uint64)
+
+
+class SlicedStream:
+    """The device side of one stream sliced over ranks (bench.py C5): this
+    rank's slice [a, b) plus its halo up to e sits at offset 0 of `arena`; a
+    plan over the whole extent chunks it from a.  `step()` runs the plan and
+    stitches: rcdc_plan_window writes the crossing window into a device
+    buffer, one all_gather of those windows (RCCL on the device; gloo
+    through the host) and the host walk of the ranks decide which part of
+    the device cut list is true.  The lists stay on their ranks; a rank whose
+    window misses the true entry re-chunks from it with a fresh plan (host
+    list).  At world 1 the chain from 0 is the truth: nothing to stitch."""
+
+    def __init__(self, ctx, arena, plan, total: int, rank: int, world: int,
+                 min_size: int, max_size: int, stream=None, group=None):
+        import torch
+        self.ctx, self.arena, self.plan = ctx, arena, plan
+        self.total, self.rank, self.world, self.group = total, rank, world, group
+        self.bounds = slice_bounds(total, world, min_size, max_size)
+        self.a, self.b, self.e = self.bounds[rank]
+        self.k = window_len(min_size, max_size)
+        self.stream = stream
+        self.win = torch.empty(3 + self.k, dtype=torch.int64, device=arena.device)
+        self.chunk_from = device_chunk_from(ctx, arena, self.a, self.b, self.e, total,
+                                            stream=stream)
+        self.last = None
+
+    def step(self):
+        self.plan.run(self.arena.data_ptr(), self.stream)
+        self.last = self.stitch()
+        return self.last
+
+    def stitch(self):
+        """(source, i0, j): this rank's true cuts are source[i0 .. j] --
+        source "plan" (the device list, relative to a) or a host array of
+        absolute cuts (a re-chunked entry).  j None: to the list's end."""
+        import torch
+        if self.world == 1 or self.a >= self.b:
+            return ("plan", 0, None) if self.a < self.b else (np.zeros(0, np.uint64), 0, -1)
+        entries = [bb[0] for bb in self.bounds]
+        mine = None  # host list once this rank has re-chunked
+        while True:
+            if mine is None:
+                self.plan.window(0, self.b - self.a, self.k, self.win.data_ptr(), self.stream)
+                if self.stream:
+                    torch.cuda.current_stream(self.arena.device).wait_stream(
+                        torch.cuda.ExternalStream(self.stream, device=self.arena.device))
+                win = self.win
+            else:
+                win = host_window(mine.astype(np.int64) - entries[self.rank],
+                                  self.b - entries[self.rank], self.k)
+            wins = _all_gather_windows(win, self.world, self.group)
+            if int(wins[self.rank][0]) == -1:  # the walk needs host completion
+                mine = self.plan.results()[0] + np.uint64(self.a)
+                if self.e < self.total:
+                    mine = mine[:int(np.searchsorted(mine, self.b)) + 1]
+                continue
+            if any(int(w[0]) == -1 for w in wins):
+                continue  # another rank completes on the host and sends again
+            spans, todo = stitch_windows(self.bounds, entries, wins, self.k)
+            if todo is None:
+                sp = spans[self.rank]
+                if sp is None:
+                    return (np.zeros(0, np.uint64), 0, -1)
+                return ("plan" if mine is None else mine, sp[0], sp[1])
+            r, x = todo
+            entries[r] = x
+            if r == self.rank:
+                mine = np.asarray(self.chunk_from(x), dtype=np.uint64)
+
+    def cuts(self, res=None) -> np.ndarray:
+        """This rank's true cuts (absolute) of the last step's result."""
+        src, i0, j = res if res is not None else self.last
+        if isinstance(src, str):
+            c = self.plan.results()[0] + np.uint64(self.a)
+            if self.e < self.total:
+                c = c[:int(np.searchsorted(c, self.b)) + 1]
+        else:
+            c = src
+        return c[i0:] if j is None else c[i0:j + 1]
 
 
 def device_chunk_from(ctx, arena, a: int, b: int, e: int, total: int, first_plan=None,

@@ -119,3 +119,45 @@ def test_read_error_after_earlier_reads(fake):
     assert e.value.kind == ErrorKind.InputOutput
     assert sum(got) <= 32 << 20 and it._stream.closed
     assert list(it) == []
+
+
+@pytest.mark.parametrize("how", ["close", "del"])
+def test_abandoned_iterator_waits_for_read_ahead(fake, monkeypatch, how):
+    """A caller that stops early (close, or drops the iterator) while a read
+    runs on a reader thread: the iterator waits for that read before its
+    blocks can be freed or reused (the thread would otherwise
+    write into a block another iterator owns)."""
+    import threading
+    import time
+    monkeypatch.setenv("RCDC_READ_AHEAD", "1")
+    log = []
+    started = threading.Event()
+
+    class _Slow(io.RawIOBase):
+        def __init__(self):
+            self.calls = 0
+
+        def readable(self):
+            return True
+
+        def readinto(self, mv):
+            self.calls += 1
+            if self.calls >= 2:  # the read-ahead
+                started.set()
+                time.sleep(0.3)
+            mv[:len(mv)] = bytes(len(mv))
+            log.append("read")
+            return len(mv)
+
+    it = C.RabinChunkIter(_Ctx(), _Slow())
+    assert len(next(it)) == K
+    assert started.wait(5) and it._ahead is not None
+    blk = it._blk
+    if how == "close":
+        it.close()
+    else:
+        del it
+        gc.collect()
+    log.append("closed")
+    assert log[-2:] == ["read", "closed"]
+    assert blk.ptr or blk._keep is not None  # still a live block

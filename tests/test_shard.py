@@ -151,8 +151,9 @@ def _long_worker(rank, world, port, errfile, kind):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("kind", ["zeros", "phase_zeros", "random", "mixed"])
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("kind,world", [(k, w) for w in (2, 3) for k in
+                                        ("zeros", "phase_zeros", "random", "mixed")] +
+                         [("phase_zeros", 8), ("mixed", 8)])
 def test_long_stream_sharded_gloo(tmp_path, kind, world):
     import torch.multiprocessing as mp
     err = str(tmp_path / "err.txt")
@@ -168,6 +169,33 @@ def test_slice_bounds():
         assert a % 4096 == 0 and bb == nxt[0] and e == min(bb + 65536 + 64, 10_000_000)
 
 
+def test_stitch_windows_rules():
+    """The host walk over crossing windows: merge at a head cut, the merged
+    rank's crossing feeds the next, and the first rank whose window misses
+    the true entry is reported."""
+    from rustic_core_amd.shard import host_window, stitch_windows
+    k = 4
+    bounds = [(0, 100, 150), (100, 200, 250), (200, 300, 300)]
+    entries = [0, 100, 200]
+    l0 = np.array([40, 80, 120], np.int64)          # crossing 120
+    l1 = np.array([20, 60, 110, 150], np.int64)     # abs 120 160 210 250: crossing 210
+    l2 = np.array([10, 50, 100], np.int64)          # abs 210 250 300
+    w = [host_window(l0, 100, k), host_window(l1, 100, k), host_window(l2, 100, k)]
+    spans, todo = stitch_windows(bounds, entries, w, k)
+    assert todo is None and spans == [(0, 2), (1, 2), (1, 2)]
+    # rank 2's chain misses 210: it must re-chunk from there
+    l2b = np.array([15, 55, 100], np.int64)
+    spans, todo = stitch_windows(bounds, entries, w[:2] + [host_window(l2b, 100, k)], k)
+    assert todo == (2, 210) and spans == [(0, 2), (1, 2)]
+    # the chain jumps over a whole slice
+    bounds = [(0, 100, 300), (100, 120, 300), (120, 300, 300)]
+    w = [host_window(np.array([40, 150, 300], np.int64), 100, k),
+         host_window(np.array([30], np.int64), 20, k),
+         host_window(np.array([30, 180], np.int64), 180, k)]
+    spans, todo = stitch_windows(bounds, [0, 100, 120], w, k)
+    assert todo is None and spans == [(0, 1), None, (1, 1)]
+
+
 def test_long_stream_single_rank_no_process_group():
     """world 1 needs no process group (bench.py C5 at N=1)."""
     from oracle import oracle
@@ -180,7 +208,7 @@ def test_long_stream_single_rank_no_process_group():
 
 
 # ------------------------------------- the device path over ranks (GPU, gloo)
-def _device_long_worker(rank, world, port, errfile, kind, params):
+def _device_long_worker(rank, world, port, errfile, kind, params, sliced=False):
     """Rank r holds only its slice + halo on cuda:0 and chunks it with the real
     device plan (shard.device_chunk_from); the cross-rank stitch runs over
     gloo (several ranks share the one GPU of the test box)."""
@@ -200,8 +228,19 @@ def _device_long_worker(rank, world, port, errfile, kind, params):
         arena = torch.zeros(e - a + 256, dtype=torch.uint8, device="cuda:0")
         arena[:e - a] = torch.from_numpy(np.ascontiguousarray(data[a:e])).to("cuda:0")
         ctx = Context.get(oracle.DEFAULT_POLY, mn, avg, mx, device=0)
-        mine = chunk_long_stream_sharded(total, rank, world, mn, mx,
-                                         device_chunk_from(ctx, arena, a, b, e, total))
+        if sliced:  # bench.py C5's path: device windows, fixed-size gather
+            from rustic_core_amd.device import DevicePlan
+            from rustic_core_amd.shard import SlicedStream
+            plan = DevicePlan(ctx, np.zeros(1, np.uint64), np.array([e - a], np.uint64),
+                              int(arena.numel()))
+            ss = SlicedStream(ctx, arena, plan, total, rank, world, mn, mx,
+                              stream=torch.cuda.Stream("cuda:0").cuda_stream)
+            ss.step()
+            mine = ss.cuts(ss.step())  # twice: the plan and its window are reused
+            plan.close()
+        else:
+            mine = chunk_long_stream_sharded(total, rank, world, mn, mx,
+                                             device_chunk_from(ctx, arena, a, b, e, total))
         parts = [None] * world
         dist.all_gather_object(parts, mine)
         got = np.concatenate([np.asarray(p, np.uint64) for p in parts])
@@ -246,4 +285,18 @@ def test_long_stream_sharded_device_gloo(tmp_path, kind, params):
     import torch.multiprocessing as mp
     err = str(tmp_path / "err.txt")
     mp.spawn(_device_long_worker, args=(2, _free_port(), err, kind, params), nprocs=2, join=True)
+    assert not os.path.exists(err)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind", ["zeros", "phase_zeros", "random", "mixed"])
+@pytest.mark.parametrize("world", [2, 4])
+def test_sliced_stream_device_gloo(tmp_path, kind, world):
+    """shard.SlicedStream (bench.py C5): every rank's crossing window from
+    rcdc_plan_window, one fixed-size all_gather, re-chunks where a window
+    misses the true entry; the concatenated true lists equal the oracle's."""
+    import torch.multiprocessing as mp
+    err = str(tmp_path / "err.txt")
+    mp.spawn(_device_long_worker, args=(world, _free_port(), err, kind, (4096, 16384, 65536),
+                                        True), nprocs=world, join=True)
     assert not os.path.exists(err)
