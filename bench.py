@@ -786,13 +786,12 @@ def main():
     plan = DevicePlan(ctx, offs, lens, int(arena.numel()))
     info = plan.info()
     pipelined = False
-    if args.workload != "C5" and not args.no_pipeline and (
-            args.pipeline or info.get("walk_pieces", 0) > 0):
+    if not args.no_pipeline and (args.pipeline or info.get("walk_pieces", 0) > 0):
         # rcdc_plan_set_pipeline: run k's chain kernels (check / fixup /
         # assemble, resolve) overlap run k + 1's hashing kernels
         plan.set_pipeline(True)
         pipelined = True
-    # Unpipelined plans (C2, C5) run on a stream of the job's own: given the
+    # Unpipelined plans (C2) run on a stream of the job's own: given the
     # legacy default stream (handle 0) every rcdc call is ordered with it
     # through two events (rcdc.h), ~20 us of cross-queue latency per C2 step.
     # A pipelined plan already spreads a run over its own streams; a fifth

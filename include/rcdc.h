@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define RCDC_ABI_VERSION 3u
+#define RCDC_ABI_VERSION 4u
 
 /* Status codes map onto rustic_core ErrorKind (crates/core/src/error.rs:108-124). */
 typedef enum {
@@ -42,7 +42,8 @@ typedef enum {
     RCDC_ERR_INVALID_INPUT = 2, /* ErrorKind::InvalidInput (configfile.rs:166-171)     */
     RCDC_ERR_INTERNAL = 3,      /* ErrorKind::Internal     (HIP runtime failures)      */
     RCDC_ERR_INPUT_OUTPUT = 4,  /* ErrorKind::InputOutput  (rabin.rs:131-138,174-180)  */
-    RCDC_ERR_CAPACITY = 5       /* caller's cut buffer too small; counts still valid   */
+    RCDC_ERR_CAPACITY = 5,      /* caller's cut buffer too small; counts still valid   */
+    RCDC_ERR_VERIFICATION = 6   /* ErrorKind::Verification (decrypt.rs:516-526)       */
 } rcdc_status;
 
 typedef struct rcdc_ctx rcdc_ctx;       /* one device + chunker parameters      */
@@ -484,6 +485,108 @@ rcdc_status rcdc_zstd_check(rcdc_ctx *ctx, const void *d_frames, const void *d_d
  * 3.1.1.3.2.2), copied to out (rcdc_zstd_tables_size() bytes): for tests. */
 void rcdc_zstd_tables(void *out);
 uint64_t rcdc_zstd_tables_size(void);
+
+/* ---- the backup data path, host memory to host memory (ABI 4) ----------
+ * FileArchiver::backup_reader (archiver/file_archiver.rs:144-160) for many
+ * files: chunk, `hash(&chunk)`, `index.has_data`, Packer::add -- zstd at the
+ * repository's level, Key::encrypt_data, extra_verify (backend/decrypt.rs:
+ * 478-529) -- PackSizer / should_save (blob/packer.rs:65-200, 659-671), the
+ * sealed header (:693-735) and the pack id, SHA-256 of the pack file
+ * (hash_reader, :826-836).  One engine per backup: the packer stays open
+ * across files and batches, and rcdc_ingest_finish closes the last pack
+ * (Packer::finalize, :385-398).
+ *
+ * Files enter page-locked input slots: rcdc_ingest_reserve hands out space
+ * for one file of known size (the node's size; the reference's size_hint),
+ * the caller reads the file into it (the Read of rabin.rs:110-191) and
+ * rcdc_ingest_commit hands it over (fewer bytes than reserved are fine).
+ * Reserve / commit may be called from many threads (archiver.rs:195).  A
+ * slot that fills becomes a device batch: H2D, chunking, the short chunks'
+ * ids on the device, the long ones' on host threads, zstd + seal + verify of
+ * every chunk, then (once the ids are in) dedup in chunk order, packs, D2H
+ * and the pack ids on host threads.  Results come back through callbacks:
+ * per file its cut offsets and chunk ids in file order (the tree's content
+ * list), per pack the pack file in host memory (valid during the call), its
+ * id and its index entries.  Callbacks run on the engine's threads, one at a
+ * time.                                                                    */
+typedef struct rcdc_ingest rcdc_ingest;
+
+typedef struct {
+    uint8_t key[64];            /* aespoly1305 Key: AES-256 || Poly1305-AES k || r     */
+    int32_t zstd_level;         /* repository version 2: zstd level (0 = zstd's 3)     */
+    uint32_t compress;          /* 1: version 2 compression; 0: stored blobs           */
+    uint32_t extra_verify;      /* 1: decrypt, decode and compare every blob (default) */
+    uint32_t hash_threads;      /* host SHA-256 threads (default 8)                    */
+    uint64_t pack_size;         /* PackSizer (configfile.rs:211-231): default 32 MiB,  */
+    uint64_t pack_grow_factor;  /*   grow factor 32,                                    */
+    uint64_t pack_size_limit;   /*   limit u32::MAX,                                    */
+    uint64_t pack_current_size; /*   the repository's data pack bytes so far           */
+    uint64_t batch_bytes;       /* input slot / device batch bytes (default 2 GiB)     */
+    uint32_t depth;             /* batches in flight on the device (default 4)         */
+    uint32_t in_slots;          /* page-locked input slots (default 4)                 */
+    uint32_t out_slots;         /* page-locked pack buffers (default 4)                */
+    uint32_t pad;
+    uint64_t long_chunk;        /* chunks above this get their id on the host (2 MiB) */
+} rcdc_ingest_config;
+
+typedef struct {
+    uint8_t id[32];
+    uint32_t offset;              /* in the pack (IndexBlob location)              */
+    uint32_t length;              /* sealed bytes                                  */
+    uint32_t uncompressed_length; /* 0: stored as is                               */
+    uint32_t type;                /* BlobType: 0 data                              */
+} rcdc_ingest_blob;               /* 48 B */
+
+typedef struct {
+    const uint8_t *data;          /* the pack file (valid during the callback)     */
+    uint64_t size;
+    uint64_t seq;                 /* packer order                                  */
+    uint8_t id[32];               /* SHA-256 of the pack file                      */
+    uint32_t nblobs, header_len;
+    const rcdc_ingest_blob *blobs;
+} rcdc_ingest_pack;
+
+typedef struct {
+    uint64_t tag;                 /* the caller's, from rcdc_ingest_commit         */
+    uint64_t len;
+    uint32_t nchunks, nnew;       /* chunks; those the packer added                */
+    const uint64_t *cuts;         /* end offset of each chunk in the file          */
+    const uint8_t *ids;           /* 32 B per chunk                                */
+} rcdc_ingest_file_result;
+
+typedef struct {
+    uint64_t bytes_in, files, chunks, new_blobs, packs, pack_bytes, batches;
+    double seconds;               /* first batch submitted .. last pack delivered  */
+} rcdc_ingest_stats;
+
+typedef void (*rcdc_ingest_pack_fn)(void *user, const rcdc_ingest_pack *pack);
+typedef void (*rcdc_ingest_file_fn)(void *user, const rcdc_ingest_file_result *file);
+
+void rcdc_ingest_config_default(rcdc_ingest_config *cfg);
+/* Allocates the slots (page-locked and device memory for a full batch
+ * each) and starts the engine's threads.                                   */
+rcdc_status rcdc_ingest_create(rcdc_ctx *ctx, const rcdc_ingest_config *cfg,
+                               rcdc_ingest_pack_fn pack_cb, rcdc_ingest_file_fn file_cb,
+                               void *user, rcdc_ingest **out);
+/* Ids the repository's index already has (Indexer::has): before the first file. */
+rcdc_status rcdc_ingest_add_index(rcdc_ingest *ing, const uint8_t *ids, uint64_t n);
+/* Space for one file of len bytes (<= batch_bytes); waits for a free slot. */
+rcdc_status rcdc_ingest_reserve(rcdc_ingest *ing, uint64_t len, uint8_t **buf, uint64_t *ticket);
+/* The file's bytes are in place: its first len bytes (<= the reservation). */
+rcdc_status rcdc_ingest_commit(rcdc_ingest *ing, uint64_t ticket, uint64_t tag, uint64_t len);
+/* reserve + memcpy + commit of a file already in memory. */
+rcdc_status rcdc_ingest_add(rcdc_ingest *ing, uint64_t tag, const void *data, uint64_t len);
+/* Submit the partly filled slot now. */
+rcdc_status rcdc_ingest_flush(rcdc_ingest *ing);
+/* No more files: process everything, close the last pack, wait for every
+ * callback; stats (optional) receives the totals.  A verification failure
+ * is RCDC_ERR_VERIFICATION.                                                */
+rcdc_status rcdc_ingest_finish(rcdc_ingest *ing, rcdc_ingest_stats *stats);
+void rcdc_ingest_destroy(rcdc_ingest *ing);
+
+/* SHA-256 of one host buffer on the calling thread (SHA extensions when the
+ * CPU has them): a pack id (packer.rs:832-834) where latency matters.      */
+rcdc_status rcdc_sha256_host_one(const void *data, uint64_t len, uint8_t *digest);
 
 /* ABI version of the loaded library (== RCDC_ABI_VERSION). */
 uint32_t rcdc_abi_version(void);

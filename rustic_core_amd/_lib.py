@@ -29,8 +29,11 @@ EXPORTS = (
     "rcdc_zstd_bound", "rcdc_zstd_compress", "rcdc_zstd_tables", "rcdc_zstd_tables_size",
     "rcdc_zstd_check", "rcdc_pack_build_raw", "rcdc_pack_build_raw_multi", "rcdc_copy_ranges",
     "rcdc_sha256_host", "rcdc_host_alloc", "rcdc_host_free", "rcdc_plan_window",
+    "rcdc_ingest_config_default", "rcdc_ingest_create", "rcdc_ingest_add_index",
+    "rcdc_ingest_reserve", "rcdc_ingest_commit", "rcdc_ingest_add", "rcdc_ingest_flush",
+    "rcdc_ingest_finish", "rcdc_ingest_destroy", "rcdc_sha256_host_one",
 )
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 
 class RcdcLibraryError(RuntimeError):
@@ -179,6 +182,26 @@ def lib() -> ctypes.CDLL:
     L.rcdc_zstd_tables.argtypes = [vp]
     L.rcdc_zstd_tables_size.restype = u64
     L.rcdc_zstd_tables_size.argtypes = []
+    L.rcdc_ingest_config_default.restype = None
+    L.rcdc_ingest_config_default.argtypes = [vp]
+    L.rcdc_ingest_create.restype = st
+    L.rcdc_ingest_create.argtypes = [vp, vp, vp, vp, vp, P(vp)]
+    L.rcdc_ingest_add_index.restype = st
+    L.rcdc_ingest_add_index.argtypes = [vp, vp, u64]
+    L.rcdc_ingest_reserve.restype = st
+    L.rcdc_ingest_reserve.argtypes = [vp, u64, P(vp), P(u64)]
+    L.rcdc_ingest_commit.restype = st
+    L.rcdc_ingest_commit.argtypes = [vp, u64, u64, u64]
+    L.rcdc_ingest_add.restype = st
+    L.rcdc_ingest_add.argtypes = [vp, u64, vp, u64]
+    L.rcdc_ingest_flush.restype = st
+    L.rcdc_ingest_flush.argtypes = [vp]
+    L.rcdc_ingest_finish.restype = st
+    L.rcdc_ingest_finish.argtypes = [vp, vp]
+    L.rcdc_ingest_destroy.restype = None
+    L.rcdc_ingest_destroy.argtypes = [vp]
+    L.rcdc_sha256_host_one.restype = st
+    L.rcdc_sha256_host_one.argtypes = [vp, u64, vp]
     L.rcdc_plan_window.restype = st
     L.rcdc_plan_window.argtypes = [vp, u32, u64, u32, vp, vp]
     L.rcdc_plan_device_digests.restype = st

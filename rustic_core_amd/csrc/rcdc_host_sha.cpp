@@ -13,6 +13,7 @@
 // AVX-512F/BW get RCDC_ERR_UNSUPPORTED (callers then use hashlib).  Host
 // code only: built with the host compiler (Makefile), no device pass.
 #include <cstdint>
+#include <cstdlib>
 #include <cstring>
 
 #include <immintrin.h>
@@ -195,6 +196,84 @@ RCDC_AVX512 static void sha256_many_avx512(const uint8_t *const *ptrs, const uin
     }
 }
 
+// ---- one message on the SHA extensions (SHA-NI): the pack ids whose
+// latency matters (the last packs of a backup), ~2 GB/s on one core.  The
+// state lives as ABEF / CDGH pairs (sha256rnds2's operand order); each
+// 4-round group adds 4 round constants to 4 schedule words (msg1 / msg2 build
+// W[t] for t >= 16 from the previous four groups, FIPS 180-4 6.2.2 step 1).
+#define RCDC_SHANI __attribute__((target("sha,sse4.1,ssse3")))
+
+RCDC_SHANI void sha256_ni_blocks(uint32_t st[8], const uint8_t *p, uint64_t nblk) {
+    const __m128i bswap = _mm_set_epi64x(0x0c0d0e0f08090a0bULL, 0x0405060700010203ULL);
+    __m128i t = _mm_shuffle_epi32(_mm_loadu_si128((const __m128i *)&st[0]), 0xB1);  // CDAB
+    __m128i s1 = _mm_shuffle_epi32(_mm_loadu_si128((const __m128i *)&st[4]), 0x1B); // EFGH
+    __m128i s0 = _mm_alignr_epi8(t, s1, 8);                                          // ABEF
+    s1 = _mm_blend_epi16(s1, t, 0xF0);                                               // CDGH
+    for (; nblk; nblk--, p += 64) {
+        const __m128i a0 = s0, c0 = s1;
+        __m128i w[4];
+        for (int j = 0; j < 16; j++) {
+            if (j < 4)
+                w[j] = _mm_shuffle_epi8(_mm_loadu_si128((const __m128i *)(p + 16 * j)), bswap);
+            else
+                w[j & 3] = _mm_sha256msg2_epu32(
+                    _mm_add_epi32(_mm_sha256msg1_epu32(w[j & 3], w[(j - 3) & 3]),
+                                  _mm_alignr_epi8(w[(j - 1) & 3], w[(j - 2) & 3], 4)),
+                    w[(j - 1) & 3]);
+            __m128i m = _mm_add_epi32(w[j & 3], _mm_load_si128((const __m128i *)&kK256[4 * j]));
+            s1 = _mm_sha256rnds2_epu32(s1, s0, m);
+            m = _mm_shuffle_epi32(m, 0x0E);
+            s0 = _mm_sha256rnds2_epu32(s0, s1, m);
+        }
+        s0 = _mm_add_epi32(s0, a0);
+        s1 = _mm_add_epi32(s1, c0);
+    }
+    t = _mm_shuffle_epi32(s0, 0x1B);           // FEBA
+    s1 = _mm_shuffle_epi32(s1, 0xB1);          // DCHG
+    s0 = _mm_blend_epi16(t, s1, 0xF0);         // DCBA
+    s1 = _mm_alignr_epi8(s1, t, 8);            // HGFE
+    _mm_storeu_si128((__m128i *)&st[0], s0);
+    _mm_storeu_si128((__m128i *)&st[4], s1);
+}
+
+// Portable fallback (no SHA extensions): FIPS 180-4 rounds, one block.
+void sha256_scalar_blocks(uint32_t st[8], const uint8_t *p, uint64_t nblk) {
+    auto rotr = [](uint32_t x, int n) { return (x >> n) | (x << (32 - n)); };
+    for (; nblk; nblk--, p += 64) {
+        uint32_t w[64];
+        for (int t = 0; t < 16; t++)
+            w[t] = (uint32_t)p[4 * t] << 24 | (uint32_t)p[4 * t + 1] << 16 |
+                   (uint32_t)p[4 * t + 2] << 8 | p[4 * t + 3];
+        for (int t = 16; t < 64; t++) {
+            const uint32_t s0 = rotr(w[t - 15], 7) ^ rotr(w[t - 15], 18) ^ (w[t - 15] >> 3);
+            const uint32_t s1 = rotr(w[t - 2], 17) ^ rotr(w[t - 2], 19) ^ (w[t - 2] >> 10);
+            w[t] = w[t - 16] + s0 + w[t - 7] + s1;
+        }
+        uint32_t a = st[0], b = st[1], c = st[2], d = st[3], e = st[4], f = st[5], g = st[6],
+                 h = st[7];
+        for (int t = 0; t < 64; t++) {
+            const uint32_t t1 = h + (rotr(e, 6) ^ rotr(e, 11) ^ rotr(e, 25)) +
+                                ((e & f) ^ (~e & g)) + kK256[t] + w[t];
+            const uint32_t t2 = (rotr(a, 2) ^ rotr(a, 13) ^ rotr(a, 22)) + ((a & b) ^ (a & c) ^ (b & c));
+            h = g; g = f; f = e; e = d + t1; d = c; c = b; b = a; a = t1 + t2;
+        }
+        st[0] += a; st[1] += b; st[2] += c; st[3] += d;
+        st[4] += e; st[5] += f; st[6] += g; st[7] += h;
+    }
+}
+
+bool host_sha_ni() {
+    static const bool ok = [] {
+        if (getenv("RCDC_NO_SHANI")) return false;  // tests: the scalar rounds
+        __builtin_cpu_init();
+        unsigned a, b, c, d;
+        // CPUID leaf 7: EBX bit 29 = SHA
+        __asm__ volatile("cpuid" : "=a"(a), "=b"(b), "=c"(c), "=d"(d) : "a"(7), "c"(0));
+        return ((b >> 29) & 1u) && __builtin_cpu_supports("sse4.1");
+    }();
+    return ok;
+}
+
 bool host_sha_supported() {
     __builtin_cpu_init();
     return __builtin_cpu_supports("avx512f") && __builtin_cpu_supports("avx512bw");
@@ -203,6 +282,30 @@ bool host_sha_supported() {
 void host_sha256_many(const uint8_t *const *ptrs, const uint64_t *lens, uint32_t n,
                       uint8_t *digests) {
     sha256_many_avx512(ptrs, lens, n, digests);
+}
+
+// SHA-256 of one host message (SHA-NI when present, else the scalar rounds).
+void host_sha256_one(const uint8_t *p, uint64_t len, uint8_t out[32]) {
+    uint32_t st[8];
+    memcpy(st, kH0, sizeof st);
+    void (*blocks)(uint32_t *, const uint8_t *, uint64_t) =
+        host_sha_ni() ? sha256_ni_blocks : sha256_scalar_blocks;
+    const uint64_t full = len / 64;
+    blocks(st, p, full);
+    uint8_t tail[128] = {0};
+    const uint64_t r = len - full * 64;
+    memcpy(tail, p + full * 64, r);
+    tail[r] = 0x80;
+    const uint64_t nt = r + 9 <= 64 ? 1 : 2;
+    const uint64_t bits = len * 8;
+    for (int i = 0; i < 8; i++) tail[nt * 64 - 1 - i] = (uint8_t)(bits >> (8 * i));
+    blocks(st, tail, nt);
+    for (int w = 0; w < 8; w++) {
+        out[4 * w] = (uint8_t)(st[w] >> 24);
+        out[4 * w + 1] = (uint8_t)(st[w] >> 16);
+        out[4 * w + 2] = (uint8_t)(st[w] >> 8);
+        out[4 * w + 3] = (uint8_t)st[w];
+    }
 }
 
 }  // namespace rcdc

@@ -1437,6 +1437,24 @@ bool valid_ctx(const rcdc_ctx *c) { return c != nullptr; }
 }  // namespace
 
 // ---------------------------------------------------------------------------
+// internal entry points for the ingest engine (rcdc_ingest.cpp), which is
+// otherwise a client of the C ABI below
+// ---------------------------------------------------------------------------
+namespace rcdc {
+// Rebuild `pl` (created by rcdc_plan_create, its last run waited for) for a
+// new batch layout, reusing its device buffers; uploads on `up`.
+rcdc_status plan_relayout(rcdc_plan *pl, const uint64_t *offs, const uint64_t *lens, uint32_t n,
+                          uint64_t arena_len, hipStream_t up) {
+    if (!pl || !pl->ctx) return fail(RCDC_ERR_INVALID_INPUT, "null plan");
+    pl->ran = false;
+    pl->finished = false;
+    return plan_build(pl->ctx, pl, offs, lens, n, arena_len, up);
+}
+int ctx_device(const rcdc_ctx *ctx) { return ctx ? ctx->device : 0; }
+rcdc_status set_error(rcdc_status st, const char *msg) { return fail(st, "%s", msg); }
+}  // namespace rcdc
+
+// ---------------------------------------------------------------------------
 // C ABI
 // ---------------------------------------------------------------------------
 extern "C" {

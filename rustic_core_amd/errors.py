@@ -34,6 +34,7 @@ _STATUS = {
     2: ErrorKind.InvalidInput,
     3: ErrorKind.Internal,
     4: ErrorKind.InputOutput,
+    6: ErrorKind.Verification,
 }
 
 

@@ -29,7 +29,7 @@ def test_header_symbols_exported(rcdc_lib):
 
 
 def test_abi_version(rcdc_lib):
-    assert rcdc_lib.rcdc_abi_version() == 3
+    assert rcdc_lib.rcdc_abi_version() == 4
 
 
 @pytest.mark.parametrize("avg,mn,mx,status", [

@@ -38,3 +38,33 @@ def test_bad_input():
     from rustic_core_amd.errors import RusticError
     with pytest.raises(RusticError):
         sha256_host([0], [5])  # a null buffer with bytes
+
+
+# ---- rcdc_sha256_host_one: one message on the SHA extensions (the pack ids
+# whose latency matters), and its portable scalar rounds
+_ONE_LENS = [0, 1, 55, 56, 63, 64, 65, 119, 120, 128, 1000, 12345, (1 << 20) + 7]
+
+
+def test_sha256_host_one_matches_hashlib():
+    from rustic_core_amd.native_ingest import sha256_host_one
+    rng = np.random.default_rng(5)
+    for n in _ONE_LENS:
+        b = rng.integers(0, 256, n, dtype=np.uint8).tobytes()
+        assert sha256_host_one(b) == hashlib.sha256(b).digest(), n
+
+
+def test_sha256_host_one_scalar_rounds():
+    """RCDC_NO_SHANI=1: the fallback for CPUs without the SHA extensions."""
+    import os
+    import subprocess
+    import sys
+    code = ("import hashlib, numpy as np\n"
+            "from rustic_core_amd.native_ingest import sha256_host_one\n"
+            "rng = np.random.default_rng(6)\n"
+            f"for n in {_ONE_LENS!r}:\n"
+            "    b = rng.integers(0, 256, n, dtype=np.uint8).tobytes()\n"
+            "    assert sha256_host_one(b) == hashlib.sha256(b).digest(), n\n")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, "-c", code], cwd=root, capture_output=True, text=True,
+                       env=dict(os.environ, RCDC_NO_SHANI="1"), timeout=120)
+    assert r.returncode == 0, r.stderr[-2000:]

@@ -1,0 +1,384 @@
+// ingest_e2e -- the host-to-host backup data path through the C ABI
+// (rcdc_ingest_*, include/rcdc.h), from files on disk, without Python.
+//
+// What a Rust `Repository::backup()` over librcdc would run:
+// `--readers` threads (pariter workers, archiver.rs:195) take files one at a
+// time, reserve the file's size in the engine's page-locked input slots,
+// read the file into it (`pread`, the reference's Read: file_archiver.rs:
+// 144-160 over backend/ignore.rs:223-245's File) and commit it.  The engine
+// chunks, hashes, dedups, compresses, seals, verifies and packs on the GPU;
+// pack files and their ids come back into host memory through the pack
+// callback (blob/packer.rs:826-836), per-file chunk lists through the file
+// callback.
+//
+// Files: `--files` files of `--file-mib` MiB under `--dir`, written by this
+// tool unless present with the right size: file f is splitmix64 words with a
+// zero run at the start of every 4 MiB block (about half zeros, tools/
+// abi_e2e.cpp's --mixed bytes).  A read pass before the timed run leaves
+// them in the page cache ("files on disk (page cache)").
+//
+// Timed: first reserve .. rcdc_ingest_finish returned (every pack id
+// computed and delivered).  Bound: the same input bytes H2D in batch-sized
+// copies from page-locked memory with the run's pack bytes D2H on a second
+// stream at the same time -- what PCIe allows this job in both directions.
+// Checks: every pack id recomputed (rcdc_sha256_host_one) over the pack
+// bytes the callback saw, blob counts, new blobs == distinct chunk ids, and
+// the pack byte total.
+//
+// Output: one JSON line (stdout; also --json FILE).
+#include <hip/hip_runtime.h>
+
+#include <fcntl.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <set>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../include/rcdc.h"
+
+static uint64_t splitmix64(uint64_t x) {
+    x += 0x9E3779B97F4A7C15ull;
+    x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+    x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+    return x ^ (x >> 31);
+}
+
+static void fill_file(uint8_t *p, uint64_t n, uint64_t f) {
+    uint64_t *w = reinterpret_cast<uint64_t *>(p);
+    for (uint64_t i = 0; i < n / 8; i++) w[i] = splitmix64(f << 40 | i);
+    for (uint64_t i = n / 8 * 8; i < n; i++)
+        p[i] = (uint8_t)(splitmix64(f << 40 | (i / 8)) >> (8 * (i % 8)));
+    const uint64_t B = 4ull << 20;
+    for (uint64_t b = 0; b * B < n; b++) {
+        const uint64_t z = splitmix64(f << 40 | 1ull << 39 | b) % B;
+        const uint64_t a = b * B, e = std::min(n, a + z);
+        memset(p + a, 0, e - a);
+    }
+}
+
+static double now() {
+    return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch())
+        .count();
+}
+
+static const char *arg(int argc, char **argv, const char *name, const char *def) {
+    for (int i = 1; i + 1 < argc; i++)
+        if (!strcmp(argv[i], name)) return argv[i + 1];
+    return def;
+}
+static bool flag(int argc, char **argv, const char *name) {
+    for (int i = 1; i < argc; i++)
+        if (!strcmp(argv[i], name)) return true;
+    return false;
+}
+
+#define CHECK(x)                                                                  \
+    do {                                                                          \
+        rcdc_status s_ = (x);                                                     \
+        if (s_) {                                                                 \
+            fprintf(stderr, "%s failed: %d %s\n", #x, (int)s_, rcdc_last_error()); \
+            exit(1);                                                              \
+        }                                                                         \
+    } while (0)
+
+struct PackRec {
+    uint64_t seq, size;
+    uint8_t id[32];
+    uint32_t nblobs;
+    bool id_ok;
+};
+
+struct Sink {
+    std::mutex mu;
+    std::vector<PackRec> packs;
+    uint64_t blobs = 0, files = 0, chunks = 0, nnew = 0;
+    std::set<std::string> chunk_ids;
+    bool check = false;
+};
+
+static void on_pack(void *user, const rcdc_ingest_pack *p) {
+    Sink *s = (Sink *)user;
+    PackRec r{};
+    r.seq = p->seq;
+    r.size = p->size;
+    memcpy(r.id, p->id, 32);
+    r.nblobs = p->nblobs;
+    r.id_ok = true;
+    if (s->check) {
+        uint8_t d[32];
+        rcdc_sha256_host_one(p->data, p->size, d);
+        r.id_ok = memcmp(d, p->id, 32) == 0;
+        // the trailing u32 is the sealed header's length (packfile.rs)
+        uint32_t hl;
+        memcpy(&hl, p->data + p->size - 4, 4);
+        r.id_ok &= hl == p->header_len;
+    }
+    std::lock_guard<std::mutex> lk(s->mu);
+    s->packs.push_back(r);
+    s->blobs += p->nblobs;
+}
+
+static void on_file(void *user, const rcdc_ingest_file_result *f) {
+    Sink *s = (Sink *)user;
+    std::lock_guard<std::mutex> lk(s->mu);
+    s->files++;
+    s->chunks += f->nchunks;
+    s->nnew += f->nnew;
+    if (s->check)
+        for (uint32_t i = 0; i < f->nchunks; i++)
+            s->chunk_ids.insert(std::string((const char *)f->ids + 32 * i, 32));
+}
+
+// H2D of `in_bytes` in batch-sized copies (4 device slots, one stream) while
+// `out_bytes` go D2H on a second stream: seconds until both are done.
+static double pcie_bound(uint64_t in_bytes, uint64_t out_bytes, uint64_t batch, double *h2d_alone) {
+    uint8_t *h_in = nullptr, *h_out = nullptr, *d_in[4] = {}, *d_out = nullptr;
+    if (hipHostMalloc((void **)&h_in, batch, hipHostMallocDefault) != hipSuccess) return -1;
+    if (hipHostMalloc((void **)&h_out, batch, hipHostMallocDefault) != hipSuccess) return -1;
+    for (auto &d : d_in)
+        if (hipMalloc((void **)&d, batch) != hipSuccess) return -1;
+    if (hipMalloc((void **)&d_out, batch) != hipSuccess) return -1;
+    memset(h_in, 1, batch);
+    hipStream_t s1, s2;
+    (void)hipStreamCreateWithFlags(&s1, hipStreamNonBlocking);
+    (void)hipStreamCreateWithFlags(&s2, hipStreamNonBlocking);
+    (void)hipMemcpy(d_in[0], h_in, batch, hipMemcpyHostToDevice);
+    (void)hipDeviceSynchronize();
+    double t0 = now();
+    for (uint64_t o = 0, k = 0; o < out_bytes; o += batch, k++)
+        (void)hipMemcpyAsync(h_out, d_out, std::min(batch, out_bytes - o), hipMemcpyDeviceToHost, s2);
+    for (uint64_t o = 0, k = 0; o < in_bytes; o += batch, k++)
+        (void)hipMemcpyAsync(d_in[k % 4], h_in, std::min(batch, in_bytes - o), hipMemcpyHostToDevice,
+                             s1);
+    (void)hipStreamSynchronize(s1);
+    (void)hipStreamSynchronize(s2);
+    const double both = now() - t0;
+    t0 = now();
+    for (uint64_t o = 0, k = 0; o < in_bytes; o += batch, k++)
+        (void)hipMemcpyAsync(d_in[k % 4], h_in, std::min(batch, in_bytes - o), hipMemcpyHostToDevice,
+                             s1);
+    (void)hipStreamSynchronize(s1);
+    *h2d_alone = (double)in_bytes / (now() - t0) / (1ull << 30);
+    (void)hipStreamDestroy(s1);
+    (void)hipStreamDestroy(s2);
+    for (auto &d : d_in) (void)hipFree(d);
+    (void)hipFree(d_out);
+    (void)hipHostFree(h_in);
+    (void)hipHostFree(h_out);
+    return both;
+}
+
+int main(int argc, char **argv) {
+    const std::string dir = arg(argc, argv, "--dir", "/tmp/rcdc_ingest_files");
+    const int nfiles = atoi(arg(argc, argv, "--files", "32"));
+    const uint64_t fsize = (uint64_t)atoll(arg(argc, argv, "--file-mib", "1024")) << 20;
+    const int readers = atoi(arg(argc, argv, "--readers", "8"));
+    const uint64_t batch = (uint64_t)atoll(arg(argc, argv, "--batch-mib", "2048")) << 20;
+    const int depth = atoi(arg(argc, argv, "--depth", "4"));
+    const int threads = atoi(arg(argc, argv, "--hash-threads", "8"));
+    const int in_slots = atoi(arg(argc, argv, "--in-slots", "4"));
+    const int reps = atoi(arg(argc, argv, "--reps", "1"));
+    const char *json = arg(argc, argv, "--json", nullptr);
+    const bool check = !flag(argc, argv, "--no-check");
+    const bool keep = flag(argc, argv, "--keep");
+    const int level = atoi(arg(argc, argv, "--level", "0"));
+
+    // ---- files on disk -----------------------------------------------------
+    double t = now();
+    (void)mkdir(dir.c_str(), 0755);
+    std::vector<std::string> paths(nfiles);
+    {
+        std::atomic<int> next{0};
+        std::vector<std::thread> ws;
+        for (int w = 0; w < 16; w++)
+            ws.emplace_back([&] {
+                std::vector<uint8_t> buf;
+                for (int f; (f = next++) < nfiles;) {
+                    paths[f] = dir + "/f" + std::to_string(f);
+                    struct stat sb;
+                    if (stat(paths[f].c_str(), &sb) == 0 && (uint64_t)sb.st_size == fsize) continue;
+                    buf.resize(fsize);
+                    fill_file(buf.data(), fsize, (uint64_t)f);
+                    const int fd = open(paths[f].c_str(), O_WRONLY | O_CREAT | O_TRUNC, 0644);
+                    uint64_t o = 0;
+                    while (o < fsize) {
+                        const ssize_t r = write(fd, buf.data() + o, fsize - o);
+                        if (r <= 0) {
+                            perror("write");
+                            exit(1);
+                        }
+                        o += (uint64_t)r;
+                    }
+                    close(fd);
+                }
+            });
+        for (auto &w : ws) w.join();
+    }
+    const double t_gen = now() - t;
+    // one read pass: the files are in the page cache for the timed run
+    t = now();
+    {
+        std::atomic<int> next{0};
+        std::vector<std::thread> ws;
+        for (int w = 0; w < 16; w++)
+            ws.emplace_back([&] {
+                std::vector<uint8_t> buf(16 << 20);
+                for (int f; (f = next++) < nfiles;) {
+                    const int fd = open(paths[f].c_str(), O_RDONLY);
+                    while (read(fd, buf.data(), buf.size()) > 0) {
+                    }
+                    close(fd);
+                }
+            });
+        for (auto &w : ws) w.join();
+    }
+    const double t_warm = now() - t;
+    fprintf(stderr, "files ready: gen %.1f s, warm read %.1f s\n", t_gen, t_warm);
+
+    // ---- engine -------------------------------------------------------------
+    rcdc_ctx *ctx = nullptr;
+    CHECK(rcdc_ctx_create(0x003DA3358B4DC173ull, 512 << 10, 1 << 20, 8 << 20, 0, &ctx));
+    rcdc_ingest_config cfg;
+    rcdc_ingest_config_default(&cfg);
+    for (int i = 0; i < 64; i++) cfg.key[i] = (uint8_t)(splitmix64(0x4A2 + i) >> 7);
+    cfg.zstd_level = level;
+    cfg.batch_bytes = batch;
+    cfg.depth = (uint32_t)depth;
+    cfg.hash_threads = (uint32_t)threads;
+    cfg.in_slots = (uint32_t)in_slots;
+
+    auto run = [&](Sink &sink, int nf, rcdc_ingest_stats *st, double *el) {
+        rcdc_ingest *ing = nullptr;
+        CHECK(rcdc_ingest_create(ctx, &cfg, on_pack, on_file, &sink, &ing));
+        const double t0 = now();
+        std::atomic<int> next{0};
+        std::vector<std::thread> ws;
+        for (int w = 0; w < readers; w++)
+            ws.emplace_back([&] {
+                for (int f; (f = next++) < nf;) {
+                    const int fd = open(paths[f].c_str(), O_RDONLY);
+                    struct stat sb;
+                    fstat(fd, &sb);
+                    const uint64_t n = (uint64_t)sb.st_size;
+                    uint8_t *buf;
+                    uint64_t ticket;
+                    CHECK(rcdc_ingest_reserve(ing, n, &buf, &ticket));
+                    uint64_t o = 0;
+                    while (o < n) {
+                        const ssize_t r = pread(fd, buf + o, n - o, (off_t)o);
+                        if (r <= 0) break;
+                        o += (uint64_t)r;
+                    }
+                    close(fd);
+                    CHECK(rcdc_ingest_commit(ing, ticket, (uint64_t)f, o));
+                }
+            });
+        for (auto &w : ws) w.join();
+        CHECK(rcdc_ingest_finish(ing, st));
+        *el = now() - t0;
+        rcdc_ingest_destroy(ing);
+    };
+    // warm-up (kernels, page-locked pools): a short run, its own repository
+    {
+        Sink w;
+        rcdc_ingest_stats st;
+        double el;
+        run(w, std::min(nfiles, (int)(batch / fsize) + 1), &st, &el);
+        fprintf(stderr, "warm-up: %.3f s\n", el);
+    }
+    double best = 1e30;
+    rcdc_ingest_stats stb{};
+    Sink sink;
+    sink.check = check;
+    for (int r = 0; r < reps; r++) {
+        Sink s;
+        s.check = check && r == reps - 1;
+        rcdc_ingest_stats st;
+        double el;
+        run(s, nfiles, &st, &el);
+        fprintf(stderr, "run %d: %.3f s, %.1f GiB/s, %llu packs\n", r, el,
+                (double)st.bytes_in / el / (1ull << 30), (unsigned long long)st.packs);
+        if (el < best) {
+            best = el;
+            stb = st;
+        }
+        if (r == reps - 1) {
+            std::lock_guard<std::mutex> lk(s.mu);
+            sink.packs = s.packs;
+            sink.blobs = s.blobs;
+            sink.files = s.files;
+            sink.chunks = s.chunks;
+            sink.nnew = s.nnew;
+            sink.chunk_ids = std::move(s.chunk_ids);
+        }
+    }
+    // ---- checks ---------------------------------------------------------------
+    bool ids_ok = true;
+    uint64_t pbytes = 0;
+    std::set<uint64_t> seqs;
+    for (auto &p : sink.packs) {
+        ids_ok &= p.id_ok;
+        pbytes += p.size;
+        seqs.insert(p.seq);
+    }
+    const bool seq_ok = seqs.size() == sink.packs.size() &&
+                        (sink.packs.empty() || *seqs.rbegin() == sink.packs.size() - 1);
+    const bool dedup_ok = !check || (sink.blobs == sink.nnew && sink.nnew == sink.chunk_ids.size());
+    const bool bytes_ok = pbytes == stb.pack_bytes;
+    // ---- bound ------------------------------------------------------------------
+    double h2d_alone = 0;
+    const double bound_s = pcie_bound(stb.bytes_in, stb.pack_bytes, batch, &h2d_alone);
+    const double gib = (double)stb.bytes_in / (1ull << 30);
+    char line[4096];
+    snprintf(line, sizeof line,
+             "{\"metric\": \"host-to-host backup data path GiB/s from files on disk (page cache) "
+             "through the C ABI (rcdc_ingest_*), 1 x MI355X\", \"value\": %.2f, \"unit\": \"GiB/s\", "
+             "\"seconds\": %.4f, \"input_bytes\": %llu, \"files\": %d, \"file_bytes\": %llu, "
+             "\"pack_bytes\": %llu, \"packs\": %zu, \"chunks\": %llu, \"new_blobs\": %llu, "
+             "\"batches\": %llu, "
+             "\"pcie_bound\": {\"gibs_input\": %.2f, \"seconds\": %.4f, \"h2d_alone_gibs\": %.2f, "
+             "\"how\": \"the run's input H2D in batch-sized copies from page-locked memory with its "
+             "pack bytes D2H on a second stream at the same time, no compute\"}, "
+             "\"frac_of_bound\": %.3f, "
+             "\"checks\": {\"pack_ids_ok\": %s, \"pack_seq_ok\": %s, \"dedup_ok\": %s, "
+             "\"pack_bytes_ok\": %s, \"checked\": %s}, "
+             "\"config\": {\"readers\": %d, \"batch_bytes\": %llu, \"depth\": %d, "
+             "\"hash_threads\": %d, \"in_slots\": %d, \"zstd_level\": %d, \"extra_verify\": true, "
+             "\"reps\": %d}, "
+             "\"data\": \"%d files x %llu MiB of splitmix64 words with a zero run at the start of "
+             "every 4 MiB block (~half zeros), written to %s and read once before the run\", "
+             "\"path\": \"tools/ingest_e2e.cpp: reader threads pread each file into "
+             "rcdc_ingest_reserve space (page-locked), rcdc_ingest_commit; the engine "
+             "(rcdc_ingest.cpp) chunks, hashes, dedups, compresses, seals, verifies, packs on "
+             "the GPU and hashes the packs on host threads; no Python\"}",
+             gib / best, best, (unsigned long long)stb.bytes_in, nfiles,
+             (unsigned long long)fsize, (unsigned long long)stb.pack_bytes, sink.packs.size(),
+             (unsigned long long)stb.chunks, (unsigned long long)stb.new_blobs,
+             (unsigned long long)stb.batches, gib / bound_s, bound_s, h2d_alone, bound_s / best,
+             ids_ok ? "true" : "false", seq_ok ? "true" : "false", dedup_ok ? "true" : "false",
+             bytes_ok ? "true" : "false", check ? "true" : "false", readers,
+             (unsigned long long)batch, depth, threads, in_slots, level, reps, nfiles,
+             (unsigned long long)(fsize >> 20), dir.c_str());
+    printf("%s\n", line);
+    if (json) {
+        FILE *f = fopen(json, "w");
+        if (f) {
+            fprintf(f, "%s\n", line);
+            fclose(f);
+        }
+    }
+    if (!keep)
+        for (auto &p : paths) unlink(p.c_str());
+    rcdc_ctx_destroy(ctx);
+    return (ids_ok && seq_ok && dedup_ok && bytes_ok) ? 0 : 3;
+}
