@@ -96,6 +96,12 @@ def parse():
                          "chunk, blob ids, dedup, zstd, seal, verify, packs) over "
                          "--ingest-streams streams; on by default for C3 at N = 1")
     ap.add_argument("--no-ingest", action="store_true")
+    ap.add_argument("--no-flush", action="store_true",
+                    help="pipelined plans: the last timed run's chain stays narrow (A/B)")
+    ap.add_argument("--no-h2h", action="store_true",
+                    help="C3 at N=1: skip the host-to-host object (tools/ingest_e2e)")
+    ap.add_argument("--h2h-files", type=int, default=16,
+                    help="files of 1 GiB for the host-to-host object")
     ap.add_argument("--ingest-streams", type=int, default=64)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-parity", action="store_true")
@@ -539,9 +545,10 @@ def run_c4(args, torch, dist, dev, rank, world, local):
     checked = torch.tensor([len(sample_cuts), bad], dtype=torch.int64, device=coll_device(dev))
     if world > 1:
         dist.all_reduce(checked)
-    c4_traffic = None
+    c4_traffic, c4_sq = None, {}
     if walked_batches == len(layouts) and args.c4_files == 1024 and world == 1:
         c4_traffic, pmc = pmc_traffic("C4", "rcdc_walk_kernel")
+        c4_sq = (pmc or {}).get("sq") or {}
     if rank == 0:
         line = {
             "metric": METRIC, "value": round(total / el_max / GiB, 2), "unit": "GiB/s",
@@ -572,7 +579,11 @@ def run_c4(args, torch, dist, dev, rank, world, local):
                          "frac_lane_hashed": round(lane_hashed / hash_s / 1e9 / HBM_PEAK_GBS, 4),
                          "hash_ms_per_pass": round(scan_ms / passes, 3),
                          "chain_ms_per_pass": round(resolve_ms / passes, 3),
-                         "timed_passes": passes, "pipelined": pipelined},
+                         "timed_passes": passes, "pipelined": pipelined,
+                         "valu_busy": c4_sq.get("valu_busy"),
+                         "valu_per_lane_byte": c4_sq.get("valu_per_lane_byte"),
+                         "limiter": "VALU issue (~7 VALU + 2 LDS reads per hashed byte; "
+                                    "DESIGN.md 3)"},
             "parity": {"files_checked": int(checked[0]), "mismatches": int(checked[1]),
                        "checker": "oracle/cdc_ref on a seeded sample of 64 files"},
         }
@@ -836,7 +847,9 @@ def main():
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     last = None
-    for _ in range(args.steps):
+    for i in range(args.steps):
+        if pipelined and i == args.steps - 1 and not args.no_flush:
+            plan.flush_next()  # the last run's chain is not beside a next walk: whole chip
         last = step()
     torch.cuda.synchronize(dev)
     el = time.perf_counter() - t0
@@ -916,6 +929,11 @@ def main():
         roofline["walk_work"] = st
     if pmc:
         roofline["traffic_source"] = pmc.get("source")
+        sq = pmc.get("sq")
+        if sq:  # the kernel's real limiter, from its SQ counters (tools/pmc_sq_json.py)
+            roofline["valu_busy"] = sq.get("valu_busy")
+            roofline["valu_per_lane_byte"] = sq.get("valu_per_lane_byte")
+            roofline["sq_source"] = sq.get("source")
     if args.workload == "C5":
         # zeros: every chunk is decided by its all-zero prefill window; the
         # kernel reads ~64 B per chunk, so an input-basis "fraction of HBM"
@@ -948,6 +966,8 @@ def main():
     if rank == 0 and not args.no_ingest and (
             args.ingest or (args.workload == "C3" and world == 1)):
         out_extra["ingest"] = ingest_measure(torch, arena, offs, lens, dev, args)
+    if rank == 0 and world == 1 and args.workload == "C3" and not args.no_h2h:
+        out_extra["h2h"] = h2h_measure(args)
     if args.zstd and rank == 0:
         out_extra["zstd"] = zstd_measure(torch, plan, arena, offs, lens, dev, args,
                                          world == 1 and not args.no_cpu_baseline)
@@ -1006,6 +1026,33 @@ def main():
     plan.close()
     if world > 1:
         dist.destroy_process_group()
+
+
+def h2h_measure(args) -> dict:
+    """The host-to-host backup data path through the C ABI (rcdc_ingest_*,
+    the native engine), from files on disk: tools/ingest_e2e writes
+    --h2h-files files of 1 GiB (mixed: about half zero runs), reads them once
+    (page cache), then times reader threads pread-ing each file into the
+    engine's page-locked slots -> chunk, ids, dedup, zstd, seal, verify,
+    packs on the GPU -> pack files and pack ids in host memory; beside it the
+    concurrent PCIe bound of the same bytes (file_archiver.rs:144-160,
+    packer.rs:826-836).  A child process (its own HIP context)."""
+    import subprocess
+    import tempfile
+    tool = os.path.join(ROOT, "tools", "ingest_e2e")
+    if not os.path.exists(tool):
+        return {"skipped": "tools/ingest_e2e not built"}
+    tmp = os.environ.get("TMPDIR", "/tmp")
+    with tempfile.TemporaryDirectory(prefix="rcdc_h2h_", dir=tmp) as d:
+        out = os.path.join(d, "h2h.json")
+        r = subprocess.run([tool, "--dir", os.path.join(d, "files"), "--files", str(args.h2h_files),
+                            "--file-mib", "1024", "--readers", "8", "--json", out],
+                           capture_output=True, text=True, timeout=600)
+        if r.returncode not in (0, 3) or not os.path.exists(out):
+            return {"error": f"ingest_e2e rc {r.returncode}: {r.stderr[-500:]}"}
+        res = json.loads(open(out).read())
+    res["log"] = r.stderr.strip().splitlines()[-4:]
+    return res
 
 
 def sha_measure(torch, plan, ptr, sptr, dev, args, arena, offs, lens, cpu: bool) -> dict:

@@ -205,7 +205,9 @@ rcdc_status rcdc_plan_window(rcdc_plan *plan, uint32_t stream, uint64_t bound, u
  * streams share a queue run in order, so a caller that adds streams of its
  * own around a pipelined plan can serialise its chain with the next walk
  * (bench.py runs pipelined plans on the default stream).  enable = 0
- * restores serial runs.                                                    */
+ * restores serial runs.  enable = 2: pipelined, and the next run is the
+ * last of the sequence: its chain kernels run on every CU instead of beside
+ * a next walk (a pipeline flush; one-shot, later runs are narrow again).    */
 rcdc_status rcdc_plan_set_pipeline(rcdc_plan *plan, int enable);
 
 /* Scan-kernel geometry chosen by the plan (for profiling / roofline). */

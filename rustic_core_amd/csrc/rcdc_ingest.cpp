@@ -38,6 +38,7 @@
 #include <cmath>
 #include <condition_variable>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <deque>
 #include <functional>
@@ -229,6 +230,10 @@ struct rcdc_ingest {
     std::string err_msg;
     rcdc_ingest_stats st{};
     double t_first = 0;
+    // RCDC_INGEST_PROF=1: per batch (stage A start, sync points, end; stage B
+    // start, ids wait end, end), printed by rcdc_ingest_finish
+    bool prof = false;
+    std::vector<std::vector<double>> tl;
 };
 
 namespace {
@@ -380,8 +385,16 @@ void waiter_main(Ing *g) {
 }
 
 // ---- stage A: one closed input slot becomes a batch in flight ------------
+void mark(Ing *g, uint64_t b, double t) {
+    if (!g->prof) return;
+    std::lock_guard<std::mutex> lk(g->cb_mu);
+    if (g->tl.size() <= b) g->tl.resize(b + 1);
+    g->tl[b].push_back(t - g->t_first);
+}
+
 bool stage_a(Ing *g, InSlot *in) {
     auto B = std::make_unique<Batch>();
+    mark(g, g->nbatches, now_s());
     B->index = g->nbatches++;
     B->pslot = (uint32_t)(B->index % g->depth);
     B->in = in;
@@ -421,6 +434,7 @@ bool stage_a(Ing *g, InSlot *in) {
         rs = rcdc_plan_results(P.plan, cuts.data(), cuts.size(), counts.data());
     }
     ING_ST(g, rs, "chunk results");
+    mark(g, B->index, now_s());
     // chunk lists
     uint64_t nchunks = 0;
     for (uint32_t i = 0; i < nf; i++) nchunks += counts[i];
@@ -511,7 +525,7 @@ bool stage_a(Ing *g, InSlot *in) {
     std::vector<uint64_t> src_off(nchunks), src_len(nchunks);
     const uint8_t *src = P.arena;
     B->ulen.assign(nchunks, 0);
-    if (g->compress) {
+    if (g->compress && nchunks) {
         uint64_t fo = 0;
         std::vector<rcdc_zstd_ref> zr(nchunks);
         for (uint64_t k = 0; k < nchunks; k++) {
@@ -527,6 +541,7 @@ bool stage_a(Ing *g, InSlot *in) {
                "zstd");
         src = g->frames;
         for (uint64_t k = 0; k < nchunks; k++) B->ulen[k] = B->c_len[k];
+        mark(g, B->index, now_s());
     } else {
         for (uint64_t k = 0; k < nchunks; k++) {
             src_off[k] = B->c_off[k];
@@ -551,9 +566,10 @@ bool stage_a(Ing *g, InSlot *in) {
         for (uint64_t k = 0; k < nchunks; k++) memcpy(ar[k].nonce, nonces.data() + 16 * k, 16);
     }
     if (!ensure_dev(g, &P.staging, &P.staging_cap, so + 64)) return false;
-    ING_ST(g, rcdc_aead_seal(g->ctx, g->cfg.key, src, ar.data(), (uint32_t)nchunks, P.staging,
-                             g->s_comp),
-           "seal");
+    if (nchunks)
+        ING_ST(g, rcdc_aead_seal(g->ctx, g->cfg.key, src, ar.data(), (uint32_t)nchunks, P.staging,
+                                 g->s_comp),
+               "seal");
     if (g->verify && nchunks) {
         // very_data (decrypt.rs:508-529): open (MAC) into the frames buffer,
         // decode, compare with the chunk in place
@@ -590,6 +606,7 @@ bool stage_a(Ing *g, InSlot *in) {
                 return false;
             }
     }
+    mark(g, B->index, now_s());
     {
         std::lock_guard<std::mutex> lk(g->mu);
         g->st.bytes_in += bytes;
@@ -605,7 +622,9 @@ bool stage_a(Ing *g, InSlot *in) {
 bool stage_b(Ing *g, Batch *B, bool finalize) {
     PSlot &P = g->ps[B->pslot];
     const uint64_t n = B->c_len.size();
+    mark(g, B->index, now_s());
     ING_HIP(g, hipEventSynchronize(P.ev_ids));
+    mark(g, B->index, now_s());
     const uint64_t ns = B->short_idx.size();
     if (ns) {
         std::vector<uint8_t> dig(ns * 32);
@@ -787,6 +806,7 @@ bool stage_b(Ing *g, Batch *B, bool finalize) {
         std::lock_guard<std::mutex> lk(g->mu);
         g->st.new_blobs += nb.size();
     }
+    mark(g, B->index, now_s());
     return true;
 }
 
@@ -831,8 +851,10 @@ void worker_main(Ing *g) {
                 next = g->ready.front();
                 g->ready.pop_front();
             }
+            bool waiting_commits = false;  // a closed slot whose files are not all in
+            for (auto &x : g->in) waiting_commits |= x->state == kClosed;
             if (!retire && !next && g->finishing && g->ready.empty() && g->inflight.empty() &&
-                g->open == nullptr) {
+                g->open == nullptr && !waiting_commits) {
                 fin_carry = !g->carry_blobs.empty();
                 all_done = true;
             }
@@ -925,6 +947,7 @@ rcdc_status rcdc_ingest_create(rcdc_ctx *ctx, const rcdc_ingest_config *cfg,
     g->file_cb = file_cb;
     g->user = user;
     g->device = ctx_device(ctx);
+    g->prof = getenv("RCDC_INGEST_PROF") != nullptr;
     g->level = cfg->zstd_level;
     g->compress = cfg->compress != 0;
     g->verify = cfg->extra_verify != 0;
@@ -1105,6 +1128,15 @@ rcdc_status rcdc_ingest_finish(rcdc_ingest *g, rcdc_ingest_stats *stats) {
         g->cv_done.wait(lk, [&] { return g->packs_pending == 0 || g->err; });
         g->st.seconds = g->t_first ? now_s() - g->t_first : 0;
         if (stats) *stats = g->st;
+        if (g->prof) {
+            std::lock_guard<std::mutex> lk2(g->cb_mu);
+            for (size_t b = 0; b < g->tl.size(); b++) {
+                fprintf(stderr, "ingest batch %zu:", b);
+                for (double t : g->tl[b]) fprintf(stderr, " %.1f", t * 1e3);
+                fprintf(stderr, " ms\n");
+            }
+            fprintf(stderr, "ingest end %.1f ms\n", g->st.seconds * 1e3);
+        }
         if (g->err) return set_error(g->err, g->err_msg.c_str());
     }
     return RCDC_OK;

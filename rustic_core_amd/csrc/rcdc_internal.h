@@ -154,7 +154,18 @@ struct WalkParams {
     uint64_t epoch;        // this run's, 1 .. 2^21 - 1 (the buffers start zeroed)
     uint32_t seed;         // seeding on
     uint32_t early;        // hit rounds stop early, the owed tails spread over the lanes
+    // The walk queue counter (ctr[0]) is never reset: every wave of a walk
+    // adds 1 per piece it takes and 1 for the failed take that ends it, so a
+    // run adds nunits + waves and the next run of the buffer set starts at
+    // qbase (mod 2^32).  The walk kernel itself zeroes the chain counters
+    // ctr[1..3] and `stats` of its set at its start (no memsets between
+    // walks on the hashing queue).
+    uint32_t qbase;
+    uint32_t flags;        // kWalk* below (A/B switches, all on by default)
 };
+constexpr uint32_t kWalkZoneFast = 1;  // zones on the scan's slide (zone_wave_fast)
+constexpr uint32_t kWalkKReset = 2;    // counters reset in the walk kernel, queue by qbase
+constexpr uint32_t kWalkSortAgg = 4;   // wave-aggregated counting sort of the queue
 constexpr uint64_t kEndOpen = 1ull << 63;
 constexpr uint64_t kEndPos = (1ull << 42) - 1;  // position bits of an end word
 constexpr uint64_t kEndNone = kEndPos;          // position: no usable end state

@@ -206,6 +206,7 @@ struct rcdc_plan {
     uint64_t *d_wstate = nullptr, *d_wstate2 = nullptr;  // WalkParams.wstate of set 0 / 1
     uint64_t cap_wstate = 0, cap_wstate2 = 0;
     uint64_t walk_epoch = 0;  // runs of the walk kernel (WalkParams.epoch)
+    uint32_t wqbase[2] = {0, 0};  // walk queue counter at the next run of set 0 / 1 (WalkParams.qbase)
     BoundRes *d_bres = nullptr;
     uint32_t *d_ctr = nullptr;
     uint32_t *d_fixlist = nullptr;
@@ -233,6 +234,8 @@ struct rcdc_plan {
     uint32_t chk_blocks_pipe = 64;
     uint32_t fix_blocks_pipe = 64;  // chain workgroups beside the next walk (RCDC_CHAIN_BLOCKS;
                                     // 64 vs 32: C3 -0.7 %, C4 +1.5 %, profiles/r04/chain_blocks.txt)
+    bool flush_next = false;          // the next pipelined run is the last: its chain runs on
+                                      // every CU (rcdc_plan_set_pipeline(plan, 2))
     uint32_t pp = 0;                  // buffer set of the next run
     uint32_t last_set = 0;            // buffer set of the last run
     uint4 *d_sums2 = nullptr;
@@ -720,6 +723,12 @@ rcdc_status plan_build(rcdc_ctx *ctx, rcdc_plan *pl, const uint64_t *offs, const
     // a hit round stops early and spreads the lanes' owed tails (round_first)
     wp.early = 1;
     if (const char *e = getenv("RCDC_WALK_EARLY")) wp.early = atoi(e) != 0;
+    // round 5: fast zones, in-kernel counter resets, aggregated queue sort
+    // (RCDC_WALK_ZONEFAST / _KRESET / _SORTAGG = 0 turn them off for A/B runs)
+    wp.flags = kWalkZoneFast | kWalkKReset | kWalkSortAgg;
+    if (const char *e = getenv("RCDC_WALK_ZONEFAST"); e && atoi(e) == 0) wp.flags &= ~kWalkZoneFast;
+    if (const char *e = getenv("RCDC_WALK_KRESET"); e && atoi(e) == 0) wp.flags &= ~kWalkKReset;
+    if (const char *e = getenv("RCDC_WALK_SORTAGG"); e && atoi(e) == 0) wp.flags &= ~kWalkSortAgg;
     if (const char *e = getenv("RCDC_CHECK_BUDGET")) wp.chk_budget = strtoull(e, nullptr, 10);
     if (const char *e = getenv("RCDC_FIX_SEG")) wp.fix_seg = (uint32_t)std::max(atoi(e) / 128 * 128, 128);
     if (const char *e = getenv("RCDC_WALK_FIXCAP")) wp.fix_cap = (uint32_t)std::max(atoi(e), 1);  // tests
@@ -774,6 +783,9 @@ rcdc_status plan_build(rcdc_ctx *ctx, rcdc_plan *pl, const uint64_t *offs, const
         }
         if ((st = ensure_dev(&pl->d_bres, &pl->cap_bres, nw))) return st;
         if ((st = ensure_dev(&pl->d_ctr, &pl->cap_ctr, 4))) return st;
+        HIP_TRY(up ? hipMemsetAsync(pl->d_ctr, 0, 16, up) : hipMemset(pl->d_ctr, 0, 16));
+        if (pl->d_ctr2) HIP_TRY(up ? hipMemsetAsync(pl->d_ctr2, 0, 16, up) : hipMemset(pl->d_ctr2, 0, 16));
+        pl->wqbase[0] = pl->wqbase[1] = 0;
         if ((st = ensure_dev(&pl->d_fixlist, &pl->cap_fixlist, nw))) return st;
         if ((st = ensure_dev(&pl->d_fixcuts, &pl->cap_fixcuts, nw * pl->wprm.fix_cap))) return st;
         if ((st = ensure_dev(&pl->d_fixres, &pl->cap_fixres, nw))) return st;
@@ -882,10 +894,16 @@ rcdc_status plan_run(rcdc_plan *pl, const void *d_arena, hipStream_t stream) {
         HIP_TRY(hipStreamSynchronize(stream));
         fprintf(stderr, "rcdc: scan done\n");
     }
+    // chain kernels beside the next walk run narrow; the last run of a
+    // pipeline (flush) has no next walk and takes every CU
+    const bool narrow = pl->pipelined && !pl->flush_next;
+    pl->flush_next = false;
+    const uint32_t wblocks = (uint32_t)std::min<uint64_t>(cus, (pl->wunits.size() + 15) / 16);
+    wprm.qbase = pl->wqbase[set];
     HIP_TRY(launch_walk((const uint8_t *)d_arena, pl->d_sds, pl->d_wunits, wprm, ctx->d_tables,
-                        wpiece, pstatus, ctr,
-                        (uint32_t)std::min<uint64_t>(cus, (pl->wunits.size() + 15) / 16), stream,
-                        ordered));
+                        wpiece, pstatus, ctr, wblocks, stream, ordered));
+    if (!pl->wunits.empty() && (wprm.flags & kWalkKReset))  // takes of this run: one per
+        pl->wqbase[set] += (uint32_t)pl->wunits.size() + wblocks * 16u;  // piece, one failed per wave
     if (dbg) {
         HIP_TRY(hipStreamSynchronize(stream));
         uint32_t h[4] = {0, 0, 0, 0};
@@ -918,8 +936,8 @@ rcdc_status plan_run(rcdc_plan *pl, const void *d_arena, hipStream_t stream) {
                               (uint32_t)pl->wstream_u0.size(), wprm, ctx->d_tables,
                               wpiece, pstatus, bres, ctr, fixlist,
                               fixcuts, fixres, pl->d_cuts, pl->d_counts,
-                              pl->pipelined ? std::min<uint32_t>(cus, pl->fix_blocks_pipe) : cus,
-                              pl->pipelined ? pl->chk_blocks_pipe : cus, stream,
+                              narrow ? std::min<uint32_t>(cus, pl->fix_blocks_pipe) : cus,
+                              narrow ? pl->chk_blocks_pipe : cus, stream,
                               pl->pipelined));
     if (ev) HIP_TRY(hipEventRecord(ev[2], stream));
     pl->last_set = set;
@@ -1697,6 +1715,7 @@ rcdc_status rcdc_plan_set_pipeline(rcdc_plan *plan, int enable) {
         plan->pp = 0;
         return RCDC_OK;
     }
+    if (enable == 2) plan->flush_next = true;  // (set up below on first use)
     if (plan->pipelined) return RCDC_OK;
     DeviceGuard g(plan->ctx->device);
     if (plan->ran) HIP_TRY(hipEventSynchronize(plan->done));  // set 0's buffers are free
@@ -1712,6 +1731,8 @@ rcdc_status rcdc_plan_set_pipeline(rcdc_plan *plan, int enable) {
         HIP_TRY(hipMemset(plan->d_wstate2, 0, 2 * nw * 8));
         if ((st = ensure_dev(&plan->d_bres2, &plan->cap_bres2, nw))) return st;
         if ((st = ensure_dev(&plan->d_ctr2, &plan->cap_ctr2, 4))) return st;
+        HIP_TRY(hipMemset(plan->d_ctr2, 0, 16));
+        plan->wqbase[1] = 0;
         if ((st = ensure_dev(&plan->d_fixlist2, &plan->cap_fixlist2, nw))) return st;
         if ((st = ensure_dev(&plan->d_fixcuts2, &plan->cap_fixcuts2, nw * plan->wprm.fix_cap)))
             return st;

@@ -127,6 +127,45 @@ __device__ uint64_t zone_wave(const uint8_t *s, uint64_t N, uint64_t z, uint64_t
     return hit ? z + (uint64_t)__builtin_ctzll(hit) : kNoCut;
 }
 
+// zone_wave on the scan's LDS tables and slide (rcdc_slide.h): lane k builds
+// its 64 bytes X[k, k+64) from the 128-byte LDS window with 17 dword reads and
+// 16 v_alignbit, then warms its state over them with the scan's slide_in
+// (6 VALU + 1 ds_read_b64 per byte) instead of the generic 64-bit loop
+// (~12 VALU + 2 LDS reads per byte).  Same positions, same first cut.
+template <int TSH>
+__device__ uint64_t zone_wave_fast(const uint8_t *s, uint64_t N, uint64_t z, uint64_t limit,
+                                   uint32_t mask, const uint8_t *tab, const Consts &kc,
+                                   uint8_t *win, uint32_t lane, bool *zero) {
+    const uint32_t w0 = s[z - 64 + lane];
+    const uint32_t w1 = (z + lane < N) ? s[z + lane] : 0u;
+    *zero = false;
+    if (__builtin_amdgcn_ballot_w64(lane < 63 && w0 != 0) == 0) {
+        *zero = true;
+        return z;
+    }
+    wave_sync();
+    if (lane < 63) win[lane + 1] = (uint8_t)w0;
+    else win[0] = 0;
+    win[64 + lane] = (uint8_t)w1;
+    wave_sync();
+    const uint32_t *wd = reinterpret_cast<const uint32_t *>(win);
+    const uint32_t d = lane >> 2, sh = (lane & 3u) * 8u;
+    Unit u;
+    uint32_t lo = wd[d];
+#pragma unroll
+    for (int j = 0; j < 16; j++) {
+        const uint32_t hi = wd[d + j + 1];
+        UDW(u, j) = __builtin_amdgcn_alignbit(hi, lo, sh);
+        lo = hi;
+    }
+    wave_sync();
+    Chain c;
+    c.h0 = c.h1 = 0;
+    warm_unit<TSH>(c, u, tab, kc);
+    const uint64_t hit = __builtin_amdgcn_ballot_w64(z + lane < limit && (c.h0 & mask) == 0);
+    return hit ? z + (uint64_t)__builtin_ctzll(hit) : kNoCut;
+}
+
 // Consecutive chunks of exactly min bytes from `pos` by the all-zero prefill
 // rule: lane i checks the chunk starting at pos + i*min.  Returns how many
 // leading lanes qualify (0..64).  (As rcdc_resolve.hip zero_hops.)
@@ -194,6 +233,7 @@ struct Walk {
     GapQueue *Q;
     uint32_t help_max;
     uint32_t early;  // walk rounds: WalkParams.early (0 elsewhere)
+    uint32_t zonefast;  // WalkParams.flags & kWalkZoneFast
 };
 
 // Segment of a round that starts at A and only needs positions below end:
@@ -463,17 +503,21 @@ __device__ uint64_t walk_next(Walk &W, uint64_t pos, uint64_t stop_scan, uint64_
     const uint64_t z = pos + W.mn;
     uint64_t zc = kNoCut;
     bool zz = false;
-    const ModRepl mod{W.tab, W.k.lwm};
     if (cont_q) {
         // (the search below resumes at cont_q)
     } else if constexpr (LANES == 64) {
         W.zones++;
-        zc = zone_wave(W.arena + W.off, W.N, z, limit, W.mask, W.shift, mod, W.win, W.lane, &zz);
+        if (W.zonefast)
+            zc = zone_wave_fast<TSH>(W.arena + W.off, W.N, z, limit, W.mask, W.tab, W.k, W.win,
+                                     W.lane, &zz);
+        else
+            zc = zone_wave(W.arena + W.off, W.N, z, limit, W.mask, W.shift, ModRepl{W.tab, W.k.lwm},
+                           W.win, W.lane, &zz);
     } else {
         W.zones++;
         if (W.wave == 0) {
-            zc = zone_wave(W.arena + W.off, W.N, z, limit, W.mask, W.shift, mod, W.win, W.lane,
-                           &zz);
+            zc = zone_wave_fast<TSH>(W.arena + W.off, W.N, z, limit, W.mask, W.tab, W.k, W.win,
+                                     W.lane, &zz);
             if (W.lane == 0) {
                 W.red[0] = zc;
                 W.red[1] = zz;
@@ -575,6 +619,14 @@ __global__ __launch_bounds__(1024, 1) void rcdc_walk_kernel(
     __shared__ __attribute__((aligned(16))) uint8_t s_win[16][128];
     __shared__ BlockStats s_st;
     __shared__ GapQueue s_q;
+    // this run's counters (WalkParams.qbase): the chain counters of the set
+    // and its work counters start at 0; the chain of the set's previous run
+    // has finished (the run waits for it), this run's chain starts after
+    // this kernel, and every workgroup adds its counters only at its end
+    if (blockIdx.x == 0 && (prm.flags & kWalkKReset)) {
+        if (threadIdx.x >= 1 && threadIdx.x < 4) ctr[threadIdx.x] = 0;
+        if (threadIdx.x < kWalkStats) prm.stats[threadIdx.x] = 0;
+    }
     stats_init(s_st);
     if (threadIdx.x == 0) {
         s_q.head = s_q.tail = 0;
@@ -602,10 +654,11 @@ __global__ __launch_bounds__(1024, 1) void rcdc_walk_kernel(
     W.Q = prm.helpers ? &s_q : nullptr;
     W.help_max = __builtin_amdgcn_readfirstlane(min(prm.helpers, kHelpMax));
     W.early = prm.early;
+    W.zonefast = __builtin_amdgcn_readfirstlane(prm.flags & kWalkZoneFast);
     uint64_t help_rounds = 0, help_bytes = 0;  // rounds this wave ran for others
     for (;;) {
         uint32_t q = 0;
-        if (lane == 0) q = atomicAdd(&ctr[0], 1u);
+        if (lane == 0) q = atomicAdd(&ctr[0], 1u) - prm.qbase;
         q = __builtin_amdgcn_readfirstlane(q);
         if (q >= prm.nunits) break;
         const uint32_t u = __builtin_amdgcn_readfirstlane(prm.order[q]);
@@ -1007,6 +1060,14 @@ __global__ __launch_bounds__(CT, 1) void rcdc_walk_check_kernel(
     __shared__ uint64_t s_hops[CT / 64][kMaxHops];  // the wave's hop entries
     __shared__ BlockStats s_st;
     __shared__ GapQueue s_q;
+    // this run's counters (WalkParams.qbase): the chain counters of the set
+    // and its work counters start at 0; the chain of the set's previous run
+    // has finished (the run waits for it), this run's chain starts after
+    // this kernel, and every workgroup adds its counters only at its end
+    if (blockIdx.x == 0 && (prm.flags & kWalkKReset)) {
+        if (threadIdx.x >= 1 && threadIdx.x < 4) ctr[threadIdx.x] = 0;
+        if (threadIdx.x < kWalkStats) prm.stats[threadIdx.x] = 0;
+    }
     stats_init(s_st);
     if (threadIdx.x == 0) {
         s_q.head = s_q.tail = 0;
@@ -1034,7 +1095,7 @@ __global__ __launch_bounds__(CT, 1) void rcdc_walk_check_kernel(
     W.Q = nullptr;
     W.help_max = 0;
     W.early = 0;
-    const ModRepl mod{s_tab, W.k.lwm};
+    W.zonefast = __builtin_amdgcn_readfirstlane(prm.flags & kWalkZoneFast);
     const uint64_t mn = prm.min_size, mx = prm.max_size;
     for (;;) {
         uint32_t u = 0;
@@ -1121,8 +1182,11 @@ __global__ __launch_bounds__(CT, 1) void rcdc_walk_check_kernel(
                 } else {
                     const uint64_t z = c + mn;
                     W.zones++;
-                    const uint64_t zc = zone_wave(s, N, z, lim, prm.mask, prm.shift, mod, W.win,
-                                                  lane, &zz);
+                    const uint64_t zc =
+                        W.zonefast ? zone_wave_fast<TSH>(s, N, z, lim, prm.mask, s_tab, W.k, W.win,
+                                                         lane, &zz)
+                                   : zone_wave(s, N, z, lim, prm.mask, prm.shift,
+                                               ModRepl{s_tab, W.k.lwm}, W.win, lane, &zz);
                     if (zc != kNoCut) nxt = zc;
                     else if (lim <= z + 64) nxt = lim;
                     else lo = z + 64;
@@ -1267,6 +1331,7 @@ __global__ __launch_bounds__(1024, 1) void rcdc_walk_fixup_kernel(
     W.Q = nullptr;
     W.help_max = 0;
     W.early = 0;
+    W.zonefast = __builtin_amdgcn_readfirstlane(prm.flags & kWalkZoneFast);
     for (uint32_t idx = blockIdx.x; idx < nfix; idx += gridDim.x) {
         const uint32_t u = fixlist[idx];
         const WalkUnit U = units[u];
@@ -1587,15 +1652,37 @@ __global__ __launch_bounds__(256) void rcdc_walk_cost_kernel(
     }
 }
 
-// One workgroup: counting sort of the queue by key, descending.
-__global__ __launch_bounds__(1024) void rcdc_walk_sort_kernel(WalkParams prm,
-                                                              const uint8_t *__restrict__ key) {
+// One workgroup: counting sort of the queue by key, descending.  The keys
+// take few values (cost classes x K), so per-lane LDS atomics on one counter
+// serialise (~35 us for C3's 26 k pieces); each wave instead aggregates the
+// lanes of one key (ballot) and adds their count with one atomic, then
+// scatters its lanes at base + rank within the key.
+__device__ __forceinline__ uint32_t wave_key_add(uint32_t *cnt, uint32_t key, bool on,
+                                                 uint32_t lane) {
+    uint32_t out = 0;
+    uint64_t todo = __builtin_amdgcn_ballot_w64(on);
+    while (todo) {
+        const uint32_t lead = (uint32_t)__builtin_ctzll(todo);
+        const uint32_t kk = __builtin_amdgcn_readlane(key, lead);
+        const uint64_t m = __builtin_amdgcn_ballot_w64(on && key == kk) & todo;
+        uint32_t base = 0;
+        if (lane == lead) base = atomicAdd(&cnt[kk], (uint32_t)__builtin_popcountll(m));
+        base = __builtin_amdgcn_readlane(base, lead);
+        if ((m >> lane) & 1u) out = base + (uint32_t)__builtin_popcountll(m & ((1ull << lane) - 1ull));
+        todo &= ~m;
+    }
+    return out;
+}
+
+// (the per-lane atomic form, kept for A/B runs: RCDC_WALK_SORTAGG=0)
+__global__ __launch_bounds__(1024) void rcdc_walk_sort_atomic_kernel(WalkParams prm,
+                                                                     const uint8_t *__restrict__ key) {
     __shared__ uint32_t s_cnt[kCostKeys];
     for (uint32_t i = threadIdx.x; i < (uint32_t)kCostKeys; i += blockDim.x) s_cnt[i] = 0;
     __syncthreads();
     for (uint32_t q = threadIdx.x; q < prm.nunits; q += blockDim.x) atomicAdd(&s_cnt[key[q]], 1u);
     __syncthreads();
-    if (threadIdx.x == 0) {  // exclusive prefix, highest key first
+    if (threadIdx.x == 0) {
         uint32_t acc = 0;
         for (int k = kCostKeys - 1; k >= 0; k--) {
             const uint32_t c = s_cnt[k];
@@ -1606,6 +1693,35 @@ __global__ __launch_bounds__(1024) void rcdc_walk_sort_kernel(WalkParams prm,
     __syncthreads();
     for (uint32_t q = threadIdx.x; q < prm.nunits; q += blockDim.x)
         prm.order_out[atomicAdd(&s_cnt[key[q]], 1u)] = prm.order_in[q];
+}
+
+__global__ __launch_bounds__(1024) void rcdc_walk_sort_kernel(WalkParams prm,
+                                                              const uint8_t *__restrict__ key) {
+    __shared__ uint32_t s_cnt[kCostKeys];
+    const uint32_t lane = threadIdx.x & 63u;
+    for (uint32_t i = threadIdx.x; i < (uint32_t)kCostKeys; i += blockDim.x) s_cnt[i] = 0;
+    __syncthreads();
+    for (uint32_t q0 = threadIdx.x - lane; q0 < prm.nunits; q0 += blockDim.x) {
+        const uint32_t q = q0 + lane;
+        const bool on = q < prm.nunits;
+        (void)wave_key_add(s_cnt, on ? key[q] : 0u, on, lane);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {  // exclusive prefix, highest key first
+        uint32_t acc = 0;
+        for (int k = kCostKeys - 1; k >= 0; k--) {
+            const uint32_t c = s_cnt[k];
+            s_cnt[k] = acc;
+            acc += c;
+        }
+    }
+    __syncthreads();
+    for (uint32_t q0 = threadIdx.x - lane; q0 < prm.nunits; q0 += blockDim.x) {
+        const uint32_t q = q0 + lane;
+        const bool on = q < prm.nunits;
+        const uint32_t at = wave_key_add(s_cnt, on ? key[q] : 0u, on, lane);
+        if (on) prm.order_out[at] = prm.order_in[q];
+    }
 }
 
 namespace rcdc {
@@ -1621,8 +1737,12 @@ hipError_t launch_walk_order(const uint8_t *arena, const StreamDesc *sds, const 
     const uint32_t cb = std::min<uint32_t>((prm.nunits + 3) / 4, 4096);
     hipLaunchKernelGGL(rcdc_walk_cost_kernel, dim3(cb), dim3(256), 0, stream, arena, sds, units,
                        prm, key);
-    hipLaunchKernelGGL(rcdc_walk_sort_kernel, dim3(1), dim3(1024), 0, stream, prm,
-                       (const uint8_t *)key);
+    if (prm.flags & kWalkSortAgg)
+        hipLaunchKernelGGL(rcdc_walk_sort_kernel, dim3(1), dim3(1024), 0, stream, prm,
+                           (const uint8_t *)key);
+    else
+        hipLaunchKernelGGL(rcdc_walk_sort_atomic_kernel, dim3(1), dim3(1024), 0, stream, prm,
+                           (const uint8_t *)key);
     return hipGetLastError();
 }
 
@@ -1633,10 +1753,13 @@ hipError_t launch_walk(const uint8_t *arena, const StreamDesc *sds, const WalkUn
                        uint64_t *pstatus, uint32_t *ctr, uint32_t blocks, hipStream_t stream,
                        bool ordered) {
     if (prm.nunits == 0) return hipSuccess;
-    hipError_t e = hipMemsetAsync(ctr, 0, 4 * sizeof(uint32_t), stream);
-    if (e == hipSuccess)
-        e = hipMemsetAsync(prm.stats, 0, kWalkStats * sizeof(unsigned long long), stream);
-    if (e != hipSuccess) return e;
+    hipError_t e = hipSuccess;
+    if (!(prm.flags & kWalkKReset)) {  // (A/B: resets on the walk's queue, queue from 0)
+        e = hipMemsetAsync(ctr, 0, 4 * sizeof(uint32_t), stream);
+        if (e == hipSuccess)
+            e = hipMemsetAsync(prm.stats, 0, kWalkStats * sizeof(unsigned long long), stream);
+        if (e != hipSuccess) return e;
+    }
     if (!ordered) {
         e = launch_walk_order(arena, sds, units, prm, stream);
         if (e != hipSuccess) return e;

@@ -124,6 +124,13 @@ class DevicePlan:
         if st:
             raise status_error(st, _lib.last_error())
 
+    def flush_next(self) -> None:
+        """The next (pipelined) run is the last of the sequence: its chain
+        kernels run on the whole chip (rcdc_plan_set_pipeline(plan, 2))."""
+        st = _lib.lib().rcdc_plan_set_pipeline(self._h, 2)
+        if st:
+            raise status_error(st, _lib.last_error())
+
     def set_timing(self, enable: bool, every: int = 1) -> None:
         """HIP events around the kernels of every ``every``-th run (see
         ``rcdc_plan_set_timing``); ``enable=False`` stops recording."""

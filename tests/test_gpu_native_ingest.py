@@ -147,11 +147,11 @@ def _check_all(files, ing, stats, level, index_ids=()):
 
 
 def test_native_ingest_end_to_end(gpu_ctx):
-    """Several batches (64 MiB slots), small packs (4 MiB: packs close across
+    """Several batches (40 MiB slots), small packs (4 MiB: packs close across
     batches, the open pack carried), both id paths (long_chunk 1 MiB), zstd
     level 3 and extra_verify on."""
     files = _files()
-    ing, stats = _run(gpu_ctx, files, batch_bytes=64 << 20, pack_size=4 << 20,
+    ing, stats = _run(gpu_ctx, files, batch_bytes=40 << 20, pack_size=4 << 20,
                       pack_grow_factor=0, long_chunk=1 << 20, depth=3)
     try:
         assert stats["batches"] >= 3

@@ -187,7 +187,7 @@ int main(int argc, char **argv) {
     const int depth = atoi(arg(argc, argv, "--depth", "4"));
     const int threads = atoi(arg(argc, argv, "--hash-threads", "8"));
     const int in_slots = atoi(arg(argc, argv, "--in-slots", "4"));
-    const int reps = atoi(arg(argc, argv, "--reps", "1"));
+    const int reps = atoi(arg(argc, argv, "--reps", "2"));
     const char *json = arg(argc, argv, "--json", nullptr);
     const bool check = !flag(argc, argv, "--no-check");
     const bool keep = flag(argc, argv, "--keep");
@@ -296,13 +296,15 @@ int main(int argc, char **argv) {
         run(w, std::min(nfiles, (int)(batch / fsize) + 1), &st, &el);
         fprintf(stderr, "warm-up: %.3f s\n", el);
     }
+    // timed runs: the callbacks only record (a caller's file writer takes the
+    // pack bytes); then one more run whose callbacks re-hash every pack and
+    // collect every chunk id for the checks (untimed: the checks run inside
+    // the callbacks, serialised)
     double best = 1e30;
     rcdc_ingest_stats stb{};
     Sink sink;
-    sink.check = check;
     for (int r = 0; r < reps; r++) {
         Sink s;
-        s.check = check && r == reps - 1;
         rcdc_ingest_stats st;
         double el;
         run(s, nfiles, &st, &el);
@@ -312,15 +314,13 @@ int main(int argc, char **argv) {
             best = el;
             stb = st;
         }
-        if (r == reps - 1) {
-            std::lock_guard<std::mutex> lk(s.mu);
-            sink.packs = s.packs;
-            sink.blobs = s.blobs;
-            sink.files = s.files;
-            sink.chunks = s.chunks;
-            sink.nnew = s.nnew;
-            sink.chunk_ids = std::move(s.chunk_ids);
-        }
+    }
+    rcdc_ingest_stats stc{};
+    if (check) {
+        sink.check = true;
+        double el;
+        run(sink, nfiles, &stc, &el);
+        fprintf(stderr, "checked run: %.3f s, %llu packs\n", el, (unsigned long long)stc.packs);
     }
     // ---- checks ---------------------------------------------------------------
     bool ids_ok = true;
@@ -333,8 +333,9 @@ int main(int argc, char **argv) {
     }
     const bool seq_ok = seqs.size() == sink.packs.size() &&
                         (sink.packs.empty() || *seqs.rbegin() == sink.packs.size() - 1);
-    const bool dedup_ok = !check || (sink.blobs == sink.nnew && sink.nnew == sink.chunk_ids.size());
-    const bool bytes_ok = pbytes == stb.pack_bytes;
+    const bool dedup_ok = !check || (sink.blobs == sink.nnew && sink.nnew == sink.chunk_ids.size() &&
+                                     stc.new_blobs == stb.new_blobs && stc.chunks == stb.chunks);
+    const bool bytes_ok = !check || pbytes == stc.pack_bytes;
     // ---- bound ------------------------------------------------------------------
     double h2d_alone = 0;
     const double bound_s = pcie_bound(stb.bytes_in, stb.pack_bytes, batch, &h2d_alone);
