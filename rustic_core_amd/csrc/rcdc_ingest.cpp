@@ -158,7 +158,9 @@ struct PSlot {
     uint8_t *d_dig = nullptr;
     hipStream_t s_ids = nullptr;
     hipEvent_t ev_ids = nullptr;
-    bool busy = false;
+    hipEvent_t ev_sealed = nullptr;   // stage A's device work done (s_comp)
+    hipEvent_t ev_retired = nullptr;  // stage B done with the staging area (s_back)
+    bool busy = false;                // a batch holds this slot (submit .. stage B)
 };
 
 struct OutSlot {
@@ -207,13 +209,17 @@ struct rcdc_ingest {
     int carry_cur = 0;
     std::vector<rcdc_pack_blob> carry_blobs;  // the open pack's blobs (src = kSrcCarry)
     hipStream_t s_in = nullptr, s_comp = nullptr, s_out = nullptr;
-    hipEvent_t ev_comp = nullptr, ev_out = nullptr;
+    hipEvent_t ev_comp = nullptr, ev_out = nullptr, ev_back = nullptr;  // (front / back / out)
     std::vector<std::unique_ptr<OutSlot>> outs;
-    std::deque<std::unique_ptr<Batch>> inflight;
+    std::deque<std::unique_ptr<Batch>> submitted;  // H2D issued, stage A next (front thread)
+    std::deque<std::unique_ptr<Batch>> inflight;   // stage A done, stage B next (back thread)
+    bool front_done = false;                       // every batch has been through stage A
+    uint64_t nclosed = 0;                          // input slots closed so far
+    hipStream_t s_back = nullptr;                  // stage B's device work
     uint64_t nbatches = 0, next_seq = 0;
     std::unordered_set<Id32, Id32Hash> known;  // the index's ids + the packer's
     // threads
-    std::thread worker, waiter;
+    std::thread worker, back, waiter;
     std::vector<std::thread> pool;
     std::mutex pool_mu;
     std::condition_variable pool_cv;
@@ -279,10 +285,13 @@ bool ensure_dev(Ing *g, T **p, uint64_t *cap, uint64_t need) {
     return true;
 }
 
-void post(Ing *g, std::function<void()> fn) {
+// Host SHA-256 jobs; `urgent` ones (the long chunks' ids, which gate a
+// batch's stage B) go before the pack ids.
+void post(Ing *g, std::function<void()> fn, bool urgent = false) {
     {
         std::lock_guard<std::mutex> lk(g->pool_mu);
-        g->jobs.push_back(std::move(fn));
+        if (urgent) g->jobs.push_front(std::move(fn));
+        else g->jobs.push_back(std::move(fn));
     }
     g->pool_cv.notify_one();
 }
@@ -378,7 +387,7 @@ void waiter_main(Ing *g) {
         bool is_last;
         {
             std::lock_guard<std::mutex> lk(g->mu);
-            is_last = g->finishing && g->ready.empty() && g->inflight.empty();
+            is_last = g->front_done && g->inflight.empty();
         }
         hash_packs(g, std::move(w.second), is_last);
     }
@@ -392,13 +401,44 @@ void mark(Ing *g, uint64_t b, double t) {
     g->tl[b].push_back(t - g->t_first);
 }
 
-bool stage_a(Ing *g, InSlot *in) {
-    auto B = std::make_unique<Batch>();
-    mark(g, g->nbatches, now_s());
-    B->index = g->nbatches++;
-    B->pslot = (uint32_t)(B->index % g->depth);
-    B->in = in;
-    B->files = in->files;
+// A ready input slot becomes a batch: a free pipeline slot, and its H2D
+// enqueued at once on the copy stream (it runs while earlier batches are in
+// stage A), in slot order.
+bool submit_ready(Ing *g) {
+    for (;;) {
+        InSlot *in = nullptr;
+        uint32_t ps = 0;
+        std::unique_ptr<Batch> B;
+        {
+            std::lock_guard<std::mutex> lk(g->mu);
+            if (g->ready.empty()) return true;
+            for (ps = 0; ps < g->depth && g->ps[ps].busy; ps++) {
+            }
+            if (ps == g->depth) return true;
+            in = g->ready.front();
+            g->ready.pop_front();
+            g->ps[ps].busy = true;
+            B = std::make_unique<Batch>();
+            B->index = g->nbatches++;
+            if (g->t_first == 0) g->t_first = now_s();
+        }
+        B->pslot = ps;
+        B->in = in;
+        B->files = in->files;
+        mark(g, B->index, now_s());
+        PSlot &P = g->ps[ps];
+        const uint64_t used = in->used;
+        if (!ensure_dev(g, &P.arena, &P.arena_cap, round_up(used, 256) + 512)) return false;
+        // the arena's previous batch is retired: its ids (the last reader) are done
+        ING_HIP(g, hipMemcpyAsync(P.arena, in->host, used, hipMemcpyHostToDevice, g->s_in));
+        ING_HIP(g, hipEventRecord(in->h2d, g->s_in));
+        std::lock_guard<std::mutex> lk(g->mu);
+        g->submitted.push_back(std::move(B));
+    }
+}
+
+bool stage_a(Ing *g, Batch *B) {
+    InSlot *in = B->in;
     PSlot &P = g->ps[B->pslot];
     const uint32_t nf = (uint32_t)B->files.size();
     std::vector<uint64_t> offs(nf), lens(nf);
@@ -410,10 +450,7 @@ bool stage_a(Ing *g, InSlot *in) {
     }
     const uint64_t used = in->used;
     const uint64_t arena_len = round_up(used, 256) + 256;
-    if (!ensure_dev(g, &P.arena, &P.arena_cap, arena_len + 256)) return false;
-    // 1. H2D on the copy stream (the input slot is the source until it lands)
-    ING_HIP(g, hipMemcpyAsync(P.arena, in->host, used, hipMemcpyHostToDevice, g->s_in));
-    ING_HIP(g, hipEventRecord(in->h2d, g->s_in));
+    // 1. the H2D (submit_ready) lands before the chunking
     ING_HIP(g, hipStreamWaitEvent(g->s_comp, in->h2d, 0));
     // 2. chunk
     if (!P.plan) {
@@ -488,7 +525,7 @@ bool stage_a(Ing *g, InSlot *in) {
     // long ids: groups of up to 16 similar lengths per multi-buffer call
     std::sort(long_idx.begin(), long_idx.end(),
               [&](uint32_t a, uint32_t b) { return B->c_len[a] > B->c_len[b]; });
-    Batch *bp = B.get();
+    Batch *bp = B;
     const bool mb = host_sha_supported();
     const size_t per = mb ? 16 : 1;
     for (size_t a = 0; a < long_idx.size(); a += per) {
@@ -514,7 +551,7 @@ bool stage_a(Ing *g, InSlot *in) {
             bp->long_jobs--;
             std::lock_guard<std::mutex> lk(g->mu);
             g->cv_slot.notify_all();
-        });
+        }, true);
     }
     {  // from here the slot is freed once its H2D and long-id jobs are done
         std::lock_guard<std::mutex> lk(g->mu);
@@ -566,6 +603,8 @@ bool stage_a(Ing *g, InSlot *in) {
         for (uint64_t k = 0; k < nchunks; k++) memcpy(ar[k].nonce, nonces.data() + 16 * k, 16);
     }
     if (!ensure_dev(g, &P.staging, &P.staging_cap, so + 64)) return false;
+    // the staging area's previous batch has been packed (stage B, s_back)
+    ING_HIP(g, hipStreamWaitEvent(g->s_comp, P.ev_retired, 0));
     if (nchunks)
         ING_ST(g, rcdc_aead_seal(g->ctx, g->cfg.key, src, ar.data(), (uint32_t)nchunks, P.staging,
                                  g->s_comp),
@@ -606,6 +645,7 @@ bool stage_a(Ing *g, InSlot *in) {
                 return false;
             }
     }
+    ING_HIP(g, hipEventRecord(P.ev_sealed, g->s_comp));
     mark(g, B->index, now_s());
     {
         std::lock_guard<std::mutex> lk(g->mu);
@@ -613,7 +653,6 @@ bool stage_a(Ing *g, InSlot *in) {
         g->st.files += nf;
         g->st.chunks += nchunks;
         g->st.batches++;
-        g->inflight.push_back(std::move(B));
     }
     return true;
 }
@@ -624,6 +663,7 @@ bool stage_b(Ing *g, Batch *B, bool finalize) {
     const uint64_t n = B->c_len.size();
     mark(g, B->index, now_s());
     ING_HIP(g, hipEventSynchronize(P.ev_ids));
+    ING_HIP(g, hipStreamWaitEvent(g->s_back, P.ev_sealed, 0));
     mark(g, B->index, now_s());
     const uint64_t ns = B->short_idx.size();
     if (ns) {
@@ -714,11 +754,11 @@ bool stage_b(Ing *g, Batch *B, bool finalize) {
     if (!grp.empty()) {
         if (!ensure_dev(g, &g->d_packs, &g->d_packs_cap, total + 64)) return false;
         // the last pack build's D2H must be done with d_packs
-        ING_HIP(g, hipStreamWaitEvent(g->s_comp, g->ev_out, 0));
+        ING_HIP(g, hipStreamWaitEvent(g->s_back, g->ev_out, 0));
         ING_ST(g, rcdc_pack_build_raw_multi(g->ctx, g->cfg.key, srcs, 2, blobs.data(),
                                             (uint32_t)open_from, packs.data(),
                                             (uint32_t)packs.size(), g->d_packs, total,
-                                            boffs.data(), g->s_comp),
+                                            boffs.data(), g->s_back),
                "pack build");
         {  // a free page-locked output slot
             std::unique_lock<std::mutex> lk(g->mu);
@@ -739,8 +779,8 @@ bool stage_b(Ing *g, Batch *B, bool finalize) {
             out->cap = total + total / 4;
             ING_HIP(g, hipHostMalloc((void **)&out->host, out->cap, hipHostMallocDefault));
         }
-        ING_HIP(g, hipEventRecord(g->ev_comp, g->s_comp));
-        ING_HIP(g, hipStreamWaitEvent(g->s_out, g->ev_comp, 0));
+        ING_HIP(g, hipEventRecord(g->ev_back, g->s_back));
+        ING_HIP(g, hipStreamWaitEvent(g->s_out, g->ev_back, 0));
         ING_HIP(g, hipMemcpyAsync(out->host, g->d_packs, total, hipMemcpyDeviceToHost, g->s_out));
         ING_HIP(g, hipEventRecord(g->ev_out, g->s_out));
     }
@@ -761,7 +801,7 @@ bool stage_b(Ing *g, Batch *B, bool finalize) {
         }
         if (!ensure_dev(g, &g->carry[nx], &g->carry_cap[nx], o + 64)) return false;
         ING_ST(g, rcdc_copy_ranges(g->ctx, srcs, 2, cr.data(), (uint32_t)cr.size(), g->carry[nx],
-                                   g->s_comp),
+                                   g->s_back),
                "carry");
         g->carry_cur = nx;
     }
@@ -802,6 +842,7 @@ bool stage_b(Ing *g, Batch *B, bool finalize) {
         }
         g->wait_cv.notify_one();
     }
+    ING_HIP(g, hipEventRecord(P.ev_retired, g->s_back));
     {
         std::lock_guard<std::mutex> lk(g->mu);
         g->st.new_blobs += nb.size();
@@ -825,63 +866,84 @@ void reap_inputs(Ing *g) {
         }
 }
 
+// Front thread: the copies in (submit_ready) and stage A, in batch order.
 void worker_main(Ing *g) {
     (void)hipSetDevice(g->device);
     for (;;) {
         reap_inputs(g);
-        InSlot *next = nullptr;
-        bool retire = false, fin_carry = false, all_done = false;
+        if (!submit_ready(g)) return;
+        std::unique_ptr<Batch> B;
+        bool done = false;
         {
             std::unique_lock<std::mutex> lk(g->mu);
             if (g->err) {
                 g->cv_done.notify_all();
                 return;
             }
-            // the oldest batch goes to stage B once its ids are in, or when
-            // the pipeline is full
-            if (!g->inflight.empty()) {
-                Batch *o = g->inflight.front().get();
-                const bool ids = o->long_jobs == 0 &&
-                                 hipEventQuery(g->ps[o->pslot].ev_ids) == hipSuccess;
-                const bool full = g->inflight.size() >= g->depth;
-                const bool drain = g->ready.empty() && (g->finishing || ids);
-                retire = o->long_jobs == 0 && (ids || full || drain);
-            }
-            if (!retire && !g->ready.empty() && g->inflight.size() < g->depth) {
-                next = g->ready.front();
-                g->ready.pop_front();
-            }
-            bool waiting_commits = false;  // a closed slot whose files are not all in
-            for (auto &x : g->in) waiting_commits |= x->state == kClosed;
-            if (!retire && !next && g->finishing && g->ready.empty() && g->inflight.empty() &&
-                g->open == nullptr && !waiting_commits) {
-                fin_carry = !g->carry_blobs.empty();
-                all_done = true;
+            if (!g->submitted.empty()) {
+                B = std::move(g->submitted.front());
+                g->submitted.pop_front();
+            } else {
+                bool waiting_commits = false;  // a closed slot whose files are not all in
+                for (auto &x : g->in) waiting_commits |= x->state == kClosed;
+                done = g->finishing && g->ready.empty() && g->open == nullptr && !waiting_commits;
             }
         }
-        if (retire) {
-            std::unique_ptr<Batch> B;
-            bool last;
-            {
-                std::lock_guard<std::mutex> lk(g->mu);
-                B = std::move(g->inflight.front());
-                g->inflight.pop_front();
-                last = g->finishing && g->ready.empty() && g->inflight.empty() &&
-                       g->open == nullptr;
-            }
-            if (!stage_b(g, B.get(), last)) return;
+        if (B) {
+            if (!stage_a(g, B.get())) return;
+            std::lock_guard<std::mutex> lk(g->mu);
+            g->inflight.push_back(std::move(B));
+            g->cv_slot.notify_all();
             continue;
         }
-        if (next) {
-            if (g->t_first == 0) g->t_first = now_s();
-            if (!stage_a(g, next)) return;
+        std::unique_lock<std::mutex> lk(g->mu);
+        if (done) {
+            g->front_done = true;
+            g->cv_slot.notify_all();
+            return;
+        }
+        g->cv_slot.wait_for(lk, std::chrono::microseconds(200));
+    }
+}
+
+// Back thread: stage B in batch order once a batch's ids are in, then the
+// pipeline slot is free for the next batch; at the end, Packer::finalize.
+void back_main(Ing *g) {
+    (void)hipSetDevice(g->device);
+    for (;;) {
+        std::unique_ptr<Batch> B;
+        bool last = false, all_done = false, fin_carry = false;
+        {
+            std::unique_lock<std::mutex> lk(g->mu);
+            for (;;) {
+                if (g->err) {
+                    g->cv_done.notify_all();
+                    return;
+                }
+                if (!g->inflight.empty() && g->inflight.front()->long_jobs == 0) break;
+                if (g->inflight.empty() && g->front_done) break;
+                g->cv_slot.wait_for(lk, std::chrono::microseconds(200));
+            }
+            if (!g->inflight.empty()) {
+                B = std::move(g->inflight.front());
+                g->inflight.pop_front();
+                last = g->front_done && g->inflight.empty();
+            } else {
+                all_done = true;
+                fin_carry = !g->carry_blobs.empty();
+            }
+        }
+        if (B) {
+            if (!stage_b(g, B.get(), last)) return;
+            std::lock_guard<std::mutex> lk(g->mu);
+            g->ps[B->pslot].busy = false;
+            g->cv_slot.notify_all();
             continue;
         }
         if (all_done) {
             if (fin_carry) {  // Packer::finalize with nothing else left
                 Batch empty;
                 empty.pslot = 0;
-                if (!g->ps[0].ev_ids) return;
                 if (!stage_b(g, &empty, true)) return;
             }
             std::unique_lock<std::mutex> lk(g->mu);
@@ -889,8 +951,6 @@ void worker_main(Ing *g) {
             g->cv_done.notify_all();
             return;
         }
-        std::unique_lock<std::mutex> lk(g->mu);
-        g->cv_slot.wait_for(lk, std::chrono::microseconds(200));
     }
 }
 
@@ -898,6 +958,7 @@ void close_open_locked(Ing *g) {
     InSlot *s = g->open;
     if (!s) return;
     g->open = nullptr;
+    g->nclosed++;
     s->state = kClosed;
     if (s->open_res == 0) {
         if (s->files.empty()) {
@@ -929,8 +990,8 @@ void rcdc_ingest_config_default(rcdc_ingest_config *c) {
     c->batch_bytes = 2ull << 30;
     c->depth = 4;
     c->in_slots = 4;
-    c->out_slots = 4;
-    c->hash_threads = 8;
+    c->out_slots = 6;
+    c->hash_threads = 10;
     c->long_chunk = 2ull << 20;
 }
 
@@ -987,7 +1048,9 @@ rcdc_status rcdc_ingest_create(rcdc_ctx *ctx, const rcdc_ingest_config *cfg,
     g->ps.resize(g->depth);
     for (auto &P : g->ps) {
         if ((e = hipStreamCreateWithFlags(&P.s_ids, hipStreamNonBlocking)) != hipSuccess ||
-            (e = hipEventCreateWithFlags(&P.ev_ids, hipEventDisableTiming)) != hipSuccess)
+            (e = hipEventCreateWithFlags(&P.ev_ids, hipEventDisableTiming)) != hipSuccess ||
+            (e = hipEventCreateWithFlags(&P.ev_sealed, hipEventDisableTiming)) != hipSuccess ||
+            (e = hipEventCreateWithFlags(&P.ev_retired, hipEventDisableTiming)) != hipSuccess)
             return fail_hip(e, "stream");
         // device buffers sized for a full batch up front (a hipFree inside
         // the pipeline would synchronise the device)
@@ -999,6 +1062,12 @@ rcdc_status rcdc_ingest_create(rcdc_ctx *ctx, const rcdc_ingest_config *cfg,
         if ((e = hipMalloc((void **)&P.staging, stg)) != hipSuccess) return fail_hip(e, "staging");
         P.staging_cap = stg;
         (void)nmax;
+        // the plan built once for a full-batch layout (allocations and
+        // synchronous uploads here, not inside the pipeline); each batch then
+        // re-lays it out on its compute stream, reusing the buffers
+        const uint64_t off0 = 0, len0 = g->batch_cap;
+        if (rcdc_status ps = rcdc_plan_create(ctx, &off0, &len0, 1, g->batch_cap + 256, &P.plan))
+            return ps;
     }
     {
         const uint64_t f = g->batch_cap + g->batch_cap / 64 + (64ull << 20);
@@ -1010,13 +1079,16 @@ rcdc_status rcdc_ingest_create(rcdc_ctx *ctx, const rcdc_ingest_config *cfg,
     if ((e = hipStreamCreateWithFlags(&g->s_in, hipStreamNonBlocking)) != hipSuccess ||
         (e = hipStreamCreateWithFlags(&g->s_comp, hipStreamNonBlocking)) != hipSuccess ||
         (e = hipStreamCreateWithFlags(&g->s_out, hipStreamNonBlocking)) != hipSuccess ||
+        (e = hipStreamCreateWithFlags(&g->s_back, hipStreamNonBlocking)) != hipSuccess ||
         (e = hipEventCreateWithFlags(&g->ev_comp, hipEventDisableTiming)) != hipSuccess ||
+        (e = hipEventCreateWithFlags(&g->ev_back, hipEventDisableTiming)) != hipSuccess ||
         (e = hipEventCreateWithFlags(&g->ev_out, hipEventDisableTiming)) != hipSuccess)
         return fail_hip(e, "streams");
     if ((e = hipEventRecord(g->ev_out, g->s_out)) != hipSuccess) return fail_hip(e, "event");
     for (uint32_t i = 0; i < g->nthreads; i++) g->pool.emplace_back(pool_main, gp);
     g->waiter = std::thread(waiter_main, gp);
     g->worker = std::thread(worker_main, gp);
+    g->back = std::thread(back_main, gp);
     *out = g.release();
     return RCDC_OK;
 }
@@ -1042,7 +1114,10 @@ rcdc_status rcdc_ingest_reserve(rcdc_ingest *g, uint64_t len, uint8_t **buf, uin
         if (g->err) return set_error(g->err, g->err_msg.c_str());
         if (g->finishing) return set_error(RCDC_ERR_INVALID_INPUT, "ingest already finishing");
         InSlot *s = g->open;
-        if (s && s->used + len > s->cap) {
+        // the first slot closes at a quarter: the device starts sooner
+        const uint64_t cap_now = g->nclosed == 0 ? std::max(g->batch_cap / 4, len)
+                                                 : (s ? s->cap : 0);
+        if (s && s->used + len > cap_now) {
             close_open_locked(g);
             s = nullptr;
         }
@@ -1153,6 +1228,7 @@ void rcdc_ingest_destroy(rcdc_ingest *g) {
         g->cv_slot.notify_all();
     }
     if (g->worker.joinable()) g->worker.join();
+    if (g->back.joinable()) g->back.join();
     {
         std::unique_lock<std::mutex> lk(g->mu);
         g->cv_done.wait_for(lk, std::chrono::seconds(30), [&] { return g->packs_pending == 0; });
@@ -1179,6 +1255,8 @@ void rcdc_ingest_destroy(rcdc_ingest *g) {
         (void)hipHostFree(P.h_refs);
         (void)hipStreamDestroy(P.s_ids);
         (void)hipEventDestroy(P.ev_ids);
+        (void)hipEventDestroy(P.ev_sealed);
+        (void)hipEventDestroy(P.ev_retired);
     }
     (void)hipFree(g->frames);
     (void)hipFree(g->d_packs);
@@ -1187,7 +1265,9 @@ void rcdc_ingest_destroy(rcdc_ingest *g) {
     (void)hipStreamDestroy(g->s_in);
     (void)hipStreamDestroy(g->s_comp);
     (void)hipStreamDestroy(g->s_out);
+    (void)hipStreamDestroy(g->s_back);
     (void)hipEventDestroy(g->ev_comp);
+    (void)hipEventDestroy(g->ev_back);
     (void)hipEventDestroy(g->ev_out);
     delete g;
 }

@@ -162,10 +162,19 @@ struct WalkParams {
     // walks on the hashing queue).
     uint32_t qbase;
     uint32_t flags;        // kWalk* below (A/B switches, all on by default)
+    // kWalkKReset: `stats` is slot r % 4 of four (run r); the walk kernel
+    // zeroes slot (r + 2) % 4, run r - 2's, whose chain has finished (the
+    // run waited for it) and which run r + 2 uses after this run's chain.  A
+    // walk cannot zero its own slot: its workgroups run on all XCDs, and one
+    // on a busy XCD may start after the others have added their counters.
+    unsigned long long *stats_next;
+    uint32_t cost_blocks;  // workgroups of the cost kernel (1024 threads; > 256: the old
+                           // thousands-of-256-thread grid, A/B via RCDC_COST_BLOCKS)
+    uint32_t pad_c;
 };
 constexpr uint32_t kWalkZoneFast = 1;  // zones on the scan's slide (zone_wave_fast)
 constexpr uint32_t kWalkKReset = 2;    // counters reset in the walk kernel, queue by qbase
-constexpr uint32_t kWalkSortAgg = 4;   // wave-aggregated counting sort of the queue
+
 constexpr uint64_t kEndOpen = 1ull << 63;
 constexpr uint64_t kEndPos = (1ull << 42) - 1;  // position bits of an end word
 constexpr uint64_t kEndNone = kEndPos;          // position: no usable end state

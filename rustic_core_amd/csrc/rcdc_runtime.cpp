@@ -238,6 +238,8 @@ struct rcdc_plan {
                                       // every CU (rcdc_plan_set_pipeline(plan, 2))
     uint32_t pp = 0;                  // buffer set of the next run
     uint32_t last_set = 0;            // buffer set of the last run
+    uint64_t wruns = 0;               // walk runs (the work-counter slot: wruns % 4)
+    uint32_t last_wslot = 0;          // the last run's work-counter slot
     uint4 *d_sums2 = nullptr;
     uint64_t *d_masks2 = nullptr;
     uint64_t cap_sums2 = 0, cap_masks2 = 0;
@@ -723,12 +725,14 @@ rcdc_status plan_build(rcdc_ctx *ctx, rcdc_plan *pl, const uint64_t *offs, const
     // a hit round stops early and spreads the lanes' owed tails (round_first)
     wp.early = 1;
     if (const char *e = getenv("RCDC_WALK_EARLY")) wp.early = atoi(e) != 0;
-    // round 5: fast zones, in-kernel counter resets, aggregated queue sort
-    // (RCDC_WALK_ZONEFAST / _KRESET / _SORTAGG = 0 turn them off for A/B runs)
-    wp.flags = kWalkZoneFast | kWalkKReset | kWalkSortAgg;
+    // round 5: fast zones, in-kernel counter resets (RCDC_WALK_ZONEFAST /
+    // RCDC_WALK_KRESET = 0 turn them off for A/B runs); the cost kernel on a
+    // few fat workgroups (RCDC_COST_BLOCKS; 4096 restores the old grid)
+    wp.flags = kWalkZoneFast | kWalkKReset;
     if (const char *e = getenv("RCDC_WALK_ZONEFAST"); e && atoi(e) == 0) wp.flags &= ~kWalkZoneFast;
     if (const char *e = getenv("RCDC_WALK_KRESET"); e && atoi(e) == 0) wp.flags &= ~kWalkKReset;
-    if (const char *e = getenv("RCDC_WALK_SORTAGG"); e && atoi(e) == 0) wp.flags &= ~kWalkSortAgg;
+    wp.cost_blocks = 16;
+    if (const char *e = getenv("RCDC_COST_BLOCKS")) wp.cost_blocks = (uint32_t)std::max(atoi(e), 1);
     if (const char *e = getenv("RCDC_CHECK_BUDGET")) wp.chk_budget = strtoull(e, nullptr, 10);
     if (const char *e = getenv("RCDC_FIX_SEG")) wp.fix_seg = (uint32_t)std::max(atoi(e) / 128 * 128, 128);
     if (const char *e = getenv("RCDC_WALK_FIXCAP")) wp.fix_cap = (uint32_t)std::max(atoi(e), 1);  // tests
@@ -789,7 +793,12 @@ rcdc_status plan_build(rcdc_ctx *ctx, rcdc_plan *pl, const uint64_t *offs, const
         if ((st = ensure_dev(&pl->d_fixlist, &pl->cap_fixlist, nw))) return st;
         if ((st = ensure_dev(&pl->d_fixcuts, &pl->cap_fixcuts, nw * pl->wprm.fix_cap))) return st;
         if ((st = ensure_dev(&pl->d_fixres, &pl->cap_fixres, nw))) return st;
-        if ((st = ensure_dev(&pl->d_wstats, &pl->cap_wstats, kWalkStats))) return st;
+        // four slots of work counters (WalkParams.stats_next); slot 0 is also
+        // the single buffer of set 0 when counters are reset by memsets
+        if ((st = ensure_dev(&pl->d_wstats, &pl->cap_wstats, 4 * kWalkStats))) return st;
+        HIP_TRY(up ? hipMemsetAsync(pl->d_wstats, 0, 4 * kWalkStats * 8, up)
+                   : hipMemset(pl->d_wstats, 0, 4 * kWalkStats * 8));
+        pl->wruns = 0;
         pl->wprm.stats = pl->d_wstats;
         pl->wprm.trace = nullptr;
         if (const char *e = getenv("RCDC_WALK_TRACE"); e && atoi(e) > 0) {
@@ -900,6 +909,16 @@ rcdc_status plan_run(rcdc_plan *pl, const void *d_arena, hipStream_t stream) {
     pl->flush_next = false;
     const uint32_t wblocks = (uint32_t)std::min<uint64_t>(cus, (pl->wunits.size() + 15) / 16);
     wprm.qbase = pl->wqbase[set];
+    wprm.stats_next = nullptr;
+    if ((wprm.flags & kWalkKReset) && !pl->wunits.empty()) {
+        const uint32_t slot = (uint32_t)(pl->wruns % 4);
+        wprm.stats = pl->d_wstats + slot * kWalkStats;
+        wprm.stats_next = pl->d_wstats + ((slot + 2) % 4) * kWalkStats;
+        pl->last_wslot = slot;
+        pl->wruns++;
+    } else {
+        pl->last_wslot = set ? 4 : 0;  // (4: d_wstats2)
+    }
     HIP_TRY(launch_walk((const uint8_t *)d_arena, pl->d_sds, pl->d_wunits, wprm, ctx->d_tables,
                         wpiece, pstatus, ctr, wblocks, stream, ordered));
     if (!pl->wunits.empty() && (wprm.flags & kWalkKReset))  // takes of this run: one per
@@ -1806,7 +1825,9 @@ rcdc_status rcdc_plan_walk_stats(rcdc_plan *plan, uint64_t *stats, uint64_t *tra
     DeviceGuard g(plan->ctx->device);
     HIP_TRY(hipEventSynchronize(plan->done));
     static_assert(RCDC_WALK_STATS == kWalkStats, "stats slots");
-    HIP_TRY(hipMemcpy(stats, plan->last_set ? plan->d_wstats2 : plan->d_wstats, kWalkStats * 8,
+    HIP_TRY(hipMemcpy(stats, plan->last_wslot == 4 ? plan->d_wstats2
+                                                    : plan->d_wstats + plan->last_wslot * kWalkStats,
+                      kWalkStats * 8,
                       hipMemcpyDeviceToHost));
     const uint64_t nw = 2 * plan->wunits.size() * kTraceWords;  // walk rows, then check rows
     if (trace && trace_cap && plan->wprm.trace)

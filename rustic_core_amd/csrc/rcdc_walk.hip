@@ -620,12 +620,14 @@ __global__ __launch_bounds__(1024, 1) void rcdc_walk_kernel(
     __shared__ BlockStats s_st;
     __shared__ GapQueue s_q;
     // this run's counters (WalkParams.qbase): the chain counters of the set
-    // and its work counters start at 0; the chain of the set's previous run
-    // has finished (the run waits for it), this run's chain starts after
-    // this kernel, and every workgroup adds its counters only at its end
+    // start at 0 (the chain of the set's previous run has finished -- the run
+    // waits for it -- and this run's chain starts after this kernel), and the
+    // work counters of run r + 2 (WalkParams.stats_next)
+    // (device-scope atomics, like the adds: a plain store could sit in this
+    // XCD's L2 and be written back over the other XCDs' atomic adds)
     if (blockIdx.x == 0 && (prm.flags & kWalkKReset)) {
-        if (threadIdx.x >= 1 && threadIdx.x < 4) ctr[threadIdx.x] = 0;
-        if (threadIdx.x < kWalkStats) prm.stats[threadIdx.x] = 0;
+        if (threadIdx.x >= 1 && threadIdx.x < 4) atomicExch(&ctr[threadIdx.x], 0u);
+        if (threadIdx.x < kWalkStats && prm.stats_next) atomicExch(&prm.stats_next[threadIdx.x], 0ull);
     }
     stats_init(s_st);
     if (threadIdx.x == 0) {
@@ -1061,12 +1063,14 @@ __global__ __launch_bounds__(CT, 1) void rcdc_walk_check_kernel(
     __shared__ BlockStats s_st;
     __shared__ GapQueue s_q;
     // this run's counters (WalkParams.qbase): the chain counters of the set
-    // and its work counters start at 0; the chain of the set's previous run
-    // has finished (the run waits for it), this run's chain starts after
-    // this kernel, and every workgroup adds its counters only at its end
+    // start at 0 (the chain of the set's previous run has finished -- the run
+    // waits for it -- and this run's chain starts after this kernel), and the
+    // work counters of run r + 2 (WalkParams.stats_next)
+    // (device-scope atomics, like the adds: a plain store could sit in this
+    // XCD's L2 and be written back over the other XCDs' atomic adds)
     if (blockIdx.x == 0 && (prm.flags & kWalkKReset)) {
-        if (threadIdx.x >= 1 && threadIdx.x < 4) ctr[threadIdx.x] = 0;
-        if (threadIdx.x < kWalkStats) prm.stats[threadIdx.x] = 0;
+        if (threadIdx.x >= 1 && threadIdx.x < 4) atomicExch(&ctr[threadIdx.x], 0u);
+        if (threadIdx.x < kWalkStats && prm.stats_next) atomicExch(&prm.stats_next[threadIdx.x], 0ull);
     }
     stats_init(s_st);
     if (threadIdx.x == 0) {
@@ -1628,7 +1632,7 @@ __global__ __launch_bounds__(kAsmB) void rcdc_walk_assemble_kernel(
 // starts after its predecessor has finished and continues its chain.
 constexpr int kCostKeys = 256;
 
-__global__ __launch_bounds__(256) void rcdc_walk_cost_kernel(
+__global__ __launch_bounds__(1024) void rcdc_walk_cost_kernel(
     const uint8_t *__restrict__ arena, const StreamDesc *__restrict__ sds,
     const WalkUnit *__restrict__ units, WalkParams prm, uint8_t *__restrict__ key) {
     const uint32_t lane = threadIdx.x & 63u;
@@ -1652,37 +1656,17 @@ __global__ __launch_bounds__(256) void rcdc_walk_cost_kernel(
     }
 }
 
-// One workgroup: counting sort of the queue by key, descending.  The keys
-// take few values (cost classes x K), so per-lane LDS atomics on one counter
-// serialise (~35 us for C3's 26 k pieces); each wave instead aggregates the
-// lanes of one key (ballot) and adds their count with one atomic, then
-// scatters its lanes at base + rank within the key.
-__device__ __forceinline__ uint32_t wave_key_add(uint32_t *cnt, uint32_t key, bool on,
-                                                 uint32_t lane) {
-    uint32_t out = 0;
-    uint64_t todo = __builtin_amdgcn_ballot_w64(on);
-    while (todo) {
-        const uint32_t lead = (uint32_t)__builtin_ctzll(todo);
-        const uint32_t kk = __builtin_amdgcn_readlane(key, lead);
-        const uint64_t m = __builtin_amdgcn_ballot_w64(on && key == kk) & todo;
-        uint32_t base = 0;
-        if (lane == lead) base = atomicAdd(&cnt[kk], (uint32_t)__builtin_popcountll(m));
-        base = __builtin_amdgcn_readlane(base, lead);
-        if ((m >> lane) & 1u) out = base + (uint32_t)__builtin_popcountll(m & ((1ull << lane) - 1ull));
-        todo &= ~m;
-    }
-    return out;
-}
-
-// (the per-lane atomic form, kept for A/B runs: RCDC_WALK_SORTAGG=0)
-__global__ __launch_bounds__(1024) void rcdc_walk_sort_atomic_kernel(WalkParams prm,
-                                                                     const uint8_t *__restrict__ key) {
+// One workgroup: counting sort of the queue by key, descending (LDS atomics
+// per lane: 23 us for C3's 26 k pieces; a wave-aggregated form, one atomic
+// per key and wave, was 10x slower -- the keys of a wave are mostly distinct).
+__global__ __launch_bounds__(1024) void rcdc_walk_sort_kernel(WalkParams prm,
+                                                              const uint8_t *__restrict__ key) {
     __shared__ uint32_t s_cnt[kCostKeys];
     for (uint32_t i = threadIdx.x; i < (uint32_t)kCostKeys; i += blockDim.x) s_cnt[i] = 0;
     __syncthreads();
     for (uint32_t q = threadIdx.x; q < prm.nunits; q += blockDim.x) atomicAdd(&s_cnt[key[q]], 1u);
     __syncthreads();
-    if (threadIdx.x == 0) {
+    if (threadIdx.x == 0) {  // exclusive prefix, highest key first
         uint32_t acc = 0;
         for (int k = kCostKeys - 1; k >= 0; k--) {
             const uint32_t c = s_cnt[k];
@@ -1695,35 +1679,6 @@ __global__ __launch_bounds__(1024) void rcdc_walk_sort_atomic_kernel(WalkParams 
         prm.order_out[atomicAdd(&s_cnt[key[q]], 1u)] = prm.order_in[q];
 }
 
-__global__ __launch_bounds__(1024) void rcdc_walk_sort_kernel(WalkParams prm,
-                                                              const uint8_t *__restrict__ key) {
-    __shared__ uint32_t s_cnt[kCostKeys];
-    const uint32_t lane = threadIdx.x & 63u;
-    for (uint32_t i = threadIdx.x; i < (uint32_t)kCostKeys; i += blockDim.x) s_cnt[i] = 0;
-    __syncthreads();
-    for (uint32_t q0 = threadIdx.x - lane; q0 < prm.nunits; q0 += blockDim.x) {
-        const uint32_t q = q0 + lane;
-        const bool on = q < prm.nunits;
-        (void)wave_key_add(s_cnt, on ? key[q] : 0u, on, lane);
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {  // exclusive prefix, highest key first
-        uint32_t acc = 0;
-        for (int k = kCostKeys - 1; k >= 0; k--) {
-            const uint32_t c = s_cnt[k];
-            s_cnt[k] = acc;
-            acc += c;
-        }
-    }
-    __syncthreads();
-    for (uint32_t q0 = threadIdx.x - lane; q0 < prm.nunits; q0 += blockDim.x) {
-        const uint32_t q = q0 + lane;
-        const bool on = q < prm.nunits;
-        const uint32_t at = wave_key_add(s_cnt, on ? key[q] : 0u, on, lane);
-        if (on) prm.order_out[at] = prm.order_in[q];
-    }
-}
-
 namespace rcdc {
 
 // The queue's cost order of a run (reads only the arena and the units;
@@ -1734,15 +1689,19 @@ hipError_t launch_walk_order(const uint8_t *arena, const StreamDesc *sds, const 
     if (prm.nunits == 0 || !prm.order_in || !prm.order_out) return hipSuccess;
     // the key bytes follow order_out in the same buffer (plan_build)
     uint8_t *key = reinterpret_cast<uint8_t *>(prm.order_out + prm.nunits);
-    const uint32_t cb = std::min<uint32_t>((prm.nunits + 3) / 4, 4096);
-    hipLaunchKernelGGL(rcdc_walk_cost_kernel, dim3(cb), dim3(256), 0, stream, arena, sds, units,
-                       prm, key);
-    if (prm.flags & kWalkSortAgg)
-        hipLaunchKernelGGL(rcdc_walk_sort_kernel, dim3(1), dim3(1024), 0, stream, prm,
-                           (const uint8_t *)key);
-    else
-        hipLaunchKernelGGL(rcdc_walk_sort_atomic_kernel, dim3(1), dim3(1024), 0, stream, prm,
-                           (const uint8_t *)key);
+    // A run's order is computed right after the walk before the last on its
+    // hashing stream ends: with thousands of workgroups the cost kernel took
+    // every CU that walk freed and the next walk (other stream, ready) waited
+    // ~100 us for it (profiles/r05/gaps_*.txt).  A few fat workgroups leave
+    // the CUs to that walk and finish long before this run's walk is due.
+    const bool fat = prm.cost_blocks <= 256;  // (> 256: round 4's grid, a wave per piece)
+    const uint32_t per = fat ? 16u : 4u;        // waves per workgroup
+    const uint32_t cb = std::max<uint32_t>(
+        std::min<uint32_t>((prm.nunits + per - 1) / per, prm.cost_blocks), 1);
+    hipLaunchKernelGGL(rcdc_walk_cost_kernel, dim3(cb), dim3(64 * per), 0, stream, arena, sds,
+                       units, prm, key);
+    hipLaunchKernelGGL(rcdc_walk_sort_kernel, dim3(1), dim3(1024), 0, stream, prm,
+                       (const uint8_t *)key);
     return hipGetLastError();
 }
 

@@ -179,13 +179,18 @@ static double pcie_bound(uint64_t in_bytes, uint64_t out_bytes, uint64_t batch, 
 }
 
 int main(int argc, char **argv) {
+    // More hardware queues than HIP's default 4, before the first HIP call:
+    // the engine's copy, compute, id and pack streams (8 + the context's)
+    // would otherwise share queues, and a small upload or kernel queued
+    // behind a 2 GiB copy on a shared queue waits for it.
+    setenv("GPU_MAX_HW_QUEUES", arg(argc, argv, "--hw-queues", "16"), 1);
     const std::string dir = arg(argc, argv, "--dir", "/tmp/rcdc_ingest_files");
     const int nfiles = atoi(arg(argc, argv, "--files", "32"));
     const uint64_t fsize = (uint64_t)atoll(arg(argc, argv, "--file-mib", "1024")) << 20;
     const int readers = atoi(arg(argc, argv, "--readers", "8"));
     const uint64_t batch = (uint64_t)atoll(arg(argc, argv, "--batch-mib", "2048")) << 20;
     const int depth = atoi(arg(argc, argv, "--depth", "4"));
-    const int threads = atoi(arg(argc, argv, "--hash-threads", "8"));
+    const int threads = atoi(arg(argc, argv, "--hash-threads", "10"));
     const int in_slots = atoi(arg(argc, argv, "--in-slots", "4"));
     const int reps = atoi(arg(argc, argv, "--reps", "2"));
     const char *json = arg(argc, argv, "--json", nullptr);
@@ -355,7 +360,7 @@ int main(int argc, char **argv) {
              "\"pack_bytes_ok\": %s, \"checked\": %s}, "
              "\"config\": {\"readers\": %d, \"batch_bytes\": %llu, \"depth\": %d, "
              "\"hash_threads\": %d, \"in_slots\": %d, \"zstd_level\": %d, \"extra_verify\": true, "
-             "\"reps\": %d}, "
+             "\"reps\": %d, \"gpu_max_hw_queues\": \"%s\"}, "
              "\"data\": \"%d files x %llu MiB of splitmix64 words with a zero run at the start of "
              "every 4 MiB block (~half zeros), written to %s and read once before the run\", "
              "\"path\": \"tools/ingest_e2e.cpp: reader threads pread each file into "
@@ -368,7 +373,8 @@ int main(int argc, char **argv) {
              (unsigned long long)stb.batches, gib / bound_s, bound_s, h2d_alone, bound_s / best,
              ids_ok ? "true" : "false", seq_ok ? "true" : "false", dedup_ok ? "true" : "false",
              bytes_ok ? "true" : "false", check ? "true" : "false", readers,
-             (unsigned long long)batch, depth, threads, in_slots, level, reps, nfiles,
+             (unsigned long long)batch, depth, threads, in_slots, level, reps,
+             getenv("GPU_MAX_HW_QUEUES"), nfiles,
              (unsigned long long)(fsize >> 20), dir.c_str());
     printf("%s\n", line);
     if (json) {
