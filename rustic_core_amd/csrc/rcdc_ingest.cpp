@@ -190,6 +190,7 @@ struct rcdc_ingest {
     int level = 0;
     bool compress = true, verify = true;
     uint64_t batch_cap = 0, long_chunk = 0;
+    uint64_t copy_piece = 64ull << 20;  // bytes per H2D / D2H copy (RCDC_INGEST_COPY_PIECE)
     uint32_t depth = 4, nin = 4, nout = 4, nthreads = 8;
     PackSizer sizer{};
     // input slots
@@ -276,6 +277,10 @@ void set_err(Ing *g, rcdc_status s, const std::string &m) {
 template <typename T>
 bool ensure_dev(Ing *g, T **p, uint64_t *cap, uint64_t need) {
     if (*p && *cap >= need) return true;
+    static const bool log = getenv("RCDC_ALLOC_LOG") != nullptr;
+    if (log && *p)
+        fprintf(stderr, "rcdc ingest: regrow %llu -> %llu x %zu B (hipFree: device sync)\n",
+                (unsigned long long)*cap, (unsigned long long)need, sizeof(T));
     if (*p) ING_HIP(g, hipFree(*p));
     *p = nullptr;
     *cap = 0;
@@ -430,7 +435,12 @@ bool submit_ready(Ing *g) {
         const uint64_t used = in->used;
         if (!ensure_dev(g, &P.arena, &P.arena_cap, round_up(used, 256) + 512)) return false;
         // the arena's previous batch is retired: its ids (the last reader) are done
-        ING_HIP(g, hipMemcpyAsync(P.arena, in->host, used, hipMemcpyHostToDevice, g->s_in));
+        // in pieces: a small upload or read-back of stage A on the same DMA
+        // engine waits for at most one piece, not a whole batch (r5f trace:
+        // the plan's uploads sat behind 2 GiB copies, 17-37 ms each)
+        for (uint64_t o = 0; o < used; o += g->copy_piece)
+            ING_HIP(g, hipMemcpyAsync(P.arena + o, in->host + o, std::min(g->copy_piece, used - o),
+                                      hipMemcpyHostToDevice, g->s_in));
         ING_HIP(g, hipEventRecord(in->h2d, g->s_in));
         std::lock_guard<std::mutex> lk(g->mu);
         g->submitted.push_back(std::move(B));
@@ -501,6 +511,9 @@ bool stage_a(Ing *g, Batch *B) {
               [&](uint32_t a, uint32_t b) { return B->c_len[a] > B->c_len[b]; });
     const uint64_t ns = B->short_idx.size();
     if (ns > P.refs_cap) {
+        if (getenv("RCDC_ALLOC_LOG") && P.refs_cap)
+            fprintf(stderr, "rcdc ingest: regrow refs %llu -> %llu\n", (unsigned long long)P.refs_cap,
+                    (unsigned long long)ns);
         if (P.h_refs) ING_HIP(g, hipHostFree(P.h_refs));
         if (P.d_refs) ING_HIP(g, hipFree(P.d_refs));
         if (P.d_dig) ING_HIP(g, hipFree(P.d_dig));
@@ -775,13 +788,18 @@ bool stage_b(Ing *g, Batch *B, bool finalize) {
             out->busy = true;
         }
         if (out->cap < total) {
+            if (getenv("RCDC_ALLOC_LOG") && out->cap)
+                fprintf(stderr, "rcdc ingest: regrow out slot %llu -> %llu\n",
+                        (unsigned long long)out->cap, (unsigned long long)total);
             if (out->host) ING_HIP(g, hipHostFree(out->host));
             out->cap = total + total / 4;
             ING_HIP(g, hipHostMalloc((void **)&out->host, out->cap, hipHostMallocDefault));
         }
         ING_HIP(g, hipEventRecord(g->ev_back, g->s_back));
         ING_HIP(g, hipStreamWaitEvent(g->s_out, g->ev_back, 0));
-        ING_HIP(g, hipMemcpyAsync(out->host, g->d_packs, total, hipMemcpyDeviceToHost, g->s_out));
+        for (uint64_t o = 0; o < total; o += g->copy_piece)
+            ING_HIP(g, hipMemcpyAsync(out->host + o, g->d_packs + o, std::min(g->copy_piece, total - o),
+                                      hipMemcpyDeviceToHost, g->s_out));
         ING_HIP(g, hipEventRecord(g->ev_out, g->s_out));
     }
     // the still open pack: its blobs into the other carry buffer
@@ -1014,6 +1032,8 @@ rcdc_status rcdc_ingest_create(rcdc_ctx *ctx, const rcdc_ingest_config *cfg,
     g->verify = cfg->extra_verify != 0;
     g->batch_cap = round_up(cfg->batch_bytes ? cfg->batch_bytes : (2ull << 30), 256);
     g->long_chunk = cfg->long_chunk ? cfg->long_chunk : (2ull << 20);
+    if (const char *e = getenv("RCDC_INGEST_COPY_PIECE"))
+        g->copy_piece = std::max<uint64_t>(strtoull(e, nullptr, 10), 1ull << 20);
     g->depth = cfg->depth ? cfg->depth : 4;
     g->nin = std::max(cfg->in_slots ? cfg->in_slots : 4u, 2u);
     g->nout = std::max(cfg->out_slots ? cfg->out_slots : 4u, 1u);

@@ -76,11 +76,14 @@ hipError_t launch_aead(bool open, const uint8_t *in, uint8_t *out, const AeadBlo
                        const uint32_t *unit0, const AeadKeyDev *key, uint32_t *partials,
                        uint32_t *status, uint32_t cus, hipStream_t stream);
 uint32_t zstd_block_grid(uint32_t cus, int level);
+uint64_t zstd_far_words(int level, uint64_t nblk);
 void zstd_prof_dump();
+void zstd_check_prof_dump();
 hipError_t launch_zstd(const uint8_t *in, uint8_t *out, const ZstdBlob *blobs, uint32_t nblobs,
                        const ZstdBlk *blks, uint32_t nblk, const ZstdTables *tabs, uint8_t *slots,
                        uint64_t *seqbuf, uint32_t grid, uint2 *res, uint64_t *bpos,
-                       uint64_t *out_lens, uint32_t *queue, int level, hipStream_t stream);
+                       uint64_t *out_lens, uint32_t *queue, uint32_t *far, int level,
+                       hipStream_t stream);
 uint64_t zstd_check_scratch_bytes(uint32_t grid);
 uint64_t zstd_blkdesc_bytes();
 hipError_t launch_zstd_check_blocks(const uint8_t *frames, const uint8_t *data, const void *refs,
@@ -315,6 +318,8 @@ struct rcdc_ctx {
     AeadUnit *d_aead_units = nullptr;
     uint32_t *d_aead_unit0 = nullptr, *d_aead_partials = nullptr, *d_aead_status = nullptr;
     uint8_t *d_aead_stage = nullptr;  // pack headers
+    uint8_t *h_aead_up = nullptr;     // page-locked source of a call's uploads
+    uint64_t cap_aead_up = 0;
     uint64_t cap_aead_key = 0, cap_aead_blobs = 0, cap_aead_units = 0, cap_aead_unit0 = 0,
              cap_aead_partials = 0, cap_aead_status = 0, cap_aead_stage = 0;
     hipEvent_t aead_done = nullptr;
@@ -336,6 +341,8 @@ struct rcdc_ctx {
     uint32_t *d_zstd_queue = nullptr;  // per window: blocks taken past the first grid
     uint64_t cap_zstd_queue = 0;
     uint8_t *d_zstd_slots = nullptr;
+    uint32_t *d_zstd_far = nullptr;  // far candidates: tables + maps per block (levels >= 3)
+    uint64_t cap_zstd_far = 0;
     uint64_t cap_zstd_tabs = 0, cap_zstd_blobs = 0, cap_zstd_blks = 0, cap_zstd_res = 0,
              cap_zstd_bpos = 0, cap_zstd_lens = 0, cap_zstd_seq = 0, cap_zstd_slots = 0;
     // frame checks (rcdc_zstd_check): calls on one context take turns
@@ -409,6 +416,10 @@ rcdc_status null_leave(rcdc_ctx *ctx, const void *hip_stream, hipStream_t st) {
 template <typename T>
 rcdc_status ensure_dev(T **p, uint64_t *cap, uint64_t need) {
     if (need <= *cap && *p) return RCDC_OK;
+    static const bool log = getenv("RCDC_ALLOC_LOG") != nullptr;
+    if (log && *p)
+        fprintf(stderr, "rcdc: regrow %llu -> %llu x %zu B (hipFree: device sync)\n",
+                (unsigned long long)*cap, (unsigned long long)need, sizeof(T));
     if (*p) HIP_TRY(hipFree(*p));
     *p = nullptr;
     *cap = 0;
@@ -727,11 +738,12 @@ rcdc_status plan_build(rcdc_ctx *ctx, rcdc_plan *pl, const uint64_t *offs, const
     if (const char *e = getenv("RCDC_WALK_EARLY")) wp.early = atoi(e) != 0;
     // round 5: fast zones, in-kernel counter resets (RCDC_WALK_ZONEFAST /
     // RCDC_WALK_KRESET = 0 turn them off for A/B runs); the cost kernel on a
-    // few fat workgroups (RCDC_COST_BLOCKS; 4096 restores the old grid)
+    // few fat workgroups with RCDC_COST_BLOCKS <= 256 (16: 312 us against 48 us
+    // on the default grid, r5e)
     wp.flags = kWalkZoneFast | kWalkKReset;
     if (const char *e = getenv("RCDC_WALK_ZONEFAST"); e && atoi(e) == 0) wp.flags &= ~kWalkZoneFast;
     if (const char *e = getenv("RCDC_WALK_KRESET"); e && atoi(e) == 0) wp.flags &= ~kWalkKReset;
-    wp.cost_blocks = 16;
+    wp.cost_blocks = 4096;
     if (const char *e = getenv("RCDC_COST_BLOCKS")) wp.cost_blocks = (uint32_t)std::max(atoi(e), 1);
     if (const char *e = getenv("RCDC_CHECK_BUDGET")) wp.chk_budget = strtoull(e, nullptr, 10);
     if (const char *e = getenv("RCDC_FIX_SEG")) wp.fix_seg = (uint32_t)std::max(atoi(e) / 128 * 128, 128);
@@ -1628,6 +1640,7 @@ void rcdc_ctx_destroy(rcdc_ctx *c) {
         (void)hipFree(c->d_aead_partials);
         (void)hipFree(c->d_aead_status);
         (void)hipFree(c->d_aead_stage);
+        (void)hipHostFree(c->h_aead_up);
         if (c->aead_done) (void)hipEventDestroy(c->aead_done);
         if (c->ev_null_in) (void)hipEventDestroy(c->ev_null_in);
         if (c->ev_null_out) (void)hipEventDestroy(c->ev_null_out);
@@ -1641,6 +1654,7 @@ void rcdc_ctx_destroy(rcdc_ctx *c) {
         (void)hipFree(c->d_zstd_queue);
         (void)hipFree(c->d_zstd_seq);
         (void)hipFree(c->d_zstd_slots);
+        (void)hipFree(c->d_zstd_far);
         (void)hipFree(c->d_zck_refs);
         (void)hipFree(c->d_zck_order);
         (void)hipFree(c->d_zck_status);
@@ -2177,24 +2191,45 @@ rcdc_status aead_launch(rcdc_ctx *ctx, bool open, const uint8_t key[64], std::ve
     if ((rs = ensure_dev(&ctx->d_aead_unit0, &ctx->cap_aead_unit0, nb + bt.size()))) return rs;
     if ((rs = ensure_dev(&ctx->d_aead_partials, &ctx->cap_aead_partials, nu * 5))) return rs;
     if ((rs = ensure_dev(&ctx->d_aead_status, &ctx->cap_aead_status, nb))) return rs;
+    // the call's uploads go async on st from one page-locked buffer (free
+    // again: the last call's work is done, aead_done above).  Synchronous
+    // copies from pageable memory queued behind other streams' multi-GiB
+    // copies on the DMA engine (the ingest engine's batches) and stalled
+    // the calling thread for up to a whole copy.
+    auto r16 = [](uint64_t x) { return (x + 15) & ~15ull; };
+    uint64_t up = staging ? r16(staging->size()) : 0;
+    for (AeadBatch &B : bt)
+        up += r16(B.blobs.size() * sizeof(AeadBlob)) + r16(B.unit0.size() * 4) +
+              r16(B.units.size() * sizeof(AeadUnit));
+    if (up > ctx->cap_aead_up) {
+        if (ctx->h_aead_up) HIP_TRY(hipHostFree(ctx->h_aead_up));
+        ctx->h_aead_up = nullptr;
+        ctx->cap_aead_up = 0;
+        const uint64_t c = up + up / 2 + 4096;
+        HIP_TRY(hipHostMalloc((void **)&ctx->h_aead_up, c, hipHostMallocDefault));
+        ctx->cap_aead_up = c;
+    }
+    uint64_t hp = 0;
+    auto upload = [&](void *dst, const void *src, uint64_t n) -> hipError_t {
+        if (!n) return hipSuccess;
+        memcpy(ctx->h_aead_up + hp, src, n);
+        const hipError_t e = hipMemcpyAsync(dst, ctx->h_aead_up + hp, n, hipMemcpyHostToDevice, st);
+        hp += r16(n);
+        return e;
+    };
     if (staging && !staging->empty()) {
         if ((rs = ensure_dev(&ctx->d_aead_stage, &ctx->cap_aead_stage, staging->size() + 16)))
             return rs;
-        HIP_TRY(hipMemcpy(ctx->d_aead_stage, staging->data(), staging->size(),
-                          hipMemcpyHostToDevice));
+        HIP_TRY(upload(ctx->d_aead_stage, staging->data(), staging->size()));
     }
     uint64_t ob = 0, ou = 0, o0 = 0;
     for (AeadBatch &B : bt) {
         const uint32_t m = (uint32_t)B.blobs.size(), u = (uint32_t)B.units.size();
         if (m) {
-            HIP_TRY(hipMemcpy(ctx->d_aead_blobs + ob, B.blobs.data(), m * sizeof(AeadBlob),
-                              hipMemcpyHostToDevice));
-            HIP_TRY(hipMemcpy(ctx->d_aead_unit0 + o0, B.unit0.data(), (m + 1) * 4,
-                              hipMemcpyHostToDevice));
+            HIP_TRY(upload(ctx->d_aead_blobs + ob, B.blobs.data(), m * sizeof(AeadBlob)));
+            HIP_TRY(upload(ctx->d_aead_unit0 + o0, B.unit0.data(), (m + 1) * 4));
         }
-        if (u)
-            HIP_TRY(hipMemcpy(ctx->d_aead_units + ou, B.units.data(), u * sizeof(AeadUnit),
-                              hipMemcpyHostToDevice));
+        if (u) HIP_TRY(upload(ctx->d_aead_units + ou, B.units.data(), u * sizeof(AeadUnit)));
         const uint8_t *in = B.in ? B.in : ctx->d_aead_stage;
         HIP_TRY(launch_aead(open, in, out, ctx->d_aead_blobs + ob, m, ctx->d_aead_units + ou, u,
                             ctx->d_aead_unit0 + o0, ctx->d_aead_key, ctx->d_aead_partials + ou * 5,
@@ -2203,7 +2238,19 @@ rcdc_status aead_launch(rcdc_ctx *ctx, bool open, const uint8_t key[64], std::ve
         ou += u;
         o0 += m + 1;
     }
-    HIP_TRY(hipEventRecord(ctx->aead_done, st));
+    // aead_done marks the scratch busy until this work is done, and the next
+    // call waits on it from the host: recorded on the context's own stream
+    // (after st's work), never on the caller's stream, which may be destroyed
+    // before that call (an engine's streams end with the engine; HIP then
+    // reads the freed stream when synchronising: r5g)
+    {
+        hipEvent_t relay;
+        HIP_TRY(hipEventCreateWithFlags(&relay, hipEventDisableTiming));
+        HIP_TRY(hipEventRecord(relay, st));
+        HIP_TRY(hipStreamWaitEvent(ctx->stream, relay, 0));
+        HIP_TRY(hipEventDestroy(relay));
+    }
+    HIP_TRY(hipEventRecord(ctx->aead_done, ctx->stream));
     if (open && status) {
         HIP_TRY(hipEventSynchronize(ctx->aead_done));
         status->assign(nb, 0);
@@ -2547,6 +2594,8 @@ rcdc_status zstd_compress(rcdc_ctx *ctx, int level, const void *d_in, const rcdc
     if ((rs = ensure_dev(&ctx->d_zstd_bpos, &ctx->cap_zstd_bpos, nbl))) return rs;
     if ((rs = ensure_dev(&ctx->d_zstd_lens, &ctx->cap_zstd_lens, nbo))) return rs;
     if ((rs = ensure_dev(&ctx->d_zstd_slots, &ctx->cap_zstd_slots, maxw * kZstdSlot))) return rs;
+    const uint64_t farw = zstd_far_words(level, maxw);
+    if (farw && (rs = ensure_dev(&ctx->d_zstd_far, &ctx->cap_zstd_far, farw))) return rs;
     // the block kernel's queue: 8 counters 64 B apart per window
     if ((rs = ensure_dev(&ctx->d_zstd_queue, &ctx->cap_zstd_queue, wins.size() * 128))) return rs;
     HIP_TRY(hipMemsetAsync(ctx->d_zstd_queue, 0, wins.size() * 128 * 4, st));
@@ -2560,7 +2609,8 @@ rcdc_status zstd_compress(rcdc_ctx *ctx, int level, const void *d_in, const rcdc
                             (uint32_t)w.nblob, ctx->d_zstd_blks + w.blk0, (uint32_t)w.nblk,
                             ctx->d_zstd_tabs, ctx->d_zstd_slots, ctx->d_zstd_seq, grid,
                             ctx->d_zstd_res + w.blk0, ctx->d_zstd_bpos + w.blk0,
-                            ctx->d_zstd_lens + w.blob0, ctx->d_zstd_queue + 128 * k, level, st));
+                            ctx->d_zstd_lens + w.blob0, ctx->d_zstd_queue + 128 * k,
+                            farw ? ctx->d_zstd_far : nullptr, level, st));
     }
     HIP_TRY(hipMemcpyAsync(out_lens, ctx->d_zstd_lens, nbo * 8, hipMemcpyDeviceToHost, st));
     // the host descriptors die with this call
@@ -2632,6 +2682,8 @@ rcdc_status zstd_check(rcdc_ctx *ctx, const void *d_frames, const void *d_data,
         HIP_TRY(hipMemcpyAsync(status, ctx->d_zck_status, 4ull * n, hipMemcpyDeviceToHost, st));
         HIP_TRY(hipStreamSynchronize(st));
     }
+    if (const char *e = getenv("RCDC_ZSTD_DBG"))
+        if (atoi(e) & 8) zstd_check_prof_dump();
     return null_leave(ctx, hip_stream, st);
 }
 

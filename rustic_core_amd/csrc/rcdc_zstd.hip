@@ -159,7 +159,69 @@ __device__ __forceinline__ uint32_t narrow_cand(uint32_t e, uint32_t p) {
 // repcode check: taken before a table match, and one position later wins
 // over a table match here)
 constexpr uint32_t kZstdRep = 0x100u, kZstdRepCheck = 0x200u, kZstdInsAll = 0x400u,
-                   kZstdRep1 = 0x800u, kZstdLazyRep = 0x1000u, kZstdAdaptKey = 0x2000u;
+                   kZstdRep1 = 0x800u, kZstdLazyRep = 0x1000u, kZstdAdaptKey = 0x2000u,
+                   kZstdFar = 0x4000u;
+
+// ---- far candidates (levels >= 3): matches into the blob's two previous
+// blocks ----------------------------------------------------------------------
+// A block's wave keeps only its own 64 KiB of history in LDS; zstd's level 3
+// looks back over a 2 MiB window, and structured data repeats at such
+// distances (CSV rows whose columns cycle every few hundred KiB).  Blocks stay
+// independent: two kernels run before the parse,
+//   far_build: per block, a table of 2^13 buckets holding the latest *sampled*
+//     position (content-defined: the 8-byte key's hash has bits 20-21 zero, one
+//     position in four; zstd's long-distance matcher samples with a rolling
+//     hash mask the same way) with a 15-bit tag, in HBM;
+//   far_map: per block and 16-byte group, the offset of a sampled position's
+//     candidate in the tables of blocks b-1 and b-2 whose first kZstdFarMin
+//     bytes agree (0: none);
+// and the parse tries p - map[p / 16] beside its own table's candidate,
+// keeping the longer match.  A single-segment frame's window is its content,
+// so any offset into the blob is valid.  tools/zstd_ldm_model.py: CSV rows
+// 0.195 -> 0.145, code lines 0.117 -> 0.108, word text unchanged (1 MiB blobs).
+constexpr int kZstdFarLog = 13;
+constexpr uint32_t kZstdFarTab = 1u << kZstdFarLog;
+constexpr uint32_t kZstdFarGroups = kZstdBlock / 16u;
+constexpr uint32_t kZstdFarSample = 3u;  // hash bits 20-21: one position in four
+
+struct FarLayout {
+    uint32_t *tab;   // [nblk][kZstdFarTab]: (position + 1) << 15 | tag, 0 empty
+    uint32_t *map;   // [nblk][kZstdFarGroups]: offset (blob-relative distance), 0 none
+    uint32_t *comp;  // [nblk]: the block looked compressible (its table is built)
+    uint32_t *has;   // [nblk]: its map holds an offset
+};
+__device__ __forceinline__ FarLayout far_layout(uint32_t *far, uint32_t nblk) {
+    FarLayout L;
+    L.tab = far;
+    L.map = far + (size_t)nblk * kZstdFarTab;
+    L.comp = L.map + (size_t)nblk * kZstdFarGroups;
+    L.has = L.comp + nblk;
+    return L;
+}
+
+__device__ __forceinline__ uint64_t far_hash(uint64_t k6) { return k6 * 0x9E3779B97F4A7C15ull; }
+__device__ __forceinline__ bool far_sampled(uint64_t hv) { return ((hv >> 20) & kZstdFarSample) == 0; }
+__device__ __forceinline__ uint32_t far_bucket(uint64_t hv) { return (uint32_t)(hv >> (64 - kZstdFarLog)); }
+__device__ __forceinline__ uint32_t far_tag(uint64_t hv) { return (uint32_t)(hv >> 36) & 0x7FFFu; }
+
+// 16 bytes at p where only [p, lim) may be read; missing bytes read as 0.
+__device__ __forceinline__ uint4 ld16_lim(const uint8_t *p, const uint8_t *lim) {
+    if (p + 20 <= lim) return ld16(p);
+    return make_uint4(ld4_hi(p, lim), ld4_hi(p + 4, lim), ld4_hi(p + 8, lim), ld4_hi(p + 12, lim));
+}
+
+// The 8 bytes at byte j (0..23) of the 32 bytes u[0..3] (little-endian words).
+__device__ __forceinline__ uint64_t bytes8_at(const uint64_t u[4], uint32_t j) {
+    const uint32_t i = j >> 3, sh = (j & 7u) * 8u;
+    const uint64_t lo = u[i] >> sh, hi = sh ? u[i + 1] << (64u - sh) : 0ull;
+    return lo | hi;
+}
+
+// Far matches shorter than this are not worth their offset's bits (word
+// text: one or two words at 100+ KiB cost more than their literals,
+// r5h: 0.365 -> 0.373 when kept); the map keeps only candidates whose first
+// kZstdFarMin bytes agree, so a block with none skips the far path.
+constexpr uint32_t kZstdFarMin = 16;
 
 // Equal bytes of a[0..) and b[0..), at most maxlen (wave-uniform result).
 // Lane l compares 16 bytes per round (1 KiB per wave round); the last,
@@ -1079,6 +1141,156 @@ __device__ bool wave_is_rle(const uint8_t *src, uint32_t n, const uint8_t *lim) 
 
 }  // namespace
 
+// far_build: a workgroup per block.  The gate is the block kernel's (order-0
+// entropy of four 1 KiB windows): random or single-valued samples build no
+// table (comp = 0), so incompressible data pays 4 KiB of reads here.  A
+// blob's last block has no later block to serve and builds none either.
+__global__ __launch_bounds__(256) void rcdc_zstd_far_build_kernel(
+    const uint8_t *__restrict__ in, const ZstdBlob *__restrict__ blobs,
+    const ZstdBlk *__restrict__ blks, uint32_t nblk, uint32_t *__restrict__ far) {
+    __shared__ uint32_t t[kZstdFarTab];
+    __shared__ float wnd[4];
+    const uint32_t b = blockIdx.x, tid = threadIdx.x;
+    const FarLayout L = far_layout(far, nblk);
+    const ZstdBlk k = blks[b];
+    const ZstdBlob B = blobs[k.blob];
+    const uint8_t *src = in + B.in_off + k.start;
+    const uint8_t *lim = in + B.in_off + B.len;
+    const uint32_t n = k.len;
+    // structured data only: each of four 1 KiB windows at 1.5-7 bits per
+    // byte (order-0).  Random, already-compressed and constant windows (and
+    // blocks mixing them: C3's random and zero runs) have no far matches
+    // worth the reads.
+    uint32_t comp = 1;
+    if (n >= 8192) {
+        uint32_t *hs = t;  // 4 windows x 256 counts
+        for (uint32_t i = tid; i < 1024; i += 256) hs[i] = 0;
+        __syncthreads();
+        const uint32_t w0 = tid >> 6, kk = (tid & 63u) * 16u;
+        const uint4 v = ld16(src + (((n / 4) * w0) & ~15u) + kk);
+        for (uint32_t q = 0; q < 16; q++) atomicAdd(&hs[w0 * 256u + byte_of(v, q)], 1u);
+        __syncthreads();
+        float e = 0.f;  // wave w0: window w0's entropy (bits over 1024 bytes)
+        for (uint32_t i = tid & 63u; i < 256; i += 64) {
+            const uint32_t c = hs[w0 * 256u + i];
+            if (c) e += (float)c * __log2f(1024.f / (float)c);
+        }
+        for (int x = 32; x >= 1; x >>= 1) e += __shfl_xor(e, x);
+        if ((tid & 63u) == 0) wnd[w0] = e;
+        __syncthreads();
+        for (uint32_t w = 0; w < 4; w++) comp &= wnd[w] > 1.5f * 1024.f && wnd[w] < 7.0f * 1024.f;
+        __syncthreads();
+    }
+    if (n < 16u) comp = 0;
+    if (tid == 0) L.comp[b] = comp;
+    if (!comp || (k.flags & 2u)) return;
+    for (uint32_t i = tid; i < kZstdFarTab; i += 256) t[i] = 0;
+    __syncthreads();
+    // 8 positions per thread and round from 16 bytes; positions <= n - 8
+    for (uint32_t q = tid * 8u; q + 8u <= n; q += 2048u) {
+        const uint4 v = ld16_lim(src + q, lim);
+        const uint64_t u[4] = {(uint64_t)v.x | (uint64_t)v.y << 32, (uint64_t)v.z | (uint64_t)v.w << 32,
+                               0ull, 0ull};
+#pragma unroll
+        for (uint32_t j = 0; j < 8; j++) {
+            const uint32_t p = q + j;
+            const uint64_t hv = far_hash(bytes8_at(u, j));
+            if (p + 8u <= n && far_sampled(hv))
+                atomicMax(&t[far_bucket(hv)], (p + 1u) << 15 | far_tag(hv));
+        }
+    }
+    __syncthreads();
+    uint32_t *dst = L.tab + (size_t)b * kZstdFarTab;
+    for (uint32_t i = tid; i < kZstdFarTab; i += 256) dst[i] = t[i];
+}
+
+// far_map: a workgroup per block, a thread per 16-byte group: each sampled
+// position looks up the tables of blocks b-1 then b-2 (same blob), verifies
+// the 6 key bytes, and the group keeps the last verified offset.
+__global__ __launch_bounds__(256) void rcdc_zstd_far_map_kernel(
+    const uint8_t *__restrict__ in, const ZstdBlob *__restrict__ blobs,
+    const ZstdBlk *__restrict__ blks, uint32_t nblk, uint32_t *__restrict__ far) {
+    __shared__ uint32_t any;
+    const uint32_t b = blockIdx.x, tid = threadIdx.x;
+    const FarLayout L = far_layout(far, nblk);
+    const ZstdBlk k = blks[b];
+    const uint32_t kidx = k.start / kZstdBlock;
+    const bool ok1 = kidx >= 1u && L.comp[b - 1];
+    const bool ok2 = kidx >= 2u && L.comp[b - 2];
+    if (!L.comp[b] || !(ok1 || ok2) || k.len < 16u) {
+        if (tid == 0) L.has[b] = 0;
+        return;
+    }
+    if (tid == 0) any = 0;
+    __syncthreads();
+    const ZstdBlob B = blobs[k.blob];
+    const uint8_t *bsrc = in + B.in_off;
+    const uint8_t *src = bsrc + k.start;
+    const uint8_t *lim = bsrc + B.len;
+    const uint32_t n = k.len;
+    const uint32_t *t1 = L.tab + (size_t)(b - (ok1 ? 1u : 0u)) * kZstdFarTab;
+    const uint32_t *t2 = L.tab + (size_t)(b - (ok2 ? 2u : 0u)) * kZstdFarTab;
+    uint32_t *map = L.map + (size_t)b * kZstdFarGroups;
+    bool found = false;
+    for (uint32_t g = tid; g * 16u < n; g += 256) {
+        // every load of a round is independent of the others in flight: the
+        // group's bytes, then all sampled positions' b-1 buckets, then the
+        // misses' b-2 buckets, then one verification (the last hit)
+        const uint32_t p0 = g * 16u;
+        const uint4 a = ld16_lim(src + p0, lim), c = ld16_lim(src + p0 + 16u, lim);
+        const uint64_t u[4] = {(uint64_t)a.x | (uint64_t)a.y << 32, (uint64_t)a.z | (uint64_t)a.w << 32,
+                               (uint64_t)c.x | (uint64_t)c.y << 32, (uint64_t)c.z | (uint64_t)c.w << 32};
+        uint32_t bk[16], tg[16], e[16];
+        uint32_t smp = 0;
+#pragma unroll
+        for (uint32_t j = 0; j < 16u; j++) {
+            const uint64_t hv = far_hash(bytes8_at(u, j));
+            bk[j] = far_bucket(hv);
+            tg[j] = far_tag(hv);
+            if (far_sampled(hv) && p0 + j + kZstdFarMin <= n) smp |= 1u << j;
+        }
+#pragma unroll
+        for (uint32_t j = 0; j < 16u; j++) e[j] = (ok1 && ((smp >> j) & 1u)) ? t1[bk[j]] : 0u;
+        uint32_t hit1 = 0, miss = 0;
+#pragma unroll
+        for (uint32_t j = 0; j < 16u; j++) {
+            const bool h = e[j] && (e[j] & 0x7FFFu) == tg[j];
+            hit1 |= (h ? 1u : 0u) << j;
+            miss |= ((!h && ((smp >> j) & 1u)) ? 1u : 0u) << j;
+        }
+        uint32_t hit2 = 0;
+        if (ok2 && miss) {
+#pragma unroll
+            for (uint32_t j = 0; j < 16u; j++)
+                if ((miss >> j) & 1u) {
+                    const uint32_t x = t2[bk[j]];
+                    if (x && (x & 0x7FFFu) == tg[j]) {
+                        e[j] = x;
+                        hit2 |= 1u << j;
+                    }
+                }
+        }
+        uint32_t off = 0;
+        if (hit1 | hit2) {
+            const uint32_t j = 31u - (uint32_t)__clz(hit1 | hit2);  // the last hit
+            uint32_t ej = 0;
+#pragma unroll
+            for (uint32_t i = 0; i < 16u; i++) ej = i == j ? e[i] : ej;
+            const uint32_t d = ((hit2 >> j) & 1u) ? 2u : 1u;
+            const uint32_t q = k.start - d * kZstdBlock + (ej >> 15) - 1u;  // blob-relative
+            const uint4 v = ld16(bsrc + q);  // q + 20 is inside the blob: block b - d ends above it
+            if (((uint64_t)v.x | (uint64_t)v.y << 32) == bytes8_at(u, j) &&
+                ((uint64_t)v.z | (uint64_t)v.w << 32) == bytes8_at(u, j + 8))
+                off = k.start + p0 + j - q;
+        }
+        map[g] = off;
+        found |= off != 0u;
+    }
+    if (found) any = 1u;
+    __syncthreads();
+    if (tid == 0) L.has[b] = any;
+}
+
 // res[b] = {type | rle byte << 8, content bytes}.  HL: hash table of 2^HL
 // positions (LDS 4 * 2^HL bytes per wave, 2 * 2^HL when NARROW: more buckets,
 // or more waves per CU)
@@ -1087,7 +1299,7 @@ __global__ __launch_bounds__(64, (NARROW ? HL - 1 : HL) == 11 ? 4 : 2) void rcdc
     const uint8_t *__restrict__ in, const ZstdBlob *__restrict__ blobs,
     const ZstdBlk *__restrict__ blks, uint32_t nblk, const ZstdTables *__restrict__ tabs,
     uint8_t *__restrict__ slots, uint64_t *__restrict__ seqbuf, uint2 *__restrict__ res,
-    uint32_t dbg, uint32_t key, uint32_t *__restrict__ queue) {
+    uint32_t dbg, uint32_t key, uint32_t *__restrict__ queue, uint32_t *__restrict__ far) {
     __shared__ uint32_t table[NARROW ? 1 << (HL - 1) : 1 << HL];
     uint16_t *const t16 = reinterpret_cast<uint16_t *>(table);
     constexpr uint32_t kTabWords = NARROW ? 1u << (HL - 1) : 1u << HL;
@@ -1114,10 +1326,18 @@ __global__ __launch_bounds__(64, (NARROW ? HL - 1 : HL) == 11 ? 4 : 2) void rcdc
         if (b + G >= S && lane == 0) nx = atomicAdd(queue + 16u * qx, 1u);
         const ZstdBlk k = blks[b];
         const ZstdBlob B = blobs[k.blob];
-        const uint8_t *src = in + B.in_off + k.start;
+        // candidates are blob-relative (bsrc + c): far ones lie in earlier blocks
+        const uint8_t *bsrc = in + B.in_off;
+        const uint32_t ks = k.start;
+        const uint8_t *src = bsrc + ks;
         const uint8_t *lim = in + B.in_off + B.len;  // readable bytes end
         const uint32_t n = k.len;
         uint8_t *slot = slots + (uint64_t)b * kZstdSlot;
+        const uint32_t *fmap = nullptr;  // this block's far offsets per 16-byte group
+        if (far) {
+            const FarLayout L = far_layout(far, nblk);
+            if (L.has[b]) fmap = L.map + (size_t)b * kZstdFarGroups;
+        }
         if (n < 16) {  // too small to gain: raw (ZSTD_compressBlock_internal's floor)
             if (lane == 0) res[b] = make_uint2(kZstdTypeRaw, n);
             continue;
@@ -1185,37 +1405,44 @@ __global__ __launch_bounds__(64, (NARROW ? HL - 1 : HL) == 11 ? 4 : 2) void rcdc
                 if (stride > kZstdMaxStride) stride = kZstdMaxStride;
                 const uint32_t p = base + lane * stride;
                 const bool act = p <= ilimit;
-                uint32_t w = 0, wr = 0, wr1 = 0, wr2 = 0, h = 0, tg = 0, c = kZstdNone;
+                uint32_t w = 0, wr = 0, wr1 = 0, wr2 = 0, h = 0, tg = 0, c = kZstdNone, fo = 0;
                 bool isrep = false, rc = false, rc1 = false, rc2 = false;
+                const uint32_t pb = ks + p;  // blob-relative
                 if (act) {
                     // the last offsets' 4 bytes load with the position's own
-                    rc = (key & kZstdRepCheck) && rep0 != 0u && p >= rep0;
-                    rc1 = (key & kZstdRep1) && rep1 != 0u && p >= rep1;
-                    rc2 = (key & kZstdRep1) && rep2 != 0u && p >= rep2;
+                    rc = (key & kZstdRepCheck) && rep0 != 0u && pb >= rep0;
+                    rc1 = (key & kZstdRep1) && rep1 != 0u && pb >= rep1;
+                    rc2 = (key & kZstdRep1) && rep2 != 0u && pb >= rep2;
+                    if (fmap) fo = fmap[p >> 4];
                     w = ld4(src + p);
-                    wr = ld4(src + (rc ? p - rep0 : p));
-                    wr1 = ld4(src + (rc1 ? p - rep1 : p));
-                    wr2 = ld4(src + (rc2 ? p - rep2 : p));
+                    wr = ld4(bsrc + (rc ? pb - rep0 : pb));
+                    wr1 = ld4(bsrc + (rc1 ? pb - rep1 : pb));
+                    wr2 = ld4(bsrc + (rc2 ? pb - rep2 : pb));
                     const uint64_t k6 = key48(w, keyb > 4 ? ld4(src + p + 4) : 0u, keyb);
                     h = zhash<HL>(k6);
                     if constexpr (!NARROW) {
                         tg = ztag(k6);
                         const uint32_t e = table[h];
-                        if (e != kZstdNone && (e >> 17) == tg) c = e & kZstdPosMask;
+                        if (e != kZstdNone && (e >> 17) == tg) c = ks + (e & kZstdPosMask);
                     }
                 }
                 if constexpr (NARROW)
-                    if (act) c = narrow_cand(t16[h], p);
+                    if (act) {
+                        c = narrow_cand(t16[h], p);
+                        if (c != kZstdNone) c += ks;
+                    }
                 if (rc && wr == w) {
-                    c = p - rep0;
+                    c = pb - rep0;
                     isrep = true;
                 } else if (rc1 && wr1 == w) {  // the step's matches may have moved them
-                    c = p - rep1;
+                    c = pb - rep1;
                     isrep = true;
                 } else if (rc2 && wr2 == w) {
-                    c = p - rep2;
+                    c = pb - rep2;
                     isrep = true;
                 }
+                // the far map's offset (from the group's sampled position)
+                const uint32_t cf = !isrep && fo && pb >= fo && n - p - 4 >= 16 ? pb - fo : kZstdNone;
                 // a candidate's 4 bytes are checked from memory, in the same
                 // round trip as its extension: every candidate lane extends
                 // its own match by up to 16 bytes each way (most matches end
@@ -1226,18 +1453,18 @@ __global__ __launch_bounds__(64, (NARROW ? HL - 1 : HL) == 11 ? 4 : 2) void rcdc
                     const uint32_t limf = n - p - 4;
                     uint32_t wc;
                     if (limf >= 16) {
-                        wc = ld4(src + c);
-                        fl = first_diff16(ld16(src + p + 4), ld16(src + c + 4));
+                        wc = ld4(bsrc + c);
+                        fl = first_diff16(ld16(src + p + 4), ld16(bsrc + c + 4));
                     } else {  // the block's last bytes: independent 4-byte loads
                         uint4 va, vb;
-                        wc = ld4(src + c);
+                        wc = ld4(bsrc + c);
                         va.x = ld4_hi(src + p + 4, lim);
                         va.y = ld4_hi(src + p + 8, lim);
                         va.z = ld4_hi(src + p + 12, lim);
                         va.w = 0;
-                        vb.x = ld4_hi(src + c + 4, lim);
-                        vb.y = ld4_hi(src + c + 8, lim);
-                        vb.z = ld4_hi(src + c + 12, lim);
+                        vb.x = ld4_hi(bsrc + c + 4, lim);
+                        vb.y = ld4_hi(bsrc + c + 8, lim);
+                        vb.z = ld4_hi(bsrc + c + 12, lim);
                         vb.w = 0xFFFFFFFFu;
                         fl = first_diff16(va, vb);
                         if (fl > limf) fl = limf;
@@ -1246,12 +1473,30 @@ __global__ __launch_bounds__(64, (NARROW ? HL - 1 : HL) == 11 ? 4 : 2) void rcdc
                     // readable, merely not matchable: clamp)
                     const uint32_t limb = p - anchor < c ? p - anchor : c;
                     if (c >= 16) {
-                        bl = last_eq16(ld16(src + p - 16), ld16(src + c - 16));
+                        bl = last_eq16(ld16(src + p - 16), ld16(bsrc + c - 16));
                         if (bl > limb) bl = limb;
                     }
                     ok = wc == w && (isrep || 4 + fl >= keyb);  // last offset: 4 bytes
                     if (ok && c < 16)
-                        while (bl < limb && src[p - 1 - bl] == src[c - 1 - bl]) bl++;
+                        while (bl < limb && src[p - 1 - bl] == bsrc[c - 1 - bl]) bl++;
+                }
+                if (act && cf != kZstdNone) {  // the far candidate: kept if longer
+                    const uint32_t wf = ld4(bsrc + cf);
+                    const uint32_t ff = first_diff16(ld16(src + p + 4), ld16(bsrc + cf + 4));
+                    const uint32_t limb = p - anchor < cf ? p - anchor : cf;
+                    uint32_t bf = 0;
+                    if (cf >= 16) {
+                        bf = last_eq16(ld16(src + p - 16), ld16(bsrc + cf - 16));
+                        if (bf > limb) bf = limb;
+                    }
+                    if (wf == w && 4 + ff >= keyb && (!ok || ff > fl)) {
+                        if (cf < 16)
+                            while (bf < limb && src[p - 1 - bf] == bsrc[cf - 1 - bf]) bf++;
+                        c = cf;
+                        fl = ff;
+                        bl = bf;
+                        ok = true;
+                    }
                 }
                 uint64_t m = __ballot(ok);
                 // lazy step, per lane in VALU: the next position's match, if
@@ -1285,18 +1530,18 @@ __global__ __launch_bounds__(64, (NARROW ? HL - 1 : HL) == 11 ? 4 : 2) void rcdc
                     const uint32_t bb = rdl(bl, j);
                     uint32_t len = 4 + f;
                     if (f == 16 && n - pj > 20)
-                        len += wave_match_fwd(src + pj + 20, src + cj + 20, n - pj - 20, lim);
+                        len += wave_match_fwd(src + pj + 20, bsrc + cj + 20, n - pj - 20, lim);
                     const uint32_t mb = pj - anchor < cj ? pj - anchor : cj;
                     uint32_t bk = bb < mb ? bb : mb;
                     if (bb == 16 && mb > 16)
-                        bk += wave_match_back(src + pj - 16, src + cj - 16, mb - 16, src);
+                        bk += wave_match_back(src + pj - 16, bsrc + cj - 16, mb - 16, bsrc);
                     pj -= bk;
                     cj -= bk;
                     len += bk;
                     // offset value: a repeat code when the offset is in the
                     // block-local history (RFC 8878 3.1.2.5; entries from
                     // earlier blocks are unknown here: 0), else offset + 3
-                    const uint32_t off = pj - cj, ll = pj - anchor;
+                    const uint32_t off = ks + pj - cj, ll = pj - anchor;
                     uint32_t ofv;
                     if (!(key & kZstdRep)) {  // RCDC_ZSTD_REP=0 (A/B): literal offsets only
                         ofv = off + 3;
@@ -1686,6 +1931,7 @@ static ZstdStrategy zstd_strategy(int level) {
     static const bool insall = getenv("RCDC_ZSTD_INSALL") && atoi(getenv("RCDC_ZSTD_INSALL")) == 1;
     static const bool rep1 = !(getenv("RCDC_ZSTD_REP1") && atoi(getenv("RCDC_ZSTD_REP1")) == 0);
     static const bool lazyrep = getenv("RCDC_ZSTD_LAZYREP") && atoi(getenv("RCDC_ZSTD_LAZYREP")) == 1;
+    static const bool farc = !(getenv("RCDC_ZSTD_FAR") && atoi(getenv("RCDC_ZSTD_FAR")) == 0);
     if (level == 0) level = 3;  // ZSTD_CLEVEL_DEFAULT
     ZstdStrategy z{11, false, level <= 1 ? 6u : 4u};
     if (level >= 3) z = ZstdStrategy{level >= 4 ? 13 : 12, true, 6u};
@@ -1698,10 +1944,18 @@ static ZstdStrategy zstd_strategy(int level) {
     if (insall) z.key |= kZstdInsAll;
     if (rep && rchk && rep1) z.key |= kZstdRep1;
     if (lazyrep) z.key |= kZstdLazyRep;
+    if (farc && z.narrow) z.key |= kZstdFar;  // levels >= 3 (RCDC_ZSTD_FAR=0: off)
     return z;
 }
 
 // LDS per wave: 8 KiB table (16 waves per CU) or 16 KiB (8)
+// 32-bit words of the far scratch for nblk blocks (0: far candidates off at
+// this level)
+uint64_t zstd_far_words(int level, uint64_t nblk) {
+    const ZstdStrategy z = zstd_strategy(level);
+    return (z.key & kZstdFar) ? nblk * (kZstdFarTab + kZstdFarGroups + 2ull) : 0ull;
+}
+
 uint32_t zstd_block_grid(uint32_t cus, int level) {
     const ZstdStrategy z = zstd_strategy(level);
     return cus * ((z.narrow ? z.hlog - 1 : z.hlog) == 11 ? 16u : 8u);
@@ -1710,9 +1964,17 @@ uint32_t zstd_block_grid(uint32_t cus, int level) {
 hipError_t launch_zstd(const uint8_t *in, uint8_t *out, const ZstdBlob *blobs, uint32_t nblobs,
                        const ZstdBlk *blks, uint32_t nblk, const ZstdTables *tabs, uint8_t *slots,
                        uint64_t *seqbuf, uint32_t grid, uint2 *res, uint64_t *bpos,
-                       uint64_t *out_lens, uint32_t *queue, int level, hipStream_t stream) {
+                       uint64_t *out_lens, uint32_t *queue, uint32_t *far, int level,
+                       hipStream_t stream) {
     if (nblobs == 0) return hipSuccess;
     const ZstdStrategy z = zstd_strategy(level);
+    if (!(z.key & kZstdFar)) far = nullptr;
+    if (far && nblk) {
+        hipLaunchKernelGGL(rcdc_zstd_far_build_kernel, dim3(nblk), dim3(256), 0, stream, in, blobs,
+                           blks, nblk, far);
+        hipLaunchKernelGGL(rcdc_zstd_far_map_kernel, dim3(nblk), dim3(256), 0, stream, in, blobs,
+                           blks, nblk, far);
+    }
     static const uint32_t dbg = getenv("RCDC_ZSTD_DBG") ? (uint32_t)atoi(getenv("RCDC_ZSTD_DBG")) : 0u;
     const uint32_t g = nblk < grid ? nblk : grid;
     if (g) {
@@ -1720,7 +1982,7 @@ hipError_t launch_zstd(const uint8_t *in, uint8_t *out, const ZstdBlob *blobs, u
                   : z.hlog == 12 ? rcdc_zstd_block_kernel<12, true>
                                  : rcdc_zstd_block_kernel<13, true>;
         hipLaunchKernelGGL(k, dim3(g), dim3(64), 0, stream, in, blobs, blks, nblk, tabs, slots,
-                           seqbuf, res, dbg, z.key, queue);
+                           seqbuf, res, dbg, z.key, queue, far);
     }
     hipLaunchKernelGGL(rcdc_zstd_frame_kernel, dim3((nblobs + 255) / 256), dim3(256), 0, stream,
                        blobs, nblobs, res, bpos, out, out_lens);

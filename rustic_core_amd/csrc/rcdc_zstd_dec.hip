@@ -28,10 +28,17 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
 
 #include "rcdc_internal.h"
 
 using namespace rcdc;
+
+// RCDC_ZSTD_DBG bit 3: wall-clock sums (100 MHz) over compressed blocks:
+// literals section, sequences, whole block; literals, sequences, blocks
+__device__ unsigned long long g_zck_prof[8];
 
 namespace {
 
@@ -72,6 +79,10 @@ struct HufD {
 // LDS of one wave (workgroup = one wave)
 struct DecLds {
     FseD ll[512], ml[512], of[256];
+    // per LL / ML state: the code's baseline | extra bits << 24 (as zstd's
+    // ZSTD_seqSymbol), so a sequence's lengths need one LDS read each and no
+    // dependent constant-table lookup
+    uint32_t llx[512], mlx[512];
     FseD hw[64];  // FSE table of Huffman weights (log <= 6)
     HufD huf[2048];
     int16_t norm[64];
@@ -147,17 +158,22 @@ __device__ __forceinline__ uint64_t brev_bits(BRev &r, uint32_t n) {
 }
 
 // The same bitstream read through a 64-bit window that slides down 32 bits
-// at a time, with the next three dwords already in flight: a refill never
-// waits on memory (the serial FSE and Huffman decodes stalled ~500 cycles on
-// each refill otherwise).  Reads are at most 32 bits.  Invariant: the
-// window holds bits [B, B + 64) and B <= pos (pos - B < 64).
+// at a time, with the next 16 dwords (four 16-byte groups) already loaded or
+// in flight: a refill never waits on memory.  Three dwords ahead were not
+// enough: a sequence consumes ~40 bits, so a refill's load was needed two
+// sequences after it was issued and the serial sequence decode stalled on
+// it every ~32 bits (r5h: 94 % of the check's time on word text in the
+// sequences phase).  Reads are at most 32 bits.  Invariant: the window
+// holds bits [B, B + 64) and B <= pos (pos - B < 64); g0.w is the dword of
+// bits [B - 32, B), then g0.z, g0.y, g0.x, g1.w, ... g3.x.
 struct BRevQ {
     const uint8_t *base;
     int64_t len;
     int64_t pos;
     int64_t B;
     uint64_t acc;
-    uint32_t q0, q1, q2;  // dwords of bits [B-32, B), [B-64, B-32), [B-96, B-64)
+    uint4 g0, g1, g2, g3;
+    uint32_t used;  // dwords of the original g0 shifted in (0..3)
 };
 
 // 4 bytes at base + byte (any alignment), bytes outside [0, len) as 0
@@ -169,7 +185,13 @@ __device__ __forceinline__ uint32_t brq_ld4(const uint8_t *base, int64_t len, in
     return v;
 }
 
-__device__ bool brq_init(BRevQ &r, const uint8_t *p, int64_t len) {
+// the 16 bytes [byte, byte + 16) as dwords x (lowest) .. w
+__device__ __forceinline__ uint4 brq_ld16(const uint8_t *base, int64_t len, int64_t byte) {
+    return make_uint4(brq_ld4(base, len, byte), brq_ld4(base, len, byte + 4),
+                      brq_ld4(base, len, byte + 8), brq_ld4(base, len, byte + 12));
+}
+
+__device__ __forceinline__ bool brq_init(BRevQ &r, const uint8_t *p, int64_t len) {
     r.base = p;
     r.len = len;
     if (len <= 0) return false;
@@ -179,18 +201,27 @@ __device__ bool brq_init(BRevQ &r, const uint8_t *p, int64_t len) {
     r.B = ((r.pos >> 5) << 5) - 32;  // arithmetic shifts: floor
     const int64_t by = r.B >> 3;
     r.acc = (uint64_t)brq_ld4(p, len, by) | (uint64_t)brq_ld4(p, len, by + 4) << 32;
-    r.q0 = brq_ld4(p, len, by - 4);
-    r.q1 = brq_ld4(p, len, by - 8);
-    r.q2 = brq_ld4(p, len, by - 12);
+    r.g0 = brq_ld16(p, len, by - 16);
+    r.g1 = brq_ld16(p, len, by - 32);
+    r.g2 = brq_ld16(p, len, by - 48);
+    r.g3 = brq_ld16(p, len, by - 64);
+    r.used = 0;
     return true;
 }
 
 __device__ __forceinline__ void brq_slide(BRevQ &r) {
-    r.acc = (r.acc << 32) | r.q0;
+    r.acc = (r.acc << 32) | r.g0.w;
     r.B -= 32;
-    r.q0 = r.q1;
-    r.q1 = r.q2;
-    r.q2 = brq_ld4(r.base, r.len, (r.B >> 3) - 12);
+    r.g0.w = r.g0.z;
+    r.g0.z = r.g0.y;
+    r.g0.y = r.g0.x;
+    if (++r.used == 4) {
+        r.g0 = r.g1;
+        r.g1 = r.g2;
+        r.g2 = r.g3;
+        r.g3 = brq_ld16(r.base, r.len, (r.B >> 3) - 64);
+        r.used = 0;
+    }
 }
 
 __device__ __forceinline__ uint32_t brq_peek(BRevQ &r, uint32_t n) {
@@ -335,6 +366,7 @@ struct Dec {
     uint32_t al_ll, al_ml, al_of;  // 255: no table yet
     uint32_t bad;         // status
     bool block_mode;      // earlier blocks' state unknown: using it -> kCkSeq
+    bool prof;            // RCDC_ZSTD_DBG bit 3: phase clocks into g_zck_prof
 };
 
 // ---- comparisons (the whole wave) -----------------------------------------
@@ -521,6 +553,7 @@ __device__ bool huf_stream(const DecLds &L, uint32_t tl, const uint8_t *p, int64
 __device__ void check_compressed(Dec &D, DecLds &L, const uint8_t *p, uint32_t bs, uint8_t *scratch,
                                  uint32_t lane) {
     const uint8_t *end = p + bs;
+    const uint64_t t0 = D.prof ? wall_clock64() : 0;
     // -- literals section header (3.1.1.3.1.1)
     const uint32_t b0 = p[0];
     const uint32_t ltype = b0 & 3u, sf = (b0 >> 2) & 3u;
@@ -614,7 +647,12 @@ __device__ void check_compressed(Dec &D, DecLds &L, const uint8_t *p, uint32_t b
         __syncthreads();
         lits = scratch;
         q += csize;
+        if (D.prof && lane == 0) {
+            atomicAdd(&g_zck_prof[0], wall_clock64() - t0);
+            atomicAdd(&g_zck_prof[3], (unsigned long long)regen);
+        }
     }
+    const uint64_t t1 = D.prof ? wall_clock64() : 0;
     // -- sequences section header (3.1.1.3.2.1)
     if (q >= end) { D.bad = kCkCorrupt; return; }
     uint32_t nseq = q[0];
@@ -673,6 +711,15 @@ __device__ void check_compressed(Dec &D, DecLds &L, const uint8_t *p, uint32_t b
                 return;
             }
         }
+        for (uint32_t u = lane; u < (1u << D.al_ll); u += 64) {
+            const uint32_t c = L.ll[u].sym < 36 ? L.ll[u].sym : 0u;
+            L.llx[u] = kLLBase[c] | (uint32_t)kLLBits[c] << 24;
+        }
+        for (uint32_t u = lane; u < (1u << D.al_ml); u += 64) {
+            const uint32_t c = L.ml[u].sym < 53 ? L.ml[u].sym : 0u;
+            L.mlx[u] = kMLBase[c] | (uint32_t)kMLBits[c] << 24;
+        }
+        wsync();
         BRevQ r;
         if (!brq_init(r, q, end - q)) { D.bad = kCkCorrupt; return; }
         uint32_t sll = brq_bits(r, D.al_ll);
@@ -687,11 +734,12 @@ __device__ void check_compressed(Dec &D, DecLds &L, const uint8_t *p, uint32_t b
             bool err = false;
             for (uint32_t j = 0; j < nb; j++) {
                 const FseD eo = L.of[sof], el = L.ll[sll], em = L.ml[sml];
+                const uint32_t xl = L.llx[sll], xm = L.mlx[sml];
                 const uint32_t ofc = eo.sym, llc = el.sym, mlc = em.sym;
                 if (ofc > 31 || llc > 35 || mlc > 52) err = true;
                 const uint64_t ofv = (1ull << ofc) + brq_bits(r, ofc);
-                const uint32_t ml = kMLBase[mlc] + brq_bits(r, kMLBits[mlc]);
-                const uint32_t ll = kLLBase[llc] + brq_bits(r, kLLBits[llc]);
+                const uint32_t ml = (xm & 0xFFFFFFu) + brq_bits(r, xm >> 24);
+                const uint32_t ll = (xl & 0xFFFFFFu) + brq_bits(r, xl >> 24);
                 uint32_t off;
                 if (ofv > 3) {
                     off = (uint32_t)(ofv - 3);
@@ -790,6 +838,10 @@ __device__ void check_compressed(Dec &D, DecLds &L, const uint8_t *p, uint32_t b
             D.out += tot_o;
         }
         if (r.pos != 0) { D.bad = kCkCorrupt; return; }
+        if (D.prof && lane == 0) {
+            atomicAdd(&g_zck_prof[1], wall_clock64() - t1);
+            atomicAdd(&g_zck_prof[4], (unsigned long long)nseq);
+        }
         D.rep[0] = r0;
         D.rep[1] = r1;
         D.rep[2] = r2;
@@ -806,11 +858,15 @@ __device__ void check_compressed(Dec &D, DecLds &L, const uint8_t *p, uint32_t b
         return;
     }
     D.out += rest;
+    if (D.prof && lane == 0) {
+        atomicAdd(&g_zck_prof[2], wall_clock64() - t0);
+        atomicAdd(&g_zck_prof[5], 1ull);
+    }
 }
 
 // One frame; returns its status.
 __device__ uint32_t check_frame(const uint8_t *f, uint64_t flen, const uint8_t *data, uint64_t dlen,
-                                DecLds &L, uint8_t *scratch, uint32_t lane) {
+                                DecLds &L, uint8_t *scratch, uint32_t lane, bool prof) {
     const uint8_t *end = f + flen;
     if (flen < 6) return kCkCorrupt;
     const uint32_t magic = f[0] | (f[1] << 8) | (f[2] << 16) | ((uint32_t)f[3] << 24);
@@ -846,6 +902,7 @@ __device__ uint32_t check_frame(const uint8_t *f, uint64_t flen, const uint8_t *
     D.al_ll = D.al_ml = D.al_of = 255u;
     D.bad = kCkOk;
     D.block_mode = false;
+    D.prof = prof;
     for (;;) {
         if (q + 3 > end) return kCkCorrupt;
         const uint32_t bh = q[0] | (q[1] << 8) | ((uint32_t)q[2] << 16);
@@ -881,10 +938,13 @@ __device__ uint32_t check_frame(const uint8_t *f, uint64_t flen, const uint8_t *
 
 // refs: frame_off, frame_len, data_off, data_len (rcdc_zstd_check_ref);
 // order: the queue order; ctr: the queue counter (zeroed by the host).
-__global__ __launch_bounds__(64) void rcdc_zstd_check_kernel(
+// OCC: waves per SIMD the registers are budgeted for (2: no spills, 3: more
+// waves in flight; RCDC_ZCK_OCC picks, A/B)
+template <int OCC>
+__global__ __launch_bounds__(64, OCC) void rcdc_zstd_check_kernel(
     const uint8_t *__restrict__ frames, const uint8_t *__restrict__ data,
     const ulonglong4 *__restrict__ refs, const uint32_t *__restrict__ order, uint32_t n,
-    uint32_t stored, uint8_t *scratch, uint32_t *__restrict__ status, uint32_t *ctr) {
+    uint32_t stored, uint8_t *scratch, uint32_t *__restrict__ status, uint32_t *ctr, uint32_t dbg) {
     __shared__ DecLds L;
     const uint32_t lane = threadIdx.x;
     uint8_t *scr = scratch + (uint64_t)blockIdx.x * (kBlockMax + 64);
@@ -900,7 +960,7 @@ __global__ __launch_bounds__(64) void rcdc_zstd_check_kernel(
             st = r.y != r.w ? kCkMismatch
                             : (wave_cmp(data + r.z, frames + r.x, 0, 0, r.w, lane) ? kCkOk : kCkMismatch);
         else
-            st = check_frame(frames + r.x, r.y, data + r.z, r.w, L, scr, lane);
+            st = check_frame(frames + r.x, r.y, data + r.z, r.w, L, scr, lane, dbg & 8u);
         if (lane == 0) status[i] = st;
         __syncthreads();  // LDS tables are rebuilt by the next frame
     }
@@ -985,10 +1045,11 @@ __global__ __launch_bounds__(256) void rcdc_zstd_blocks_kernel(
     status[i] = st;
 }
 
-__global__ __launch_bounds__(64) void rcdc_zstd_block_check_kernel(
+template <int OCC>
+__global__ __launch_bounds__(64, OCC) void rcdc_zstd_block_check_kernel(
     const uint8_t *__restrict__ frames, const uint8_t *__restrict__ data,
     const ulonglong4 *__restrict__ refs, const BlkDesc *__restrict__ blks, uint64_t nblk,
-    uint8_t *scratch, uint32_t *status, uint32_t *ctr) {
+    uint8_t *scratch, uint32_t *status, uint32_t *ctr, uint32_t dbg) {
     __shared__ DecLds L;
     const uint32_t lane = threadIdx.x;
     uint8_t *scr = scratch + (uint64_t)blockIdx.x * (kBlockMax + 64);
@@ -1021,6 +1082,7 @@ __global__ __launch_bounds__(64) void rcdc_zstd_block_check_kernel(
             D.al_ll = D.al_ml = D.al_of = 255u;
             D.bad = kCkOk;
             D.block_mode = true;
+            D.prof = dbg & 8u;
             check_compressed(D, L, frames + b.content, b.size, scr, lane);
             st = (D.bad || D.out != D.dlen) ? kCkSeq : kCkOk;
         }
@@ -1033,6 +1095,26 @@ namespace rcdc {
 
 uint64_t zstd_check_scratch_bytes(uint32_t grid) { return (uint64_t)grid * (kBlockMax + 64); }
 
+static int zck_occ() {
+    static const int o = getenv("RCDC_ZCK_OCC") ? atoi(getenv("RCDC_ZCK_OCC")) : 2;
+    return o;
+}
+
+static uint32_t zck_dbg() {
+    static const uint32_t d = getenv("RCDC_ZSTD_DBG") ? (uint32_t)atoi(getenv("RCDC_ZSTD_DBG")) : 0u;
+    return d;
+}
+
+void zstd_check_prof_dump() {
+    unsigned long long h[8];
+    if (hipMemcpyFromSymbol(h, HIP_SYMBOL(g_zck_prof), sizeof h) != hipSuccess) return;
+    fprintf(stderr, "rcdc zstd check phases (wave-ms, 100 MHz clock): literals %.1f sequences %.1f "
+            "blocks %.1f; literals %llu sequences %llu compressed blocks %llu\n",
+            h[0] / 1e5, h[1] / 1e5, h[2] / 1e5, h[3], h[4], h[5]);
+    memset(h, 0, sizeof h);
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(g_zck_prof), h, sizeof h);
+}
+
 uint64_t zstd_blkdesc_bytes() { return sizeof(BlkDesc); }
 
 hipError_t launch_zstd_check(const uint8_t *frames, const uint8_t *data, const void *refs,
@@ -1040,8 +1122,10 @@ hipError_t launch_zstd_check(const uint8_t *frames, const uint8_t *data, const v
                              uint32_t grid, uint32_t *status, uint32_t *ctr, hipStream_t stream) {
     if (n == 0) return hipSuccess;
     const uint32_t g = n < grid ? n : grid;
-    hipLaunchKernelGGL(rcdc_zstd_check_kernel, dim3(g), dim3(64), 0, stream, frames, data,
-                       (const ulonglong4 *)refs, order, n, stored ? 1u : 0u, scratch, status, ctr);
+    hipLaunchKernelGGL(zck_occ() == 3 ? rcdc_zstd_check_kernel<3> : rcdc_zstd_check_kernel<2>,
+                       dim3(g), dim3(64), 0, stream, frames, data,
+                       (const ulonglong4 *)refs, order, n, stored ? 1u : 0u, scratch, status, ctr,
+                       zck_dbg());
     return hipGetLastError();
 }
 
@@ -1055,9 +1139,11 @@ hipError_t launch_zstd_check_blocks(const uint8_t *frames, const uint8_t *data, 
                        (const ulonglong4 *)refs, blk0, n, (BlkDesc *)blks, status);
     const uint32_t g = nblk < grid ? (uint32_t)nblk : grid;
     if (g)
-        hipLaunchKernelGGL(rcdc_zstd_block_check_kernel, dim3(g), dim3(64), 0, stream, frames, data,
+        hipLaunchKernelGGL(zck_occ() == 3 ? rcdc_zstd_block_check_kernel<3>
+                                          : rcdc_zstd_block_check_kernel<2>,
+                           dim3(g), dim3(64), 0, stream, frames, data,
                            (const ulonglong4 *)refs, (const BlkDesc *)blks, nblk, scratch, status,
-                           ctr);
+                           ctr, zck_dbg());
     return hipGetLastError();
 }
 

@@ -178,6 +178,38 @@ static double pcie_bound(uint64_t in_bytes, uint64_t out_bytes, uint64_t batch, 
     return both;
 }
 
+// The files read by `readers` threads (pread, as the timed run) into
+// page-locked memory with no engine: the page-cache copy rate the run's
+// readers can reach on this host (GiB/s).
+static double read_bound(const std::vector<std::string> &paths, uint64_t fsize, int readers) {
+    uint8_t *buf = nullptr;
+    const uint64_t span = 2 * fsize;
+    if (hipHostMalloc((void **)&buf, span, hipHostMallocDefault) != hipSuccess) return -1;
+    memset(buf, 0, span);
+    const double t0 = now();
+    std::atomic<int> next{0};
+    std::vector<std::thread> ws;
+    const int nf = (int)paths.size();
+    for (int w = 0; w < readers; w++)
+        ws.emplace_back([&] {
+            for (int f; (f = next++) < nf;) {
+                const int fd = open(paths[f].c_str(), O_RDONLY);
+                uint8_t *dst = buf + (uint64_t)(f & 1) * fsize;
+                uint64_t o = 0;
+                while (o < fsize) {
+                    const ssize_t r = pread(fd, dst + o, fsize - o, (off_t)o);
+                    if (r <= 0) break;
+                    o += (uint64_t)r;
+                }
+                close(fd);
+            }
+        });
+    for (auto &w : ws) w.join();
+    const double el = now() - t0;
+    (void)hipHostFree(buf);
+    return (double)nf * (double)fsize / el / (1ull << 30);
+}
+
 int main(int argc, char **argv) {
     // More hardware queues than HIP's default 4, before the first HIP call:
     // the engine's copy, compute, id and pack streams (8 + the context's)
@@ -344,6 +376,7 @@ int main(int argc, char **argv) {
     // ---- bound ------------------------------------------------------------------
     double h2d_alone = 0;
     const double bound_s = pcie_bound(stb.bytes_in, stb.pack_bytes, batch, &h2d_alone);
+    const double rd = read_bound(paths, fsize, readers);
     const double gib = (double)stb.bytes_in / (1ull << 30);
     char line[4096];
     snprintf(line, sizeof line,
@@ -355,6 +388,8 @@ int main(int argc, char **argv) {
              "\"pcie_bound\": {\"gibs_input\": %.2f, \"seconds\": %.4f, \"h2d_alone_gibs\": %.2f, "
              "\"how\": \"the run's input H2D in batch-sized copies from page-locked memory with its "
              "pack bytes D2H on a second stream at the same time, no compute\"}, "
+             "\"read_bound\": {\"gibs\": %.2f, \"how\": \"the same readers pread every file into "
+             "page-locked memory, no engine\"}, "
              "\"frac_of_bound\": %.3f, "
              "\"checks\": {\"pack_ids_ok\": %s, \"pack_seq_ok\": %s, \"dedup_ok\": %s, "
              "\"pack_bytes_ok\": %s, \"checked\": %s}, "
@@ -370,7 +405,7 @@ int main(int argc, char **argv) {
              gib / best, best, (unsigned long long)stb.bytes_in, nfiles,
              (unsigned long long)fsize, (unsigned long long)stb.pack_bytes, sink.packs.size(),
              (unsigned long long)stb.chunks, (unsigned long long)stb.new_blobs,
-             (unsigned long long)stb.batches, gib / bound_s, bound_s, h2d_alone, bound_s / best,
+             (unsigned long long)stb.batches, gib / bound_s, bound_s, h2d_alone, rd, bound_s / best,
              ids_ok ? "true" : "false", seq_ok ? "true" : "false", dedup_ok ? "true" : "false",
              bytes_ok ? "true" : "false", check ? "true" : "false", readers,
              (unsigned long long)batch, depth, threads, in_slots, level, reps,
