@@ -55,6 +55,7 @@ namespace rcdc {
 rcdc_status plan_relayout(rcdc_plan *pl, const uint64_t *offs, const uint64_t *lens, uint32_t n,
                           uint64_t arena_len, hipStream_t up);
 int ctx_device(const rcdc_ctx *ctx);
+uint64_t ctx_min_size(const rcdc_ctx *ctx);
 rcdc_status set_error(rcdc_status st, const char *msg);
 void host_sha256_many(const uint8_t *const *ptrs, const uint64_t *lens, uint32_t n,
                       uint8_t *digests);
@@ -220,7 +221,8 @@ struct rcdc_ingest {
     uint64_t nbatches = 0, next_seq = 0;
     std::unordered_set<Id32, Id32Hash> known;  // the index's ids + the packer's
     // threads
-    std::thread worker, back, waiter;
+    std::thread worker, back, waiter, feeder;
+    int submitting = 0;  // slots taken from `ready` whose batch is not in `submitted` yet
     std::vector<std::thread> pool;
     std::mutex pool_mu;
     std::condition_variable pool_cv;
@@ -422,6 +424,7 @@ bool submit_ready(Ing *g) {
             if (ps == g->depth) return true;
             in = g->ready.front();
             g->ready.pop_front();
+            g->submitting++;
             g->ps[ps].busy = true;
             B = std::make_unique<Batch>();
             B->index = g->nbatches++;
@@ -444,6 +447,25 @@ bool submit_ready(Ing *g) {
         ING_HIP(g, hipEventRecord(in->h2d, g->s_in));
         std::lock_guard<std::mutex> lk(g->mu);
         g->submitted.push_back(std::move(B));
+        g->submitting--;
+        g->cv_slot.notify_all();
+    }
+}
+
+void reap_inputs(Ing *g);
+
+// Feeder thread: a ready input slot's H2D is enqueued as soon as a pipeline
+// slot is free, whatever stage A is doing (the front thread used to enqueue
+// it only between two stage A runs: each copy then started only after the
+// previous batch's stage A, r5g timeline).
+void feeder_main(Ing *g) {
+    (void)hipSetDevice(g->device);
+    for (;;) {
+        reap_inputs(g);
+        if (!submit_ready(g)) return;
+        std::unique_lock<std::mutex> lk(g->mu);
+        if (g->err || g->front_done) return;
+        g->cv_slot.wait_for(lk, std::chrono::microseconds(200));
     }
 }
 
@@ -504,9 +526,20 @@ bool stage_a(Ing *g, Batch *B) {
     B->ids.assign(nchunks * 32, 0);
     // 3. ids: short chunks on the device (own stream per pipeline slot), long
     // ones on host threads from the input slot
+    // The last batch's ids bound the run's end: its longest device chain
+    // (~34 MB/s per lane: 62 ms for a 2 MiB chunk) would outlast everything
+    // else, so the host takes its chunks above 1 MiB too and both sides end
+    // together (~30 ms).
+    bool tail;
+    {
+        std::lock_guard<std::mutex> lk(g->mu);
+        tail = g->finishing && g->ready.empty() && g->open == nullptr && g->submitted.empty() &&
+               g->submitting == 0;
+    }
+    const uint64_t long_thr = tail ? std::min<uint64_t>(g->long_chunk, 1ull << 20) : g->long_chunk;
     std::vector<uint32_t> long_idx;
     for (uint64_t k = 0; k < nchunks; k++)
-        (B->c_len[k] > g->long_chunk ? long_idx : B->short_idx).push_back((uint32_t)k);
+        (B->c_len[k] > long_thr ? long_idx : B->short_idx).push_back((uint32_t)k);
     std::sort(B->short_idx.begin(), B->short_idx.end(),
               [&](uint32_t a, uint32_t b) { return B->c_len[a] > B->c_len[b]; });
     const uint64_t ns = B->short_idx.size();
@@ -797,9 +830,9 @@ bool stage_b(Ing *g, Batch *B, bool finalize) {
         }
         ING_HIP(g, hipEventRecord(g->ev_back, g->s_back));
         ING_HIP(g, hipStreamWaitEvent(g->s_out, g->ev_back, 0));
-        for (uint64_t o = 0; o < total; o += g->copy_piece)
-            ING_HIP(g, hipMemcpyAsync(out->host + o, g->d_packs + o, std::min(g->copy_piece, total - o),
-                                      hipMemcpyDeviceToHost, g->s_out));
+        // one copy: in pieces, the H2D and D2H pieces took turns on one DMA
+        // engine instead of running in both directions at once (r5j trace)
+        ING_HIP(g, hipMemcpyAsync(out->host, g->d_packs, total, hipMemcpyDeviceToHost, g->s_out));
         ING_HIP(g, hipEventRecord(g->ev_out, g->s_out));
     }
     // the still open pack: its blobs into the other carry buffer
@@ -888,8 +921,6 @@ void reap_inputs(Ing *g) {
 void worker_main(Ing *g) {
     (void)hipSetDevice(g->device);
     for (;;) {
-        reap_inputs(g);
-        if (!submit_ready(g)) return;
         std::unique_ptr<Batch> B;
         bool done = false;
         {
@@ -904,7 +935,8 @@ void worker_main(Ing *g) {
             } else {
                 bool waiting_commits = false;  // a closed slot whose files are not all in
                 for (auto &x : g->in) waiting_commits |= x->state == kClosed;
-                done = g->finishing && g->ready.empty() && g->open == nullptr && !waiting_commits;
+                done = g->finishing && g->ready.empty() && g->open == nullptr && !waiting_commits &&
+                       g->submitting == 0;
             }
         }
         if (B) {
@@ -1065,6 +1097,12 @@ rcdc_status rcdc_ingest_create(rcdc_ctx *ctx, const rcdc_ingest_config *cfg,
             return fail_hip(e, "output slot");
         g->outs.push_back(std::move(o));
     }
+    // the open pack's carry buffers, sized for a default pack and its slack
+    for (int c = 0; c < 2; c++) {
+        const uint64_t cc = std::max<uint64_t>(g->sizer.pack_size() * 2, 128ull << 20);
+        if ((e = hipMalloc((void **)&g->carry[c], cc)) != hipSuccess) return fail_hip(e, "carry");
+        g->carry_cap[c] = cc;
+    }
     g->ps.resize(g->depth);
     for (auto &P : g->ps) {
         if ((e = hipStreamCreateWithFlags(&P.s_ids, hipStreamNonBlocking)) != hipSuccess ||
@@ -1085,9 +1123,25 @@ rcdc_status rcdc_ingest_create(rcdc_ctx *ctx, const rcdc_ingest_config *cfg,
         // the plan built once for a full-batch layout (allocations and
         // synchronous uploads here, not inside the pipeline); each batch then
         // re-lays it out on its compute stream, reusing the buffers
-        const uint64_t off0 = 0, len0 = g->batch_cap;
-        if (rcdc_status ps = rcdc_plan_create(ctx, &off0, &len0, 1, g->batch_cap + 256, &P.plan))
+        // (256 streams: its per-stream arrays then hold any batch of up to
+        // 256 files without a regrow; r5j logged five regrows per slot with
+        // a one-stream layout, each a device-wide hipFree)
+        constexpr uint32_t kPlanStreams = 256;
+        std::vector<uint64_t> off0(kPlanStreams), len0(kPlanStreams);
+        const uint64_t per = (g->batch_cap / kPlanStreams) & ~255ull;
+        for (uint32_t i = 0; i < kPlanStreams; i++) {
+            off0[i] = i * per;
+            len0[i] = per;
+        }
+        if (rcdc_status ps = rcdc_plan_create(ctx, off0.data(), len0.data(), kPlanStreams,
+                                              g->batch_cap + 256, &P.plan))
             return ps;
+        // short-chunk refs for a batch of minimum-size chunks
+        P.refs_cap = g->batch_cap / std::max<uint64_t>(rcdc::ctx_min_size(ctx), 4096) * 2 + 1024;
+        if ((e = hipHostMalloc((void **)&P.h_refs, P.refs_cap * 16, hipHostMallocDefault)) != hipSuccess ||
+            (e = hipMalloc((void **)&P.d_refs, P.refs_cap * 16)) != hipSuccess ||
+            (e = hipMalloc((void **)&P.d_dig, P.refs_cap * 32)) != hipSuccess)
+            return fail_hip(e, "refs");
     }
     {
         const uint64_t f = g->batch_cap + g->batch_cap / 64 + (64ull << 20);
@@ -1108,6 +1162,7 @@ rcdc_status rcdc_ingest_create(rcdc_ctx *ctx, const rcdc_ingest_config *cfg,
     for (uint32_t i = 0; i < g->nthreads; i++) g->pool.emplace_back(pool_main, gp);
     g->waiter = std::thread(waiter_main, gp);
     g->worker = std::thread(worker_main, gp);
+    g->feeder = std::thread(feeder_main, gp);
     g->back = std::thread(back_main, gp);
     *out = g.release();
     return RCDC_OK;
@@ -1248,6 +1303,7 @@ void rcdc_ingest_destroy(rcdc_ingest *g) {
         g->cv_slot.notify_all();
     }
     if (g->worker.joinable()) g->worker.join();
+    if (g->feeder.joinable()) g->feeder.join();
     if (g->back.joinable()) g->back.join();
     {
         std::unique_lock<std::mutex> lk(g->mu);

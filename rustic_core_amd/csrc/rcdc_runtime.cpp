@@ -1500,6 +1500,7 @@ rcdc_status plan_relayout(rcdc_plan *pl, const uint64_t *offs, const uint64_t *l
     return plan_build(pl->ctx, pl, offs, lens, n, arena_len, up);
 }
 int ctx_device(const rcdc_ctx *ctx) { return ctx ? ctx->device : 0; }
+uint64_t ctx_min_size(const rcdc_ctx *ctx) { return ctx ? ctx->min : 0; }
 rcdc_status set_error(rcdc_status st, const char *msg) { return fail(st, "%s", msg); }
 }  // namespace rcdc
 

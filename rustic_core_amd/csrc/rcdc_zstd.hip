@@ -217,11 +217,10 @@ __device__ __forceinline__ uint64_t bytes8_at(const uint64_t u[4], uint32_t j) {
     return lo | hi;
 }
 
-// Far matches shorter than this are not worth their offset's bits (word
-// text: one or two words at 100+ KiB cost more than their literals,
-// r5h: 0.365 -> 0.373 when kept); the map keeps only candidates whose first
-// kZstdFarMin bytes agree, so a block with none skips the far path.
-constexpr uint32_t kZstdFarMin = 16;
+// The map keeps only candidates whose first kZstdFarMin bytes agree (the
+// 8-byte key itself: tools/zstd_ldm_model.py CSV rows 0.143 at 8, 0.156 at
+// 12, 0.182 at 16), so a block with none skips the far path.
+constexpr uint32_t kZstdFarMin = 8;
 
 // Equal bytes of a[0..) and b[0..), at most maxlen (wave-uniform result).
 // Lane l compares 16 bytes per round (1 KiB per wave round); the last,
@@ -1278,10 +1277,9 @@ __global__ __launch_bounds__(256) void rcdc_zstd_far_map_kernel(
             for (uint32_t i = 0; i < 16u; i++) ej = i == j ? e[i] : ej;
             const uint32_t d = ((hit2 >> j) & 1u) ? 2u : 1u;
             const uint32_t q = k.start - d * kZstdBlock + (ej >> 15) - 1u;  // blob-relative
-            const uint4 v = ld16(bsrc + q);  // q + 20 is inside the blob: block b - d ends above it
-            if (((uint64_t)v.x | (uint64_t)v.y << 32) == bytes8_at(u, j) &&
-                ((uint64_t)v.z | (uint64_t)v.w << 32) == bytes8_at(u, j + 8))
-                off = k.start + p0 + j - q;
+            // q + 8 is inside the blob: block b - d ends above it
+            const uint64_t v = (uint64_t)ld4(bsrc + q) | (uint64_t)ld4(bsrc + q + 4) << 32;
+            if (v == bytes8_at(u, j)) off = k.start + p0 + j - q;
         }
         map[g] = off;
         found |= off != 0u;
@@ -1480,7 +1478,7 @@ __global__ __launch_bounds__(64, (NARROW ? HL - 1 : HL) == 11 ? 4 : 2) void rcdc
                     if (ok && c < 16)
                         while (bl < limb && src[p - 1 - bl] == bsrc[c - 1 - bl]) bl++;
                 }
-                if (act && cf != kZstdNone) {  // the far candidate: kept if longer
+                if (act && cf != kZstdNone && !ok) {  // the far candidate, when the table's fails
                     const uint32_t wf = ld4(bsrc + cf);
                     const uint32_t ff = first_diff16(ld16(src + p + 4), ld16(bsrc + cf + 4));
                     const uint32_t limb = p - anchor < cf ? p - anchor : cf;
@@ -1489,7 +1487,7 @@ __global__ __launch_bounds__(64, (NARROW ? HL - 1 : HL) == 11 ? 4 : 2) void rcdc
                         bf = last_eq16(ld16(src + p - 16), ld16(bsrc + cf - 16));
                         if (bf > limb) bf = limb;
                     }
-                    if (wf == w && 4 + ff >= keyb && (!ok || ff > fl)) {
+                    if (wf == w && 4 + ff >= keyb) {
                         if (cf < 16)
                             while (bf < limb && src[p - 1 - bf] == bsrc[cf - 1 - bf]) bf++;
                         c = cf;

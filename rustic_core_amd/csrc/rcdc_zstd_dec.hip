@@ -158,57 +158,72 @@ __device__ __forceinline__ uint64_t brev_bits(BRev &r, uint32_t n) {
 }
 
 // The same bitstream read through a 64-bit window that slides down 32 bits
-// at a time, with the next 16 dwords (four 16-byte groups) already loaded or
-// in flight: a refill never waits on memory.  Three dwords ahead were not
-// enough: a sequence consumes ~40 bits, so a refill's load was needed two
-// sequences after it was issued and the serial sequence decode stalled on
-// it every ~32 bits (r5h: 94 % of the check's time on word text in the
-// sequences phase).  Reads are at most 32 bits.  Invariant: the window
-// holds bits [B, B + 64) and B <= pos (pos - B < 64); g0.w is the dword of
-// bits [B - 32, B), then g0.z, g0.y, g0.x, g1.w, ... g3.x.
-struct BRevQ {
+// at a time, with the next 4-8 dwords (two 16-byte groups) already loaded or
+// in flight: a refill never waits on memory.  Reads are at most 32 bits.
+// Invariant: the window holds bits [B, B + 64) and B <= pos (pos - B < 64);
+// g0.w is the dword of bits [B - 32, B), then g0.z, g0.y, g0.x, g1.w, ...
+struct BRevQ {  // 32-bit positions: the scalar unit has no 64-bit signed compare
     const uint8_t *base;
-    int64_t len;
-    int64_t pos;
-    int64_t B;
+    int32_t len;
+    int32_t pos;
+    int32_t B;
     uint64_t acc;
-    uint4 g0, g1, g2, g3;
+    uint4 g0, g1;
     uint32_t used;  // dwords of the original g0 shifted in (0..3)
 };
 
-// 4 bytes at base + byte (any alignment), bytes outside [0, len) as 0
+// A wave-uniform value in a scalar register: the serial sequence decode then
+// runs on the scalar unit (a wave64 VALU op takes 4 cycles for one useful
+// lane; r5j: 0.7 us per sequence, VALU-issue bound).
+__device__ __forceinline__ uint32_t rfl(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
+__device__ __forceinline__ uint64_t rfl64(uint64_t v) {
+    return (uint64_t)rfl((uint32_t)v) | (uint64_t)rfl((uint32_t)(v >> 32)) << 32;
+}
+
+// 4 bytes at base + byte (any alignment), bytes outside [0, len) as 0; U:
+// the reader is wave-uniform (every lane reads the same stream)
+template <bool U = false>
 __device__ __forceinline__ uint32_t brq_ld4(const uint8_t *base, int64_t len, int64_t byte) {
-    if (byte >= 0 && byte + 4 <= len) return ld4u(base + byte);
     uint32_t v = 0;
-    for (int i = 0; i < 4; i++)
-        if (byte + i >= 0 && byte + i < len) v |= (uint32_t)base[byte + i] << (8 * i);
-    return v;
+    if (byte >= 0 && byte + 4 <= len) {
+        v = ld4u(base + byte);
+    } else {
+        for (int i = 0; i < 4; i++)
+            if (byte + i >= 0 && byte + i < len) v |= (uint32_t)base[byte + i] << (8 * i);
+    }
+    return U ? rfl(v) : v;
 }
 
 // the 16 bytes [byte, byte + 16) as dwords x (lowest) .. w
+template <bool U = false>
 __device__ __forceinline__ uint4 brq_ld16(const uint8_t *base, int64_t len, int64_t byte) {
-    return make_uint4(brq_ld4(base, len, byte), brq_ld4(base, len, byte + 4),
-                      brq_ld4(base, len, byte + 8), brq_ld4(base, len, byte + 12));
+    return make_uint4(brq_ld4<U>(base, len, byte), brq_ld4<U>(base, len, byte + 4),
+                      brq_ld4<U>(base, len, byte + 8), brq_ld4<U>(base, len, byte + 12));
 }
 
-__device__ __forceinline__ bool brq_init(BRevQ &r, const uint8_t *p, int64_t len) {
+template <bool U = false>
+__device__ __forceinline__ bool brq_init(BRevQ &r, const uint8_t *p, int64_t len64) {
+    if (len64 <= 0 || len64 > (1 << 27)) return false;  // streams of one block
+    int32_t len = (int32_t)len64;
+    if (U) {
+        p = reinterpret_cast<const uint8_t *>(rfl64(reinterpret_cast<uintptr_t>(p)));
+        len = (int32_t)rfl((uint32_t)len);
+    }
     r.base = p;
     r.len = len;
-    if (len <= 0) return false;
-    const uint32_t last = p[len - 1];
+    const uint32_t last = U ? rfl(p[len - 1]) : p[len - 1];
     if (last == 0) return false;
-    r.pos = 8 * (len - 1) + (int64_t)highbit32(last);
+    r.pos = 8 * (len - 1) + (int32_t)highbit32(last);
     r.B = ((r.pos >> 5) << 5) - 32;  // arithmetic shifts: floor
-    const int64_t by = r.B >> 3;
-    r.acc = (uint64_t)brq_ld4(p, len, by) | (uint64_t)brq_ld4(p, len, by + 4) << 32;
-    r.g0 = brq_ld16(p, len, by - 16);
-    r.g1 = brq_ld16(p, len, by - 32);
-    r.g2 = brq_ld16(p, len, by - 48);
-    r.g3 = brq_ld16(p, len, by - 64);
+    const int32_t by = r.B >> 3;
+    r.acc = (uint64_t)brq_ld4<U>(p, len, by) | (uint64_t)brq_ld4<U>(p, len, by + 4) << 32;
+    r.g0 = brq_ld16<U>(p, len, by - 16);
+    r.g1 = brq_ld16<U>(p, len, by - 32);
     r.used = 0;
     return true;
 }
 
+template <bool U = false>
 __device__ __forceinline__ void brq_slide(BRevQ &r) {
     r.acc = (r.acc << 32) | r.g0.w;
     r.B -= 32;
@@ -217,22 +232,22 @@ __device__ __forceinline__ void brq_slide(BRevQ &r) {
     r.g0.y = r.g0.x;
     if (++r.used == 4) {
         r.g0 = r.g1;
-        r.g1 = r.g2;
-        r.g2 = r.g3;
-        r.g3 = brq_ld16(r.base, r.len, (r.B >> 3) - 64);
+        r.g1 = brq_ld16<U>(r.base, r.len, (r.B >> 3) - 32);
         r.used = 0;
     }
 }
 
+template <bool U = false>
 __device__ __forceinline__ uint32_t brq_peek(BRevQ &r, uint32_t n) {
     if (n == 0) return 0;
-    const int64_t lo = r.pos - (int64_t)n;
-    if (lo < r.B) brq_slide(r);
+    const int32_t lo = r.pos - (int32_t)n;
+    if (lo < r.B) brq_slide<U>(r);
     return (uint32_t)((r.acc >> (uint32_t)(lo - r.B)) & ((1ull << n) - 1ull));
 }
 
+template <bool U = false>
 __device__ __forceinline__ uint32_t brq_bits(BRevQ &r, uint32_t n) {
-    const uint32_t v = brq_peek(r, n);
+    const uint32_t v = brq_peek<U>(r, n);
     r.pos -= n;
     return v;
 }
@@ -670,6 +685,7 @@ __device__ void check_compressed(Dec &D, DecLds &L, const uint8_t *p, uint32_t b
         q += 3;
     }
     uint64_t litpos = 0;  // literals consumed
+    nseq = rfl(nseq);     // wave-uniform (the decode loop's trip count)
     if (nseq) {
         if (q >= end) { D.bad = kCkCorrupt; return; }
         const uint32_t modes = *q++;
@@ -721,10 +737,11 @@ __device__ void check_compressed(Dec &D, DecLds &L, const uint8_t *p, uint32_t b
         }
         wsync();
         BRevQ r;
-        if (!brq_init(r, q, end - q)) { D.bad = kCkCorrupt; return; }
-        uint32_t sll = brq_bits(r, D.al_ll);
-        uint32_t sof = brq_bits(r, D.al_of);
-        uint32_t sml = brq_bits(r, D.al_ml);
+        if (!brq_init<true>(r, q, end - q)) { D.bad = kCkCorrupt; return; }
+        const uint32_t al_ll = rfl(D.al_ll), al_of = rfl(D.al_of), al_ml = rfl(D.al_ml);
+        uint32_t sll = brq_bits<true>(r, al_ll);
+        uint32_t sof = brq_bits<true>(r, al_of);
+        uint32_t sml = brq_bits<true>(r, al_ml);
         uint32_t r0 = D.rep[0], r1 = D.rep[1], r2 = D.rep[2];
         bool u0 = D.rep_unk & 1u, u1 = (D.rep_unk >> 1) & 1u, u2 = (D.rep_unk >> 2) & 1u;
         bool unk_used = false;
@@ -732,14 +749,35 @@ __device__ void check_compressed(Dec &D, DecLds &L, const uint8_t *p, uint32_t b
             const uint32_t nb = min(64u, nseq - s0);
             uint32_t myll = 0, myml = 0, myoff = 0;
             bool err = false;
+            // the decode state is wave-uniform: say so each round (the
+            // compare loops below diverge, and the compiler then kept the
+            // reader in VGPRs with 64-bit VALU compares per bit read)
+            r.pos = (int32_t)rfl((uint32_t)r.pos);
+            r.B = (int32_t)rfl((uint32_t)r.B);
+            r.acc = rfl64(r.acc);
+            r.used = rfl(r.used);
+            r.len = (int32_t)rfl((uint32_t)r.len);
+            r.base = reinterpret_cast<const uint8_t *>(rfl64(reinterpret_cast<uintptr_t>(r.base)));
+            r.g0 = make_uint4(rfl(r.g0.x), rfl(r.g0.y), rfl(r.g0.z), rfl(r.g0.w));
+            r.g1 = make_uint4(rfl(r.g1.x), rfl(r.g1.y), rfl(r.g1.z), rfl(r.g1.w));
+            sll = rfl(sll);
+            sof = rfl(sof);
+            sml = rfl(sml);
+            r0 = rfl(r0);
+            r1 = rfl(r1);
+            r2 = rfl(r2);
             for (uint32_t j = 0; j < nb; j++) {
-                const FseD eo = L.of[sof], el = L.ll[sll], em = L.ml[sml];
-                const uint32_t xl = L.llx[sll], xm = L.mlx[sml];
-                const uint32_t ofc = eo.sym, llc = el.sym, mlc = em.sym;
+                // the entries as one dword each (sym | nb << 8 | next << 16),
+                // wave-uniform
+                const uint32_t eo = rfl(reinterpret_cast<const uint32_t *>(L.of)[sof]);
+                const uint32_t el = rfl(reinterpret_cast<const uint32_t *>(L.ll)[sll]);
+                const uint32_t em = rfl(reinterpret_cast<const uint32_t *>(L.ml)[sml]);
+                const uint32_t xl = rfl(L.llx[sll]), xm = rfl(L.mlx[sml]);
+                const uint32_t ofc = eo & 0xFFu, llc = el & 0xFFu, mlc = em & 0xFFu;
                 if (ofc > 31 || llc > 35 || mlc > 52) err = true;
-                const uint64_t ofv = (1ull << ofc) + brq_bits(r, ofc);
-                const uint32_t ml = (xm & 0xFFFFFFu) + brq_bits(r, xm >> 24);
-                const uint32_t ll = (xl & 0xFFFFFFu) + brq_bits(r, xl >> 24);
+                const uint64_t ofv = (1ull << ofc) + brq_bits<true>(r, ofc);
+                const uint32_t ml = (xm & 0xFFFFFFu) + brq_bits<true>(r, xm >> 24);
+                const uint32_t ll = (xl & 0xFFFFFFu) + brq_bits<true>(r, xl >> 24);
                 uint32_t off;
                 if (ofv > 3) {
                     off = (uint32_t)(ofv - 3);
@@ -783,15 +821,16 @@ __device__ void check_compressed(Dec &D, DecLds &L, const uint8_t *p, uint32_t b
                 }
                 if (off == 0) err = true;
                 if (s0 + j + 1 < nseq) {
-                    sll = el.next + brq_bits(r, el.nb);
-                    sml = em.next + brq_bits(r, em.nb);
-                    sof = eo.next + brq_bits(r, eo.nb);
+                    sll = (el >> 16) + brq_bits<true>(r, (el >> 8) & 0xFFu);
+                    sml = (em >> 16) + brq_bits<true>(r, (em >> 8) & 0xFFu);
+                    sof = (eo >> 16) + brq_bits<true>(r, (eo >> 8) & 0xFFu);
                 }
-                if (lane == j) {
-                    myll = ll;
-                    myml = ml;
-                    myoff = off;
-                }
+                // selects, not a branch on the lane: a divergent branch here
+                // made the compiler keep the reader's state in VGPRs
+                const bool me = lane == j;
+                myll = me ? ll : myll;
+                myml = me ? ml : myml;
+                myoff = me ? off : myoff;
             }
             if (unk_used) { D.bad = kCkSeq; return; }  // (block mode only)
             if (err || r.pos < 0) { D.bad = kCkCorrupt; return; }

@@ -38,6 +38,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <condition_variable>
 #include <mutex>
 #include <set>
 #include <string>
@@ -181,6 +182,8 @@ static double pcie_bound(uint64_t in_bytes, uint64_t out_bytes, uint64_t batch, 
 // The files read by `readers` threads (pread, as the timed run) into
 // page-locked memory with no engine: the page-cache copy rate the run's
 // readers can reach on this host (GiB/s).
+constexpr uint64_t kRange = 64ull << 20;  // bytes per reader job
+
 static double read_bound(const std::vector<std::string> &paths, uint64_t fsize, int readers) {
     uint8_t *buf = nullptr;
     const uint64_t span = 2 * fsize;
@@ -298,26 +301,64 @@ int main(int argc, char **argv) {
         rcdc_ingest *ing = nullptr;
         CHECK(rcdc_ingest_create(ctx, &cfg, on_pack, on_file, &sink, &ing));
         const double t0 = now();
-        std::atomic<int> next{0};
+        // The readers take 64 MiB ranges in file order, several readers per
+        // file: the engine's first batch is filled at the page-cache copy
+        // rate, not one file per reader (8 whole files read side by side
+        // closed the first 2 GiB slot only after ~100 ms, r5j).  The first
+        // reader of a file reserves its space; the last to finish commits it.
+        struct FileJob {
+            std::mutex m;
+            std::condition_variable cv;
+            uint8_t *buf = nullptr;
+            uint64_t ticket = 0, len = 0;
+            bool ready = false;
+            std::atomic<int> left{0};
+        };
+        std::vector<FileJob> fj(nf);
+        struct Range {
+            int file;
+            uint64_t off, len;
+        };
+        std::vector<Range> jobs;
+        for (int f = 0; f < nf; f++) {
+            struct stat sb;
+            stat(paths[f].c_str(), &sb);
+            fj[f].len = (uint64_t)sb.st_size;
+            int k = 0;
+            for (uint64_t o = 0; o < fj[f].len || (o == 0 && k == 0); o += kRange, k++)
+                jobs.push_back({f, o, std::min<uint64_t>(kRange, fj[f].len - o)});
+            fj[f].left = k;
+        }
+        std::atomic<size_t> next{0};
         std::vector<std::thread> ws;
         for (int w = 0; w < readers; w++)
             ws.emplace_back([&] {
-                for (int f; (f = next++) < nf;) {
-                    const int fd = open(paths[f].c_str(), O_RDONLY);
-                    struct stat sb;
-                    fstat(fd, &sb);
-                    const uint64_t n = (uint64_t)sb.st_size;
+                for (size_t j; (j = next++) < jobs.size();) {
+                    const Range &r = jobs[j];
+                    FileJob &F = fj[r.file];
                     uint8_t *buf;
-                    uint64_t ticket;
-                    CHECK(rcdc_ingest_reserve(ing, n, &buf, &ticket));
+                    if (r.off == 0) {
+                        uint64_t t;
+                        CHECK(rcdc_ingest_reserve(ing, F.len, &buf, &t));
+                        std::lock_guard<std::mutex> lk(F.m);
+                        F.buf = buf;
+                        F.ticket = t;
+                        F.ready = true;
+                        F.cv.notify_all();
+                    } else {
+                        std::unique_lock<std::mutex> lk(F.m);
+                        F.cv.wait(lk, [&] { return F.ready; });
+                        buf = F.buf;
+                    }
+                    const int fd = open(paths[r.file].c_str(), O_RDONLY);
                     uint64_t o = 0;
-                    while (o < n) {
-                        const ssize_t r = pread(fd, buf + o, n - o, (off_t)o);
-                        if (r <= 0) break;
-                        o += (uint64_t)r;
+                    while (o < r.len) {
+                        const ssize_t n = pread(fd, buf + r.off + o, r.len - o, (off_t)(r.off + o));
+                        if (n <= 0) break;
+                        o += (uint64_t)n;
                     }
                     close(fd);
-                    CHECK(rcdc_ingest_commit(ing, ticket, (uint64_t)f, o));
+                    if (--F.left == 0) CHECK(rcdc_ingest_commit(ing, F.ticket, (uint64_t)r.file, F.len));
                 }
             });
         for (auto &w : ws) w.join();
