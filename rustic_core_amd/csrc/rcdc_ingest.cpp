@@ -127,6 +127,7 @@ struct InSlot {
     hipEvent_t h2d = nullptr;
     bool h2d_pending = false;
     std::atomic<int> host_jobs{0};  // long-id jobs still reading this slot
+    std::atomic<bool> h2d_issued{false};  // its last H2D piece and h2d are enqueued
 };
 
 // A batch between stage A and stage B.
@@ -222,6 +223,14 @@ struct rcdc_ingest {
     std::unordered_set<Id32, Id32Hash> known;  // the index's ids + the packer's
     // threads
     std::thread worker, back, waiter, feeder;
+    // the feeder's copy pump: batches waiting for their H2D pieces
+    struct H2DJob {
+        uint8_t *dst;
+        const uint8_t *src;
+        uint64_t len, done;
+        InSlot *in;
+    };
+    std::deque<H2DJob> h2d_q;
     int submitting = 0;  // slots taken from `ready` whose batch is not in `submitted` yet
     std::vector<std::thread> pool;
     std::mutex pool_mu;
@@ -437,14 +446,10 @@ bool submit_ready(Ing *g) {
         PSlot &P = g->ps[ps];
         const uint64_t used = in->used;
         if (!ensure_dev(g, &P.arena, &P.arena_cap, round_up(used, 256) + 512)) return false;
-        // the arena's previous batch is retired: its ids (the last reader) are done
-        // in pieces: a small upload or read-back of stage A on the same DMA
-        // engine waits for at most one piece, not a whole batch (r5f trace:
-        // the plan's uploads sat behind 2 GiB copies, 17-37 ms each)
-        for (uint64_t o = 0; o < used; o += g->copy_piece)
-            ING_HIP(g, hipMemcpyAsync(P.arena + o, in->host + o, std::min(g->copy_piece, used - o),
-                                      hipMemcpyHostToDevice, g->s_in));
-        ING_HIP(g, hipEventRecord(in->h2d, g->s_in));
+        // the arena's previous batch is retired: its ids (the last reader)
+        // are done.  The copy goes to the pump (feeder_main), piece by piece.
+        in->h2d_issued = false;
+        g->h2d_q.push_back({P.arena, in->host, used, 0, in});
         std::lock_guard<std::mutex> lk(g->mu);
         g->submitted.push_back(std::move(B));
         g->submitting--;
@@ -458,14 +463,69 @@ void reap_inputs(Ing *g);
 // slot is free, whatever stage A is doing (the front thread used to enqueue
 // it only between two stage A runs: each copy then started only after the
 // previous batch's stage A, r5g timeline).
+//
+// It also pumps the H2D copies: at most two 64 MiB pieces are enqueued at a
+// time.  HIP's copies go to DMA engine queues in order, and stage A's small
+// uploads (plan tables, AEAD and zstd descriptors) landed behind every piece
+// already queued: with a whole 2 GiB batch enqueued at once each upload
+// waited ~40 ms (r5n: seal 40 ms after zstd; the next batch's stage A
+// started only after the previous chunk ids).  With two pieces in flight an
+// upload waits ~2.4 ms at most and the engine never idles.
+bool pump_h2d(Ing *g, std::deque<hipEvent_t> &inflight, std::vector<hipEvent_t> &free_ev) {
+    while (!inflight.empty() && hipEventQuery(inflight.front()) == hipSuccess) {
+        free_ev.push_back(inflight.front());
+        inflight.pop_front();
+    }
+    while (!g->h2d_q.empty() && inflight.size() < 2 && !free_ev.empty()) {
+        Ing::H2DJob &J = g->h2d_q.front();
+        const uint64_t n = std::min(g->copy_piece, J.len - J.done);
+        if (n) {
+            ING_HIP(g, hipMemcpyAsync(J.dst + J.done, J.src + J.done, n, hipMemcpyHostToDevice, g->s_in));
+            hipEvent_t ev = free_ev.back();
+            free_ev.pop_back();
+            ING_HIP(g, hipEventRecord(ev, g->s_in));
+            inflight.push_back(ev);
+            J.done += n;
+        }
+        if (J.done == J.len) {
+            ING_HIP(g, hipEventRecord(J.in->h2d, g->s_in));
+            J.in->h2d_issued = true;
+            g->h2d_q.pop_front();
+            std::lock_guard<std::mutex> lk(g->mu);
+            g->cv_slot.notify_all();
+        }
+    }
+    return true;
+}
+
 void feeder_main(Ing *g) {
     (void)hipSetDevice(g->device);
+    std::deque<hipEvent_t> inflight;
+    std::vector<hipEvent_t> free_ev(4, nullptr);
+    for (auto &e : free_ev)
+        if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) {
+            set_err(g, RCDC_ERR_INTERNAL, "feeder events");
+            return;
+        }
+    auto release = [&] {
+        (void)hipStreamSynchronize(g->s_in);
+        for (auto e : inflight) free_ev.push_back(e);
+        for (auto e : free_ev) (void)hipEventDestroy(e);
+    };
     for (;;) {
         reap_inputs(g);
-        if (!submit_ready(g)) return;
+        if (!submit_ready(g) || !pump_h2d(g, inflight, free_ev)) {
+            release();
+            return;
+        }
         std::unique_lock<std::mutex> lk(g->mu);
-        if (g->err || g->front_done) return;
-        g->cv_slot.wait_for(lk, std::chrono::microseconds(200));
+        if (g->err || (g->front_done && g->h2d_q.empty())) {
+            lk.unlock();
+            release();
+            return;
+        }
+        // a piece is ~1.2 ms: poll often while copies are queued
+        g->cv_slot.wait_for(lk, std::chrono::microseconds(g->h2d_q.empty() ? 200 : 50));
     }
 }
 
@@ -482,7 +542,13 @@ bool stage_a(Ing *g, Batch *B) {
     }
     const uint64_t used = in->used;
     const uint64_t arena_len = round_up(used, 256) + 256;
-    // 1. the H2D (submit_ready) lands before the chunking
+    // 1. the H2D (the feeder's pump) lands before the chunking: wait until
+    // its event is enqueued, then order the compute stream after it
+    {
+        std::unique_lock<std::mutex> lk(g->mu);
+        while (!in->h2d_issued && !g->err) g->cv_slot.wait_for(lk, std::chrono::microseconds(100));
+        if (g->err) return false;
+    }
     ING_HIP(g, hipStreamWaitEvent(g->s_comp, in->h2d, 0));
     // 2. chunk
     if (!P.plan) {
@@ -714,7 +780,9 @@ bool stage_b(Ing *g, Batch *B, bool finalize) {
     const uint64_t ns = B->short_idx.size();
     if (ns) {
         std::vector<uint8_t> dig(ns * 32);
-        ING_HIP(g, hipMemcpy(dig.data(), P.d_dig, ns * 32, hipMemcpyDeviceToHost));
+        // on the ids' own stream (not the legacy default stream's queue)
+        ING_HIP(g, hipMemcpyAsync(dig.data(), P.d_dig, ns * 32, hipMemcpyDeviceToHost, P.s_ids));
+        ING_HIP(g, hipStreamSynchronize(P.s_ids));
         for (uint64_t j = 0; j < ns; j++)
             memcpy(B->ids.data() + 32ull * B->short_idx[j], dig.data() + 32 * j, 32);
     }

@@ -1033,8 +1033,15 @@ rcdc_status plan_finish(rcdc_plan *pl) {
     HIP_TRY(hipEventSynchronize(pl->done));
     std::vector<uint64_t> &cnt = pl->fin_counts;
     cnt.assign(pl->n, 0);
-    if (pl->n)
-        HIP_TRY(hipMemcpy(cnt.data(), pl->d_counts, pl->n * 8, hipMemcpyDeviceToHost));
+    // read-backs on the run's own stream, not hipMemcpy: the legacy default
+    // stream sits on one of HIP's hardware queues too, and a copy queued
+    // there waits for whatever long kernel another stream put on that queue
+    // (the ingest's 62 ms chunk-id kernels serialised its batches, r5l)
+    if (pl->n) {
+        HIP_TRY(hipMemcpyAsync(cnt.data(), pl->d_counts, pl->n * 8, hipMemcpyDeviceToHost,
+                               pl->last_stream));
+        HIP_TRY(hipStreamSynchronize(pl->last_stream));
+    }
     if (const char *e = getenv("RCDC_WALK_DUMP"); e && !pl->wunits.empty()) {  // debugging aid
         const uint32_t want = (uint32_t)atoi(e);
         const size_t nw = pl->wunits.size();
@@ -1133,8 +1140,11 @@ rcdc_status plan_results(rcdc_plan *pl, uint64_t *cuts, uint64_t cap, uint64_t *
                                  (unsigned long long)total, (unsigned long long)cap);
     DeviceGuard g(pl->ctx->device);
     std::vector<uint64_t> all(pl->ncuts);
-    if (pl->ncuts)
-        HIP_TRY(hipMemcpy(all.data(), pl->d_cuts, pl->ncuts * 8, hipMemcpyDeviceToHost));
+    if (pl->ncuts) {
+        HIP_TRY(hipMemcpyAsync(all.data(), pl->d_cuts, pl->ncuts * 8, hipMemcpyDeviceToHost,
+                               pl->last_stream));
+        HIP_TRY(hipStreamSynchronize(pl->last_stream));
+    }
     uint64_t o = 0;
     for (uint32_t i = 0; i < pl->n; i++) {
         memcpy(cuts + o, all.data() + pl->cut_base[i], cnt[i] * 8);
@@ -2170,8 +2180,8 @@ rcdc_status aead_launch(rcdc_ctx *ctx, bool open, const uint8_t key[64], std::ve
                         std::vector<uint32_t> *status) {
     std::lock_guard<std::mutex> lk(ctx->aead_mu);
     DeviceGuard g(ctx->device);
-    if (ctx->aead_done) HIP_TRY(hipEventSynchronize(ctx->aead_done));  // the scratch is free
-    else HIP_TRY(hipEventCreateWithFlags(&ctx->aead_done, hipEventDisableTiming));
+    // (the last call's work is done: every call ends synchronised)
+    if (!ctx->aead_done) HIP_TRY(hipEventCreateWithFlags(&ctx->aead_done, hipEventDisableTiming));
     rcdc_status rs;
     if ((rs = ensure_dev(&ctx->d_aead_key, &ctx->cap_aead_key, 1))) return rs;
     if (!ctx->aead_key_set || memcmp(ctx->aead_key, key, 64) != 0) {
@@ -2239,23 +2249,21 @@ rcdc_status aead_launch(rcdc_ctx *ctx, bool open, const uint8_t key[64], std::ve
         ou += u;
         o0 += m + 1;
     }
-    // aead_done marks the scratch busy until this work is done, and the next
-    // call waits on it from the host: recorded on the context's own stream
-    // (after st's work), never on the caller's stream, which may be destroyed
-    // before that call (an engine's streams end with the engine; HIP then
-    // reads the freed stream when synchronising: r5g)
-    {
-        hipEvent_t relay;
-        HIP_TRY(hipEventCreateWithFlags(&relay, hipEventDisableTiming));
-        HIP_TRY(hipEventRecord(relay, st));
-        HIP_TRY(hipStreamWaitEvent(ctx->stream, relay, 0));
-        HIP_TRY(hipEventDestroy(relay));
-    }
-    HIP_TRY(hipEventRecord(ctx->aead_done, ctx->stream));
+    // The call returns once its work is done: the context's scratch is then
+    // free for the next call with no event kept across calls.  (An event
+    // recorded on the caller's stream and synchronised in the next call
+    // failed once that stream had been destroyed in between, r5g; one
+    // recorded on the context's stream waited behind whatever long kernel
+    // shared that stream's hardware queue, r5l.)
+    HIP_TRY(hipEventRecord(ctx->aead_done, st));
+    HIP_TRY(hipEventSynchronize(ctx->aead_done));
     if (open && status) {
         HIP_TRY(hipEventSynchronize(ctx->aead_done));
         status->assign(nb, 0);
-        if (nb) HIP_TRY(hipMemcpy(status->data(), ctx->d_aead_status, nb * 4, hipMemcpyDeviceToHost));
+        if (nb) {  // on st (see plan_finish: not the legacy default stream)
+            HIP_TRY(hipMemcpyAsync(status->data(), ctx->d_aead_status, nb * 4, hipMemcpyDeviceToHost, st));
+            HIP_TRY(hipStreamSynchronize(st));
+        }
     }
     return RCDC_OK;
 }
@@ -2315,7 +2323,6 @@ rcdc_status copy_units_run(rcdc_ctx *ctx, const std::vector<uint64_t> &copies, v
                            hipStream_t st) {
     if (copies.empty()) return RCDC_OK;
     std::lock_guard<std::mutex> lk(ctx->aead_mu);
-    if (ctx->aead_done) HIP_TRY(hipEventSynchronize(ctx->aead_done));
     const uint64_t nu = copies.size() / 4;
     rcdc_status rs;
     if ((rs = ensure_dev(&ctx->d_copy_units, &ctx->cap_copy_units, copies.size()))) return rs;

@@ -221,6 +221,7 @@ __device__ __forceinline__ uint64_t bytes8_at(const uint64_t u[4], uint32_t j) {
 // 8-byte key itself: tools/zstd_ldm_model.py CSV rows 0.143 at 8, 0.156 at
 // 12, 0.182 at 16), so a block with none skips the far path.
 constexpr uint32_t kZstdFarMin = 8;
+constexpr uint32_t kZstdFarDense = 8;  // far path when >= 1/8 of the groups hold an offset
 
 // Equal bytes of a[0..) and b[0..), at most maxlen (wave-uniform result).
 // Lane l compares 16 bytes per round (1 KiB per wave round); the last,
@@ -1230,7 +1231,7 @@ __global__ __launch_bounds__(256) void rcdc_zstd_far_map_kernel(
     const uint32_t *t1 = L.tab + (size_t)(b - (ok1 ? 1u : 0u)) * kZstdFarTab;
     const uint32_t *t2 = L.tab + (size_t)(b - (ok2 ? 2u : 0u)) * kZstdFarTab;
     uint32_t *map = L.map + (size_t)b * kZstdFarGroups;
-    bool found = false;
+    uint32_t found = 0;
     for (uint32_t g = tid; g * 16u < n; g += 256) {
         // every load of a round is independent of the others in flight: the
         // group's bytes, then all sampled positions' b-1 buckets, then the
@@ -1282,11 +1283,15 @@ __global__ __launch_bounds__(256) void rcdc_zstd_far_map_kernel(
             if (v == bytes8_at(u, j)) off = k.start + p0 + j - q;
         }
         map[g] = off;
-        found |= off != 0u;
+        found += off != 0u;
     }
-    if (found) any = 1u;
+    if (found) atomicAdd(&any, found);
     __syncthreads();
-    if (tid == 0) L.has[b] = any;
+    // the far path only where the map is dense: on word text one group in
+    // many finds a far 8-byte repeat that rarely beats the block's own table,
+    // and every step of the parse would pay the map load for it (r5l: text
+    // 34.9 -> 27.2 GiB/s at an unchanged ratio)
+    if (tid == 0) L.has[b] = any * kZstdFarDense >= (n + 15u) / 16u;
 }
 
 // res[b] = {type | rle byte << 8, content bytes}.  HL: hash table of 2^HL

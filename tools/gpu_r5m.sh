@@ -13,5 +13,5 @@ for i in 1 2; do
   N=c2_pipe$i XB=--pipeline run X=1
   N=c2_pair$i XB= run RCDC_SCAN_VARIANT=31
 done
-timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE -d $OUT/pmc_pair -o run --output-format csv -- python -u bench.py --workload C2 --no-cpu-baseline --steps 10 --warmup 1 --prewarm 0 --no-parity > $OUT/pmc_pair.log 2>&1 || { tail -5 $OUT/pmc_pair.log; exit 1; }
+RCDC_SCAN_VARIANT=31 timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE -d $OUT/pmc_pair -o run --output-format csv -- python -u bench.py --workload C2 --no-cpu-baseline --steps 10 --warmup 1 --prewarm 0 --no-parity > $OUT/pmc_pair.log 2>&1 || { tail -5 $OUT/pmc_pair.log; exit 1; }
 echo done
