@@ -60,6 +60,8 @@ rcdc_status set_error(rcdc_status st, const char *msg);
 void host_sha256_many(const uint8_t *const *ptrs, const uint64_t *lens, uint32_t n,
                       uint8_t *digests);
 void host_sha256_one(const uint8_t *p, uint64_t len, uint8_t out[32]);
+hipError_t launch_stream_copy(void *dst, const void *src, uint64_t len, uint32_t blocks,
+                              hipStream_t stream);
 bool host_sha_supported();
 }  // namespace rcdc
 
@@ -193,6 +195,7 @@ struct rcdc_ingest {
     bool compress = true, verify = true;
     uint64_t batch_cap = 0, long_chunk = 0;
     uint64_t copy_piece = 64ull << 20;  // bytes per H2D / D2H copy (RCDC_INGEST_COPY_PIECE)
+    uint32_t kcopy = 0;  // RCDC_INGEST_KCOPY: batch copies by a shader kernel on this many workgroups
     uint32_t depth = 4, nin = 4, nout = 4, nthreads = 8;
     PackSizer sizer{};
     // input slots
@@ -231,6 +234,19 @@ struct rcdc_ingest {
         InSlot *in;
     };
     std::deque<H2DJob> h2d_q;
+    // ... and the pack bytes' D2H, queued by stage B (back thread)
+    struct D2HJob {
+        uint8_t *dst;
+        const uint8_t *src;
+        uint64_t len, done;
+        hipEvent_t after;  // the pack build (s_back); the first piece waits on it
+        hipEvent_t fin;    // recorded after the last piece (the waiter syncs on it)
+        std::shared_ptr<std::atomic<bool>> issued;  // ev_out and fin are enqueued
+        bool waited;
+    };
+    std::mutex d2h_mu;
+    std::deque<D2HJob> d2h_q;
+    std::shared_ptr<std::atomic<bool>> last_d2h;  // the last D2H job's `issued`
     int submitting = 0;  // slots taken from `ready` whose batch is not in `submitted` yet
     std::vector<std::thread> pool;
     std::mutex pool_mu;
@@ -238,7 +254,12 @@ struct rcdc_ingest {
     std::deque<std::function<void()>> jobs;
     std::mutex wait_mu;
     std::condition_variable wait_cv;
-    std::deque<std::pair<hipEvent_t, std::vector<std::shared_ptr<PackJob>>>> wait_q;
+    struct WaitItem {
+        hipEvent_t ev;
+        std::shared_ptr<std::atomic<bool>> issued;
+        std::vector<std::shared_ptr<PackJob>> jobs;
+    };
+    std::deque<WaitItem> wait_q;
     std::mutex cb_mu;  // callbacks run one at a time
     std::atomic<bool> stop{false};
     bool finishing = false, finished = false;
@@ -250,7 +271,7 @@ struct rcdc_ingest {
     double t_first = 0;
     // RCDC_INGEST_PROF=1: per batch (stage A start, sync points, end; stage B
     // start, ids wait end, end), printed by rcdc_ingest_finish
-    bool prof = false;
+    int prof = 0;
     std::vector<std::vector<double>> tl;
 };
 
@@ -326,6 +347,20 @@ void pool_main(Ing *g) {
     }
 }
 
+// Wait for an event by polling (RCDC_INGEST_POLL, default on) instead of
+// hipEventSynchronize: a thread blocked in a HIP synchronisation call for a
+// 60-70 ms chunk-id kernel held up the other threads' launches (r5r: each
+// batch's chunking started only after the previous batch's ids were done).
+hipError_t wait_event(hipEvent_t ev) {
+    static const bool poll = !(getenv("RCDC_INGEST_POLL") && atoi(getenv("RCDC_INGEST_POLL")) == 0);
+    if (!poll) return hipEventSynchronize(ev);
+    for (;;) {
+        const hipError_t e = hipEventQuery(ev);
+        if (e != hipErrorNotReady) return e;
+        std::this_thread::sleep_for(std::chrono::microseconds(50));
+    }
+}
+
 // Hand one finished pack to the caller (pack ids are computed by then).
 void deliver(Ing *g, const std::shared_ptr<PackJob> &pj) {
     rcdc_ingest_pack p{};
@@ -387,7 +422,7 @@ void hash_packs(Ing *g, std::vector<std::shared_ptr<PackJob>> packs, bool last) 
 void waiter_main(Ing *g) {
     (void)hipSetDevice(g->device);
     for (;;) {
-        std::pair<hipEvent_t, std::vector<std::shared_ptr<PackJob>>> w;
+        Ing::WaitItem w;
         {
             std::unique_lock<std::mutex> lk(g->wait_mu);
             g->wait_cv.wait(lk, [&] { return g->stop || !g->wait_q.empty(); });
@@ -395,17 +430,21 @@ void waiter_main(Ing *g) {
             w = std::move(g->wait_q.front());
             g->wait_q.pop_front();
         }
-        if (hipEventSynchronize(w.first) != hipSuccess) {
+        // the pump enqueues the copy's last piece and its event later
+        while (!w.issued->load() && !g->err && !g->stop)
+            std::this_thread::sleep_for(std::chrono::microseconds(50));
+        if (!w.issued->load()) continue;
+        if (wait_event(w.ev) != hipSuccess) {
             set_err(g, RCDC_ERR_INTERNAL, "pack copy-back failed");
             continue;
         }
-        (void)hipEventDestroy(w.first);
+        (void)hipEventDestroy(w.ev);
         bool is_last;
         {
             std::lock_guard<std::mutex> lk(g->mu);
             is_last = g->front_done && g->inflight.empty();
         }
-        hash_packs(g, std::move(w.second), is_last);
+        hash_packs(g, std::move(w.jobs), is_last);
     }
 }
 
@@ -480,7 +519,12 @@ bool pump_h2d(Ing *g, std::deque<hipEvent_t> &inflight, std::vector<hipEvent_t> 
         Ing::H2DJob &J = g->h2d_q.front();
         const uint64_t n = std::min(g->copy_piece, J.len - J.done);
         if (n) {
-            ING_HIP(g, hipMemcpyAsync(J.dst + J.done, J.src + J.done, n, hipMemcpyHostToDevice, g->s_in));
+            if (g->kcopy)
+                ING_HIP(g, launch_stream_copy(J.dst + J.done, J.src + J.done, (n + 15) & ~15ull,
+                                              g->kcopy, g->s_in));
+            else
+                ING_HIP(g, hipMemcpyAsync(J.dst + J.done, J.src + J.done, n, hipMemcpyHostToDevice,
+                                          g->s_in));
             hipEvent_t ev = free_ev.back();
             free_ev.pop_back();
             ING_HIP(g, hipEventRecord(ev, g->s_in));
@@ -498,34 +542,84 @@ bool pump_h2d(Ing *g, std::deque<hipEvent_t> &inflight, std::vector<hipEvent_t> 
     return true;
 }
 
+// The D2H of the pack bytes the same way (small read-backs of stage A wait
+// behind a whole 1 GiB pack copy otherwise: r5p, the next batch's chunking
+// started only when the previous batch's packs were in host memory).
+bool pump_d2h(Ing *g, std::deque<hipEvent_t> &inflight, std::vector<hipEvent_t> &free_ev) {
+    while (!inflight.empty() && hipEventQuery(inflight.front()) == hipSuccess) {
+        free_ev.push_back(inflight.front());
+        inflight.pop_front();
+    }
+    std::lock_guard<std::mutex> lq(g->d2h_mu);
+    while (!g->d2h_q.empty() && inflight.size() < 2 && !free_ev.empty()) {
+        Ing::D2HJob &J = g->d2h_q.front();
+        if (!J.waited) {
+            ING_HIP(g, hipStreamWaitEvent(g->s_out, J.after, 0));
+            ING_HIP(g, hipEventDestroy(J.after));
+            J.waited = true;
+        }
+        const uint64_t n = std::min(g->copy_piece, J.len - J.done);
+        if (n) {
+            if (g->kcopy)
+                ING_HIP(g, launch_stream_copy(J.dst + J.done, J.src + J.done, (n + 15) & ~15ull,
+                                              g->kcopy, g->s_out));
+            else
+                ING_HIP(g, hipMemcpyAsync(J.dst + J.done, J.src + J.done, n, hipMemcpyDeviceToHost,
+                                          g->s_out));
+            hipEvent_t ev = free_ev.back();
+            free_ev.pop_back();
+            ING_HIP(g, hipEventRecord(ev, g->s_out));
+            inflight.push_back(ev);
+            J.done += n;
+        }
+        if (J.done == J.len) {
+            ING_HIP(g, hipEventRecord(g->ev_out, g->s_out));
+            ING_HIP(g, hipEventRecord(J.fin, g->s_out));
+            J.issued->store(true);
+            g->d2h_q.pop_front();
+        }
+    }
+    return true;
+}
+
 void feeder_main(Ing *g) {
     (void)hipSetDevice(g->device);
-    std::deque<hipEvent_t> inflight;
-    std::vector<hipEvent_t> free_ev(4, nullptr);
-    for (auto &e : free_ev)
-        if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) {
-            set_err(g, RCDC_ERR_INTERNAL, "feeder events");
-            return;
-        }
+    std::deque<hipEvent_t> inflight, inflight_o;
+    std::vector<hipEvent_t> free_ev(4, nullptr), free_o(4, nullptr);
+    for (auto *v : {&free_ev, &free_o})
+        for (auto &e : *v)
+            if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) {
+                set_err(g, RCDC_ERR_INTERNAL, "feeder events");
+                return;
+            }
     auto release = [&] {
         (void)hipStreamSynchronize(g->s_in);
+        (void)hipStreamSynchronize(g->s_out);
         for (auto e : inflight) free_ev.push_back(e);
+        for (auto e : inflight_o) free_o.push_back(e);
         for (auto e : free_ev) (void)hipEventDestroy(e);
+        for (auto e : free_o) (void)hipEventDestroy(e);
     };
     for (;;) {
         reap_inputs(g);
-        if (!submit_ready(g) || !pump_h2d(g, inflight, free_ev)) {
+        if (!submit_ready(g) || !pump_h2d(g, inflight, free_ev) || !pump_d2h(g, inflight_o, free_o)) {
             release();
             return;
         }
+        bool d2h_idle;
+        {
+            std::lock_guard<std::mutex> lq(g->d2h_mu);
+            d2h_idle = g->d2h_q.empty();
+        }
         std::unique_lock<std::mutex> lk(g->mu);
-        if (g->err || (g->front_done && g->h2d_q.empty())) {
+        // the back thread queues D2H jobs until the very end (finalize)
+        if (g->err || (g->finished && g->h2d_q.empty() && d2h_idle)) {
             lk.unlock();
             release();
             return;
         }
         // a piece is ~1.2 ms: poll often while copies are queued
-        g->cv_slot.wait_for(lk, std::chrono::microseconds(g->h2d_q.empty() ? 200 : 50));
+        g->cv_slot.wait_for(lk, std::chrono::microseconds(g->h2d_q.empty() && d2h_idle ? 200 : 50));
     }
 }
 
@@ -550,6 +644,7 @@ bool stage_a(Ing *g, Batch *B) {
         if (g->err) return false;
     }
     ING_HIP(g, hipStreamWaitEvent(g->s_comp, in->h2d, 0));
+    if (g->prof > 1) mark(g, B->index, now_s());
     // 2. chunk
     if (!P.plan) {
         ING_ST(g, rcdc_plan_create(g->ctx, offs.data(), lens.data(), nf, arena_len, &P.plan),
@@ -558,7 +653,12 @@ bool stage_a(Ing *g, Batch *B) {
         ING_ST(g, plan_relayout(P.plan, offs.data(), lens.data(), nf, arena_len, g->s_comp),
                "plan");
     }
+    if (g->prof > 1) mark(g, B->index, now_s());
     ING_ST(g, rcdc_plan_run(P.plan, P.arena, g->s_comp), "chunk");
+    if (g->prof > 1) {  // (RCDC_INGEST_PROF=2: the H2D's and the chunking's own ends)
+        (void)hipEventSynchronize(in->h2d);
+        mark(g, B->index, now_s());
+    }
     const uint64_t cap = (uint64_t)nf + used / 4096 + 16;  // min >= 4096 (rcdc_check_params)
     std::vector<uint64_t> cuts(std::max<uint64_t>(cap, 1)), counts(std::max<uint32_t>(nf, 1));
     rcdc_status rs = rcdc_plan_results(P.plan, cuts.data(), cuts.size(), counts.data());
@@ -774,7 +874,7 @@ bool stage_b(Ing *g, Batch *B, bool finalize) {
     PSlot &P = g->ps[B->pslot];
     const uint64_t n = B->c_len.size();
     mark(g, B->index, now_s());
-    ING_HIP(g, hipEventSynchronize(P.ev_ids));
+    ING_HIP(g, wait_event(P.ev_ids));
     ING_HIP(g, hipStreamWaitEvent(g->s_back, P.ev_sealed, 0));
     mark(g, B->index, now_s());
     const uint64_t ns = B->short_idx.size();
@@ -782,7 +882,8 @@ bool stage_b(Ing *g, Batch *B, bool finalize) {
         std::vector<uint8_t> dig(ns * 32);
         // on the ids' own stream (not the legacy default stream's queue)
         ING_HIP(g, hipMemcpyAsync(dig.data(), P.d_dig, ns * 32, hipMemcpyDeviceToHost, P.s_ids));
-        ING_HIP(g, hipStreamSynchronize(P.s_ids));
+        ING_HIP(g, hipEventRecord(P.ev_ids, P.s_ids));
+        ING_HIP(g, wait_event(P.ev_ids));
         for (uint64_t j = 0; j < ns; j++)
             memcpy(B->ids.data() + 32ull * B->short_idx[j], dig.data() + 32 * j, 32);
     }
@@ -865,9 +966,16 @@ bool stage_b(Ing *g, Batch *B, bool finalize) {
     const void *srcs[2] = {P.staging, g->carry[g->carry_cur] ? g->carry[g->carry_cur] : P.staging};
     std::vector<uint32_t> boffs(std::max<size_t>(open_from, 1));
     OutSlot *out = nullptr;
+    hipEvent_t d2h_fin = nullptr;
+    std::shared_ptr<std::atomic<bool>> d2h_flag;
     if (!grp.empty()) {
         if (!ensure_dev(g, &g->d_packs, &g->d_packs_cap, total + 64)) return false;
-        // the last pack build's D2H must be done with d_packs
+        // the last pack build's D2H must be done with d_packs (once the pump
+        // has enqueued it, ev_out marks its end)
+        if (g->last_d2h)
+            while (!g->last_d2h->load() && !g->err)
+                std::this_thread::sleep_for(std::chrono::microseconds(50));
+        if (g->err) return false;
         ING_HIP(g, hipStreamWaitEvent(g->s_back, g->ev_out, 0));
         ING_ST(g, rcdc_pack_build_raw_multi(g->ctx, g->cfg.key, srcs, 2, blobs.data(),
                                             (uint32_t)open_from, packs.data(),
@@ -896,12 +1004,19 @@ bool stage_b(Ing *g, Batch *B, bool finalize) {
             out->cap = total + total / 4;
             ING_HIP(g, hipHostMalloc((void **)&out->host, out->cap, hipHostMallocDefault));
         }
-        ING_HIP(g, hipEventRecord(g->ev_back, g->s_back));
-        ING_HIP(g, hipStreamWaitEvent(g->s_out, g->ev_back, 0));
-        // one copy: in pieces, the H2D and D2H pieces took turns on one DMA
-        // engine instead of running in both directions at once (r5j trace)
-        ING_HIP(g, hipMemcpyAsync(out->host, g->d_packs, total, hipMemcpyDeviceToHost, g->s_out));
-        ING_HIP(g, hipEventRecord(g->ev_out, g->s_out));
+        // the D2H goes to the feeder's pump, piece by piece, after the build
+        hipEvent_t after, fin;
+        ING_HIP(g, hipEventCreateWithFlags(&after, hipEventDisableTiming));
+        ING_HIP(g, hipEventCreateWithFlags(&fin, hipEventDisableTiming));
+        ING_HIP(g, hipEventRecord(after, g->s_back));
+        d2h_fin = fin;
+        d2h_flag = std::make_shared<std::atomic<bool>>(false);
+        {
+            std::lock_guard<std::mutex> lq(g->d2h_mu);
+            g->d2h_q.push_back({out->host, g->d_packs, total, 0, after, fin, d2h_flag, false});
+        }
+        g->last_d2h = d2h_flag;
+        g->cv_slot.notify_all();
     }
     // the still open pack: its blobs into the other carry buffer
     std::vector<rcdc_pack_blob> rest(blobs.begin() + open_from, blobs.end());
@@ -952,12 +1067,9 @@ bool stage_b(Ing *g, Batch *B, bool finalize) {
             g->st.packs += jobs.size();
             g->st.pack_bytes += total;
         }
-        hipEvent_t ev;
-        ING_HIP(g, hipEventCreateWithFlags(&ev, hipEventDisableTiming));
-        ING_HIP(g, hipEventRecord(ev, g->s_out));
         {
             std::lock_guard<std::mutex> lk(g->wait_mu);
-            g->wait_q.push_back({ev, std::move(jobs)});
+            g->wait_q.push_back({d2h_fin, d2h_flag, std::move(jobs)});
         }
         g->wait_cv.notify_one();
     }
@@ -1126,12 +1238,13 @@ rcdc_status rcdc_ingest_create(rcdc_ctx *ctx, const rcdc_ingest_config *cfg,
     g->file_cb = file_cb;
     g->user = user;
     g->device = ctx_device(ctx);
-    g->prof = getenv("RCDC_INGEST_PROF") != nullptr;
+    g->prof = getenv("RCDC_INGEST_PROF") ? std::max(atoi(getenv("RCDC_INGEST_PROF")), 1) : 0;
     g->level = cfg->zstd_level;
     g->compress = cfg->compress != 0;
     g->verify = cfg->extra_verify != 0;
     g->batch_cap = round_up(cfg->batch_bytes ? cfg->batch_bytes : (2ull << 30), 256);
     g->long_chunk = cfg->long_chunk ? cfg->long_chunk : (2ull << 20);
+    if (const char *e = getenv("RCDC_INGEST_KCOPY")) g->kcopy = (uint32_t)std::max(atoi(e), 0);
     if (const char *e = getenv("RCDC_INGEST_COPY_PIECE"))
         g->copy_piece = std::max<uint64_t>(strtoull(e, nullptr, 10), 1ull << 20);
     g->depth = cfg->depth ? cfg->depth : 4;
@@ -1173,7 +1286,14 @@ rcdc_status rcdc_ingest_create(rcdc_ctx *ctx, const rcdc_ingest_config *cfg,
     }
     g->ps.resize(g->depth);
     for (auto &P : g->ps) {
-        if ((e = hipStreamCreateWithFlags(&P.s_ids, hipStreamNonBlocking)) != hipSuccess ||
+        // the chunk-id kernel runs for up to ~60 ms (a 2 MiB chunk's
+        // SHA-256 chain on one lane): its stream gets the lowest priority, so
+        // HIP puts it on a hardware queue of its own class -- a stream that
+        // shared its queue waited behind it in order (r5o: each batch's
+        // chunking started only when the previous batch's ids were done)
+        int prio_lo = 0, prio_hi = 0;
+        (void)hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi);
+        if ((e = hipStreamCreateWithPriority(&P.s_ids, hipStreamNonBlocking, prio_lo)) != hipSuccess ||
             (e = hipEventCreateWithFlags(&P.ev_ids, hipEventDisableTiming)) != hipSuccess ||
             (e = hipEventCreateWithFlags(&P.ev_sealed, hipEventDisableTiming)) != hipSuccess ||
             (e = hipEventCreateWithFlags(&P.ev_retired, hipEventDisableTiming)) != hipSuccess)
@@ -1204,6 +1324,33 @@ rcdc_status rcdc_ingest_create(rcdc_ctx *ctx, const rcdc_ingest_config *cfg,
         if (rcdc_status ps = rcdc_plan_create(ctx, off0.data(), len0.data(), kPlanStreams,
                                               g->batch_cap + 256, &P.plan))
             return ps;
+        // ... and run once in that layout and in the one-stream layout (the
+        // walk path's buffers at full size; the arena's bytes do not matter):
+        // a plan's first run in a new layout allocated inside the pipeline,
+        // and each allocation's hipFree waited for every queued copy and
+        // kernel (r5u: 30-55 ms in each slot's first relayout)
+        {
+            std::vector<uint64_t> wc(g->batch_cap / 4096 + kPlanStreams + 16), wn(kPlanStreams);
+            if (rcdc_status ps = rcdc_plan_run(P.plan, P.arena, nullptr)) return ps;
+            if (rcdc_status ps = rcdc_plan_results(P.plan, wc.data(), wc.size(), wn.data());
+                ps && ps != RCDC_ERR_CAPACITY)
+                return ps;
+            for (uint32_t ns : {1u, 2u, 4u, 16u}) {  // walked layouts of 1-16 streams
+                std::vector<uint64_t> o(ns), l(ns);
+                const uint64_t each = (g->batch_cap / ns) & ~255ull;
+                for (uint32_t i = 0; i < ns; i++) {
+                    o[i] = i * each;
+                    l[i] = each;
+                }
+                if (rcdc_status ps = rcdc::plan_relayout(P.plan, o.data(), l.data(), ns,
+                                                         g->batch_cap + 256, nullptr))
+                    return ps;
+                if (rcdc_status ps = rcdc_plan_run(P.plan, P.arena, nullptr)) return ps;
+                if (rcdc_status ps = rcdc_plan_results(P.plan, wc.data(), wc.size(), wn.data());
+                    ps && ps != RCDC_ERR_CAPACITY)
+                    return ps;
+            }
+        }
         // short-chunk refs for a batch of minimum-size chunks
         P.refs_cap = g->batch_cap / std::max<uint64_t>(rcdc::ctx_min_size(ctx), 4096) * 2 + 1024;
         if ((e = hipHostMalloc((void **)&P.h_refs, P.refs_cap * 16, hipHostMallocDefault)) != hipSuccess ||

@@ -22,6 +22,7 @@
 #include <condition_variable>
 #include <deque>
 #include <mutex>
+#include <thread>
 #include <string>
 #include <vector>
 
@@ -409,6 +410,36 @@ rcdc_status null_leave(rcdc_ctx *ctx, const void *hip_stream, hipStream_t st) {
     return RCDC_OK;
 }
 
+// Waits of the library's own calls poll (hipEventQuery + a 50 us sleep)
+// instead of blocking in HIP: a thread blocked in hipStreamSynchronize /
+// hipEventSynchronize held up other threads' launches and copies (the
+// ingest engine's threads, r5r).  RCDC_POLL=0: blocking calls.
+static bool poll_mode() {
+    static const bool p = !(getenv("RCDC_POLL") && atoi(getenv("RCDC_POLL")) == 0);
+    return p;
+}
+
+hipError_t poll_event(hipEvent_t ev) {
+    if (!poll_mode()) return hipEventSynchronize(ev);
+    for (;;) {
+        const hipError_t e = hipEventQuery(ev);
+        if (e != hipErrorNotReady) return e;
+        std::this_thread::sleep_for(std::chrono::microseconds(50));
+    }
+}
+
+hipError_t poll_stream(hipStream_t st) {
+    if (!poll_mode()) return hipStreamSynchronize(st);
+    thread_local hipEvent_t ev = nullptr;
+    if (!ev) {
+        const hipError_t e = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
+        if (e != hipSuccess) return e;
+    }
+    const hipError_t e = hipEventRecord(ev, st);
+    if (e != hipSuccess) return e;
+    return poll_event(ev);
+}
+
 // Device buffer of at least `need` elements.  Grows with 25 % headroom: a
 // reallocation's hipFree synchronises the whole device (every lane of every
 // thread), so slowly varying sizes (stream passes of batch + tail bytes)
@@ -423,7 +454,10 @@ rcdc_status ensure_dev(T **p, uint64_t *cap, uint64_t need) {
     if (*p) HIP_TRY(hipFree(*p));
     *p = nullptr;
     *cap = 0;
-    const uint64_t n = std::max<uint64_t>(need + need / 4, 1);
+    // at least 64 KiB: small per-stream arrays (walk streams, piece cuts)
+    // otherwise regrew from 1-2 elements when a layout first had more of
+    // them, each regrow a device-wide sync inside a pipeline (r5u)
+    const uint64_t n = std::max<uint64_t>(need + need / 4, std::max<uint64_t>(65536 / sizeof(T), 1));
     HIP_TRY(hipMalloc((void **)p, n * sizeof(T)));
     *cap = n;
     return RCDC_OK;
@@ -1030,7 +1064,7 @@ rcdc_status plan_finish(rcdc_plan *pl) {
     if (!pl->ran) return fail(RCDC_ERR_INVALID_INPUT, "plan has not been run");
     if (pl->finished) return RCDC_OK;
     DeviceGuard g(pl->ctx->device);
-    HIP_TRY(hipEventSynchronize(pl->done));
+    HIP_TRY(poll_event(pl->done));
     std::vector<uint64_t> &cnt = pl->fin_counts;
     cnt.assign(pl->n, 0);
     // read-backs on the run's own stream, not hipMemcpy: the legacy default
@@ -1040,7 +1074,7 @@ rcdc_status plan_finish(rcdc_plan *pl) {
     if (pl->n) {
         HIP_TRY(hipMemcpyAsync(cnt.data(), pl->d_counts, pl->n * 8, hipMemcpyDeviceToHost,
                                pl->last_stream));
-        HIP_TRY(hipStreamSynchronize(pl->last_stream));
+        HIP_TRY(poll_stream(pl->last_stream));
     }
     if (const char *e = getenv("RCDC_WALK_DUMP"); e && !pl->wunits.empty()) {  // debugging aid
         const uint32_t want = (uint32_t)atoi(e);
@@ -1143,7 +1177,7 @@ rcdc_status plan_results(rcdc_plan *pl, uint64_t *cuts, uint64_t cap, uint64_t *
     if (pl->ncuts) {
         HIP_TRY(hipMemcpyAsync(all.data(), pl->d_cuts, pl->ncuts * 8, hipMemcpyDeviceToHost,
                                pl->last_stream));
-        HIP_TRY(hipStreamSynchronize(pl->last_stream));
+        HIP_TRY(poll_stream(pl->last_stream));
     }
     uint64_t o = 0;
     for (uint32_t i = 0; i < pl->n; i++) {
@@ -2256,13 +2290,13 @@ rcdc_status aead_launch(rcdc_ctx *ctx, bool open, const uint8_t key[64], std::ve
     // recorded on the context's stream waited behind whatever long kernel
     // shared that stream's hardware queue, r5l.)
     HIP_TRY(hipEventRecord(ctx->aead_done, st));
-    HIP_TRY(hipEventSynchronize(ctx->aead_done));
+    HIP_TRY(poll_event(ctx->aead_done));
     if (open && status) {
-        HIP_TRY(hipEventSynchronize(ctx->aead_done));
+        HIP_TRY(poll_event(ctx->aead_done));
         status->assign(nb, 0);
         if (nb) {  // on st (see plan_finish: not the legacy default stream)
             HIP_TRY(hipMemcpyAsync(status->data(), ctx->d_aead_status, nb * 4, hipMemcpyDeviceToHost, st));
-            HIP_TRY(hipStreamSynchronize(st));
+            HIP_TRY(poll_stream(st));
         }
     }
     return RCDC_OK;
@@ -2331,7 +2365,7 @@ rcdc_status copy_units_run(rcdc_ctx *ctx, const std::vector<uint64_t> &copies, v
     HIP_TRY(launch_copy_ranges((uint8_t *)d_out, ctx->d_copy_units, (uint32_t)nu,
                                (uint32_t)std::max(ctx->num_cus, 1), st));
     // the host vector dies with the caller's call
-    HIP_TRY(hipStreamSynchronize(st));
+    HIP_TRY(poll_stream(st));
     return RCDC_OK;
 }
 
@@ -2622,7 +2656,7 @@ rcdc_status zstd_compress(rcdc_ctx *ctx, int level, const void *d_in, const rcdc
     }
     HIP_TRY(hipMemcpyAsync(out_lens, ctx->d_zstd_lens, nbo * 8, hipMemcpyDeviceToHost, st));
     // the host descriptors die with this call
-    HIP_TRY(hipStreamSynchronize(st));
+    HIP_TRY(poll_stream(st));
     if (const char *e = getenv("RCDC_ZSTD_DBG"))
         if (atoi(e) & 4) zstd_prof_dump();
     return null_leave(ctx, hip_stream, st);
@@ -2670,7 +2704,7 @@ rcdc_status zstd_check(rcdc_ctx *ctx, const void *d_frames, const void *d_data,
                                          ctx->d_zck_refs, ctx->d_zck_blk0, n, ctx->d_zck_blks, nblk,
                                          ctx->d_zck_scratch, grid, ctx->d_zck_status, ctr, st));
         HIP_TRY(hipMemcpyAsync(status, ctx->d_zck_status, 4ull * n, hipMemcpyDeviceToHost, st));
-        HIP_TRY(hipStreamSynchronize(st));
+        HIP_TRY(poll_stream(st));
         for (uint32_t i = 0; i < n; i++)
             if (status[i] == 3u) order.push_back(i);
     } else {
@@ -2688,7 +2722,7 @@ rcdc_status zstd_check(rcdc_ctx *ctx, const void *d_frames, const void *d_data,
                                   ctx->d_zck_order, (uint32_t)order.size(), stored,
                                   ctx->d_zck_scratch, grid, ctx->d_zck_status, ctr, st));
         HIP_TRY(hipMemcpyAsync(status, ctx->d_zck_status, 4ull * n, hipMemcpyDeviceToHost, st));
-        HIP_TRY(hipStreamSynchronize(st));
+        HIP_TRY(poll_stream(st));
     }
     if (const char *e = getenv("RCDC_ZSTD_DBG"))
         if (atoi(e) & 8) zstd_check_prof_dump();

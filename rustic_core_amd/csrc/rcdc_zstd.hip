@@ -1204,13 +1204,80 @@ __global__ __launch_bounds__(256) void rcdc_zstd_far_build_kernel(
     for (uint32_t i = tid; i < kZstdFarTab; i += 256) dst[i] = t[i];
 }
 
+// One 16-byte group of far_map: every load of a round is independent of the
+// others in flight -- the group's bytes, then all sampled positions' b-1
+// buckets, then the misses' b-2 buckets, then one verification (the last
+// hit).  Returns the offset (0: none); *lng: its first 16 bytes agree.
+__device__ __forceinline__ uint32_t far_group(const uint8_t *bsrc, const uint8_t *src,
+                                              const uint8_t *lim, uint32_t start, uint32_t n,
+                                              uint32_t g, bool ok1, bool ok2, const uint32_t *t1,
+                                              const uint32_t *t2, bool *lng) {
+    const uint32_t p0 = g * 16u;
+    const uint4 a = ld16_lim(src + p0, lim), c = ld16_lim(src + p0 + 16u, lim);
+    const uint64_t u[4] = {(uint64_t)a.x | (uint64_t)a.y << 32, (uint64_t)a.z | (uint64_t)a.w << 32,
+                           (uint64_t)c.x | (uint64_t)c.y << 32, (uint64_t)c.z | (uint64_t)c.w << 32};
+    uint32_t bk[16], tg[16], e[16];
+    uint32_t smp = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < 16u; j++) {
+        const uint64_t hv = far_hash(bytes8_at(u, j));
+        bk[j] = far_bucket(hv);
+        tg[j] = far_tag(hv);
+        if (far_sampled(hv) && p0 + j + kZstdFarMin <= n) smp |= 1u << j;
+    }
+#pragma unroll
+    for (uint32_t j = 0; j < 16u; j++) e[j] = (ok1 && ((smp >> j) & 1u)) ? t1[bk[j]] : 0u;
+    uint32_t hit1 = 0, miss = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < 16u; j++) {
+        const bool h = e[j] && (e[j] & 0x7FFFu) == tg[j];
+        hit1 |= (h ? 1u : 0u) << j;
+        miss |= ((!h && ((smp >> j) & 1u)) ? 1u : 0u) << j;
+    }
+    uint32_t hit2 = 0;
+    if (ok2 && miss) {
+#pragma unroll
+        for (uint32_t j = 0; j < 16u; j++)
+            if ((miss >> j) & 1u) {
+                const uint32_t x = t2[bk[j]];
+                if (x && (x & 0x7FFFu) == tg[j]) {
+                    e[j] = x;
+                    hit2 |= 1u << j;
+                }
+            }
+    }
+    *lng = false;
+    if (!(hit1 | hit2)) return 0;
+    const uint32_t j = 31u - (uint32_t)__clz(hit1 | hit2);  // the last hit
+    uint32_t ej = 0;
+#pragma unroll
+    for (uint32_t i = 0; i < 16u; i++) ej = i == j ? e[i] : ej;
+    const uint32_t d = ((hit2 >> j) & 1u) ? 2u : 1u;
+    const uint32_t q = start - d * kZstdBlock + (ej >> 15) - 1u;  // blob-relative
+    // q + 8 is inside the blob (block b - d ends above it); the next 8
+    // bytes are read bounded by the blob's end
+    const uint64_t v = (uint64_t)ld4(bsrc + q) | (uint64_t)ld4(bsrc + q + 4) << 32;
+    if (v != bytes8_at(u, j)) return 0;
+    if (p0 + j + 16u <= n) {
+        const uint64_t w = (uint64_t)ld4_hi(bsrc + q + 8, lim) | (uint64_t)ld4_hi(bsrc + q + 12, lim) << 32;
+        *lng = w == bytes8_at(u, j + 8);
+    }
+    return start + p0 + j - q;
+}
+
 // far_map: a workgroup per block, a thread per 16-byte group: each sampled
 // position looks up the tables of blocks b-1 then b-2 (same blob), verifies
-// the 6 key bytes, and the group keeps the last verified offset.
+// the 8 key bytes, and the group keeps the last verified offset.  A probe of
+// 1/32 of the groups first counts the groups with an offset; below one in
+// `dense` the block skips the full map and the far path (data without far
+// repeats pays the probe only).  A finer gate was tried: counting only
+// 16-byte repeats excluded word text (whose far repeats do not pay: r5p,
+// 33.9 -> 27.1 GiB/s at an unchanged ratio) but CSV rows too, whose gain
+// comes from many 8-12 byte repeats (0.133 -> 0.198, r5q).
 __global__ __launch_bounds__(256) void rcdc_zstd_far_map_kernel(
     const uint8_t *__restrict__ in, const ZstdBlob *__restrict__ blobs,
-    const ZstdBlk *__restrict__ blks, uint32_t nblk, uint32_t *__restrict__ far) {
-    __shared__ uint32_t any;
+    const ZstdBlk *__restrict__ blks, uint32_t nblk, uint32_t *__restrict__ far, uint32_t dense) {
+    __shared__ uint32_t nlong;
     const uint32_t b = blockIdx.x, tid = threadIdx.x;
     const FarLayout L = far_layout(far, nblk);
     const ZstdBlk k = blks[b];
@@ -1221,77 +1288,36 @@ __global__ __launch_bounds__(256) void rcdc_zstd_far_map_kernel(
         if (tid == 0) L.has[b] = 0;
         return;
     }
-    if (tid == 0) any = 0;
+    if (tid == 0) nlong = 0;
     __syncthreads();
     const ZstdBlob B = blobs[k.blob];
     const uint8_t *bsrc = in + B.in_off;
     const uint8_t *src = bsrc + k.start;
     const uint8_t *lim = bsrc + B.len;
     const uint32_t n = k.len;
+    const uint32_t ng = (n + 15u) / 16u;
     const uint32_t *t1 = L.tab + (size_t)(b - (ok1 ? 1u : 0u)) * kZstdFarTab;
     const uint32_t *t2 = L.tab + (size_t)(b - (ok2 ? 2u : 0u)) * kZstdFarTab;
-    uint32_t *map = L.map + (size_t)b * kZstdFarGroups;
-    uint32_t found = 0;
-    for (uint32_t g = tid; g * 16u < n; g += 256) {
-        // every load of a round is independent of the others in flight: the
-        // group's bytes, then all sampled positions' b-1 buckets, then the
-        // misses' b-2 buckets, then one verification (the last hit)
-        const uint32_t p0 = g * 16u;
-        const uint4 a = ld16_lim(src + p0, lim), c = ld16_lim(src + p0 + 16u, lim);
-        const uint64_t u[4] = {(uint64_t)a.x | (uint64_t)a.y << 32, (uint64_t)a.z | (uint64_t)a.w << 32,
-                               (uint64_t)c.x | (uint64_t)c.y << 32, (uint64_t)c.z | (uint64_t)c.w << 32};
-        uint32_t bk[16], tg[16], e[16];
-        uint32_t smp = 0;
-#pragma unroll
-        for (uint32_t j = 0; j < 16u; j++) {
-            const uint64_t hv = far_hash(bytes8_at(u, j));
-            bk[j] = far_bucket(hv);
-            tg[j] = far_tag(hv);
-            if (far_sampled(hv) && p0 + j + kZstdFarMin <= n) smp |= 1u << j;
-        }
-#pragma unroll
-        for (uint32_t j = 0; j < 16u; j++) e[j] = (ok1 && ((smp >> j) & 1u)) ? t1[bk[j]] : 0u;
-        uint32_t hit1 = 0, miss = 0;
-#pragma unroll
-        for (uint32_t j = 0; j < 16u; j++) {
-            const bool h = e[j] && (e[j] & 0x7FFFu) == tg[j];
-            hit1 |= (h ? 1u : 0u) << j;
-            miss |= ((!h && ((smp >> j) & 1u)) ? 1u : 0u) << j;
-        }
-        uint32_t hit2 = 0;
-        if (ok2 && miss) {
-#pragma unroll
-            for (uint32_t j = 0; j < 16u; j++)
-                if ((miss >> j) & 1u) {
-                    const uint32_t x = t2[bk[j]];
-                    if (x && (x & 0x7FFFu) == tg[j]) {
-                        e[j] = x;
-                        hit2 |= 1u << j;
-                    }
-                }
-        }
-        uint32_t off = 0;
-        if (hit1 | hit2) {
-            const uint32_t j = 31u - (uint32_t)__clz(hit1 | hit2);  // the last hit
-            uint32_t ej = 0;
-#pragma unroll
-            for (uint32_t i = 0; i < 16u; i++) ej = i == j ? e[i] : ej;
-            const uint32_t d = ((hit2 >> j) & 1u) ? 2u : 1u;
-            const uint32_t q = k.start - d * kZstdBlock + (ej >> 15) - 1u;  // blob-relative
-            // q + 8 is inside the blob: block b - d ends above it
-            const uint64_t v = (uint64_t)ld4(bsrc + q) | (uint64_t)ld4(bsrc + q + 4) << 32;
-            if (v == bytes8_at(u, j)) off = k.start + p0 + j - q;
-        }
-        map[g] = off;
-        found += off != 0u;
+    // the probe: groups tid * 32 (256 of the block's 8192)
+    uint32_t np = 0;
+    for (uint32_t g = tid * 32u; g < ng; g += 256u * 32u) {
+        bool lng;
+        np += far_group(bsrc, src, lim, k.start, n, g, ok1, ok2, t1, t2, &lng) != 0u;
     }
-    if (found) atomicAdd(&any, found);
+    if (np) atomicAdd(&nlong, np);
+    const uint32_t nprobe = (ng + 31u) / 32u;
     __syncthreads();
-    // the far path only where the map is dense: on word text one group in
-    // many finds a far 8-byte repeat that rarely beats the block's own table,
-    // and every step of the parse would pay the map load for it (r5l: text
-    // 34.9 -> 27.2 GiB/s at an unchanged ratio)
-    if (tid == 0) L.has[b] = any * kZstdFarDense >= (n + 15u) / 16u;
+    const bool h = nlong * dense >= nprobe;
+    if (tid == 0) {
+        L.has[b] = h;
+        if (h) atomicAdd(&g_zstd_prof[7], 1ull);  // blocks on the far path (RCDC_ZSTD_DBG bit 2)
+    }
+    if (!h) return;
+    uint32_t *map = L.map + (size_t)b * kZstdFarGroups;
+    for (uint32_t g = tid; g < ng; g += 256) {
+        bool lng;
+        map[g] = far_group(bsrc, src, lim, k.start, n, g, ok1, ok2, t1, t2, &lng);
+    }
 }
 
 // res[b] = {type | rle byte << 8, content bytes}.  HL: hash table of 2^HL
@@ -1906,8 +1932,9 @@ void zstd_prof_dump() {
     unsigned long long h[8];
     if (hipMemcpyFromSymbol(h, HIP_SYMBOL(g_zstd_prof), sizeof h) != hipSuccess) return;
     fprintf(stderr, "rcdc zstd phases (wave-ms, 100 MHz clock): rle %.1f parse %.1f "
-            "literals+sequences %.1f (literals %.1f) tail %.1f; blocks %llu sequences %llu\n",
-            h[0] / 1e5, h[1] / 1e5, h[2] / 1e5, h[6] / 1e5, h[3] / 1e5, h[4], h[5]);
+            "literals+sequences %.1f (literals %.1f) tail %.1f; blocks %llu sequences %llu; "
+            "far-path blocks %llu\n",
+            h[0] / 1e5, h[1] / 1e5, h[2] / 1e5, h[6] / 1e5, h[3] / 1e5, h[4], h[5], h[7]);
     memset(h, 0, sizeof h);
     (void)hipMemcpyToSymbol(HIP_SYMBOL(g_zstd_prof), h, sizeof h);
 }
@@ -1975,8 +2002,11 @@ hipError_t launch_zstd(const uint8_t *in, uint8_t *out, const ZstdBlob *blobs, u
     if (far && nblk) {
         hipLaunchKernelGGL(rcdc_zstd_far_build_kernel, dim3(nblk), dim3(256), 0, stream, in, blobs,
                            blks, nblk, far);
+        static const uint32_t dense = getenv("RCDC_ZSTD_FARDENSE")
+                                          ? (uint32_t)std::max(atoi(getenv("RCDC_ZSTD_FARDENSE")), 1)
+                                          : kZstdFarDense;
         hipLaunchKernelGGL(rcdc_zstd_far_map_kernel, dim3(nblk), dim3(256), 0, stream, in, blobs,
-                           blks, nblk, far);
+                           blks, nblk, far, dense);
     }
     static const uint32_t dbg = getenv("RCDC_ZSTD_DBG") ? (uint32_t)atoi(getenv("RCDC_ZSTD_DBG")) : 0u;
     const uint32_t g = nblk < grid ? nblk : grid;

@@ -1290,6 +1290,35 @@ __global__ __launch_bounds__(256) void rcdc_copy_ranges_kernel(uint8_t *__restri
 
 namespace rcdc {
 
+// A plain copy by the shader, 16 bytes per lane per round, for a host <->
+// device transfer through page-locked memory the device maps (zero-copy
+// loads or stores over PCIe): the ingest's batch copies, so that HIP's DMA
+// queues stay free for the small uploads and read-backs that would wait
+// behind them (RCDC_INGEST_KCOPY).  len and both addresses 16-aligned.
+__global__ __launch_bounds__(256) void rcdc_stream_copy_kernel(uint4 *__restrict__ dst,
+                                                               const uint4 *__restrict__ src,
+                                                               uint64_t n16) {
+    const uint64_t stride = (uint64_t)gridDim.x * 256u * 4u;
+    for (uint64_t i = (uint64_t)blockIdx.x * 1024u + threadIdx.x; i < n16; i += stride) {
+        uint4 v[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++)
+            if (i + u * 256u < n16) v[u] = src[i + u * 256u];
+#pragma unroll
+        for (int u = 0; u < 4; u++)
+            if (i + u * 256u < n16) dst[i + u * 256u] = v[u];
+    }
+}
+
+hipError_t launch_stream_copy(void *dst, const void *src, uint64_t len, uint32_t blocks,
+                              hipStream_t stream) {
+    if (!len) return hipSuccess;
+    if (((uintptr_t)dst | (uintptr_t)src | len) & 15u) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(rcdc_stream_copy_kernel, dim3(blocks), dim3(256), 0, stream, (uint4 *)dst,
+                       (const uint4 *)src, len / 16u);
+    return hipGetLastError();
+}
+
 hipError_t launch_copy_ranges(uint8_t *out, const void *units, uint32_t n, uint32_t cus,
                               hipStream_t stream) {
     if (n == 0) return hipSuccess;

@@ -221,17 +221,19 @@ def _rows(kind, n):
 def test_structured_ratio(gpu_ctx):
     """Level 3 on structured rows: 16-bit tables of 2^12 positions keyed on 6
     bytes, the three last offsets tried at every position, the positions
-    inside taken matches left out of the table.
-    Frames decode to the data; the ratio is bounded near what the device
-    reached when this was written (CSV 0.19-0.20, code 0.11-0.12; round 3:
-    0.454 / 0.203), and level 9 is not larger."""
+    inside taken matches left out of the table, and
+    far candidates from the blob's two previous blocks (round 5: CSV rows
+    repeat 100-300 KiB back).  Frames decode to the data; the ratio is
+    bounded near what the device reached when this was written (CSV 0.13,
+    code 0.094; round 4: 0.198 / 0.105; round 3: 0.454 / 0.203), and level 9
+    is not larger."""
     datas = [_rows("csv", 4 * MiB), _rows("code", 4 * MiB)]
     fr = _compress(gpu_ctx, datas)
     _check(fr, datas)
     ratio = [len(f) / len(d) for f, d in zip(fr, datas)]
     ref = [len(zr.compress(d, 3)) / len(d) for d in datas]
     print("device / libzstd-3 ratio (csv, code):", list(zip(ratio, ref)))
-    assert ratio[0] < 0.215 and ratio[1] < 0.13
+    assert ratio[0] < 0.16 and ratio[1] < 0.11
     fr9 = _compress(gpu_ctx, datas, level=9)
     _check(fr9, datas)
     assert all(len(a) <= len(b) for a, b in zip(fr9, fr))
