@@ -1046,7 +1046,7 @@ def h2h_measure(args) -> dict:
     with tempfile.TemporaryDirectory(prefix="rcdc_h2h_", dir=tmp) as d:
         out = os.path.join(d, "h2h.json")
         r = subprocess.run([tool, "--dir", os.path.join(d, "files"), "--files", str(args.h2h_files),
-                            "--file-mib", "1024", "--readers", "8", "--json", out],
+                            "--file-mib", "1024", "--json", out],
                            capture_output=True, text=True, timeout=600)
         if r.returncode not in (0, 3) or not os.path.exists(out):
             return {"error": f"ingest_e2e rc {r.returncode}: {r.stderr[-500:]}"}

@@ -222,10 +222,10 @@ int main(int argc, char **argv) {
     const std::string dir = arg(argc, argv, "--dir", "/tmp/rcdc_ingest_files");
     const int nfiles = atoi(arg(argc, argv, "--files", "32"));
     const uint64_t fsize = (uint64_t)atoll(arg(argc, argv, "--file-mib", "1024")) << 20;
-    const int readers = atoi(arg(argc, argv, "--readers", "8"));
+    const int readers = atoi(arg(argc, argv, "--readers", "6"));
     const uint64_t batch = (uint64_t)atoll(arg(argc, argv, "--batch-mib", "2048")) << 20;
     const int depth = atoi(arg(argc, argv, "--depth", "4"));
-    const int threads = atoi(arg(argc, argv, "--hash-threads", "10"));
+    const int threads = atoi(arg(argc, argv, "--hash-threads", "14"));
     const int in_slots = atoi(arg(argc, argv, "--in-slots", "4"));
     const int reps = atoi(arg(argc, argv, "--reps", "2"));
     const char *json = arg(argc, argv, "--json", nullptr);
