@@ -176,7 +176,7 @@ struct OutSlot {
 
 struct PackJob {
     OutSlot *out = nullptr;
-    uint64_t off = 0, size = 0, seq = 0;
+    uint64_t off = 0, size = 0, seq = 0, batch = 0;
     uint32_t header_len = 0;
     std::vector<rcdc_ingest_blob> blobs;
     uint8_t id[32];
@@ -257,6 +257,7 @@ struct rcdc_ingest {
     struct WaitItem {
         hipEvent_t ev;
         std::shared_ptr<std::atomic<bool>> issued;
+        uint64_t batch;
         std::vector<std::shared_ptr<PackJob>> jobs;
     };
     std::deque<WaitItem> wait_q;
@@ -273,6 +274,7 @@ struct rcdc_ingest {
     // start, ids wait end, end), printed by rcdc_ingest_finish
     int prof = 0;
     std::vector<std::vector<double>> tl;
+    std::vector<double> tl_d2h, tl_ids;  // per batch: packs landed, last pack id
 };
 
 namespace {
@@ -374,6 +376,10 @@ void deliver(Ing *g, const std::shared_ptr<PackJob> &pj) {
     {
         std::lock_guard<std::mutex> lk(g->cb_mu);
         if (g->pack_cb) g->pack_cb(g->user, &p);
+        if (g->prof) {
+            if (g->tl_ids.size() <= pj->batch) g->tl_ids.resize(pj->batch + 1, 0);
+            g->tl_ids[pj->batch] = std::max(g->tl_ids[pj->batch], now_s() - g->t_first);
+        }
     }
     if (--pj->out->packs_left == 0) {
         std::lock_guard<std::mutex> lk(g->mu);
@@ -439,13 +445,23 @@ void waiter_main(Ing *g) {
             continue;
         }
         (void)hipEventDestroy(w.ev);
+        if (g->prof) {
+            std::lock_guard<std::mutex> lk(g->cb_mu);
+            if (g->tl_d2h.size() <= w.batch) g->tl_d2h.resize(w.batch + 1, 0);
+            g->tl_d2h[w.batch] = now_s() - g->t_first;
+        }
         bool is_last;
         {
             std::lock_guard<std::mutex> lk(g->mu);
-            // the last three batches (every batch after rcdc_ingest_finish
+            // the last four batches (every batch after rcdc_ingest_finish
             // was too many: throughput, r5v2; the last one alone left ~100 ms
-            // of multi-buffer jobs after the last copy, r5u3)
+            // of multi-buffer jobs after the last copy, r5u3).  Once the
+            // caller has called finish, the batch count is known: a 16-pack
+            // call takes ~115 ms, so a batch landing before the last stage A
+            // (front_done) still counts as one of the last.
             is_last = g->front_done && g->inflight.size() <= 2;
+            if (!is_last && g->finishing && g->ready.size() + g->nbatches <= w.batch + 4)
+                is_last = true;
         }
         hash_packs(g, std::move(w.jobs), is_last);
     }
@@ -1052,6 +1068,7 @@ bool stage_b(Ing *g, Batch *B, bool finalize) {
             pj->size = packs[j].size;
             pj->header_len = packs[j].header_len;
             pj->seq = g->next_seq++;
+            pj->batch = B->index;
             for (uint32_t i = grp[j].first; i < grp[j].first + grp[j].second; i++) {
                 rcdc_ingest_blob e{};
                 memcpy(e.id, blobs[i].id, 32);
@@ -1072,7 +1089,7 @@ bool stage_b(Ing *g, Batch *B, bool finalize) {
         }
         {
             std::lock_guard<std::mutex> lk(g->wait_mu);
-            g->wait_q.push_back({d2h_fin, d2h_flag, std::move(jobs)});
+            g->wait_q.push_back({d2h_fin, d2h_flag, B->index, std::move(jobs)});
         }
         g->wait_cv.notify_one();
     }
@@ -1501,6 +1518,10 @@ rcdc_status rcdc_ingest_finish(rcdc_ingest *g, rcdc_ingest_stats *stats) {
             for (size_t b = 0; b < g->tl.size(); b++) {
                 fprintf(stderr, "ingest batch %zu:", b);
                 for (double t : g->tl[b]) fprintf(stderr, " %.1f", t * 1e3);
+                if (b < g->tl_d2h.size() && g->tl_d2h[b] > 0)
+                    fprintf(stderr, " | landed %.1f", g->tl_d2h[b] * 1e3);
+                if (b < g->tl_ids.size() && g->tl_ids[b] > 0)
+                    fprintf(stderr, " ids %.1f", g->tl_ids[b] * 1e3);
                 fprintf(stderr, " ms\n");
             }
             fprintf(stderr, "ingest end %.1f ms\n", g->st.seconds * 1e3);
