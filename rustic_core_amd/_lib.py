@@ -32,6 +32,7 @@ EXPORTS = (
     "rcdc_ingest_config_default", "rcdc_ingest_create", "rcdc_ingest_add_index",
     "rcdc_ingest_reserve", "rcdc_ingest_commit", "rcdc_ingest_add", "rcdc_ingest_flush",
     "rcdc_ingest_finish", "rcdc_ingest_destroy", "rcdc_sha256_host_one",
+    "rcdc_sha256_host_ni",
 )
 ABI_VERSION = 4
 
@@ -202,6 +203,8 @@ def lib() -> ctypes.CDLL:
     L.rcdc_ingest_destroy.argtypes = [vp]
     L.rcdc_sha256_host_one.restype = st
     L.rcdc_sha256_host_one.argtypes = [vp, u64, vp]
+    L.rcdc_sha256_host_ni.restype = st
+    L.rcdc_sha256_host_ni.argtypes = [vp, vp, u32, u32, vp]
     L.rcdc_plan_window.restype = st
     L.rcdc_plan_window.argtypes = [vp, u32, u64, u32, vp, vp]
     L.rcdc_plan_device_digests.restype = st

@@ -203,37 +203,70 @@ RCDC_AVX512 static void sha256_many_avx512(const uint8_t *const *ptrs, const uin
 // W[t] for t >= 16 from the previous four groups, FIPS 180-4 6.2.2 step 1).
 #define RCDC_SHANI __attribute__((target("sha,sse4.1,ssse3")))
 
-RCDC_SHANI void sha256_ni_blocks(uint32_t st[8], const uint8_t *p, uint64_t nblk) {
+// K messages interleaved on one core: sha256rnds2 is a long-latency
+// instruction and one message's rounds form a single dependency chain, so
+// one stream of them leaves the unit idle most cycles.  K independent chains
+// fill those cycles: more bytes per second per core at the same latency per
+// message (the tail of a backup, where the last packs' ids are on the
+// critical path and every thread is busy).
+template <int K>
+RCDC_SHANI void sha256_ni_blocks_k(uint32_t *const *st, const uint8_t *const *pp, uint64_t nblk) {
     const __m128i bswap = _mm_set_epi64x(0x0c0d0e0f08090a0bULL, 0x0405060700010203ULL);
-    __m128i t = _mm_shuffle_epi32(_mm_loadu_si128((const __m128i *)&st[0]), 0xB1);  // CDAB
-    __m128i s1 = _mm_shuffle_epi32(_mm_loadu_si128((const __m128i *)&st[4]), 0x1B); // EFGH
-    __m128i s0 = _mm_alignr_epi8(t, s1, 8);                                          // ABEF
-    s1 = _mm_blend_epi16(s1, t, 0xF0);                                               // CDGH
-    for (; nblk; nblk--, p += 64) {
-        const __m128i a0 = s0, c0 = s1;
-        __m128i w[4];
-        for (int j = 0; j < 16; j++) {
-            if (j < 4)
-                w[j] = _mm_shuffle_epi8(_mm_loadu_si128((const __m128i *)(p + 16 * j)), bswap);
-            else
-                w[j & 3] = _mm_sha256msg2_epu32(
-                    _mm_add_epi32(_mm_sha256msg1_epu32(w[j & 3], w[(j - 3) & 3]),
-                                  _mm_alignr_epi8(w[(j - 1) & 3], w[(j - 2) & 3], 4)),
-                    w[(j - 1) & 3]);
-            __m128i m = _mm_add_epi32(w[j & 3], _mm_load_si128((const __m128i *)&kK256[4 * j]));
-            s1 = _mm_sha256rnds2_epu32(s1, s0, m);
-            m = _mm_shuffle_epi32(m, 0x0E);
-            s0 = _mm_sha256rnds2_epu32(s0, s1, m);
-        }
-        s0 = _mm_add_epi32(s0, a0);
-        s1 = _mm_add_epi32(s1, c0);
+    __m128i s0[K], s1[K];
+    const uint8_t *p[K];
+#pragma GCC unroll 4
+    for (int k = 0; k < K; k++) {
+        const __m128i t = _mm_shuffle_epi32(_mm_loadu_si128((const __m128i *)&st[k][0]), 0xB1);  // CDAB
+        const __m128i u = _mm_shuffle_epi32(_mm_loadu_si128((const __m128i *)&st[k][4]), 0x1B);  // EFGH
+        s0[k] = _mm_alignr_epi8(t, u, 8);      // ABEF
+        s1[k] = _mm_blend_epi16(u, t, 0xF0);   // CDGH
+        p[k] = pp[k];
     }
-    t = _mm_shuffle_epi32(s0, 0x1B);           // FEBA
-    s1 = _mm_shuffle_epi32(s1, 0xB1);          // DCHG
-    s0 = _mm_blend_epi16(t, s1, 0xF0);         // DCBA
-    s1 = _mm_alignr_epi8(s1, t, 8);            // HGFE
-    _mm_storeu_si128((__m128i *)&st[0], s0);
-    _mm_storeu_si128((__m128i *)&st[4], s1);
+    for (; nblk; nblk--) {
+        __m128i a0[K], c0[K], w[K][4];
+#pragma GCC unroll 4
+        for (int k = 0; k < K; k++) {
+            a0[k] = s0[k];
+            c0[k] = s1[k];
+        }
+#pragma GCC unroll 16
+        for (int j = 0; j < 16; j++) {
+            const __m128i kk = _mm_load_si128((const __m128i *)&kK256[4 * j]);
+#pragma GCC unroll 4
+            for (int k = 0; k < K; k++) {
+                if (j < 4)
+                    w[k][j] = _mm_shuffle_epi8(_mm_loadu_si128((const __m128i *)(p[k] + 16 * j)), bswap);
+                else
+                    w[k][j & 3] = _mm_sha256msg2_epu32(
+                        _mm_add_epi32(_mm_sha256msg1_epu32(w[k][j & 3], w[k][(j - 3) & 3]),
+                                      _mm_alignr_epi8(w[k][(j - 1) & 3], w[k][(j - 2) & 3], 4)),
+                        w[k][(j - 1) & 3]);
+                __m128i m = _mm_add_epi32(w[k][j & 3], kk);
+                s1[k] = _mm_sha256rnds2_epu32(s1[k], s0[k], m);
+                m = _mm_shuffle_epi32(m, 0x0E);
+                s0[k] = _mm_sha256rnds2_epu32(s0[k], s1[k], m);
+            }
+        }
+#pragma GCC unroll 4
+        for (int k = 0; k < K; k++) {
+            s0[k] = _mm_add_epi32(s0[k], a0[k]);
+            s1[k] = _mm_add_epi32(s1[k], c0[k]);
+            p[k] += 64;
+        }
+    }
+#pragma GCC unroll 4
+    for (int k = 0; k < K; k++) {
+        const __m128i t = _mm_shuffle_epi32(s0[k], 0x1B);  // FEBA
+        const __m128i u = _mm_shuffle_epi32(s1[k], 0xB1);  // DCHG
+        _mm_storeu_si128((__m128i *)&st[k][0], _mm_blend_epi16(t, u, 0xF0));  // DCBA
+        _mm_storeu_si128((__m128i *)&st[k][4], _mm_alignr_epi8(u, t, 8));     // HGFE
+    }
+}
+
+RCDC_SHANI void sha256_ni_blocks(uint32_t st[8], const uint8_t *p, uint64_t nblk) {
+    uint32_t *s[1] = {st};
+    const uint8_t *q[1] = {p};
+    sha256_ni_blocks_k<1>(s, q, nblk);
 }
 
 // Portable fallback (no SHA extensions): FIPS 180-4 rounds, one block.
@@ -305,6 +338,57 @@ void host_sha256_one(const uint8_t *p, uint64_t len, uint8_t out[32]) {
         out[4 * w + 1] = (uint8_t)(st[w] >> 16);
         out[4 * w + 2] = (uint8_t)(st[w] >> 8);
         out[4 * w + 3] = (uint8_t)st[w];
+    }
+}
+
+
+// The SHA-256 of n host messages on the SHA extensions, up to `ways` (1-4)
+// interleaved on this thread: the blocks all messages of a group share run
+// together, then each message's remaining blocks and padding alone.  Without
+// SHA-NI: one message at a time.
+void host_sha256_ni_many(const uint8_t *const *ptrs, const uint64_t *lens, uint32_t n,
+                         uint8_t *digests, int ways) {
+    ways = ways < 1 ? 1 : ways > 4 ? 4 : ways;
+    if (!host_sha_ni()) ways = 1;
+    for (uint32_t a = 0; a < n; a += (uint32_t)ways) {
+        const int k = (int)(n - a < (uint32_t)ways ? n - a : (uint32_t)ways);
+        if (k == 1) {
+            host_sha256_one(ptrs[a], lens[a], digests + 32ull * a);
+            continue;
+        }
+        uint32_t st[4][8];
+        uint32_t *sp[4];
+        const uint8_t *pp[4];
+        uint64_t common = ~0ull;
+        for (int i = 0; i < k; i++) {
+            memcpy(st[i], kH0, sizeof st[i]);
+            sp[i] = st[i];
+            pp[i] = ptrs[a + i];
+            common = lens[a + i] / 64 < common ? lens[a + i] / 64 : common;
+        }
+        if (k == 2) sha256_ni_blocks_k<2>(sp, pp, common);
+        else if (k == 3) sha256_ni_blocks_k<3>(sp, pp, common);
+        else sha256_ni_blocks_k<4>(sp, pp, common);
+        for (int i = 0; i < k; i++) {
+            const uint8_t *p = ptrs[a + i];
+            const uint64_t len = lens[a + i], full = len / 64;
+            sha256_ni_blocks(st[i], p + common * 64, full - common);
+            uint8_t tail[128] = {0};
+            const uint64_t r = len - full * 64;
+            memcpy(tail, p + full * 64, r);
+            tail[r] = 0x80;
+            const uint64_t nt = r + 9 <= 64 ? 1 : 2;
+            const uint64_t bits = len * 8;
+            for (int b = 0; b < 8; b++) tail[nt * 64 - 1 - b] = (uint8_t)(bits >> (8 * b));
+            sha256_ni_blocks(st[i], tail, nt);
+            uint8_t *out = digests + 32ull * (a + i);
+            for (int w = 0; w < 8; w++) {
+                out[4 * w] = (uint8_t)(st[i][w] >> 24);
+                out[4 * w + 1] = (uint8_t)(st[i][w] >> 16);
+                out[4 * w + 2] = (uint8_t)(st[i][w] >> 8);
+                out[4 * w + 3] = (uint8_t)st[i][w];
+            }
+        }
     }
 }
 

@@ -60,6 +60,8 @@ rcdc_status set_error(rcdc_status st, const char *msg);
 void host_sha256_many(const uint8_t *const *ptrs, const uint64_t *lens, uint32_t n,
                       uint8_t *digests);
 void host_sha256_one(const uint8_t *p, uint64_t len, uint8_t out[32]);
+void host_sha256_ni_many(const uint8_t *const *ptrs, const uint64_t *lens, uint32_t n,
+                         uint8_t *digests, int ways);
 hipError_t launch_stream_copy(void *dst, const void *src, uint64_t len, uint32_t blocks,
                               hipStream_t stream);
 bool host_sha_supported();
@@ -398,11 +400,28 @@ void deliver(Ing *g, const std::shared_ptr<PackJob> &pj) {
 void hash_packs(Ing *g, std::vector<std::shared_ptr<PackJob>> packs, bool last) {
     const bool mb = host_sha_supported() && !last;
     if (!mb) {
-        for (auto &pj : packs)
-            post(g, [g, pj] {
-                host_sha256_one(pj->out->host + pj->off, pj->size, pj->id);
-                deliver(g, pj);
+        // `ways` packs per job, interleaved on the SHA extensions (RCDC_SHANI_WAYS)
+        static const int ways = getenv("RCDC_SHANI_WAYS") ? atoi(getenv("RCDC_SHANI_WAYS")) : 2;
+        const size_t per = (size_t)std::max(1, std::min(4, ways));
+        for (size_t a = 0; a < packs.size(); a += per) {
+            std::vector<std::shared_ptr<PackJob>> grp(
+                packs.begin() + a, packs.begin() + std::min(a + per, packs.size()));
+            post(g, [g, grp] {
+                std::vector<const uint8_t *> ptrs;
+                std::vector<uint64_t> lens;
+                std::vector<uint8_t> dig(32 * grp.size());
+                for (auto &pj : grp) {
+                    ptrs.push_back(pj->out->host + pj->off);
+                    lens.push_back(pj->size);
+                }
+                host_sha256_ni_many(ptrs.data(), lens.data(), (uint32_t)grp.size(), dig.data(),
+                                    (int)grp.size());
+                for (size_t i = 0; i < grp.size(); i++) {
+                    memcpy(grp[i]->id, dig.data() + 32 * i, 32);
+                    deliver(g, grp[i]);
+                }
             });
+        }
         return;
     }
     for (size_t a = 0; a < packs.size(); a += 16) {
@@ -711,15 +730,20 @@ bool stage_a(Ing *g, Batch *B) {
     B->ids.assign(nchunks * 32, 0);
     // 3. ids: short chunks on the device (own stream per pipeline slot), long
     // ones on host threads from the input slot
-    // The last batch's ids bound the run's end: its longest device chain
-    // (~34 MB/s per lane: 62 ms for a 2 MiB chunk) would outlast everything
-    // else, so the host takes its chunks above 1 MiB too and both sides end
-    // together (~30 ms).
+    // The last batches' ids bound the run's end: a batch's longest device
+    // chain (~34 MB/s per lane: 62 ms for a 2 MiB chunk) holds its stage B,
+    // and stage B runs in batch order, so the host takes the chunks above
+    // 1 MiB of the last RCDC_INGEST_TAIL_BATCHES (default 2) batches too and
+    // both sides end together (~30 ms).  (The last batch alone: the one
+    // before it still waited ~40 ms for its device ids, r5y.)
+    static const size_t tail_batches =
+        getenv("RCDC_INGEST_TAIL_BATCHES") ? (size_t)atoi(getenv("RCDC_INGEST_TAIL_BATCHES")) : 2;
     bool tail;
     {
         std::lock_guard<std::mutex> lk(g->mu);
-        tail = g->finishing && g->ready.empty() && g->open == nullptr && g->submitted.empty() &&
-               g->submitting == 0;
+        const size_t after = g->ready.size() + g->submitted.size() + (size_t)g->submitting +
+                             (g->open != nullptr ? 1 : 0);
+        tail = g->finishing && after < tail_batches;
     }
     const uint64_t long_thr = tail ? std::min<uint64_t>(g->long_chunk, 1ull << 20) : g->long_chunk;
     std::vector<uint32_t> long_idx;
@@ -1590,6 +1614,17 @@ void rcdc_ingest_destroy(rcdc_ingest *g) {
 rcdc_status rcdc_sha256_host_one(const void *data, uint64_t len, uint8_t *digest) {
     if ((len && !data) || !digest) return set_error(RCDC_ERR_INVALID_INPUT, "null argument");
     host_sha256_one((const uint8_t *)data, len, digest);
+    return RCDC_OK;
+}
+
+rcdc_status rcdc_sha256_host_ni(const void *const *ptrs, const uint64_t *lens, uint32_t n,
+                                uint32_t ways, uint8_t *digests) {
+    if (n && (!ptrs || !lens || !digests)) return set_error(RCDC_ERR_INVALID_INPUT, "null argument");
+    for (uint32_t i = 0; i < n; i++)
+        if (!ptrs[i] && lens[i]) return set_error(RCDC_ERR_INVALID_INPUT, "null buffer");
+    if (ways < 1 || ways > 4) return set_error(RCDC_ERR_INVALID_INPUT, "ways must be 1-4");
+    host_sha256_ni_many(reinterpret_cast<const uint8_t *const *>(ptrs), lens, n, digests,
+                        (int)ways);
     return RCDC_OK;
 }
 

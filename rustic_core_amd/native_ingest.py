@@ -177,3 +177,18 @@ def sha256_host_one(data) -> bytes:
     if st:
         raise status_error(st, _lib.last_error())
     return bytes(out)
+
+
+def sha256_host_ni(bufs, ways: int = 2) -> list:
+    """rcdc_sha256_host_ni: SHA-256 of several host buffers, `ways` of them
+    interleaved on the SHA extensions of the calling thread."""
+    arrs = [np.ascontiguousarray(np.frombuffer(b, np.uint8)) for b in bufs]  # no copy
+    n = len(arrs)
+    ptrs = (ctypes.c_void_p * max(n, 1))(*[a.ctypes.data if a.size else None for a in arrs])
+    lens = (ctypes.c_uint64 * max(n, 1))(*[a.size for a in arrs])
+    out = (u8 * (32 * max(n, 1)))()
+    st = _lib.lib().rcdc_sha256_host_ni(ptrs, lens, n, ways, out)
+    if st:
+        raise status_error(st, _lib.last_error())
+    raw = bytes(out)
+    return [raw[32 * i:32 * i + 32] for i in range(n)]

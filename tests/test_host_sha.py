@@ -68,3 +68,27 @@ def test_sha256_host_one_scalar_rounds():
     r = subprocess.run([sys.executable, "-c", code], cwd=root, capture_output=True, text=True,
                        env=dict(os.environ, RCDC_NO_SHANI="1"), timeout=120)
     assert r.returncode == 0, r.stderr[-2000:]
+
+
+@pytest.mark.parametrize("ways", [1, 2, 3, 4])
+def test_sha256_host_ni_interleaved(ways):
+    """rcdc_sha256_host_ni: `ways` messages interleaved on the SHA extensions
+    (the ingest's last pack ids).  Unequal lengths in a group (the shared
+    blocks run interleaved, the rest alone), every padding edge, and counts
+    that do not fill the last group."""
+    from rustic_core_amd.native_ingest import sha256_host_ni
+    rng = np.random.default_rng(11 + ways)
+    lens = _ONE_LENS + [int(x) for x in rng.integers(0, 300000, 9)]
+    bufs = [rng.integers(0, 256, n, dtype=np.uint8).tobytes() for n in lens]
+    assert sha256_host_ni(bufs, ways) == [hashlib.sha256(b).digest() for b in bufs]
+    assert sha256_host_ni(bufs[:ways + 1], ways) == [hashlib.sha256(b).digest()
+                                                     for b in bufs[:ways + 1]]
+
+
+def test_sha256_host_ni_rejects():
+    from rustic_core_amd.errors import RusticError
+    from rustic_core_amd.native_ingest import sha256_host_ni
+    assert sha256_host_ni([], 2) == []
+    for ways in (0, 5):
+        with pytest.raises(RusticError):
+            sha256_host_ni([b"abc"], ways)

@@ -34,4 +34,16 @@ for t in [int(x) for x in (sys.argv[1:] or ["1", "8", "14", "16"])]:
             list(pool.map(one, groups))
             el = time.perf_counter() - t0
         out[f"multibuffer_gbs_{t}_threads"] = round(len(groups) * 16 * size / el / 1e9, 2)
+    from rustic_core_amd.native_ingest import sha256_host_ni  # noqa: E402
+    for ways in (1, 2, 3, 4):  # SHA extensions, `ways` buffers interleaved per call
+        groups = [bufs[i:i + ways] for i in range(0, n_buf, ways)]
+        groups = groups[:max(t, len(groups) * t // 16)] if t < 16 else groups
+
+        def ni(g, ways=ways):
+            return sha256_host_ni([memoryview(b) for b in g], ways)
+        with ThreadPoolExecutor(t) as pool:
+            t0 = time.perf_counter()
+            list(pool.map(ni, groups))
+            el = time.perf_counter() - t0
+        out[f"shani_x{ways}_gbs_{t}_threads"] = round(sum(len(g) for g in groups) * size / el / 1e9, 2)
 print(json.dumps(out))

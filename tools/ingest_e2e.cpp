@@ -253,9 +253,10 @@ int main(int argc, char **argv) {
                     uint64_t o = 0;
                     while (o < fsize) {
                         const ssize_t r = write(fd, buf.data() + o, fsize - o);
-                        if (r <= 0) {
-                            perror("write");
-                            exit(1);
+                        if (r <= 0) {  // e.g. the disk is full: end at once (no
+                            perror("write");  // destructors racing the other threads)
+                            fflush(stderr);
+                            _exit(1);
                         }
                         o += (uint64_t)r;
                     }
