@@ -100,8 +100,9 @@ def parse():
                     help="pipelined plans: the last timed run's chain stays narrow (A/B)")
     ap.add_argument("--no-h2h", action="store_true",
                     help="C3 at N=1: skip the host-to-host object (tools/ingest_e2e)")
-    ap.add_argument("--h2h-files", type=int, default=16,
-                    help="files of 1 GiB for the host-to-host object")
+    ap.add_argument("--h2h-files", type=int, default=64,
+                    help="files of 1 GiB for the host-to-host object (fewer if the disk under "
+                         "TMPDIR cannot hold them)")
     ap.add_argument("--ingest-streams", type=int, default=64)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-parity", action="store_true")
@@ -1037,20 +1038,28 @@ def h2h_measure(args) -> dict:
     packs on the GPU -> pack files and pack ids in host memory; beside it the
     concurrent PCIe bound of the same bytes (file_archiver.rs:144-160,
     packer.rs:826-836).  A child process (its own HIP context)."""
+    import shutil
     import subprocess
     import tempfile
     tool = os.path.join(ROOT, "tools", "ingest_e2e")
     if not os.path.exists(tool):
         return {"skipped": "tools/ingest_e2e not built"}
     tmp = os.environ.get("TMPDIR", "/tmp")
+    # the files must fit the disk under TMPDIR (4 GiB to spare)
+    files = args.h2h_files
+    fit = int((shutil.disk_usage(tmp).free - (4 << 30)) // (1 << 30))
+    if fit < files:
+        files = max(min(fit, files), 4)
     with tempfile.TemporaryDirectory(prefix="rcdc_h2h_", dir=tmp) as d:
         out = os.path.join(d, "h2h.json")
-        r = subprocess.run([tool, "--dir", os.path.join(d, "files"), "--files", str(args.h2h_files),
+        r = subprocess.run([tool, "--dir", os.path.join(d, "files"), "--files", str(files),
                             "--file-mib", "1024", "--json", out],
                            capture_output=True, text=True, timeout=600)
         if r.returncode not in (0, 3) or not os.path.exists(out):
             return {"error": f"ingest_e2e rc {r.returncode}: {r.stderr[-500:]}"}
         res = json.loads(open(out).read())
+    if files != args.h2h_files:
+        res["files_reduced_for_disk"] = {"asked": args.h2h_files, "ran": files}
     res["log"] = r.stderr.strip().splitlines()[-4:]
     return res
 

@@ -65,6 +65,7 @@ void host_sha256_ni_many(const uint8_t *const *ptrs, const uint64_t *lens, uint3
 hipError_t launch_stream_copy(void *dst, const void *src, uint64_t len, uint32_t blocks,
                               hipStream_t stream);
 bool host_sha_supported();
+bool host_sha_ni();
 }  // namespace rcdc
 
 using namespace rcdc;
@@ -394,40 +395,52 @@ void deliver(Ing *g, const std::shared_ptr<PackJob> &pj) {
     }
 }
 
-// After a batch's packs are in host memory: their ids.  16 packs per call in
-// AVX-512 lanes (throughput); the last batch's packs one per job on the SHA
-// extensions (latency: ~20 ms per 40 MB pack instead of ~130 ms in a lane).
+// Host SHA-256 for pack ids and long chunk ids (RCDC_INGEST_SHA): "ni" (the
+// default on CPUs with the SHA extensions) runs `ways` messages interleaved
+// per call on one core; "mb" 16 per call in AVX-512 lanes.  On the box's
+// cores (r5z, 32 MiB messages, profiles/r05/host_sha_rate.json) SHA-NI gives
+// 2.44 / 3.51 / 3.88 / 4.30 GB/s per core at 1 / 2 / 3 / 4 ways and the
+// multi-buffer form 4.73: 4 ways match the lanes' throughput at a quarter of
+// their latency per message (a 40 MB pack: ~37 ms instead of ~130 ms), and
+// the latency of the last batches' ids is the end of the run.
+struct ShaPolicy {
+    bool mb;
+    int ways, ways_last;
+};
+const ShaPolicy &sha_policy() {
+    static const ShaPolicy p = [] {
+        ShaPolicy q{};
+        const char *m = getenv("RCDC_INGEST_SHA");
+        q.mb = host_sha_supported() && (!host_sha_ni() || (m && strcmp(m, "mb") == 0));
+        const char *w = getenv("RCDC_SHANI_WAYS"), *wl = getenv("RCDC_SHANI_WAYS_LAST");
+        q.ways = std::max(1, std::min(4, w ? atoi(w) : 4));
+        q.ways_last = std::max(1, std::min(4, wl ? atoi(wl) : 2));
+        return q;
+    }();
+    return p;
+}
+
+// SHA-256 of n host messages (one job's group).
+void hash_group(const uint8_t *const *ptrs, const uint64_t *lens, uint32_t n, uint8_t *dig,
+                bool mb) {
+    if (mb)
+        host_sha256_many(ptrs, lens, n, dig);
+    else
+        host_sha256_ni_many(ptrs, lens, n, dig, (int)n);
+}
+
+// After a batch's packs are in host memory: their ids, in groups of `ways`
+// interleaved on the SHA extensions (fewer for the last batches, whose ids
+// end the run), or 16 per call in AVX-512 lanes ("mb"; the last batches then
+// on the SHA extensions).
 void hash_packs(Ing *g, std::vector<std::shared_ptr<PackJob>> packs, bool last) {
-    const bool mb = host_sha_supported() && !last;
-    if (!mb) {
-        // `ways` packs per job, interleaved on the SHA extensions (RCDC_SHANI_WAYS)
-        static const int ways = getenv("RCDC_SHANI_WAYS") ? atoi(getenv("RCDC_SHANI_WAYS")) : 2;
-        const size_t per = (size_t)std::max(1, std::min(4, ways));
-        for (size_t a = 0; a < packs.size(); a += per) {
-            std::vector<std::shared_ptr<PackJob>> grp(
-                packs.begin() + a, packs.begin() + std::min(a + per, packs.size()));
-            post(g, [g, grp] {
-                std::vector<const uint8_t *> ptrs;
-                std::vector<uint64_t> lens;
-                std::vector<uint8_t> dig(32 * grp.size());
-                for (auto &pj : grp) {
-                    ptrs.push_back(pj->out->host + pj->off);
-                    lens.push_back(pj->size);
-                }
-                host_sha256_ni_many(ptrs.data(), lens.data(), (uint32_t)grp.size(), dig.data(),
-                                    (int)grp.size());
-                for (size_t i = 0; i < grp.size(); i++) {
-                    memcpy(grp[i]->id, dig.data() + 32 * i, 32);
-                    deliver(g, grp[i]);
-                }
-            });
-        }
-        return;
-    }
-    for (size_t a = 0; a < packs.size(); a += 16) {
+    const ShaPolicy &pol = sha_policy();
+    const bool mb = pol.mb && !last;
+    const size_t per = mb ? 16 : (size_t)(last ? pol.ways_last : pol.ways);
+    for (size_t a = 0; a < packs.size(); a += per) {
         std::vector<std::shared_ptr<PackJob>> grp(packs.begin() + a,
-                                                  packs.begin() + std::min(a + 16, packs.size()));
-        post(g, [g, grp] {
+                                                  packs.begin() + std::min(a + per, packs.size()));
+        post(g, [g, grp, mb] {
             std::vector<const uint8_t *> ptrs;
             std::vector<uint64_t> lens;
             std::vector<uint8_t> dig(32 * grp.size());
@@ -435,7 +448,7 @@ void hash_packs(Ing *g, std::vector<std::shared_ptr<PackJob>> packs, bool last) 
                 ptrs.push_back(pj->out->host + pj->off);
                 lens.push_back(pj->size);
             }
-            host_sha256_many(ptrs.data(), lens.data(), (uint32_t)grp.size(), dig.data());
+            hash_group(ptrs.data(), lens.data(), (uint32_t)grp.size(), dig.data(), mb);
             for (size_t i = 0; i < grp.size(); i++) {
                 memcpy(grp[i]->id, dig.data() + 32 * i, 32);
                 deliver(g, grp[i]);
@@ -777,12 +790,13 @@ bool stage_a(Ing *g, Batch *B) {
                "chunk ids");
     }
     ING_HIP(g, hipEventRecord(P.ev_ids, P.s_ids));
-    // long ids: groups of up to 16 similar lengths per multi-buffer call
+    // long ids: groups of similar lengths (longest first), `ways` per call on
+    // the SHA extensions or 16 per multi-buffer call (sha_policy)
     std::sort(long_idx.begin(), long_idx.end(),
               [&](uint32_t a, uint32_t b) { return B->c_len[a] > B->c_len[b]; });
     Batch *bp = B;
-    const bool mb = host_sha_supported();
-    const size_t per = mb ? 16 : 1;
+    const bool mb = sha_policy().mb;
+    const size_t per = mb ? 16 : (size_t)sha_policy().ways;
     for (size_t a = 0; a < long_idx.size(); a += per) {
         std::vector<uint32_t> grp(long_idx.begin() + a,
                                   long_idx.begin() + std::min(a + per, long_idx.size()));
@@ -796,10 +810,7 @@ bool stage_a(Ing *g, Batch *B) {
                 ptrs.push_back(in->host + bp->c_off[k]);
                 ls.push_back(bp->c_len[k]);
             }
-            if (mb)
-                host_sha256_many(ptrs.data(), ls.data(), (uint32_t)grp.size(), dig.data());
-            else
-                host_sha256_one(ptrs[0], ls[0], dig.data());
+            hash_group(ptrs.data(), ls.data(), (uint32_t)grp.size(), dig.data(), mb);
             for (size_t i = 0; i < grp.size(); i++)
                 memcpy(bp->ids.data() + 32ull * grp[i], dig.data() + 32 * i, 32);
             in->host_jobs--;

@@ -87,6 +87,7 @@ hipError_t launch_zstd(const uint8_t *in, uint8_t *out, const ZstdBlob *blobs, u
                        hipStream_t stream);
 uint64_t zstd_check_scratch_bytes(uint32_t grid);
 uint64_t zstd_blkdesc_bytes();
+uint32_t zstd_check_waves_per_cu();
 hipError_t launch_zstd_check_blocks(const uint8_t *frames, const uint8_t *data, const void *refs,
                                     const uint64_t *blk0, uint32_t n, void *blks, uint64_t nblk,
                                     uint8_t *scratch, uint32_t grid, uint32_t *status,
@@ -2679,8 +2680,8 @@ rcdc_status zstd_check(rcdc_ctx *ctx, const void *d_frames, const void *d_data,
     hipStream_t st;
     rcdc_status rs;
     if ((rs = null_enter(ctx, hip_stream, &st))) return rs;
-    // 12 waves per CU (the block kernel's registers allow 3 per SIMD)
-    const uint32_t grid = (uint32_t)std::max(ctx->num_cus, 1) * 12u;
+    // resident waves per CU (12 or 16, by the registers' budget)
+    const uint32_t grid = (uint32_t)std::max(ctx->num_cus, 1) * zstd_check_waves_per_cu();
     if ((rs = ensure_dev(&ctx->d_zck_refs, &ctx->cap_zck_refs, 4ull * n))) return rs;
     if ((rs = ensure_dev(&ctx->d_zck_order, &ctx->cap_zck_order, (uint64_t)n + 16))) return rs;
     if ((rs = ensure_dev(&ctx->d_zck_status, &ctx->cap_zck_status, n))) return rs;

@@ -76,19 +76,31 @@ struct HufD {
     uint8_t sym, nb;
 };
 
-// LDS of one wave (workgroup = one wave)
+// LDS of one wave (workgroup = one wave).  The Huffman tables live only
+// through a block's literals section (its literals are decoded to scratch
+// memory) and the LL / ML extras only through its sequences section, so the
+// two share bytes: 9984 B per wave, 16 waves per CU by LDS (14464 B and 11
+// waves before).  A treeless literals section rebuilds the Huffman table from
+// the weights kept in w.
 struct DecLds {
     FseD ll[512], ml[512], of[256];
-    // per LL / ML state: the code's baseline | extra bits << 24 (as zstd's
-    // ZSTD_seqSymbol), so a sequence's lengths need one LDS read each and no
-    // dependent constant-table lookup
-    uint32_t llx[512], mlx[512];
-    FseD hw[64];  // FSE table of Huffman weights (log <= 6)
-    HufD huf[2048];
-    int16_t norm[64];
-    uint16_t nxt[256];
-    uint8_t w[256];  // Huffman weights
+    union {
+        struct {
+            FseD hw[64];  // FSE table of Huffman weights (log <= 6)
+            HufD huf[2048];
+        } h;
+        // per LL / ML state: the code's baseline | extra bits << 24 (as
+        // zstd's ZSTD_seqSymbol), so a sequence's lengths need one LDS read
+        // each and no dependent constant-table lookup
+        struct {
+            uint32_t llx[512], mlx[512];
+        } x;
+    } u;
+    int16_t norm[64];  // (read_ncount's capacity: kNormCap)
+    uint16_t nxt[64];  // per symbol: <= 53 (ML), <= 64 by kNormCap
+    uint8_t w[256];    // Huffman weights (kept for treeless literals)
 };
+constexpr uint32_t kNormCap = 64;
 
 __device__ __forceinline__ uint32_t highbit32(uint32_t v) { return 31u - (uint32_t)__clz(v); }
 
@@ -289,7 +301,7 @@ __device__ int read_ncount(const uint8_t *p, int64_t avail, uint32_t max_sym, ui
             }
             n0 += bs & 3;
             bitpos += 2;
-            if (n0 > max_sym + 1) return -1;
+            if (n0 > max_sym + 1 || n0 > kNormCap) return -1;
             while (s < n0) norm[s++] = 0;
             if (s > max_sym) break;
             bs = rd32(bitpos);
@@ -306,6 +318,7 @@ __device__ int read_ncount(const uint8_t *p, int64_t avail, uint32_t max_sym, ui
         }
         count--;
         remaining -= count < 0 ? -count : count;
+        if (s >= kNormCap) return -1;  // (a symbol this table cannot have)
         norm[s++] = (int16_t)count;
         prev0 = count == 0;
         while (remaining < threshold) {
@@ -378,6 +391,7 @@ struct Dec {
     uint32_t rep[3];
     uint32_t rep_unk;     // bit i: rep[i] unknown (a block checked out of order)
     uint32_t huf_log;     // 0: no Huffman table yet
+    uint32_t huf_nw;      // its weights in L.w[0 .. huf_nw)
     uint32_t al_ll, al_ml, al_of;  // 255: no table yet
     uint32_t bad;         // status
     bool block_mode;      // earlier blocks' state unknown: using it -> kCkSeq
@@ -450,30 +464,30 @@ __device__ int read_huf_weights(const uint8_t *p, int64_t avail, DecLds &L, uint
         const int nc = read_ncount(p + 1, hb, 255, 6, L.norm, &nsym, &al);
         if (nc < 0) return -1;
         wsync();
-        if (!build_fse(L.hw, L.norm, nsym, al, L.nxt, lane)) return -1;
+        if (!build_fse(L.u.h.hw, L.norm, nsym, al, L.nxt, lane)) return -1;
         BRev r;
         if (!brev_init(r, p + 1 + nc, (int64_t)hb - nc)) return -1;
         uint32_t s1 = (uint32_t)brev_bits(r, al), s2 = (uint32_t)brev_bits(r, al);
         for (;;) {
             if (n >= 255) return -1;
-            FseD e = L.hw[s1];
+            FseD e = L.u.h.hw[s1];
             if (lane == 0) L.w[n] = e.sym;
             n++;
             s1 = e.next + (uint32_t)brev_bits(r, e.nb);
             if (r.pos < 0) {
                 if (n >= 255) return -1;
-                if (lane == 0) L.w[n] = L.hw[s2].sym;
+                if (lane == 0) L.w[n] = L.u.h.hw[s2].sym;
                 n++;
                 break;
             }
             if (n >= 255) return -1;
-            e = L.hw[s2];
+            e = L.u.h.hw[s2];
             if (lane == 0) L.w[n] = e.sym;
             n++;
             s2 = e.next + (uint32_t)brev_bits(r, e.nb);
             if (r.pos < 0) {
                 if (n >= 255) return -1;
-                if (lane == 0) L.w[n] = L.hw[s1].sym;
+                if (lane == 0) L.w[n] = L.u.h.hw[s1].sym;
                 n++;
                 break;
             }
@@ -523,8 +537,8 @@ __device__ uint32_t build_huf(DecLds &L, uint32_t nw, uint32_t lane) {
         const uint32_t len = 1u << (wi - 1), b = start[wi];
         start[wi] += len;
         for (uint32_t k = lane; k < len; k += 64) {
-            L.huf[b + k].sym = (uint8_t)s;
-            L.huf[b + k].nb = (uint8_t)(tl + 1 - wi);
+            L.u.h.huf[b + k].sym = (uint8_t)s;
+            L.u.h.huf[b + k].nb = (uint8_t)(tl + 1 - wi);
         }
     }
     wsync();
@@ -540,7 +554,7 @@ __device__ bool huf_stream(const DecLds &L, uint32_t tl, const uint8_t *p, int64
     uint32_t i = 0;
     // four symbols per dword store once aligned
     while (i < n && ((uintptr_t)(out + i) & 3u)) {
-        const HufD e = L.huf[brq_peek(r, tl)];
+        const HufD e = L.u.h.huf[brq_peek(r, tl)];
         out[i++] = e.sym;
         r.pos -= e.nb;
     }
@@ -548,14 +562,14 @@ __device__ bool huf_stream(const DecLds &L, uint32_t tl, const uint8_t *p, int64
         uint32_t v = 0;
 #pragma unroll
         for (int k = 0; k < 4; k++) {
-            const HufD e = L.huf[brq_peek(r, tl)];
+            const HufD e = L.u.h.huf[brq_peek(r, tl)];
             v |= (uint32_t)e.sym << (8 * k);
             r.pos -= e.nb;
         }
         *reinterpret_cast<uint32_t *>(out + i) = v;
     }
     for (; i < n; i++) {
-        const HufD e = L.huf[brq_peek(r, tl)];
+        const HufD e = L.u.h.huf[brq_peek(r, tl)];
         out[i] = e.sym;
         r.pos -= e.nb;
     }
@@ -633,11 +647,14 @@ __device__ void check_compressed(Dec &D, DecLds &L, const uint8_t *p, uint32_t b
             const int tu = read_huf_weights(cs, clen, L, &nw, lane);
             if (tu < 0) { D.bad = kCkCorrupt; return; }
             D.huf_log = build_huf(L, nw, lane);
+            D.huf_nw = nw;
             cs += tu;
             clen -= tu;
         } else if (D.huf_log == 0) {  // treeless: the previous block's table
             D.bad = D.block_mode ? kCkSeq : kCkCorrupt;
             return;
+        } else {  // its weights: the table's bytes held LL / ML extras since
+            build_huf(L, D.huf_nw, lane);
         }
         const uint32_t tl = D.huf_log;
         bool ok = true;
@@ -729,11 +746,11 @@ __device__ void check_compressed(Dec &D, DecLds &L, const uint8_t *p, uint32_t b
         }
         for (uint32_t u = lane; u < (1u << D.al_ll); u += 64) {
             const uint32_t c = L.ll[u].sym < 36 ? L.ll[u].sym : 0u;
-            L.llx[u] = kLLBase[c] | (uint32_t)kLLBits[c] << 24;
+            L.u.x.llx[u] = kLLBase[c] | (uint32_t)kLLBits[c] << 24;
         }
         for (uint32_t u = lane; u < (1u << D.al_ml); u += 64) {
             const uint32_t c = L.ml[u].sym < 53 ? L.ml[u].sym : 0u;
-            L.mlx[u] = kMLBase[c] | (uint32_t)kMLBits[c] << 24;
+            L.u.x.mlx[u] = kMLBase[c] | (uint32_t)kMLBits[c] << 24;
         }
         wsync();
         BRevQ r;
@@ -772,7 +789,7 @@ __device__ void check_compressed(Dec &D, DecLds &L, const uint8_t *p, uint32_t b
                 const uint32_t eo = rfl(reinterpret_cast<const uint32_t *>(L.of)[sof]);
                 const uint32_t el = rfl(reinterpret_cast<const uint32_t *>(L.ll)[sll]);
                 const uint32_t em = rfl(reinterpret_cast<const uint32_t *>(L.ml)[sml]);
-                const uint32_t xl = rfl(L.llx[sll]), xm = rfl(L.mlx[sml]);
+                const uint32_t xl = rfl(L.u.x.llx[sll]), xm = rfl(L.u.x.mlx[sml]);
                 const uint32_t ofc = eo & 0xFFu, llc = el & 0xFFu, mlc = em & 0xFFu;
                 if (ofc > 31 || llc > 35 || mlc > 52) err = true;
                 const uint64_t ofv = (1ull << ofc) + brq_bits<true>(r, ofc);
@@ -978,7 +995,8 @@ __device__ uint32_t check_frame(const uint8_t *f, uint64_t flen, const uint8_t *
 // refs: frame_off, frame_len, data_off, data_len (rcdc_zstd_check_ref);
 // order: the queue order; ctr: the queue counter (zeroed by the host).
 // OCC: waves per SIMD the registers are budgeted for (2: no spills, 3: more
-// waves in flight; RCDC_ZCK_OCC picks, A/B)
+// waves in flight, 4: 128 VGPRs, the 16 waves per CU the LDS now allows;
+// RCDC_ZCK_OCC picks, A/B)
 template <int OCC>
 __global__ __launch_bounds__(64, OCC) void rcdc_zstd_check_kernel(
     const uint8_t *__restrict__ frames, const uint8_t *__restrict__ data,
@@ -1156,12 +1174,19 @@ void zstd_check_prof_dump() {
 
 uint64_t zstd_blkdesc_bytes() { return sizeof(BlkDesc); }
 
+// Resident check waves per CU the grid is sized for: 16 when the registers
+// are budgeted for 4 per SIMD, else 12 (3 per SIMD: the block kernel's ~150
+// VGPRs).
+uint32_t zstd_check_waves_per_cu() { return zck_occ() == 4 ? 16u : 12u; }
+
 hipError_t launch_zstd_check(const uint8_t *frames, const uint8_t *data, const void *refs,
                              const uint32_t *order, uint32_t n, bool stored, uint8_t *scratch,
                              uint32_t grid, uint32_t *status, uint32_t *ctr, hipStream_t stream) {
     if (n == 0) return hipSuccess;
     const uint32_t g = n < grid ? n : grid;
-    hipLaunchKernelGGL(zck_occ() == 3 ? rcdc_zstd_check_kernel<3> : rcdc_zstd_check_kernel<2>,
+    hipLaunchKernelGGL(zck_occ() == 4   ? rcdc_zstd_check_kernel<4>
+                       : zck_occ() == 3 ? rcdc_zstd_check_kernel<3>
+                                        : rcdc_zstd_check_kernel<2>,
                        dim3(g), dim3(64), 0, stream, frames, data,
                        (const ulonglong4 *)refs, order, n, stored ? 1u : 0u, scratch, status, ctr,
                        zck_dbg());
@@ -1178,8 +1203,9 @@ hipError_t launch_zstd_check_blocks(const uint8_t *frames, const uint8_t *data, 
                        (const ulonglong4 *)refs, blk0, n, (BlkDesc *)blks, status);
     const uint32_t g = nblk < grid ? (uint32_t)nblk : grid;
     if (g)
-        hipLaunchKernelGGL(zck_occ() == 3 ? rcdc_zstd_block_check_kernel<3>
-                                          : rcdc_zstd_block_check_kernel<2>,
+        hipLaunchKernelGGL(zck_occ() == 4   ? rcdc_zstd_block_check_kernel<4>
+                           : zck_occ() == 3 ? rcdc_zstd_block_check_kernel<3>
+                                            : rcdc_zstd_block_check_kernel<2>,
                            dim3(g), dim3(64), 0, stream, frames, data,
                            (const ulonglong4 *)refs, (const BlkDesc *)blks, nblk, scratch, status,
                            ctr, zck_dbg());
