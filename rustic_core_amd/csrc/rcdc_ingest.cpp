@@ -254,7 +254,9 @@ struct rcdc_ingest {
     std::vector<std::thread> pool;
     std::mutex pool_mu;
     std::condition_variable pool_cv;
-    std::deque<std::function<void()>> jobs;
+    std::deque<std::function<void()>> jobs;   // pack ids, in order
+    std::deque<std::function<void()>> ujobs;  // long chunk ids (urgent), in order
+    uint32_t running_packs = 0;               // pack-id jobs running
     std::mutex wait_mu;
     std::condition_variable wait_cv;
     struct WaitItem {
@@ -328,27 +330,53 @@ bool ensure_dev(Ing *g, T **p, uint64_t *cap, uint64_t need) {
 }
 
 // Host SHA-256 jobs; `urgent` ones (the long chunks' ids, which gate a
-// batch's stage B) go before the pack ids.
+// batch's stage B) go before the pack ids, in the order posted (longest
+// first).  Pack-id jobs hold a thread for tens of ms (4 packs of ~40 MB), so
+// RCDC_INGEST_ID_THREADS (default 2) threads never take one: a long-id job
+// then starts at once instead of after the running pack jobs (r5z2: the last
+// batches' stage B waited ~14 ms for a free thread).
 void post(Ing *g, std::function<void()> fn, bool urgent = false) {
     {
         std::lock_guard<std::mutex> lk(g->pool_mu);
-        if (urgent) g->jobs.push_front(std::move(fn));
-        else g->jobs.push_back(std::move(fn));
+        (urgent ? g->ujobs : g->jobs).push_back(std::move(fn));
     }
-    g->pool_cv.notify_one();
+    if (urgent) g->pool_cv.notify_all();  // (a thread free for ids may be
+    else g->pool_cv.notify_one();         //  among the waiters)
 }
 
 void pool_main(Ing *g) {
+    static const uint32_t reserve =
+        getenv("RCDC_INGEST_ID_THREADS") ? (uint32_t)atoi(getenv("RCDC_INGEST_ID_THREADS")) : 2u;
+    const uint32_t pack_cap = g->nthreads > reserve ? g->nthreads - reserve : 1u;
     for (;;) {
         std::function<void()> fn;
+        bool pack = false;
         {
             std::unique_lock<std::mutex> lk(g->pool_mu);
-            g->pool_cv.wait(lk, [&] { return g->stop || !g->jobs.empty(); });
-            if (g->jobs.empty()) return;
-            fn = std::move(g->jobs.front());
-            g->jobs.pop_front();
+            g->pool_cv.wait(lk, [&] {
+                return g->stop || !g->ujobs.empty() ||
+                       (!g->jobs.empty() && g->running_packs < pack_cap);
+            });
+            if (!g->ujobs.empty()) {
+                fn = std::move(g->ujobs.front());
+                g->ujobs.pop_front();
+            } else if (!g->jobs.empty() && g->running_packs < pack_cap) {
+                fn = std::move(g->jobs.front());
+                g->jobs.pop_front();
+                pack = true;
+                g->running_packs++;
+            } else {
+                return;  // stop, nothing left this thread may take
+            }
         }
         fn();
+        if (pack) {
+            {
+                std::lock_guard<std::mutex> lk(g->pool_mu);
+                g->running_packs--;
+            }
+            g->pool_cv.notify_all();
+        }
     }
 }
 
