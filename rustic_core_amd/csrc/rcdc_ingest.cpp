@@ -346,7 +346,7 @@ void post(Ing *g, std::function<void()> fn, bool urgent = false) {
 
 void pool_main(Ing *g) {
     static const uint32_t reserve =
-        getenv("RCDC_INGEST_ID_THREADS") ? (uint32_t)atoi(getenv("RCDC_INGEST_ID_THREADS")) : 2u;
+        getenv("RCDC_INGEST_ID_THREADS") ? (uint32_t)atoi(getenv("RCDC_INGEST_ID_THREADS")) : 0u;
     const uint32_t pack_cap = g->nthreads > reserve ? g->nthreads - reserve : 1u;
     for (;;) {
         std::function<void()> fn;

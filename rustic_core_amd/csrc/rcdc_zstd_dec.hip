@@ -396,6 +396,7 @@ struct Dec {
     uint32_t bad;         // status
     bool block_mode;      // earlier blocks' state unknown: using it -> kCkSeq
     bool prof;            // RCDC_ZSTD_DBG bit 3: phase clocks into g_zck_prof
+    bool narrow;          // RCDC_ZSTD_DBG bit 4: 4-byte compare steps only (A/B)
 };
 
 // ---- comparisons (the whole wave) -----------------------------------------
@@ -417,11 +418,31 @@ __device__ bool wave_cmp(const uint8_t *a, const uint8_t *b, uint32_t v, int kin
     return __builtin_amdgcn_ballot_w64(!ok) == 0;
 }
 
-// one lane's comparison (kinds as wave_cmp)
-__device__ bool lane_cmp(const uint8_t *a, const uint8_t *b, uint32_t v, int kind, uint32_t n) {
+// 16 bytes at any alignment from the 4-5 aligned dwords that hold them.
+__device__ __forceinline__ uint4 ld16u(const uint8_t *p) {
+    const uint32_t b = (uint32_t)(uintptr_t)p & 3u, sh = b * 8u;
+    const uint32_t *w = (const uint32_t *)(p - b);
+    const uint32_t w0 = w[0], w1 = w[1], w2 = w[2], w3 = w[3], w4 = w[b ? 4 : 3];
+    return make_uint4(__builtin_amdgcn_alignbit(w1, w0, sh), __builtin_amdgcn_alignbit(w2, w1, sh),
+                      __builtin_amdgcn_alignbit(w3, w2, sh), __builtin_amdgcn_alignbit(w4, w3, sh));
+}
+
+// one lane's comparison (kinds as wave_cmp).  16 bytes a step while 16 fit
+// (a step's loads stay inside the dwords of [a, a + n), as ld4u's), then 4:
+// a lane compares a whole sequence, and the batch waits for its longest, so
+// the steps are memory round trips in a chain (text: many sequences of a few
+// dozen bytes)
+__device__ bool lane_cmp(const uint8_t *a, const uint8_t *b, uint32_t v, int kind, uint32_t n,
+                         bool narrow = false) {
     const uint32_t rep4 = v * 0x01010101u;
     uint32_t acc = 0;
-    for (uint32_t o = 0; o < n; o += 4) {
+    uint32_t o = 0;
+    for (; !narrow && o + 16 <= n; o += 16) {
+        const uint4 x = ld16u(a + o);
+        const uint4 y = kind == 1 ? make_uint4(rep4, rep4, rep4, rep4) : ld16u(b + o);
+        acc |= (x.x ^ y.x) | (x.y ^ y.y) | (x.z ^ y.z) | (x.w ^ y.w);
+    }
+    for (; o < n; o += 4) {
         const uint32_t x = ld4u(a + o);
         const uint32_t y = kind == 1 ? rep4 : ld4u(b + o);
         uint32_t d = x ^ y;
@@ -762,6 +783,7 @@ __device__ void check_compressed(Dec &D, DecLds &L, const uint8_t *p, uint32_t b
         uint32_t r0 = D.rep[0], r1 = D.rep[1], r2 = D.rep[2];
         bool u0 = D.rep_unk & 1u, u1 = (D.rep_unk >> 1) & 1u, u2 = (D.rep_unk >> 2) & 1u;
         bool unk_used = false;
+        uint64_t tcmp = 0;  // (phase clocks: the batches' placement + comparisons)
         for (uint32_t s0 = 0; s0 < nseq; s0 += 64) {
             const uint32_t nb = min(64u, nseq - s0);
             uint32_t myll = 0, myml = 0, myoff = 0;
@@ -851,6 +873,7 @@ __device__ void check_compressed(Dec &D, DecLds &L, const uint8_t *p, uint32_t b
             }
             if (unk_used) { D.bad = kCkSeq; return; }  // (block mode only)
             if (err || r.pos < 0) { D.bad = kCkCorrupt; return; }
+            const uint64_t tc0 = D.prof ? wall_clock64() : 0;
             // place the batch: exclusive prefix sums of ll and ll + ml
             uint64_t incl_l = myll, incl_o = (uint64_t)myll + myml;
             for (uint32_t d = 1; d < 64; d <<= 1) {
@@ -874,8 +897,8 @@ __device__ void check_compressed(Dec &D, DecLds &L, const uint8_t *p, uint32_t b
             bool eq = true;
             if (mine && !lng) {
                 const uint8_t *dst = D.data + op;
-                eq = lane_cmp(dst, lits + lp, lit_byte, lkind, myll) &&
-                     lane_cmp(dst + myll, dst + myll - myoff, 0, 2, myml);
+                eq = lane_cmp(dst, lits + lp, lit_byte, lkind, myll, D.narrow) &&
+                     lane_cmp(dst + myll, dst + myll - myoff, 0, 2, myml, D.narrow);
             }
             uint64_t longs = __builtin_amdgcn_ballot_w64(lng);
             while (longs) {
@@ -890,6 +913,7 @@ __device__ void check_compressed(Dec &D, DecLds &L, const uint8_t *p, uint32_t b
                 if (lane == (uint32_t)L0) eq = e1 && e2;
             }
             if (__builtin_amdgcn_ballot_w64(!eq)) { D.bad = kCkMismatch; return; }
+            if (D.prof) tcmp += wall_clock64() - tc0;
             litpos += tot_l;
             D.out += tot_o;
         }
@@ -897,6 +921,7 @@ __device__ void check_compressed(Dec &D, DecLds &L, const uint8_t *p, uint32_t b
         if (D.prof && lane == 0) {
             atomicAdd(&g_zck_prof[1], wall_clock64() - t1);
             atomicAdd(&g_zck_prof[4], (unsigned long long)nseq);
+            atomicAdd(&g_zck_prof[6], tcmp);
         }
         D.rep[0] = r0;
         D.rep[1] = r1;
@@ -959,6 +984,7 @@ __device__ uint32_t check_frame(const uint8_t *f, uint64_t flen, const uint8_t *
     D.bad = kCkOk;
     D.block_mode = false;
     D.prof = prof;
+    D.narrow = false;
     for (;;) {
         if (q + 3 > end) return kCkCorrupt;
         const uint32_t bh = q[0] | (q[1] << 8) | ((uint32_t)q[2] << 16);
@@ -1140,6 +1166,7 @@ __global__ __launch_bounds__(64, OCC) void rcdc_zstd_block_check_kernel(
             D.bad = kCkOk;
             D.block_mode = true;
             D.prof = dbg & 8u;
+            D.narrow = dbg & 16u;
             check_compressed(D, L, frames + b.content, b.size, scr, lane);
             st = (D.bad || D.out != D.dlen) ? kCkSeq : kCkOk;
         }
@@ -1168,8 +1195,9 @@ void zstd_check_prof_dump() {
     unsigned long long h[8];
     if (hipMemcpyFromSymbol(h, HIP_SYMBOL(g_zck_prof), sizeof h) != hipSuccess) return;
     fprintf(stderr, "rcdc zstd check phases (wave-ms, 100 MHz clock): literals %.1f sequences %.1f "
-            "blocks %.1f; literals %llu sequences %llu compressed blocks %llu\n",
-            h[0] / 1e5, h[1] / 1e5, h[2] / 1e5, h[3], h[4], h[5]);
+            "(of which placement + compares %.1f) blocks %.1f; literals %llu sequences %llu "
+            "compressed blocks %llu\n",
+            h[0] / 1e5, h[1] / 1e5, h[6] / 1e5, h[2] / 1e5, h[3], h[4], h[5]);
     memset(h, 0, sizeof h);
     (void)hipMemcpyToSymbol(HIP_SYMBOL(g_zck_prof), h, sizeof h);
 }
