@@ -1274,10 +1274,15 @@ __device__ __forceinline__ uint32_t far_group(const uint8_t *bsrc, const uint8_t
 // 16-byte repeats excluded word text (whose far repeats do not pay: r5p,
 // 33.9 -> 27.1 GiB/s at an unchanged ratio) but CSV rows too, whose gain
 // comes from many 8-12 byte repeats (0.133 -> 0.198, r5q).
-__global__ __launch_bounds__(256) void rcdc_zstd_far_map_kernel(
+// LDS: the two tables (2 x 32 KiB) are staged in LDS first, so each group's
+// ~8 random bucket reads are LDS reads instead of L2 round trips (as L2
+// gathers the kernel was 10 % of CSV's compression time, r5z6).
+template <bool LDS>
+__global__ __launch_bounds__(512) void rcdc_zstd_far_map_kernel(
     const uint8_t *__restrict__ in, const ZstdBlob *__restrict__ blobs,
     const ZstdBlk *__restrict__ blks, uint32_t nblk, uint32_t *__restrict__ far, uint32_t dense) {
     __shared__ uint32_t nlong;
+    __shared__ uint4 s_t[LDS ? kZstdFarTab / 2 : 1];  // t1 then t2
     const uint32_t b = blockIdx.x, tid = threadIdx.x;
     const FarLayout L = far_layout(far, nblk);
     const ZstdBlk k = blks[b];
@@ -1298,9 +1303,21 @@ __global__ __launch_bounds__(256) void rcdc_zstd_far_map_kernel(
     const uint32_t ng = (n + 15u) / 16u;
     const uint32_t *t1 = L.tab + (size_t)(b - (ok1 ? 1u : 0u)) * kZstdFarTab;
     const uint32_t *t2 = L.tab + (size_t)(b - (ok2 ? 2u : 0u)) * kZstdFarTab;
+    const uint32_t nt = blockDim.x;
+    if (LDS) {
+        constexpr uint32_t q = kZstdFarTab / 4;  // uint4 per table
+        const uint4 *g1 = reinterpret_cast<const uint4 *>(t1), *g2 = reinterpret_cast<const uint4 *>(t2);
+        for (uint32_t i = tid; i < q; i += nt) {
+            if (ok1) s_t[i] = g1[i];
+            if (ok2) s_t[q + i] = g2[i];
+        }
+        __syncthreads();
+        t1 = reinterpret_cast<const uint32_t *>(s_t);
+        t2 = t1 + kZstdFarTab;
+    }
     // the probe: groups tid * 32 (256 of the block's 8192)
     uint32_t np = 0;
-    for (uint32_t g = tid * 32u; g < ng; g += 256u * 32u) {
+    for (uint32_t g = tid * 32u; g < ng; g += nt * 32u) {
         bool lng;
         np += far_group(bsrc, src, lim, k.start, n, g, ok1, ok2, t1, t2, &lng) != 0u;
     }
@@ -1314,7 +1331,7 @@ __global__ __launch_bounds__(256) void rcdc_zstd_far_map_kernel(
     }
     if (!h) return;
     uint32_t *map = L.map + (size_t)b * kZstdFarGroups;
-    for (uint32_t g = tid; g < ng; g += 256) {
+    for (uint32_t g = tid; g < ng; g += nt) {
         bool lng;
         map[g] = far_group(bsrc, src, lim, k.start, n, g, ok1, ok2, t1, t2, &lng);
     }
@@ -1471,7 +1488,14 @@ __global__ __launch_bounds__(64, (NARROW ? HL - 1 : HL) == 11 ? 4 : 2) void rcdc
                     isrep = true;
                 }
                 // the far map's offset (from the group's sampled position)
-                const uint32_t cf = !isrep && fo && pb >= fo && n - p - 4 >= 16 ? pb - fo : kZstdNone;
+                uint32_t cf = !isrep && fo && pb >= fo && n - p - 4 >= 16 ? pb - fo : kZstdNone;
+                // no table or repeat candidate: the far one takes the first
+                // round trip, so the second (below) is only for lanes whose
+                // table candidate fails (RCDC_ZSTD_DBG bit 6: always second)
+                if (c == kZstdNone && cf != kZstdNone && !(dbg & 64u)) {
+                    c = cf;
+                    cf = kZstdNone;
+                }
                 // a candidate's 4 bytes are checked from memory, in the same
                 // round trip as its extension: every candidate lane extends
                 // its own match by up to 16 bytes each way (most matches end
@@ -2005,8 +2029,10 @@ hipError_t launch_zstd(const uint8_t *in, uint8_t *out, const ZstdBlob *blobs, u
         static const uint32_t dense = getenv("RCDC_ZSTD_FARDENSE")
                                           ? (uint32_t)std::max(atoi(getenv("RCDC_ZSTD_FARDENSE")), 1)
                                           : kZstdFarDense;
-        hipLaunchKernelGGL(rcdc_zstd_far_map_kernel, dim3(nblk), dim3(256), 0, stream, in, blobs,
-                           blks, nblk, far, dense);
+        static const bool lds = !(getenv("RCDC_ZSTD_FARLDS") && atoi(getenv("RCDC_ZSTD_FARLDS")) == 0);
+        hipLaunchKernelGGL(lds ? rcdc_zstd_far_map_kernel<true> : rcdc_zstd_far_map_kernel<false>,
+                           dim3(nblk), dim3(lds ? 512 : 256), 0, stream, in, blobs, blks, nblk, far,
+                           dense);
     }
     static const uint32_t dbg = getenv("RCDC_ZSTD_DBG") ? (uint32_t)atoi(getenv("RCDC_ZSTD_DBG")) : 0u;
     const uint32_t g = nblk < grid ? nblk : grid;

@@ -397,7 +397,6 @@ struct Dec {
     bool block_mode;      // earlier blocks' state unknown: using it -> kCkSeq
     bool prof;            // RCDC_ZSTD_DBG bit 3: phase clocks into g_zck_prof
     bool narrow;          // RCDC_ZSTD_DBG bit 4: 4-byte compare steps only (A/B)
-    bool coop;            // RCDC_ZSTD_DBG bit 5: wave-cooperative batch compare (A/B)
 };
 
 // ---- comparisons (the whole wave) -----------------------------------------
@@ -452,55 +451,6 @@ __device__ bool lane_cmp(const uint8_t *a, const uint8_t *b, uint32_t v, int kin
         acc |= d;
     }
     return acc == 0;
-}
-
-// A batch of up to 64 sequences compared by the whole wave, 4 bytes a lane
-// and 256 a step over the batch's output [0, tot): the lane finds the
-// sequence holding its first byte by a binary search over the lanes' output
-// starts (lane j holds sequence j: output start o, literal length ll, offset
-// off, literal start lr), and the next sequence too -- a sequence is >= 3
-// bytes (its match), so 4 bytes touch at most two.  Expected bytes: the
-// literal (lit[lr + r], or the byte v for RLE literals: kind 1) or, in the
-// match, out[p - off] (the blob's own earlier byte: equal bytes throughout
-// prove the decoded output equal to the blob, in any order).  Against a lane
-// per sequence, a batch costs its output bytes / 256 steps instead of its
-// longest sequence / 16.
-__device__ bool batch_cmp(const uint8_t *out, const uint8_t *lit, uint32_t v, int kind,
-                          uint32_t tot, uint32_t nb, uint32_t o_me, uint32_t ll_me,
-                          uint32_t off_me, uint32_t lr_me, uint32_t lane) {
-    const uint32_t o_all = lane < nb ? o_me : 0xFFFFFFFFu;
-    uint32_t bad = 0;
-    for (uint32_t base = 0; base < tot; base += 256u) {  // wave-uniform
-        const uint32_t p0 = base + lane * 4u;
-        uint32_t j = 0;  // the last sequence starting at or before p0 (o_0 = 0)
-#pragma unroll
-        for (uint32_t st = 32; st; st >>= 1) {
-            const uint32_t oc = (uint32_t)__shfl((int)o_all, (int)(j + st));
-            j = oc <= p0 ? j + st : j;
-        }
-        const uint32_t j1 = j < 63u ? j + 1u : j;
-        const uint32_t oa = (uint32_t)__shfl((int)o_all, (int)j), la = (uint32_t)__shfl((int)ll_me, (int)j),
-                       fa = (uint32_t)__shfl((int)off_me, (int)j), ra = (uint32_t)__shfl((int)lr_me, (int)j);
-        uint32_t ob = (uint32_t)__shfl((int)o_all, (int)j1);
-        const uint32_t lb = (uint32_t)__shfl((int)ll_me, (int)j1), fb = (uint32_t)__shfl((int)off_me, (int)j1),
-                       rb = (uint32_t)__shfl((int)lr_me, (int)j1);
-        if (j == 63u) ob = 0xFFFFFFFFu;
-        if (p0 < tot) {
-            const uint32_t x = ld4u(out + p0);
-            const uint32_t m = tot - p0 < 4u ? tot - p0 : 4u;
-            for (uint32_t k = 0; k < m; k++) {
-                const uint32_t p = p0 + k;
-                const bool nx = p >= ob;
-                const uint32_t o = nx ? ob : oa, l = nx ? lb : la, f = nx ? fb : fa, r0 = nx ? rb : ra;
-                const uint32_t r = p - o;
-                uint32_t e;
-                if (r < l) e = kind == 1 ? v : lit[r0 + r];
-                else e = out[(int64_t)p - (int64_t)f];
-                bad |= e ^ ((x >> (8u * k)) & 0xFFu);
-            }
-        }
-    }
-    return __builtin_amdgcn_ballot_w64(bad != 0) == 0;
 }
 
 // ---- literals ---------------------------------------------------------------
@@ -943,17 +893,6 @@ __device__ void check_compressed(Dec &D, DecLds &L, const uint8_t *p, uint32_t b
             const bool c_off = __builtin_amdgcn_ballot_w64(mine && (uint64_t)myoff > op + myll) != 0;
             if (c_lit || c_off) { D.bad = kCkCorrupt; return; }
             if (D.out + tot_o > D.dlen) { D.bad = kCkMismatch; return; }
-            if (D.coop) {
-                if (!batch_cmp(D.data + D.out, lits + litpos, lit_byte, lkind, (uint32_t)tot_o, nb,
-                               (uint32_t)(op - D.out), myll, myoff, (uint32_t)(lp - litpos), lane)) {
-                    D.bad = kCkMismatch;
-                    return;
-                }
-                if (D.prof) tcmp += wall_clock64() - tc0;
-                litpos += tot_l;
-                D.out += tot_o;
-                continue;
-            }
             const bool lng = mine && (uint64_t)myll + myml > 256;
             bool eq = true;
             if (mine && !lng) {
@@ -1046,7 +985,6 @@ __device__ uint32_t check_frame(const uint8_t *f, uint64_t flen, const uint8_t *
     D.block_mode = false;
     D.prof = prof;
     D.narrow = false;
-    D.coop = false;
     for (;;) {
         if (q + 3 > end) return kCkCorrupt;
         const uint32_t bh = q[0] | (q[1] << 8) | ((uint32_t)q[2] << 16);
@@ -1229,7 +1167,6 @@ __global__ __launch_bounds__(64, OCC) void rcdc_zstd_block_check_kernel(
             D.block_mode = true;
             D.prof = dbg & 8u;
             D.narrow = dbg & 16u;
-            D.coop = dbg & 32u;
             check_compressed(D, L, frames + b.content, b.size, scr, lane);
             st = (D.bad || D.out != D.dlen) ? kCkSeq : kCkOk;
         }
