@@ -1495,6 +1495,10 @@ __global__ __launch_bounds__(64, (NARROW ? HL - 1 : HL) == 11 ? 4 : 2) void rcdc
                 if (c == kZstdNone && cf != kZstdNone && !(dbg & 64u)) {
                     c = cf;
                     cf = kZstdNone;
+                } else if ((dbg & 128u) && !isrep && cf != kZstdNone) {  // (A/B: far first)
+                    const uint32_t t = c;
+                    c = cf;
+                    cf = t;
                 }
                 // a candidate's 4 bytes are checked from memory, in the same
                 // round trip as its extension: every candidate lane extends

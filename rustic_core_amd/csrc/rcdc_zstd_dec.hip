@@ -815,8 +815,13 @@ __device__ void check_compressed(Dec &D, DecLds &L, const uint8_t *p, uint32_t b
                 const uint32_t ofc = eo & 0xFFu, llc = el & 0xFFu, mlc = em & 0xFFu;
                 if (ofc > 31 || llc > 35 || mlc > 52) err = true;
                 const uint64_t ofv = (1ull << ofc) + brq_bits<true>(r, ofc);
-                const uint32_t ml = (xm & 0xFFFFFFu) + brq_bits<true>(r, xm >> 24);
-                const uint32_t ll = (xl & 0xFFFFFFu) + brq_bits<true>(r, xl >> 24);
+                // ML's then LL's extra bits (<= 16 each) in one read: the
+                // decode is bound by the scalar unit's issue rate, and each
+                // read is a window check, a 64-bit shift and a mask
+                const uint32_t nm = xm >> 24, nl = xl >> 24;
+                const uint32_t vx = brq_bits<true>(r, nm + nl);
+                const uint32_t ml = (xm & 0xFFFFFFu) + (uint32_t)((uint64_t)vx >> nl);
+                const uint32_t ll = (xl & 0xFFFFFFu) + (vx & (uint32_t)((1ull << nl) - 1ull));
                 uint32_t off;
                 if (ofv > 3) {
                     off = (uint32_t)(ofv - 3);
@@ -860,9 +865,13 @@ __device__ void check_compressed(Dec &D, DecLds &L, const uint8_t *p, uint32_t b
                 }
                 if (off == 0) err = true;
                 if (s0 + j + 1 < nseq) {
-                    sll = (el >> 16) + brq_bits<true>(r, (el >> 8) & 0xFFu);
-                    sml = (em >> 16) + brq_bits<true>(r, (em >> 8) & 0xFFu);
-                    sof = (eo >> 16) + brq_bits<true>(r, (eo >> 8) & 0xFFu);
+                    // the three state updates (<= 9 + 9 + 8 bits) in one read
+                    const uint32_t bl = (el >> 8) & 0xFFu, bm = (em >> 8) & 0xFFu,
+                                   bo = (eo >> 8) & 0xFFu;
+                    const uint32_t v = brq_bits<true>(r, bl + bm + bo);
+                    sll = (el >> 16) + (uint32_t)((uint64_t)v >> (bm + bo));
+                    sml = (em >> 16) + ((v >> bo) & ((1u << bm) - 1u));
+                    sof = (eo >> 16) + (v & ((1u << bo) - 1u));
                 }
                 // selects, not a branch on the lane: a divergent branch here
                 // made the compiler keep the reader's state in VGPRs
