@@ -109,11 +109,22 @@ __device__ __forceinline__ void wsync() {
     __syncthreads();
 }
 
+// Frames, blobs and the literal scratch are global memory: loads through a
+// global-address-space pointer are global_load (counted by vmcnt only).  A
+// generic pointer gives flat_load, which also counts in lgkmcnt, so every
+// LDS wait of the sequence loop (its table reads) also waited for the
+// bitstream's prefetch loads in flight (r5zpmc ISA: 24 flat loads in the
+// decode loop).
+template <typename T>
+__device__ __forceinline__ const __attribute__((address_space(1))) T *gptr(const T *p) {
+    return (const __attribute__((address_space(1))) T *)p;
+}
+
 // 4 bytes at any alignment from the aligned dwords that hold them (a dword
 // holding a readable byte is readable: allocations are 4-byte granular).
 __device__ __forceinline__ uint32_t ld4u(const uint8_t *p) {
     const uint32_t b = (uint32_t)(uintptr_t)p & 3u;
-    const uint32_t *w = (const uint32_t *)(p - b);
+    const auto *w = gptr((const uint32_t *)(p - b));
     const uint32_t lo = w[0];
     const uint32_t hi = w[b ? 1 : 0];
     return __builtin_amdgcn_alignbit(hi, lo, b * 8u);
@@ -201,7 +212,7 @@ __device__ __forceinline__ uint32_t brq_ld4(const uint8_t *base, int64_t len, in
         v = ld4u(base + byte);
     } else {
         for (int i = 0; i < 4; i++)
-            if (byte + i >= 0 && byte + i < len) v |= (uint32_t)base[byte + i] << (8 * i);
+            if (byte + i >= 0 && byte + i < len) v |= (uint32_t)gptr(base)[byte + i] << (8 * i);
     }
     return U ? rfl(v) : v;
 }
@@ -421,7 +432,7 @@ __device__ bool wave_cmp(const uint8_t *a, const uint8_t *b, uint32_t v, int kin
 // 16 bytes at any alignment from the 4-5 aligned dwords that hold them.
 __device__ __forceinline__ uint4 ld16u(const uint8_t *p) {
     const uint32_t b = (uint32_t)(uintptr_t)p & 3u, sh = b * 8u;
-    const uint32_t *w = (const uint32_t *)(p - b);
+    const auto *w = gptr((const uint32_t *)(p - b));
     const uint32_t w0 = w[0], w1 = w[1], w2 = w[2], w3 = w[3], w4 = w[b ? 4 : 3];
     return make_uint4(__builtin_amdgcn_alignbit(w1, w0, sh), __builtin_amdgcn_alignbit(w2, w1, sh),
                       __builtin_amdgcn_alignbit(w3, w2, sh), __builtin_amdgcn_alignbit(w4, w3, sh));
