@@ -99,6 +99,7 @@ struct DecLds {
     int16_t norm[64];  // (read_ncount's capacity: kNormCap)
     uint16_t nxt[64];  // per symbol: <= 53 (ML), <= 64 by kNormCap
     uint8_t w[256];    // Huffman weights (kept for treeless literals)
+    uint32_t pf[8];    // the sequence reader's next group, loaded straight to LDS
 };
 constexpr uint32_t kNormCap = 64;
 
@@ -193,6 +194,13 @@ struct BRevQ {  // 32-bit positions: the scalar unit has no 64-bit signed compar
     uint64_t acc;
     uint4 g0, g1;
     uint32_t used;  // dwords of the original g0 shifted in (0..3)
+    // LDS prefetch (the wave-uniform sequence reader): the group after g0,
+    // bytes [nbyte, nbyte + 16), loaded by the global_load_lds of lanes 0-4
+    // into pf when g0 was taken and read 4 slides later.  With the dwords
+    // loaded into registers and aligned at once, every 4th slide waited for
+    // a memory round trip; keeping them in VGPRs spilled (128 VGPRs).
+    __attribute__((address_space(3))) uint32_t *pf;
+    int32_t nbyte;
 };
 
 // A wave-uniform value in a scalar register: the serial sequence decode then
@@ -224,6 +232,28 @@ __device__ __forceinline__ uint4 brq_ld16(const uint8_t *base, int64_t len, int6
                       brq_ld4<U>(base, len, byte + 8), brq_ld4<U>(base, len, byte + 12));
 }
 
+// issue the next group's load into LDS (lanes 0-4, one dword each; no wait)
+__device__ __forceinline__ void brq_fetch_lds(BRevQ &r, int32_t byte) {
+    r.nbyte = byte;
+    if (byte < 0 || byte + 20 > r.len) return;  // (the stream's ends: slow path)
+    const uint8_t *a = r.base + byte;
+    const uint32_t *w = (const uint32_t *)(a - ((uintptr_t)a & 3u));
+    const uint32_t lane = __lane_id();
+    if (lane < 5)
+        __builtin_amdgcn_global_load_lds(
+            (const __attribute__((address_space(1))) void *)(w + lane), r.pf, 4, 0, 0);
+}
+
+// the fetched group, wave-uniform (x lowest)
+__device__ __forceinline__ uint4 brq_take_lds(BRevQ &r) {
+    if (r.nbyte < 0 || r.nbyte + 20 > r.len) return brq_ld16<true>(r.base, r.len, r.nbyte);
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the wave's LDS load has landed
+    const uint32_t sh = (uint32_t)((uintptr_t)(r.base + r.nbyte) & 3u) * 8u;
+    const uint32_t w0 = r.pf[0], w1 = r.pf[1], w2 = r.pf[2], w3 = r.pf[3], w4 = r.pf[4];
+    return make_uint4(rfl(__builtin_amdgcn_alignbit(w1, w0, sh)), rfl(__builtin_amdgcn_alignbit(w2, w1, sh)),
+                      rfl(__builtin_amdgcn_alignbit(w3, w2, sh)), rfl(__builtin_amdgcn_alignbit(w4, w3, sh)));
+}
+
 template <bool U = false>
 __device__ __forceinline__ bool brq_init(BRevQ &r, const uint8_t *p, int64_t len64) {
     if (len64 <= 0 || len64 > (1 << 27)) return false;  // streams of one block
@@ -241,7 +271,10 @@ __device__ __forceinline__ bool brq_init(BRevQ &r, const uint8_t *p, int64_t len
     const int32_t by = r.B >> 3;
     r.acc = (uint64_t)brq_ld4<U>(p, len, by) | (uint64_t)brq_ld4<U>(p, len, by + 4) << 32;
     r.g0 = brq_ld16<U>(p, len, by - 16);
-    r.g1 = brq_ld16<U>(p, len, by - 32);
+    if (U && r.pf)
+        brq_fetch_lds(r, by - 32);
+    else
+        r.g1 = brq_ld16<U>(p, len, by - 32);
     r.used = 0;
     return true;
 }
@@ -254,8 +287,13 @@ __device__ __forceinline__ void brq_slide(BRevQ &r) {
     r.g0.z = r.g0.y;
     r.g0.y = r.g0.x;
     if (++r.used == 4) {
-        r.g0 = r.g1;
-        r.g1 = brq_ld16<U>(r.base, r.len, (r.B >> 3) - 32);
+        if (U && r.pf) {
+            r.g0 = brq_take_lds(r);
+            brq_fetch_lds(r, (r.B >> 3) - 32);
+        } else {
+            r.g0 = r.g1;
+            r.g1 = brq_ld16<U>(r.base, r.len, (r.B >> 3) - 32);
+        }
         r.used = 0;
     }
 }
@@ -581,6 +619,7 @@ __device__ uint32_t build_huf(DecLds &L, uint32_t nw, uint32_t lane) {
 __device__ bool huf_stream(const DecLds &L, uint32_t tl, const uint8_t *p, int64_t len,
                            uint8_t *out, uint32_t n) {
     BRevQ r;
+    r.pf = nullptr;  // (per-lane streams: no LDS prefetch)
     if (n == 0) return len == 0 || (brq_init(r, p, len) && r.pos == 0);
     if (!brq_init(r, p, len)) return false;
     uint32_t i = 0;
@@ -786,6 +825,7 @@ __device__ void check_compressed(Dec &D, DecLds &L, const uint8_t *p, uint32_t b
         }
         wsync();
         BRevQ r;
+        r.pf = (__attribute__((address_space(3))) uint32_t *)L.pf;
         if (!brq_init<true>(r, q, end - q)) { D.bad = kCkCorrupt; return; }
         const uint32_t al_ll = rfl(D.al_ll), al_of = rfl(D.al_of), al_ml = rfl(D.al_ml);
         uint32_t sll = brq_bits<true>(r, al_ll);
@@ -809,7 +849,7 @@ __device__ void check_compressed(Dec &D, DecLds &L, const uint8_t *p, uint32_t b
             r.len = (int32_t)rfl((uint32_t)r.len);
             r.base = reinterpret_cast<const uint8_t *>(rfl64(reinterpret_cast<uintptr_t>(r.base)));
             r.g0 = make_uint4(rfl(r.g0.x), rfl(r.g0.y), rfl(r.g0.z), rfl(r.g0.w));
-            r.g1 = make_uint4(rfl(r.g1.x), rfl(r.g1.y), rfl(r.g1.z), rfl(r.g1.w));
+            r.nbyte = (int32_t)rfl((uint32_t)r.nbyte);
             sll = rfl(sll);
             sof = rfl(sof);
             sml = rfl(sml);
