@@ -859,10 +859,16 @@ __device__ void check_compressed(Dec &D, DecLds &L, const uint8_t *p, uint32_t b
             for (uint32_t j = 0; j < nb; j++) {
                 // the entries as one dword each (sym | nb << 8 | next << 16),
                 // wave-uniform
-                const uint32_t eo = rfl(reinterpret_cast<const uint32_t *>(L.of)[sof]);
-                const uint32_t el = rfl(reinterpret_cast<const uint32_t *>(L.ll)[sll]);
-                const uint32_t em = rfl(reinterpret_cast<const uint32_t *>(L.ml)[sml]);
-                const uint32_t xl = rfl(L.u.x.llx[sll]), xm = rfl(L.u.x.mlx[sml]);
+                // the five reads issued together, then one wait: the
+                // scheduler otherwise waited after each (3 LDS round trips
+                // per sequence on the critical path)
+                const uint32_t veo = reinterpret_cast<const uint32_t *>(L.of)[sof];
+                const uint32_t vel = reinterpret_cast<const uint32_t *>(L.ll)[sll];
+                const uint32_t vem = reinterpret_cast<const uint32_t *>(L.ml)[sml];
+                const uint32_t vxl = L.u.x.llx[sll], vxm = L.u.x.mlx[sml];
+                __builtin_amdgcn_sched_barrier(0);
+                const uint32_t eo = rfl(veo), el = rfl(vel), em = rfl(vem);
+                const uint32_t xl = rfl(vxl), xm = rfl(vxm);
                 const uint32_t ofc = eo & 0xFFu, llc = el & 0xFFu, mlc = em & 0xFFu;
                 if (ofc > 31 || llc > 35 || mlc > 52) err = true;
                 const uint64_t ofv = (1ull << ofc) + brq_bits<true>(r, ofc);
