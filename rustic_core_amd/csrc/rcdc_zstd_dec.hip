@@ -879,47 +879,24 @@ __device__ void check_compressed(Dec &D, DecLds &L, const uint8_t *p, uint32_t b
                 const uint32_t vx = brq_bits<true>(r, nm + nl);
                 const uint32_t ml = (xm & 0xFFFFFFu) + (uint32_t)((uint64_t)vx >> nl);
                 const uint32_t ll = (xl & 0xFFFFFFu) + (vx & (uint32_t)((1ull << nl) - 1ull));
-                uint32_t off;
-                if (ofv > 3) {
-                    off = (uint32_t)(ofv - 3);
-                    r2 = r1;
-                    r1 = r0;
-                    r0 = off;
-                    u2 = u1;
-                    u1 = u0;
-                    u0 = false;
-                } else {
-                    const uint32_t idx = (uint32_t)ofv - 1u + (ll == 0 ? 1u : 0u);
-                    if (idx == 0) {
-                        off = r0;
-                        unk_used |= u0;
-                    } else if (idx == 1) {
-                        off = r1;
-                        unk_used |= u1;
-                        r1 = r0;
-                        u1 = u0;
-                        r0 = off;
-                        u0 = false;
-                    } else if (idx == 2) {
-                        off = r2;
-                        unk_used |= u2;
-                        r2 = r1;
-                        u2 = u1;
-                        r1 = r0;
-                        u1 = u0;
-                        r0 = off;
-                        u0 = false;
-                    } else {
-                        off = r0 - 1u;
-                        unk_used |= u0;
-                        r2 = r1;
-                        u2 = u1;
-                        r1 = r0;
-                        u1 = u0;
-                        r0 = off;
-                        u0 = false;
-                    }
-                }
+                // the repeat-offset history (RFC 8878 3.1.1.5) without
+                // branches: the decode is bound by the scalar unit's issue
+                // rate, and a branch per case was a good part of a sequence's
+                const bool lr = ofv <= 3;  // a repeat code
+                const uint32_t idx = (uint32_t)ofv - 1u + (ll == 0 ? 1u : 0u);
+                const uint32_t rsel = idx == 1 ? r1 : idx == 2 ? r2 : idx == 0 ? r0 : r0 - 1u;
+                const bool usel = idx == 1 ? u1 : idx == 2 ? u2 : u0;
+                const uint32_t off = lr ? rsel : (uint32_t)(ofv - 3);
+                unk_used |= lr && usel;
+                const bool k1 = lr && idx == 0, k2 = lr && idx <= 1;  // r1 / r2 kept
+                const uint32_t n2 = k2 ? r2 : r1, n1 = k1 ? r1 : r0;
+                const bool nu2 = k2 ? u2 : u1, nu1 = k1 ? u1 : u0, nu0 = k1 ? u0 : false;
+                r2 = n2;
+                r1 = n1;
+                r0 = off;
+                u2 = nu2;
+                u1 = nu1;
+                u0 = nu0;
                 if (off == 0) err = true;
                 if (s0 + j + 1 < nseq) {
                     // the three state updates (<= 9 + 9 + 8 bits) in one read
