@@ -1048,8 +1048,16 @@ bool stage_b(Ing *g, Batch *B, bool finalize) {
     const void *srcs[2] = {P.staging, g->carry[g->carry_cur] ? g->carry[g->carry_cur] : P.staging};
     std::vector<uint32_t> boffs(std::max<size_t>(open_from, 1));
     OutSlot *out = nullptr;
-    hipEvent_t d2h_fin = nullptr;
-    std::shared_ptr<std::atomic<bool>> d2h_flag;
+    // The packs go back in groups of whole packs of ~256 MiB, each with its
+    // own end event: a group's pack ids start as soon as it has landed, not
+    // after the batch's whole D2H (~20 ms for a 2 GiB batch's ~1 GB of packs;
+    // the last batch's ids end the run).
+    struct D2HGroup {
+        size_t first, last;  // packs [first, last)
+        hipEvent_t fin;
+        std::shared_ptr<std::atomic<bool>> flag;
+    };
+    std::vector<D2HGroup> d2h_groups;
     if (!grp.empty()) {
         if (!ensure_dev(g, &g->d_packs, &g->d_packs_cap, total + 64)) return false;
         // the last pack build's D2H must be done with d_packs (once the pump
@@ -1087,17 +1095,29 @@ bool stage_b(Ing *g, Batch *B, bool finalize) {
             ING_HIP(g, hipHostMalloc((void **)&out->host, out->cap, hipHostMallocDefault));
         }
         // the D2H goes to the feeder's pump, piece by piece, after the build
-        hipEvent_t after, fin;
+        // (the first group's job orders the copy stream after it; the rest
+        // follow on that stream)
+        hipEvent_t after;
         ING_HIP(g, hipEventCreateWithFlags(&after, hipEventDisableTiming));
-        ING_HIP(g, hipEventCreateWithFlags(&fin, hipEventDisableTiming));
         ING_HIP(g, hipEventRecord(after, g->s_back));
-        d2h_fin = fin;
-        d2h_flag = std::make_shared<std::atomic<bool>>(false);
-        {
-            std::lock_guard<std::mutex> lq(g->d2h_mu);
-            g->d2h_q.push_back({out->host, g->d_packs, total, 0, after, fin, d2h_flag, false});
+        static const uint64_t group_bytes =
+            getenv("RCDC_INGEST_D2H_GROUP") ? strtoull(getenv("RCDC_INGEST_D2H_GROUP"), nullptr, 10)
+                                            : 256ull << 20;
+        for (size_t a = 0; a < grp.size();) {
+            size_t b = a + 1;
+            while (b < grp.size() && packs[b].out_off - packs[a].out_off < group_bytes) b++;
+            D2HGroup G{a, b, nullptr, std::make_shared<std::atomic<bool>>(false)};
+            ING_HIP(g, hipEventCreateWithFlags(&G.fin, hipEventDisableTiming));
+            const uint64_t lo = packs[a].out_off, hi = b < grp.size() ? packs[b].out_off : total;
+            {
+                std::lock_guard<std::mutex> lq(g->d2h_mu);
+                g->d2h_q.push_back({out->host + lo, g->d_packs + lo, hi - lo, 0,
+                                    a == 0 ? after : nullptr, G.fin, G.flag, a != 0});
+            }
+            g->last_d2h = G.flag;
+            d2h_groups.push_back(G);
+            a = b;
         }
-        g->last_d2h = d2h_flag;
         g->cv_slot.notify_all();
     }
     // the still open pack: its blobs into the other carry buffer
@@ -1152,7 +1172,10 @@ bool stage_b(Ing *g, Batch *B, bool finalize) {
         }
         {
             std::lock_guard<std::mutex> lk(g->wait_mu);
-            g->wait_q.push_back({d2h_fin, d2h_flag, B->index, std::move(jobs)});
+            for (const D2HGroup &G : d2h_groups)
+                g->wait_q.push_back({G.fin, G.flag, B->index,
+                                     std::vector<std::shared_ptr<PackJob>>(
+                                         jobs.begin() + G.first, jobs.begin() + G.last)});
         }
         g->wait_cv.notify_one();
     }
