@@ -869,8 +869,10 @@ __device__ void check_compressed(Dec &D, DecLds &L, const uint8_t *p, uint32_t b
                 __builtin_amdgcn_sched_barrier(0);
                 const uint32_t eo = rfl(veo), el = rfl(vel), em = rfl(vem);
                 const uint32_t xl = rfl(vxl), xm = rfl(vxm);
-                const uint32_t ofc = eo & 0xFFu, llc = el & 0xFFu, mlc = em & 0xFFu;
-                if (ofc > 31 || llc > 35 || mlc > 52) err = true;
+                // (no per-sequence symbol range check: read_ncount bounds every
+                // FSE table's symbols by its alphabet, as do the predefined and
+                // RLE tables; a repeat table is an earlier one of these)
+                const uint32_t ofc = eo & 0xFFu;
                 const uint64_t ofv = (1ull << ofc) + brq_bits<true>(r, ofc);
                 // ML's then LL's extra bits (<= 16 each) in one read: the
                 // decode is bound by the scalar unit's issue rate, and each
