@@ -1438,15 +1438,21 @@ __global__ __launch_bounds__(1024, 1) void rcdc_walk_fixup_kernel(
 // and a block prefix sum places each on-chain node's segment.
 // counts[stream] = ~0 flags a stream whose fixup overflowed (the host redoes
 // it on the scan path).
+// Round 5: the workgroup places the segments and leaves each on-chain node's
+// output offset in its BoundRes (fix_from, dead after the fixups; kOffNone
+// off the chain); rcdc_walk_scatter_kernel then writes every node's
+// segment, a thread per node over the whole grid.  A long stream has
+// thousands of nodes (C5: 3 200), and copying them one workgroup per stream
+// made the chain outlast the walk beside it (assemble 74.5 us, r5c5prof).
 constexpr int kAsmB = 1024;
+constexpr uint64_t kOffNone = ~0ull;
 
 __global__ __launch_bounds__(kAsmB) void rcdc_walk_assemble_kernel(
     const StreamDesc *__restrict__ sds, const WalkUnit *__restrict__ units,
     const uint32_t *__restrict__ stream_unit0, uint32_t nstreams, WalkParams prm,
     const uint64_t *__restrict__ piece_cuts, const uint64_t *__restrict__ pstatus,
-    const BoundRes *__restrict__ bres, const uint64_t *__restrict__ fix_cuts,
-    const FixRes *__restrict__ fixres, uint64_t *__restrict__ cuts,
-    uint64_t *__restrict__ counts) {
+    BoundRes *__restrict__ bres, uint64_t *__restrict__ cuts, uint64_t *__restrict__ counts,
+    const FixRes *__restrict__ fixres) {
     constexpr int NW = kAsmB / 64;
     __shared__ uint64_t s_ns[NW];          // bitmap: node is not simple
     __shared__ uint32_t s_next[kAsmB];     // next node (stream piece index)
@@ -1467,6 +1473,9 @@ __global__ __launch_bounds__(kAsmB) void rcdc_walk_assemble_kernel(
     const uint64_t n0 = list_n(u0);
     for (uint64_t i = tid; i < n0 && i < cap; i += kAsmB)
         out[i] = piece_cuts[U0.out_base + i] & kCutVal;
+    // every node off the chain until placed (the thread that places node j
+    // below, j = b + tid, is the one that clears it here)
+    for (uint32_t j = 1 + tid; j < P; j += kAsmB) bres[u0 + j].fix_from = kOffNone;
     uint64_t nc = n0;
     bool bad = false;
     uint32_t cur = 1, done = P <= 1;
@@ -1586,29 +1595,7 @@ __global__ __launch_bounds__(kAsmB) void rcdc_walk_assemble_kernel(
             if (w < wave) base += t;
             total += t;
         }
-        if (on) {
-            uint64_t o = nc + base + v - len;
-            uint64_t pv = 0;
-            for (uint32_t i = 0; i < nh; i++) {
-                const uint64_t e = bres[u].hops[i], v = e & kCutVal;
-                if ((e >> 62) == kHopRun) {
-                    for (uint64_t x = pv + prm.min_size; x <= v && o < cap; x += prm.min_size, o++)
-                        out[o] = x;
-                } else {
-                    if (o < cap) out[o] = v;
-                    o++;
-                }
-                pv = v;
-            }
-            const uint64_t *fsrc = fix_cuts + (uint64_t)u * prm.fix_cap;
-            for (uint32_t i = 0; i < fc; i++, o++)
-                if (o < cap) out[o] = fsrc[i];
-            if (mu != kNoUnit) {
-                const uint64_t *L = piece_cuts + units[mu].out_base;
-                for (uint64_t i = tail_lo; i < tail_hi; i++, o++)
-                    if (o < cap) out[o] = L[i] & kCutVal;
-            }
-        }
+        if (on && !nbad) bres[u].fix_from = nc + base + v - len;  // (the scatter writes it)
         nc += total;
         cur = __builtin_amdgcn_readfirstlane(s_st[0]);
         done = __builtin_amdgcn_readfirstlane(s_st[1]);
@@ -1616,6 +1603,62 @@ __global__ __launch_bounds__(kAsmB) void rcdc_walk_assemble_kernel(
     }
     const bool any_bad = __syncthreads_or(bad);
     if (tid == 0) counts[U0.stream] = (any_bad || nc > cap) ? ~0ull : nc;
+}
+
+// A thread per node of every walked stream: an on-chain node's segment --
+// its hops (single cuts, or runs of min-sized chunks), its fixup cuts and the
+// tail of the list it merged into -- at the offset the assembly left in its
+// BoundRes.
+__global__ __launch_bounds__(256) void rcdc_walk_scatter_kernel(
+    const StreamDesc *__restrict__ sds, const WalkUnit *__restrict__ units, WalkParams prm,
+    const uint64_t *__restrict__ piece_cuts, const uint64_t *__restrict__ pstatus,
+    const BoundRes *__restrict__ bres, const uint64_t *__restrict__ fix_cuts,
+    const FixRes *__restrict__ fixres, uint64_t *__restrict__ cuts) {
+    const uint32_t u = blockIdx.x * blockDim.x + threadIdx.x;
+    if (u >= prm.nunits) return;
+    const WalkUnit U = units[u];
+    if (U.piece == 0) return;
+    const BoundRes &R = bres[u];
+    uint64_t o = R.fix_from;
+    if (o == kOffNone) return;
+    const StreamDesc d = sds[U.stream];
+    uint64_t *out = cuts + d.cut_base;
+    const uint64_t cap = d.cut_cap;
+    const uint32_t kind = R.kind;
+    const uint32_t nh = kind != kBoundNone ? min(R.nhops, (uint32_t)kMaxHops) : 0u;
+    uint32_t fc = 0, mu = kNoUnit;
+    int32_t mi = 0;
+    if (kind == kBoundMerged) {
+        mu = R.merge_unit;
+        mi = R.merge_idx;
+    } else if (kind == kBoundFixup) {
+        const FixRes F = fixres[u];
+        if (F.count > prm.fix_cap) return;  // (flagged by the assembly)
+        fc = F.count;
+        mu = F.merge_unit;
+        mi = F.merge_idx;
+    }
+    uint64_t pv = 0;
+    for (uint32_t i = 0; i < nh; i++) {
+        const uint64_t e = R.hops[i], v = e & kCutVal;
+        if ((e >> 62) == kHopRun) {
+            for (uint64_t x = pv + prm.min_size; x <= v && o < cap; x += prm.min_size, o++)
+                out[o] = x;
+        } else {
+            if (o < cap) out[o] = v;
+            o++;
+        }
+        pv = v;
+    }
+    const uint64_t *fsrc = fix_cuts + (uint64_t)u * prm.fix_cap;
+    for (uint32_t i = 0; i < fc; i++, o++)
+        if (o < cap) out[o] = fsrc[i];
+    if ((kind == kBoundMerged || kind == kBoundFixup) && mu != kNoUnit) {
+        const uint64_t *L = piece_cuts + units[mu].out_base;
+        const uint64_t hi = pstatus[mu] & 0xFFFFFFFFu;
+        for (uint64_t i = (uint64_t)(mi + 1); i < hi; i++, o++)
+            if (o < cap) out[o] = L[i] & kCutVal;
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -1777,8 +1820,10 @@ hipError_t launch_walk_chain(const uint8_t *arena, const StreamDesc *sds, const 
         fprintf(stderr, "rcdc: fixup done\n");
     }
     hipLaunchKernelGGL(rcdc_walk_assemble_kernel, dim3(nstreams), dim3(kAsmB), 0, stream, sds, units,
-                       stream_unit0, nstreams, prm, piece_cuts, pstatus, bres, fix_cuts, fixres,
-                       cuts, counts);
+                       stream_unit0, nstreams, prm, piece_cuts, pstatus, bres, cuts, counts,
+                       fixres);
+    hipLaunchKernelGGL(rcdc_walk_scatter_kernel, dim3((prm.nunits + 255) / 256), dim3(256), 0, stream,
+                       sds, units, prm, piece_cuts, pstatus, bres, fix_cuts, fixres, cuts);
     return hipGetLastError();
 }
 
