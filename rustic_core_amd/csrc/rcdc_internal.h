@@ -170,7 +170,8 @@ struct WalkParams {
     unsigned long long *stats_next;
     uint32_t cost_blocks;  // workgroups of the cost kernel (1024 threads; > 256: the old
                            // thousands-of-256-thread grid, A/B via RCDC_COST_BLOCKS)
-    uint32_t pad_c;
+    uint32_t cost_samples; // 8-byte words the cost kernel samples per piece (16-64;
+                           // each pulls a whole cache line: RCDC_COST_SAMPLES A/B)
 };
 constexpr uint32_t kWalkZoneFast = 1;  // zones on the scan's slide (zone_wave_fast)
 constexpr uint32_t kWalkKReset = 2;    // counters reset in the walk kernel, queue by qbase

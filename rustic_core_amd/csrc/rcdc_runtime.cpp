@@ -779,6 +779,11 @@ rcdc_status plan_build(rcdc_ctx *ctx, rcdc_plan *pl, const uint64_t *offs, const
     if (const char *e = getenv("RCDC_WALK_ZONEFAST"); e && atoi(e) == 0) wp.flags &= ~kWalkZoneFast;
     if (const char *e = getenv("RCDC_WALK_KRESET"); e && atoi(e) == 0) wp.flags &= ~kWalkKReset;
     wp.cost_blocks = 4096;
+    wp.cost_samples = 64;
+    if (const char *e = getenv("RCDC_COST_SAMPLES")) {
+        const int v = atoi(e);
+        wp.cost_samples = v >= 64 ? 64u : v >= 32 ? 32u : 16u;
+    }
     if (const char *e = getenv("RCDC_COST_BLOCKS")) wp.cost_blocks = (uint32_t)std::max(atoi(e), 1);
     if (const char *e = getenv("RCDC_CHECK_BUDGET")) wp.chk_budget = strtoull(e, nullptr, 10);
     if (const char *e = getenv("RCDC_FIX_SEG")) wp.fix_seg = (uint32_t)std::max(atoi(e) / 128 * 128, 128);

@@ -1685,9 +1685,11 @@ __global__ __launch_bounds__(1024) void rcdc_walk_cost_kernel(
         const WalkUnit U = units[u];
         const StreamDesc d = sds[U.stream];
         const uint64_t len = U.stop - U.start;
-        const uint64_t a = (d.off + U.start + (len * lane) / 64u) & ~7ull;
-        const uint64_t w = a + 8 <= d.off + d.n ? *reinterpret_cast<const uint64_t *>(arena + a) : 0;
-        const uint32_t cls = (uint32_t)__builtin_popcountll(__ballot(w != 0));
+        const uint32_t ns = prm.cost_samples ? prm.cost_samples : 64u;
+        const uint64_t a = (d.off + U.start + (len * lane) / ns) & ~7ull;
+        const uint64_t w = lane < ns && a + 8 <= d.off + d.n
+                               ? *reinterpret_cast<const uint64_t *>(arena + a) : 0;
+        const uint32_t cls = (uint32_t)__builtin_popcountll(__ballot(w != 0)) * (64u / ns);
         const uint64_t quantum = max(prm.piece_bytes / 48, (uint64_t)1);
         // K classes by piece index: at equal cost, a stream's pieces 0, K,
         // 2K, ... go first, then 1, K + 1, ... (each then mostly starts
