@@ -97,6 +97,12 @@ def slice_bounds(total: int, world: int, min_size: int, max_size: int):
     [a_r, e_r): the slice and a halo of max + 64 bytes from the next slice,
     enough for the chain that starts before b_r to reach its crossing cut
     exactly (no hop from s < b_r looks past s + max + 63).
+
+    Slices may be EMPTY (a_r == b_r == total): rounding the share up to a
+    multiple of min leaves the trailing ranks nothing when the stream is
+    short for the world (8 MiB + 1 byte over 8 ranks at min 512 KiB: ranks
+    6 and 7).  Callers keep such ranks in every collective of the stitch
+    (chunk_long_stream_sharded, SlicedStream.stitch).
     """
     per = -(-total // world)
     per = -(-per // min_size) * min_size
@@ -255,12 +261,18 @@ class SlicedStream:
         source "plan" (the device list, relative to a) or a host array of
         absolute cuts (a re-chunked entry).  j None: to the list's end."""
         import torch
-        if self.world == 1 or self.a >= self.b:
-            return ("plan", 0, None) if self.a < self.b else (np.zeros(0, np.uint64), 0, -1)
+        empty = self.a >= self.b
+        if self.world == 1:
+            return ("plan", 0, None) if not empty else (np.zeros(0, np.uint64), 0, -1)
         entries = [bb[0] for bb in self.bounds]
         mine = None  # host list once this rank has re-chunked
         while True:
-            if mine is None:
+            if empty:
+                # an empty slice (slice_bounds: trailing ranks of a short
+                # stream) owns no cut, but every all_gather of the stitch
+                # needs every rank: it sends a window of n = 0 each round
+                win = host_window(np.zeros(0, np.int64), 0, self.k)
+            elif mine is None:
                 self.plan.window(0, self.b - self.a, self.k, self.win.data_ptr(), self.stream)
                 if self.stream:
                     torch.cuda.current_stream(self.arena.device).wait_stream(
@@ -270,7 +282,7 @@ class SlicedStream:
                 win = host_window(mine.astype(np.int64) - entries[self.rank],
                                   self.b - entries[self.rank], self.k)
             wins = _all_gather_windows(win, self.world, self.group)
-            if int(wins[self.rank][0]) == -1:  # the walk needs host completion
+            if not empty and int(wins[self.rank][0]) == -1:  # the walk needs host completion
                 mine = self.plan.results()[0] + np.uint64(self.a)
                 if self.e < self.total:
                     mine = mine[:int(np.searchsorted(mine, self.b)) + 1]

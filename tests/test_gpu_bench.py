@@ -60,8 +60,10 @@ def test_bench_two_ranks_c4(gpu_ctx):
 
 def test_bench_two_ranks_c5(gpu_ctx):
     """C5 over two ranks: one 512 MiB zero stream sliced with max + 64 halos,
-    the cross-rank stitch (all_gather_object of cut lists) inside every
-    timed step; rank 0's cuts against the closed form and the oracle."""
+    the cross-rank stitch (shard.SlicedStream: the crossing window of each
+    rank's device cut list, rcdc_plan_window, in one fixed-size all_gather)
+    inside every timed step; rank 0's cuts against the closed form and the
+    oracle."""
     line = _two_ranks(["--workload", "C5", "--stream-bytes", str(256 << 20), "--steps", "2"])
     assert line["parity"]["mismatches"] == 0
     assert line["parity"]["cuts"] >= (256 << 20) // (512 << 10) - 1

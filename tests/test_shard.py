@@ -167,6 +167,88 @@ def test_slice_bounds():
     assert b[0][0] == 0 and b[-1][1] == 10_000_000
     for (a, bb, e), nxt in zip(b, b[1:] + [(10_000_000, 0, 0)]):
         assert a % 4096 == 0 and bb == nxt[0] and e == min(bb + 65536 + 64, 10_000_000)
+    # a short stream leaves the trailing slices empty (documented)
+    total = (8 << 20) + 1
+    b = slice_bounds(total, 8, 512 << 10, 8 << 20)
+    assert [r for r, (a, bb, _) in enumerate(b) if a >= bb] == [6, 7]
+    assert b[5][1] == total and all(x == (total, total, total) for x in b[6:])
+
+
+class _HostPlan:
+    """Stand-in for DevicePlan on the CPU: the oracle chunks the rank's extent
+    [a, e) as one stream; window() writes the crossing window into the tensor
+    whose data_ptr SlicedStream passes (what rcdc_plan_window does on the
+    device)."""
+
+    def __init__(self, local, params, win_tensor):
+        self.local, self.params, self.win_tensor = local, params, win_tensor
+        self.cuts = None
+
+    def run(self, ptr, stream):
+        from oracle import oracle
+        self.cuts = oracle.chunk_cuts(self.local, oracle.DEFAULT_POLY, *self.params)
+
+    def window(self, stream_i, bound, k, ptr, stream):
+        import torch
+        from rustic_core_amd.shard import host_window
+        assert ptr == self.win_tensor.data_ptr()
+        self.win_tensor.copy_(torch.from_numpy(host_window(self.cuts.astype(np.int64), bound, k)))
+
+    def results(self):
+        return [self.cuts]
+
+
+def _sliced_host_worker(rank, world, port, errfile, total, kind):
+    import torch
+    import torch.distributed as dist
+    from oracle import oracle
+    from rustic_core_amd.shard import SlicedStream, slice_bounds
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        params = (512 << 10, 1 << 20, 8 << 20)
+        rng = np.random.default_rng(31)
+        data = (np.zeros(total, np.uint8) if kind == "zeros"
+                else rng.integers(0, 256, total, dtype=np.uint8))
+        a, b, e = slice_bounds(total, world, params[0], params[2])[rank]
+        arena = torch.zeros(e - a + 256, dtype=torch.uint8)
+
+        class _Ctx:  # SlicedStream builds its re-chunk closure lazily
+            pass
+        ss = SlicedStream(_Ctx(), arena, None, total, rank, world, params[0], params[2])
+        ss.plan = _HostPlan(data[a:e], params, ss.win)
+
+        def chunk_from(s):
+            cuts = oracle.chunk_cuts(data[s:e], oracle.DEFAULT_POLY, *params) + np.uint64(s)
+            if e < total:
+                cuts = cuts[:int(np.searchsorted(cuts, b)) + 1]
+            return cuts
+        ss.chunk_from = chunk_from
+        mine = ss.cuts(ss.step())
+        parts = [None] * world
+        dist.all_gather_object(parts, np.asarray(mine, np.uint64))
+        got = np.concatenate(parts)
+        want = oracle.chunk_cuts(data, oracle.DEFAULT_POLY, *params)
+        assert np.array_equal(got, want), (len(got), len(want))
+        dist.barrier()
+    except Exception as ex:  # pragma: no cover
+        with open(errfile, "a") as f:
+            f.write(f"rank {rank}: {ex!r}\n")
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("kind", ["zeros", "random"])
+def test_sliced_stream_empty_slices_gloo_world8(tmp_path, kind):
+    """SlicedStream.stitch with empty trailing slices (8 MiB + 1 over 8 ranks
+    at the default parameters: ranks 6 and 7 own nothing) -- they still take
+    part in every all_gather, so the stitch returns instead of deadlocking."""
+    import torch.multiprocessing as mp
+    err = str(tmp_path / "err.txt")
+    mp.spawn(_sliced_host_worker, args=(8, _free_port(), err, (8 << 20) + 1, kind), nprocs=8,
+             join=True)
+    assert not os.path.exists(err)
 
 
 def test_stitch_windows_rules():
@@ -259,6 +341,8 @@ def _long_data_big(kind):
     """40 MiB + 3 for the default parameters (min 512 KiB)."""
     rng = np.random.default_rng(22)
     n = 40 * (1 << 20) + 3
+    if kind == "short_random":  # 8 MiB + 1: over 8 ranks, ranks 6 and 7 get empty slices
+        return rng.integers(0, 256, (8 << 20) + 1, dtype=np.uint8)
     if kind == "zeros":
         return np.zeros(n, np.uint8)
     if kind == "phase_zeros":
@@ -299,4 +383,16 @@ def test_sliced_stream_device_gloo(tmp_path, kind, world):
     err = str(tmp_path / "err.txt")
     mp.spawn(_device_long_worker, args=(world, _free_port(), err, kind, (4096, 16384, 65536),
                                         True), nprocs=world, join=True)
+    assert not os.path.exists(err)
+
+
+@pytest.mark.gpu
+def test_sliced_stream_device_gloo_empty_slices(tmp_path):
+    """The device C5 path at world 8 with empty trailing slices (8 MiB + 1 at
+    the default parameters): ranks 6 and 7 send n = 0 windows and the stitch
+    returns on every rank."""
+    import torch.multiprocessing as mp
+    err = str(tmp_path / "err.txt")
+    mp.spawn(_device_long_worker, args=(8, _free_port(), err, "short_random",
+                                        (512 << 10, 1 << 20, 8 << 20), True), nprocs=8, join=True)
     assert not os.path.exists(err)
