@@ -92,9 +92,10 @@ def parse():
                     help="also compress the chunks as blobs on the device (rcdc_zstd_compress)")
     ap.add_argument("--zstd-level", type=int, default=0)
     ap.add_argument("--ingest", action="store_true",
-                    help="run the whole version-2 backup byte path on the device (DeviceIngest: "
-                         "chunk, blob ids, dedup, zstd, seal, verify, packs) over "
-                         "--ingest-streams streams; on by default for C3 at N = 1")
+                    help="also run the Python/torch device-resident backup byte path "
+                         "(rustic_core_amd.ingest.DeviceIngest, a test reference: chunk, blob "
+                         "ids, dedup, zstd, seal, verify, packs) over --ingest-streams streams; "
+                         "the default C3 line measures the native engine instead (h2h)")
     ap.add_argument("--no-ingest", action="store_true")
     ap.add_argument("--no-flush", action="store_true",
                     help="pipelined plans: the last timed run's chain stays narrow (A/B)")
@@ -464,6 +465,7 @@ def run_c4(args, torch, dist, dev, rank, world, local):
     rng = np.random.default_rng(4001)
     sample = set(int(x) for x in rng.choice(args.c4_files, size=min(64, args.c4_files),
                                              replace=False))
+    parity_acc = [0, 0, 0, 0.0]  # files diffed, mismatches, cuts diffed, seconds
     if single and layouts:
         b, offs, plan = layouts[0]
         plan.set_timing(True, every=args.time_every)
@@ -488,8 +490,15 @@ def run_c4(args, torch, dist, dev, rank, world, local):
             walked_batches = 1
         else:
             lane_hashed = inf["scanned_bytes"] + 64 * inf["segments"]
+        if not args.no_parity:  # every file of the share (untimed)
+            t_p = time.perf_counter()
+            bad_b, cuts_b = oracle_diff(arena, offs, [sizes[f] for f in b], got, cpu_threads()[0])
+            parity_acc[0] += len(b)
+            parity_acc[1] += bad_b
+            parity_acc[2] += cuts_b
+            parity_acc[3] += time.perf_counter() - t_p
         for i, f in enumerate(b):
-            if f in sample and not args.no_parity:
+            if f in sample and not args.no_cpu_baseline:
                 o = int(offs[i])
                 sample_cuts[f] = (got[i], arena[o:o + sizes[f]].cpu().numpy())
     for step in range(args.steps if not single else 0):
@@ -527,8 +536,16 @@ def run_c4(args, torch, dist, dev, rank, world, local):
                     walked_batches += 1
                 else:
                     lane_hashed += inf["scanned_bytes"] + 64 * inf["segments"]
+                if not args.no_parity:
+                    t_p = time.perf_counter()
+                    bad_b, cuts_b = oracle_diff(arena, offs, [sizes[f] for f in b], got,
+                                                cpu_threads()[0])
+                    parity_acc[0] += len(b)
+                    parity_acc[1] += bad_b
+                    parity_acc[2] += cuts_b
+                    parity_acc[3] += time.perf_counter() - t_p
                 for i, f in enumerate(b):
-                    if f in sample and not args.no_parity:
+                    if f in sample and not args.no_cpu_baseline:
                         o = int(offs[i])
                         sample_cuts[f] = (got[i], arena[o:o + sizes[f]].cpu().numpy())
     t = torch.tensor([el], dtype=torch.float64, device=coll_device(dev))
@@ -539,17 +556,18 @@ def run_c4(args, torch, dist, dev, rank, world, local):
     share = sum(sizes[f] for f in mine)
     passes = max(runs if single else args.steps, 1)  # timed passes behind scan_ms
     hash_s = max(scan_ms / 1e3 / passes, 1e-9)  # hashing kernels per pass
-    bad = 0
-    for f, (cuts, host) in sample_cuts.items():
-        from oracle import oracle
-        bad += not np.array_equal(cuts, oracle.chunk_cuts(host, POLY, MIN, AVG, MAX))
-    checked = torch.tensor([len(sample_cuts), bad], dtype=torch.int64, device=coll_device(dev))
+    checked = torch.tensor([parity_acc[0], parity_acc[1], parity_acc[2]], dtype=torch.int64,
+                           device=coll_device(dev))
     if world > 1:
         dist.all_reduce(checked)
-    c4_traffic, c4_sq = None, {}
+    c4_traffic, c4_sq, c4_read = None, {}, None
     if walked_batches == len(layouts) and args.c4_files == 1024 and world == 1:
         c4_traffic, pmc = pmc_traffic("C4", "rcdc_walk_kernel")
         c4_sq = (pmc or {}).get("sq") or {}
+        c4_read = (pmc or {}).get("hbm_read_bytes_per_launch")
+    # north_star's fraction: HBM bytes read (rocprof FETCH_SIZE, calibrated)
+    # / kernel time; the lanes' bytes stand in without a PMC file
+    c4_phys = c4_read if c4_read else lane_hashed
     if rank == 0:
         line = {
             "metric": METRIC, "value": round(total / el_max / GiB, 2), "unit": "GiB/s",
@@ -567,13 +585,19 @@ def run_c4(args, torch, dist, dev, rank, world, local):
                          "kernel": ("rcdc_walk_kernel" if walked_batches == len(layouts) else
                                     f"rcdc_walk_kernel ({walked_batches} batches) + "
                                     f"rcdc_scan_kernel ({len(layouts) - walked_batches})"),
-                         "achieved": round(share / hash_s / 1e9, 1) if runs else None,
+                         "achieved": round(c4_phys / hash_s / 1e9, 1) if runs else None,
                          "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(share / hash_s / 1e9 / HBM_PEAK_GBS, 4) if runs else None,
-                         "basis": "input bytes of the rank's files per pass / hashing-kernel time",
+                         "frac": round(c4_phys / hash_s / 1e9 / HBM_PEAK_GBS, 4) if runs else None,
+                         "basis": ("HBM bytes read per pass: rocprof FETCH_SIZE (calibrated, "
+                                   "profiles/pmc_C4.json) / hashing-kernel time" if c4_read else
+                                   "bytes the lanes read per pass (device work counters) / "
+                                   "hashing-kernel time (no PMC file for this configuration)"),
                          "traffic": c4_traffic,
-                         "frac_fetch": (round(c4_traffic / hash_s / 1e9 / HBM_PEAK_GBS, 4)
-                                        if c4_traffic else None),
+                         "frac_fetch": (round(c4_read / hash_s / 1e9 / HBM_PEAK_GBS, 4)
+                                        if c4_read else None),
+                         "achieved_input_basis_gbs": round(share / hash_s / 1e9, 1) if runs else None,
+                         "frac_input_basis": (round(share / hash_s / 1e9 / HBM_PEAK_GBS, 4)
+                                              if runs else None),
                          "ref_hashed_bytes_per_pass": ref_hashed,
                          "frac_ref_hashed": round(ref_hashed / hash_s / 1e9 / HBM_PEAK_GBS, 4),
                          "lane_hashed_bytes_per_pass": lane_hashed,
@@ -585,8 +609,11 @@ def run_c4(args, torch, dist, dev, rank, world, local):
                          "valu_per_lane_byte": c4_sq.get("valu_per_lane_byte"),
                          "limiter": "VALU issue (~7 VALU + 2 LDS reads per hashed byte; "
                                     "DESIGN.md 3)"},
-            "parity": {"files_checked": int(checked[0]), "mismatches": int(checked[1]),
-                       "checker": "oracle/cdc_ref on a seeded sample of 64 files"},
+            "parity": {"files_checked": int(checked[0]), "files_total": len(sizes),
+                       "mismatches": int(checked[1]), "cuts_diffed": int(checked[2]),
+                       "seconds_rank0": round(parity_acc[3], 2),
+                       "checker": "oracle/cdc_ref on every file of every rank's share "
+                                  "(untimed, after the timed passes)"},
         }
         if world == 1 and not args.no_cpu_baseline and sample_cuts:
             from rustic_core_amd.device import pack_offsets
@@ -897,20 +924,34 @@ def main():
         lane_hashed = info["scanned_bytes"] + 64 * info["segments"]
         kernel = "rcdc_scan_kernel"
     traffic, pmc = pmc_traffic(args.workload, kernel)
+    # The headline fraction is north_star's: HBM bytes READ per launch (rocprof
+    # FETCH_SIZE, calibrated for gfx950, profiles/pmc_<workload>.json) / kernel
+    # time / 8 TB/s -- a real bandwidth fraction, never above 1.  Without a PMC
+    # file for the workload, the bytes the lanes read stand in (they are within
+    # ~1 % of FETCH on C3/C4).  The input-basis rate (input bytes / time:
+    # the kernel skips the min prefixes the reference skips) is beside it.
+    read_bytes = (pmc or {}).get("hbm_read_bytes_per_launch") if traffic else None
+    phys = read_bytes if read_bytes else lane_hashed
     roofline = {
         "bound": "hbm",
         "kernel": kernel,
-        "achieved": round(achieved, 1),
+        "achieved": round(phys / scan_s / 1e9, 1),
         "peak": HBM_PEAK_GBS,
         "unit": "GB/s",
-        "frac": round(achieved / HBM_PEAK_GBS, 4),
+        "frac": round(phys / scan_s / 1e9 / HBM_PEAK_GBS, 4),
+        "basis": ("HBM bytes read per launch: rocprof FETCH_SIZE (calibrated) of this kernel "
+                  "on this workload (traffic_source) / HIP-event kernel time"
+                  if read_bytes else
+                  "bytes the lanes read per launch (device work counters) / HIP-event kernel "
+                  "time (no PMC file for this workload)"),
         "traffic": traffic,
-        # HBM bytes the PMC counters saw (FETCH_SIZE calibrated + WRITE_SIZE,
-        # profiles/pmc_<workload>.json) / kernel time: the physical fraction
-        "frac_fetch": round(traffic / scan_s / 1e9 / HBM_PEAK_GBS, 4) if traffic else None,
+        "frac_fetch": round(read_bytes / scan_s / 1e9 / HBM_PEAK_GBS, 4) if read_bytes else None,
         "algorithmic_bytes_per_launch": in_bytes,
-        "basis": "input bytes per launch (SURVEY.md 8(d)); the kernel skips what the reference "
-                 "skips, so hashed-byte rates are reported beside it",
+        "achieved_input_basis_gbs": round(achieved, 1),
+        "frac_input_basis": round(achieved / HBM_PEAK_GBS, 4),
+        "input_basis_note": "input bytes per launch (SURVEY.md 8(d)) / kernel time: the kernel "
+                            "skips the min prefixes the reference skips, so this exceeds the "
+                            "bytes read",
         "kernel_us_per_launch": round(scan_s * 1e6, 2),
         "timed_launches": runs,
         ("chain_us_per_launch" if walked else "resolve_us_per_launch"):
@@ -946,7 +987,6 @@ def main():
             "algorithmic_bytes_per_launch": read,
             "basis": "bytes the walk reads (zone windows + 64-B zero-run prefill windows); "
                      "input-basis rate beside it",
-            "input_basis_gbs": round(achieved, 1),
             "limiter": "latency of the zero-run hops (64 chunks per wave step), not bandwidth",
         })
 
@@ -964,8 +1004,10 @@ def main():
                                          world == 1 and not args.no_cpu_baseline)
     if args.pack and rank == 0:
         out_extra["pack"] = pack_measure(torch, plan, arena, offs, lens, dev, args)
-    if rank == 0 and not args.no_ingest and (
-            args.ingest or (args.workload == "C3" and world == 1)):
+    # the backup data path is measured through the native engine (the C ABI's
+    # rcdc_ingest_*, the `h2h` object); --ingest adds the Python/torch
+    # device-resident variant (rustic_core_amd.ingest, a test reference)
+    if rank == 0 and args.ingest and not args.no_ingest:
         out_extra["ingest"] = ingest_measure(torch, arena, offs, lens, dev, args)
     if rank == 0 and world == 1 and args.workload == "C3" and not args.no_h2h:
         out_extra["h2h"] = h2h_measure(args)
@@ -1052,16 +1094,55 @@ def h2h_measure(args) -> dict:
         files = max(min(fit, files), 4)
     with tempfile.TemporaryDirectory(prefix="rcdc_h2h_", dir=tmp) as d:
         out = os.path.join(d, "h2h.json")
-        r = subprocess.run([tool, "--dir", os.path.join(d, "files"), "--files", str(files),
-                            "--file-mib", "1024", "--json", out],
+        cuts_out = os.path.join(d, "cuts.bin")
+        fdir = os.path.join(d, "files")
+        r = subprocess.run([tool, "--dir", fdir, "--files", str(files), "--file-mib", "1024",
+                            "--json", out, "--keep", "--cuts-out", cuts_out],
                            capture_output=True, text=True, timeout=600)
         if r.returncode not in (0, 3) or not os.path.exists(out):
             return {"error": f"ingest_e2e rc {r.returncode}: {r.stderr[-500:]}"}
         res = json.loads(open(out).read())
+        if not args.no_parity and os.path.exists(cuts_out):
+            res["checks"]["oracle"] = h2h_oracle_diff(fdir, cuts_out, files)
     if files != args.h2h_files:
         res["files_reduced_for_disk"] = {"asked": args.h2h_files, "ran": files}
     res["log"] = r.stderr.strip().splitlines()[-4:]
     return res
+
+
+def h2h_oracle_diff(fdir: str, cuts_path: str, nfiles: int) -> dict:
+    """The h2h run's cut lists (tools/ingest_e2e --cuts-out, the checked
+    run) against the oracle, every file re-read from disk: untimed."""
+    from oracle import oracle
+    t0 = time.perf_counter()
+    raw = np.fromfile(cuts_path, dtype=np.uint64)
+    got, i = {}, 0
+    while i < raw.size:
+        f, n = int(raw[i]), int(raw[i + 1])
+        got[f] = raw[i + 2:i + 2 + n]
+        i += 2 + n
+    threads = cpu_threads()[0]
+    bad = diffed = 0
+    group = 16  # files of 1 GiB per host batch
+    for a in range(0, nfiles, group):
+        fs = list(range(a, min(a + group, nfiles)))
+        data = [np.fromfile(os.path.join(fdir, f"f{f}"), dtype=np.uint8) for f in fs]
+        hoffs, pos = [], 0
+        for x in data:
+            hoffs.append(pos)
+            pos += (x.size + 255) // 256 * 256
+        host = np.empty(max(pos, 1), np.uint8)
+        for o, x in zip(hoffs, data):
+            host[o:o + x.size] = x
+        want = oracle.chunk_many_cuts(host, hoffs, [x.size for x in data], POLY, MIN, AVG, MAX,
+                                      nthreads=threads)
+        for f, w in zip(fs, want):
+            bad += f not in got or not np.array_equal(got[f], w)
+            diffed += len(w)
+        del host, data
+    return {"files_checked": nfiles, "mismatches": bad, "cuts_diffed": diffed,
+            "seconds": round(time.perf_counter() - t0, 2),
+            "checker": f"oracle/cdc_ref on {threads} host threads, every file re-read from disk"}
 
 
 def sha_measure(torch, plan, ptr, sptr, dev, args, arena, offs, lens, cpu: bool) -> dict:
@@ -1549,12 +1630,25 @@ def parity_check(args, arena, offs, lens, plan, last, desc) -> dict:
     n = len(lens)
     if args.parity_streams:
         n = min(len(lens), args.parity_streams)
-    import torch
     threads = cpu_threads()[0]
-    bad = diffed = 0
     t0 = time.perf_counter()
-    # every stream, in host batches of <= 16 GiB (D2H copy, then the oracle on
-    # the host's threads, one stream per thread as archiver.rs:195)
+    bad, diffed = oracle_diff(arena, offs[:n], lens[:n], got[:n], threads)
+    return {"streams_checked": n, "streams_total": int(len(lens)), "mismatches": bad,
+            "cuts_diffed": int(diffed), "cuts_total": int(sum(len(x) for x in got)),
+            "seconds": round(time.perf_counter() - t0, 2),
+            "checker": f"oracle/cdc_ref reference-equivalent mode on {threads} host threads, "
+                       "every stream of the measured run"}
+
+
+def oracle_diff(arena, offs, lens, got, threads: int):
+    """Diff device cut lists got[k] of streams [offs[k], +lens[k]) of the
+    device arena against the oracle: in host batches of <= 16 GiB (D2H
+    copy, then the oracle on the host's threads, one stream per thread as
+    archiver.rs:195).  Returns (streams that differ, cuts diffed)."""
+    import torch
+    from oracle import oracle
+    n = len(lens)
+    bad = diffed = 0
     i = 0
     while i < n:
         j, tot = i, 0
@@ -1577,11 +1671,7 @@ def parity_check(args, arena, offs, lens, plan, last, desc) -> dict:
             diffed += len(w)
         del host, ht
         i = j
-    return {"streams_checked": n, "streams_total": int(len(lens)), "mismatches": bad,
-            "cuts_diffed": int(diffed), "cuts_total": int(sum(len(x) for x in got)),
-            "seconds": round(time.perf_counter() - t0, 2),
-            "checker": f"oracle/cdc_ref reference-equivalent mode on {threads} host threads, "
-                       "every stream of the measured run"}
+    return bad, diffed
 
 
 def e2e_rate(torch, arena, offs, lens, plan, workload, reps: int = 5) -> dict:

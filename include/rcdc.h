@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define RCDC_ABI_VERSION 4u
+#define RCDC_ABI_VERSION 5u
 
 /* Status codes map onto rustic_core ErrorKind (crates/core/src/error.rs:108-124). */
 typedef enum {
@@ -488,29 +488,49 @@ rcdc_status rcdc_zstd_check(rcdc_ctx *ctx, const void *d_frames, const void *d_d
 void rcdc_zstd_tables(void *out);
 uint64_t rcdc_zstd_tables_size(void);
 
-/* ---- the backup data path, host memory to host memory (ABI 4) ----------
+/* ---- the backup data path, host memory to host memory (ABI 4, 5) -------
  * FileArchiver::backup_reader (archiver/file_archiver.rs:144-160) for many
  * files: chunk, `hash(&chunk)`, `index.has_data`, Packer::add -- zstd at the
  * repository's level, Key::encrypt_data, extra_verify (backend/decrypt.rs:
  * 478-529) -- PackSizer / should_save (blob/packer.rs:65-200, 659-671), the
  * sealed header (:693-735) and the pack id, SHA-256 of the pack file
- * (hash_reader, :826-836).  One engine per backup: the packer stays open
- * across files and batches, and rcdc_ingest_finish closes the last pack
- * (Packer::finalize, :385-398).
+ * (hash_reader, :826-836).  One engine per backup (per device): the packer
+ * stays open across files and batches, and rcdc_ingest_finish closes the
+ * last pack (Packer::finalize, :385-398).
  *
- * Files enter page-locked input slots: rcdc_ingest_reserve hands out space
- * for one file of known size (the node's size; the reference's size_hint),
- * the caller reads the file into it (the Read of rabin.rs:110-191) and
- * rcdc_ingest_commit hands it over (fewer bytes than reserved are fine).
+ * Files enter page-locked input slots.  Two ways in:
+ *  - a file of known size: rcdc_ingest_reserve hands out space for it (the
+ *    node's size; at most batch_bytes), the caller reads the file into it
+ *    (the Read of rabin.rs:110-191) and rcdc_ingest_commit hands it over
+ *    (fewer bytes than reserved are fine);
+ *  - any Read, of any or unknown length (a file larger than a batch, stdin,
+ *    a child's stdout: commands/backup.rs:336-346): rcdc_ingest_stream_open,
+ *    then pieces -- rcdc_ingest_stream_reserve + rcdc_ingest_commit, each
+ *    piece any size up to batch_bytes, the stream's bytes in reservation
+ *    order -- then rcdc_ingest_stream_close (EOF).  The size is only a hint
+ *    (chunker.rs:22-47, size_hint): cuts never depend on how the bytes were
+ *    split into pieces or batches.  The engine carries each stream's open
+ *    chunk (at most max bytes) from batch to batch on the device, as
+ *    rcdc_stream_feed does for the chunk-only path.
  * Reserve / commit may be called from many threads (archiver.rs:195).  A
- * slot that fills becomes a device batch: H2D, chunking, the short chunks'
- * ids on the device, the long ones' on host threads, zstd + seal + verify of
- * every chunk, then (once the ids are in) dedup in chunk order, packs, D2H
- * and the pack ids on host threads.  Results come back through callbacks:
- * per file its cut offsets and chunk ids in file order (the tree's content
- * list), per pack the pack file in host memory (valid during the call), its
- * id and its index entries.  Callbacks run on the engine's threads, one at a
- * time.                                                                    */
+ * reservation whose read fails is dropped with rcdc_ingest_cancel (the
+ * reference logs and skips the file, archiver.rs:197-203); a stream whose
+ * read fails is ended with rcdc_ingest_stream_abort (the chunks it completed
+ * before the error stay packed, as the reference's Packer::add calls did).
+ * A slot that fills (or whose first file is slot_max_age_ms old) becomes a
+ * device batch: H2D, chunking, the short chunks' ids on the device, the long
+ * ones' on host threads, zstd + seal + verify of every chunk, then (once the
+ * ids are in) dedup in chunk order, packs, D2H and the pack ids on host
+ * threads.  Results come back through callbacks: per file (or stream) its
+ * cut offsets and chunk ids in file order (the tree's content list), per
+ * pack the pack file in host memory (valid during the call), its id and its
+ * index entries.  Callbacks run on the engine's threads, one at a time.
+ *
+ * Memory (rcdc_ingest_footprint gives the exact figures for a config):
+ * page-locked in_slots x batch_bytes + out_slots x (batch_bytes + 1/16 +
+ * 64 MiB) -- about 21 GiB at the defaults (4 + 6 slots of 2 GiB) -- and
+ * device depth x (2 x batch_bytes + max_streams x max) plus ~2.1 batches of
+ * compression / pack buffers (~21 GiB at the defaults on a 288 GB GPU).     */
 typedef struct rcdc_ingest rcdc_ingest;
 
 typedef struct {
@@ -518,7 +538,7 @@ typedef struct {
     int32_t zstd_level;         /* repository version 2: zstd level (0 = zstd's 3)     */
     uint32_t compress;          /* 1: version 2 compression; 0: stored blobs           */
     uint32_t extra_verify;      /* 1: decrypt, decode and compare every blob (default) */
-    uint32_t hash_threads;      /* host SHA-256 threads (default 8)                    */
+    uint32_t hash_threads;      /* host SHA-256 threads (default 10)                   */
     uint64_t pack_size;         /* PackSizer (configfile.rs:211-231): default 32 MiB,  */
     uint64_t pack_grow_factor;  /*   grow factor 32,                                    */
     uint64_t pack_size_limit;   /*   limit u32::MAX,                                    */
@@ -526,9 +546,14 @@ typedef struct {
     uint64_t batch_bytes;       /* input slot / device batch bytes (default 2 GiB)     */
     uint32_t depth;             /* batches in flight on the device (default 4)         */
     uint32_t in_slots;          /* page-locked input slots (default 4)                 */
-    uint32_t out_slots;         /* page-locked pack buffers (default 4)                */
-    uint32_t pad;
+    uint32_t out_slots;         /* page-locked pack buffers (default 6)                */
+    uint32_t max_streams;       /* streams open at once (default 16; each holds a
+                                   device carry of max bytes)                          */
     uint64_t long_chunk;        /* chunks above this get their id on the host (2 MiB) */
+    uint32_t pack_max_age_ms;   /* should_save's MAX_AGE (packer.rs:63,668-670): an open
+                                   pack this old is saved (default 300000 = 5 min)      */
+    uint32_t slot_max_age_ms;   /* an open input slot whose first file is this old is
+                                   submitted unfilled (default 1000)                   */
 } rcdc_ingest_config;
 
 typedef struct {
@@ -549,7 +574,7 @@ typedef struct {
 } rcdc_ingest_pack;
 
 typedef struct {
-    uint64_t tag;                 /* the caller's, from rcdc_ingest_commit         */
+    uint64_t tag;                 /* the caller's (rcdc_ingest_commit / _stream_open) */
     uint64_t len;
     uint32_t nchunks, nnew;       /* chunks; those the packer added                */
     const uint64_t *cuts;         /* end offset of each chunk in the file          */
@@ -565,8 +590,14 @@ typedef void (*rcdc_ingest_pack_fn)(void *user, const rcdc_ingest_pack *pack);
 typedef void (*rcdc_ingest_file_fn)(void *user, const rcdc_ingest_file_result *file);
 
 void rcdc_ingest_config_default(rcdc_ingest_config *cfg);
+/* Bytes rcdc_ingest_create allocates for cfg on ctx: page-locked host memory
+ * and device memory (the engine's own buffers; the context's scratch and the
+ * plans' work lists come on top).                                          */
+rcdc_status rcdc_ingest_footprint(const rcdc_ctx *ctx, const rcdc_ingest_config *cfg,
+                                  uint64_t *pinned_bytes, uint64_t *device_bytes);
 /* Allocates the slots (page-locked and device memory for a full batch
- * each) and starts the engine's threads.                                   */
+ * each) and starts the engine's threads.  On failure nothing stays
+ * allocated.                                                               */
 rcdc_status rcdc_ingest_create(rcdc_ctx *ctx, const rcdc_ingest_config *cfg,
                                rcdc_ingest_pack_fn pack_cb, rcdc_ingest_file_fn file_cb,
                                void *user, rcdc_ingest **out);
@@ -574,17 +605,66 @@ rcdc_status rcdc_ingest_create(rcdc_ctx *ctx, const rcdc_ingest_config *cfg,
 rcdc_status rcdc_ingest_add_index(rcdc_ingest *ing, const uint8_t *ids, uint64_t n);
 /* Space for one file of len bytes (<= batch_bytes); waits for a free slot. */
 rcdc_status rcdc_ingest_reserve(rcdc_ingest *ing, uint64_t len, uint8_t **buf, uint64_t *ticket);
-/* The file's bytes are in place: its first len bytes (<= the reservation). */
+/* The file's (or piece's) bytes are in place: its first len bytes (<= the
+ * reservation).  tag: the file's (ignored for a stream piece). */
 rcdc_status rcdc_ingest_commit(rcdc_ingest *ing, uint64_t ticket, uint64_t tag, uint64_t len);
-/* reserve + memcpy + commit of a file already in memory. */
+/* Drop a reservation that will not be committed (its read failed): no
+ * result for it, and rcdc_ingest_finish does not wait for it.  For a stream
+ * piece: the piece is empty (end the stream with rcdc_ingest_stream_abort). */
+rcdc_status rcdc_ingest_cancel(rcdc_ingest *ing, uint64_t ticket);
+/* reserve + memcpy + commit of a file already in memory (a file larger than
+ * batch_bytes goes in as a stream of pieces). */
 rcdc_status rcdc_ingest_add(rcdc_ingest *ing, uint64_t tag, const void *data, uint64_t len);
+
+/* One file (any Read) fed in pieces: ChunkIter::from_config(cfg, reader,
+ * size_hint) (chunker.rs:22-47) + its iterator (rabin.rs:110-191).  size_hint
+ * is only a hint (0: unknown).  Waits while max_streams streams are closing;
+ * RCDC_ERR_UNSUPPORTED if max_streams are open.  *stream: the handle.      */
+rcdc_status rcdc_ingest_stream_open(rcdc_ingest *ing, uint64_t tag, uint64_t size_hint,
+                                    uint64_t *stream);
+/* Space for the stream's next len bytes (<= batch_bytes); commit it with
+ * rcdc_ingest_commit(ticket, 0, n).  Consecutive pieces of one stream that
+ * land in the same slot are laid out back to back. */
+rcdc_status rcdc_ingest_stream_reserve(rcdc_ingest *ing, uint64_t stream, uint64_t len,
+                                       uint8_t **buf, uint64_t *ticket);
+/* EOF (Ok(0), rabin.rs:164-166): the stream's last chunk ends at its last
+ * byte, and its file result (all cuts and ids, in order) follows.  Every
+ * piece must be committed or cancelled first.  The handle is then invalid. */
+rcdc_status rcdc_ingest_stream_close(rcdc_ingest *ing, uint64_t stream);
+/* The stream's read failed: the chunk in progress is dropped, no file
+ * result is delivered; chunks it completed before stay packed.  The handle
+ * is then invalid. */
+rcdc_status rcdc_ingest_stream_abort(rcdc_ingest *ing, uint64_t stream);
+
 /* Submit the partly filled slot now. */
 rcdc_status rcdc_ingest_flush(rcdc_ingest *ing);
 /* No more files: process everything, close the last pack, wait for every
  * callback; stats (optional) receives the totals.  A verification failure
- * is RCDC_ERR_VERIFICATION.                                                */
+ * is RCDC_ERR_VERIFICATION.  Every stream must be closed or aborted.       */
 rcdc_status rcdc_ingest_finish(rcdc_ingest *ing, rcdc_ingest_stats *stats);
 void rcdc_ingest_destroy(rcdc_ingest *ing);
+
+/* ---- one dedup set for several engines (multi-device ingest) ------------
+ * The reference has ONE Packer per backup, so a blob is stored once however
+ * many file workers found it (archiver.rs:195, blob/packer.rs:304-315, the
+ * index check of file_archiver.rs:153).  N engines -- one per GPU, fed by a
+ * file router -- keep that property by sharing one id set: an engine packs
+ * a chunk only if its insert into the set is the first.  The set is
+ * thread-safe (sharded locks).                                             */
+typedef struct rcdc_index rcdc_index;
+rcdc_status rcdc_index_create(rcdc_index **out);
+void rcdc_index_destroy(rcdc_index *idx);       /* after every engine using it */
+/* Ids the repository already has (Indexer::has). */
+rcdc_status rcdc_index_add(rcdc_index *idx, const uint8_t *ids, uint64_t n);
+uint64_t rcdc_index_size(const rcdc_index *idx);
+/* Dedup against idx (not the engine's own set) from now on; before the
+ * engine's first batch.  Ids already given to rcdc_ingest_add_index move
+ * into idx.                                                                */
+rcdc_status rcdc_ingest_set_index(rcdc_ingest *ing, rcdc_index *idx);
+
+/* Page-locked and device bytes currently held by all ingest engines of the
+ * process (their own buffers, as rcdc_ingest_footprint counts them).        */
+void rcdc_ingest_mem_live(uint64_t *pinned_bytes, uint64_t *device_bytes);
 
 /* SHA-256 of one host buffer on the calling thread (SHA extensions when the
  * CPU has them): a pack id (packer.rs:832-834) where latency matters.      */

@@ -32,9 +32,12 @@ EXPORTS = (
     "rcdc_ingest_config_default", "rcdc_ingest_create", "rcdc_ingest_add_index",
     "rcdc_ingest_reserve", "rcdc_ingest_commit", "rcdc_ingest_add", "rcdc_ingest_flush",
     "rcdc_ingest_finish", "rcdc_ingest_destroy", "rcdc_sha256_host_one",
-    "rcdc_sha256_host_ni",
+    "rcdc_sha256_host_ni", "rcdc_ingest_cancel", "rcdc_ingest_stream_open",
+    "rcdc_ingest_stream_reserve", "rcdc_ingest_stream_close", "rcdc_ingest_stream_abort",
+    "rcdc_ingest_footprint", "rcdc_ingest_mem_live", "rcdc_index_create", "rcdc_index_destroy",
+    "rcdc_index_add", "rcdc_index_size", "rcdc_ingest_set_index",
 )
-ABI_VERSION = 4
+ABI_VERSION = 5
 
 
 class RcdcLibraryError(RuntimeError):
@@ -205,6 +208,30 @@ def lib() -> ctypes.CDLL:
     L.rcdc_sha256_host_one.argtypes = [vp, u64, vp]
     L.rcdc_sha256_host_ni.restype = st
     L.rcdc_sha256_host_ni.argtypes = [vp, vp, u32, u32, vp]
+    L.rcdc_ingest_cancel.restype = st
+    L.rcdc_ingest_cancel.argtypes = [vp, u64]
+    L.rcdc_ingest_stream_open.restype = st
+    L.rcdc_ingest_stream_open.argtypes = [vp, u64, u64, P(u64)]
+    L.rcdc_ingest_stream_reserve.restype = st
+    L.rcdc_ingest_stream_reserve.argtypes = [vp, u64, u64, P(vp), P(u64)]
+    L.rcdc_ingest_stream_close.restype = st
+    L.rcdc_ingest_stream_close.argtypes = [vp, u64]
+    L.rcdc_ingest_stream_abort.restype = st
+    L.rcdc_ingest_stream_abort.argtypes = [vp, u64]
+    L.rcdc_ingest_footprint.restype = st
+    L.rcdc_ingest_footprint.argtypes = [vp, vp, P(u64), P(u64)]
+    L.rcdc_ingest_mem_live.restype = None
+    L.rcdc_ingest_mem_live.argtypes = [P(u64), P(u64)]
+    L.rcdc_index_create.restype = st
+    L.rcdc_index_create.argtypes = [P(vp)]
+    L.rcdc_index_destroy.restype = None
+    L.rcdc_index_destroy.argtypes = [vp]
+    L.rcdc_index_add.restype = st
+    L.rcdc_index_add.argtypes = [vp, vp, u64]
+    L.rcdc_index_size.restype = u64
+    L.rcdc_index_size.argtypes = [vp]
+    L.rcdc_ingest_set_index.restype = st
+    L.rcdc_ingest_set_index.argtypes = [vp, vp]
     L.rcdc_plan_window.restype = st
     L.rcdc_plan_window.argtypes = [vp, u32, u64, u32, vp, vp]
     L.rcdc_plan_device_digests.restype = st

@@ -28,6 +28,17 @@
 //                pool, whose last job per pack calls the caller's callback.
 // Stage A of batch b + 1 .. b + depth - 1 runs before stage B of batch b, so
 // the short ids' device chains of several batches overlap.
+//
+// Streams (rcdc_ingest_stream_*): a file of any length arrives as pieces in
+// several slots.  Each batch chunks a stream's bytes of that batch after
+// its carry -- the open chunk of the previous batch, at most max bytes, kept
+// in a device carry slot (and a host copy for host-hashed ids) -- as one
+// plan stream; all but the last chunk are final (a cut at L depends only on
+// the bytes before L and the chunk start, rabin.rs:153-188), the last one
+// becomes the next carry.  Pieces that are not contiguous in the slot, or
+// follow a carry, are gathered into the arena's assembly region first
+// (one D2D copy at HBM rate, against the piece's PCIe copy).  Slots holding
+// stream pieces enter the pipeline in the order they closed.
 #include <hip/hip_runtime.h>
 
 #include <sys/random.h>
@@ -46,6 +57,7 @@
 #include <mutex>
 #include <string>
 #include <thread>
+#include <unordered_map>
 #include <unordered_set>
 #include <vector>
 
@@ -56,6 +68,7 @@ rcdc_status plan_relayout(rcdc_plan *pl, const uint64_t *offs, const uint64_t *l
                           uint64_t arena_len, hipStream_t up);
 int ctx_device(const rcdc_ctx *ctx);
 uint64_t ctx_min_size(const rcdc_ctx *ctx);
+uint64_t ctx_max_size(const rcdc_ctx *ctx);
 rcdc_status set_error(rcdc_status st, const char *msg);
 void host_sha256_many(const uint8_t *const *ptrs, const uint64_t *lens, uint32_t n,
                       uint8_t *digests);
@@ -113,12 +126,48 @@ struct PackSizer {
     }
 };
 
+// One stream (rcdc_ingest_stream_open .. close): its carry between batches
+// and its results so far.  Fields by owner: `fed`, `open_pieces`, `closed`
+// under the engine's mutex (callers); `base`, `carry_len`, `hcarry`,
+// `cslot` on the worker thread (stage A, in batch order); `cuts`, `ids`,
+// `nnew` on the back thread (stage B, in batch order).
+struct StreamSt {
+    uint64_t handle = 0, tag = 0, hint = 0;
+    uint64_t fed = 0;          // bytes committed
+    uint32_t open_pieces = 0;  // reserved, not committed or cancelled
+    bool closed = false, aborted = false;
+    int cslot = -1;            // device carry slot
+    uint64_t base = 0;         // stream offset of the carry's first byte (the last final cut)
+    uint64_t carry_len = 0;
+    std::vector<uint8_t> hcarry;
+    std::vector<uint64_t> cuts;
+    std::vector<uint8_t> ids;
+    uint32_t nnew = 0;
+};
+
 struct FileEnt {
     uint64_t tag = 0;
-    uint64_t off = 0;   // in the batch (256-aligned)
+    uint64_t off = 0;   // in the batch (whole files 256-aligned)
     uint64_t res = 0;   // bytes reserved
     uint64_t len = 0;   // bytes committed
     bool done = false;
+    bool cancelled = false;
+    bool final = false;  // a stream's end (close / abort): zero bytes
+    std::shared_ptr<StreamSt> st;  // null: a whole file
+};
+
+// One plan stream of a batch: a whole file in place, or a stream's bytes of
+// this batch (after its carry), in place or gathered in the assembly region.
+struct Unit {
+    uint64_t tag = 0;
+    std::shared_ptr<StreamSt> st;
+    bool final = true, aborted = false;
+    uint64_t base = 0;       // stream offset of the unit's first byte
+    uint64_t carry = 0;      // leading carry bytes
+    uint64_t off = 0, len = 0;
+    uint64_t fresh = 0;      // bytes new in this batch
+    std::vector<std::pair<uint64_t, uint64_t>> segs;          // (slot offset, len)
+    std::vector<std::pair<const uint8_t *, uint64_t>> host;   // the unit's bytes in host memory
 };
 
 enum SlotState { kFree = 0, kOpen, kClosed, kSubmitted };
@@ -133,6 +182,9 @@ struct InSlot {
     bool h2d_pending = false;
     std::atomic<int> host_jobs{0};  // long-id jobs still reading this slot
     std::atomic<bool> h2d_issued{false};  // its last H2D piece and h2d are enqueued
+    uint64_t close_seq = 0;
+    bool has_stream = false;        // holds stream pieces: enters the pipeline in close order
+    double t_first = 0;             // its first reservation (slot_max_age_ms)
 };
 
 // A batch between stage A and stage B.
@@ -141,9 +193,12 @@ struct Batch {
     uint32_t pslot = 0;             // pipeline slot (device buffers, plan)
     InSlot *in = nullptr;
     std::vector<FileEnt> files;
-    std::vector<uint64_t> cuts;     // per file, consecutive (relative to the file)
-    std::vector<uint32_t> ncuts;    // per file
+    std::vector<Unit> units;
+    std::vector<uint64_t> cuts;     // per unit, consecutive (relative to the unit)
+    std::vector<uint32_t> ncuts;    // per unit: chunks final in this batch
     std::vector<uint64_t> c_off, c_len;  // per chunk: arena offset, length
+    std::vector<const uint8_t *> c_host;  // long chunks: their bytes in host memory
+    std::vector<std::vector<uint8_t>> gathers;  // long chunks split over host pieces
     std::vector<uint8_t> ids;            // 32 B per chunk
     std::vector<uint32_t> short_idx;     // chunks whose ids the device computes
     std::vector<uint64_t> seal_off, seal_len, ulen;
@@ -187,6 +242,31 @@ struct PackJob {
 
 }  // namespace
 
+// One dedup set (the packer's ids + the index's), shareable by the engines of
+// several devices: 64 shards, one lock each.
+struct rcdc_index {
+    static constexpr int kShards = 64;
+    struct Shard {
+        std::mutex mu;
+        std::unordered_set<Id32, Id32Hash> set;
+    };
+    Shard sh[kShards];
+    // true: the id was not in the set (the caller packs it)
+    bool insert(const Id32 &id) {
+        Shard &s = sh[id.b[31] & (kShards - 1)];
+        std::lock_guard<std::mutex> lk(s.mu);
+        return s.set.insert(id).second;
+    }
+    uint64_t size() {
+        uint64_t n = 0;
+        for (auto &s : sh) {
+            std::lock_guard<std::mutex> lk(s.mu);
+            n += s.set.size();
+        }
+        return n;
+    }
+};
+
 struct rcdc_ingest {
     rcdc_ctx *ctx = nullptr;
     rcdc_ingest_config cfg{};
@@ -226,7 +306,22 @@ struct rcdc_ingest {
     uint64_t nclosed = 0;                          // input slots closed so far
     hipStream_t s_back = nullptr;                  // stage B's device work
     uint64_t nbatches = 0, next_seq = 0;
-    std::unordered_set<Id32, Id32Hash> known;  // the index's ids + the packer's
+    rcdc_index *idx = nullptr;  // the index's ids + the packer's (own, or shared)
+    bool own_idx = true;
+    // streams
+    uint64_t max_chunk = 0;          // ctx max: a carry's bound
+    uint64_t asm_base = 0, asm_cap = 0;  // the arena's assembly region
+    uint8_t *carry_pool = nullptr;   // max_streams device carry slots of max_chunk bytes
+    std::vector<int> free_cslots;
+    std::unordered_map<uint64_t, std::shared_ptr<StreamSt>> streams;  // open handles
+    uint64_t next_stream = 1;
+    uint32_t closing_streams = 0;    // closed, carry slot not yet released
+    std::deque<InSlot *> closed_q;   // closed slots not yet ready, in close order
+    double pack_t0 = 0;              // the open pack's first blob (MAX_AGE)
+    double pack_max_age = 300, slot_max_age = 1;
+    // allocations of this engine (rcdc_ingest_mem_live); RCDC_INGEST_FAIL_ALLOC
+    // = k fails the k-th allocation of create (tests)
+    uint32_t nalloc = 0, fail_alloc = 0;
     // threads
     std::thread worker, back, waiter, feeder;
     // the feeder's copy pump: batches waiting for their H2D pieces
@@ -313,6 +408,50 @@ void set_err(Ing *g, rcdc_status s, const std::string &m) {
         }                                                                                 \
     } while (0)
 
+// ---- the engine's allocations: counted (rcdc_ingest_mem_live), freed on
+// every path (free_all), and failable on demand (RCDC_INGEST_FAIL_ALLOC)
+std::mutex g_alloc_mu;
+std::unordered_map<void *, std::pair<uint64_t, bool>> g_allocs;  // ptr -> (bytes, pinned)
+uint64_t g_live_pinned = 0, g_live_dev = 0;
+
+hipError_t ing_alloc(Ing *g, void **p, uint64_t n, bool pinned) {
+    *p = nullptr;
+    if (g && g->fail_alloc && ++g->nalloc == g->fail_alloc) return hipErrorOutOfMemory;
+    const hipError_t e = pinned ? hipHostMalloc(p, n, hipHostMallocDefault) : hipMalloc(p, n);
+    if (e != hipSuccess) {
+        *p = nullptr;
+        return e;
+    }
+    std::lock_guard<std::mutex> lk(g_alloc_mu);
+    g_allocs[*p] = {n, pinned};
+    (pinned ? g_live_pinned : g_live_dev) += n;
+    return hipSuccess;
+}
+
+template <typename T>
+hipError_t ing_alloc(Ing *g, T **p, uint64_t n, bool pinned) {
+    return ing_alloc(g, (void **)p, n, pinned);
+}
+
+// Frees and nulls *p (no-op on null).
+template <typename T>
+hipError_t ing_free(T **p) {
+    if (!*p) return hipSuccess;
+    void *q = (void *)*p;
+    *p = nullptr;
+    bool pinned = false;
+    {
+        std::lock_guard<std::mutex> lk(g_alloc_mu);
+        auto it = g_allocs.find(q);
+        if (it != g_allocs.end()) {
+            pinned = it->second.second;
+            (pinned ? g_live_pinned : g_live_dev) -= it->second.first;
+            g_allocs.erase(it);
+        }
+    }
+    return pinned ? hipHostFree(q) : hipFree(q);
+}
+
 template <typename T>
 bool ensure_dev(Ing *g, T **p, uint64_t *cap, uint64_t need) {
     if (*p && *cap >= need) return true;
@@ -320,11 +459,10 @@ bool ensure_dev(Ing *g, T **p, uint64_t *cap, uint64_t need) {
     if (log && *p)
         fprintf(stderr, "rcdc ingest: regrow %llu -> %llu x %zu B (hipFree: device sync)\n",
                 (unsigned long long)*cap, (unsigned long long)need, sizeof(T));
-    if (*p) ING_HIP(g, hipFree(*p));
-    *p = nullptr;
+    ING_HIP(g, ing_free(p));
     *cap = 0;
     const uint64_t n = need + need / 8 + 1;
-    ING_HIP(g, hipMalloc((void **)p, n * sizeof(T)));
+    ING_HIP(g, ing_alloc(g, p, n * sizeof(T), false));
     *cap = n;
     return true;
 }
@@ -576,6 +714,7 @@ bool submit_ready(Ing *g) {
 }
 
 void reap_inputs(Ing *g);
+void close_open_locked(Ing *g);
 
 // Feeder thread: a ready input slot's H2D is enqueued as soon as a pipeline
 // slot is free, whatever stage A is doing (the front thread used to enqueue
@@ -691,6 +830,10 @@ void feeder_main(Ing *g) {
             d2h_idle = g->d2h_q.empty();
         }
         std::unique_lock<std::mutex> lk(g->mu);
+        // an open slot with files that stopped filling goes to the device
+        // (a trickle of small files is not held back until finish)
+        if (g->open && !g->open->files.empty() && now_s() - g->open->t_first >= g->slot_max_age)
+            close_open_locked(g);
         // the back thread queues D2H jobs until the very end (finalize)
         if (g->err || (g->finished && g->h2d_q.empty() && d2h_idle)) {
             lk.unlock();
@@ -702,19 +845,114 @@ void feeder_main(Ing *g) {
     }
 }
 
+// The bytes [rel, rel + len) of a unit in host memory: a pointer into one of
+// its host pieces, or null when they span pieces.
+const uint8_t *unit_host(const Unit &u, uint64_t rel, uint64_t len) {
+    uint64_t at = 0;
+    for (const auto &h : u.host) {
+        if (rel >= at && rel + len <= at + h.second) return h.first + (rel - at);
+        at += h.second;
+    }
+    return nullptr;
+}
+
+void unit_gather(const Unit &u, uint64_t rel, uint64_t len, uint8_t *dst) {
+    uint64_t at = 0;
+    for (const auto &h : u.host) {
+        const uint64_t a = std::max(rel, at), e = std::min(rel + len, at + h.second);
+        if (a < e) memcpy(dst + (a - rel), h.first + (a - at), e - a);
+        at += h.second;
+    }
+}
+
+// The batch's plan streams: whole files in place; per stream, its carry and
+// its pieces of this batch, in place when that is one contiguous piece and
+// no carry, else gathered into the assembly region (copies appended to cr).
+bool build_units(Ing *g, Batch *B, std::vector<rcdc_copy_ref> &cr, uint64_t *asm_used) {
+    InSlot *in = B->in;
+    std::unordered_map<StreamSt *, size_t> unit_of;
+    for (const FileEnt &f : B->files) {
+        if (f.cancelled) continue;
+        if (!f.st) {
+            Unit u;
+            u.tag = f.tag;
+            u.off = f.off;
+            u.len = u.fresh = f.len;
+            u.segs.push_back({f.off, f.len});
+            B->units.push_back(std::move(u));
+            continue;
+        }
+        auto it = unit_of.find(f.st.get());
+        if (it == unit_of.end()) {
+            Unit u;
+            u.st = f.st;
+            u.tag = f.st->tag;
+            u.final = false;
+            u.base = f.st->base;
+            u.carry = f.st->carry_len;
+            it = unit_of.emplace(f.st.get(), B->units.size()).first;
+            B->units.push_back(std::move(u));
+        }
+        Unit &u = B->units[it->second];
+        if (f.final) {
+            u.final = true;
+            u.aborted = f.st->aborted;
+        }
+        if (!f.len) continue;
+        if (!u.segs.empty() && u.segs.back().first + u.segs.back().second == f.off)
+            u.segs.back().second += f.len;  // laid out back to back (stream_reserve)
+        else
+            u.segs.push_back({f.off, f.len});
+        u.fresh += f.len;
+    }
+    uint64_t ao = 0;
+    for (Unit &u : B->units) {
+        if (!u.st) {
+            u.host.push_back({in->host + u.off, u.len});
+            continue;
+        }
+        u.len = u.carry + u.fresh;
+        if (!u.carry && u.segs.size() <= 1) {  // in place
+            u.off = u.segs.empty() ? 0 : u.segs[0].first;
+            if (u.fresh) u.host.push_back({in->host + u.off, u.fresh});
+            continue;
+        }
+        u.off = g->asm_base + ao;
+        uint64_t o = u.off;
+        if (u.carry) {
+            rcdc_copy_ref c{};
+            c.in_off = (uint64_t)u.st->cslot * g->max_chunk;
+            c.out_off = o;
+            c.len = u.carry;
+            c.src = 1;
+            cr.push_back(c);
+            u.host.push_back({u.st->hcarry.data(), u.carry});
+            o += u.carry;
+        }
+        for (const auto &sg : u.segs) {
+            rcdc_copy_ref c{};
+            c.in_off = sg.first;
+            c.out_off = o;
+            c.len = sg.second;
+            c.src = 0;
+            cr.push_back(c);
+            u.host.push_back({in->host + sg.first, sg.second});
+            o += sg.second;
+        }
+        ao = round_up(ao + u.len, 256);
+        if (ao > g->asm_cap) {
+            set_err(g, RCDC_ERR_INTERNAL, "ingest: assembly region overflow");
+            return false;
+        }
+    }
+    *asm_used = ao;
+    return true;
+}
+
 bool stage_a(Ing *g, Batch *B) {
     InSlot *in = B->in;
     PSlot &P = g->ps[B->pslot];
-    const uint32_t nf = (uint32_t)B->files.size();
-    std::vector<uint64_t> offs(nf), lens(nf);
-    uint64_t bytes = 0;
-    for (uint32_t i = 0; i < nf; i++) {
-        offs[i] = B->files[i].off;
-        lens[i] = B->files[i].len;
-        bytes += lens[i];
-    }
     const uint64_t used = in->used;
-    const uint64_t arena_len = round_up(used, 256) + 256;
     // 1. the H2D (the feeder's pump) lands before the chunking: wait until
     // its event is enqueued, then order the compute stream after it
     {
@@ -724,7 +962,29 @@ bool stage_a(Ing *g, Batch *B) {
     }
     ING_HIP(g, hipStreamWaitEvent(g->s_comp, in->h2d, 0));
     if (g->prof > 1) mark(g, B->index, now_s());
-    // 2. chunk
+    // 2. the plan streams; streams' carries and scattered pieces gathered
+    std::vector<rcdc_copy_ref> gcr;
+    uint64_t asm_used = 0;
+    if (!build_units(g, B, gcr, &asm_used)) return false;
+    if (!gcr.empty()) {
+        const void *gsrc[2] = {P.arena, g->carry_pool};
+        ING_ST(g, rcdc_copy_ranges(g->ctx, gsrc, 2, gcr.data(), (uint32_t)gcr.size(), P.arena,
+                                   g->s_comp),
+               "stream gather");
+    }
+    const uint32_t nf = (uint32_t)B->units.size();
+    std::vector<uint64_t> offs(nf), lens(nf);
+    uint64_t bytes = 0, ubytes = 0, nfiles = 0;
+    for (uint32_t i = 0; i < nf; i++) {
+        offs[i] = B->units[i].off;
+        lens[i] = B->units[i].len;
+        bytes += B->units[i].fresh;
+        ubytes += lens[i];
+        nfiles += !B->units[i].st || (B->units[i].final && !B->units[i].aborted);
+    }
+    const uint64_t arena_len =
+        std::max(round_up(used, 256) + 256, asm_used ? g->asm_base + asm_used + 256 : 0);
+    // 3. chunk
     if (!P.plan) {
         ING_ST(g, rcdc_plan_create(g->ctx, offs.data(), lens.data(), nf, arena_len, &P.plan),
                "plan");
@@ -738,7 +998,7 @@ bool stage_a(Ing *g, Batch *B) {
         (void)hipEventSynchronize(in->h2d);
         mark(g, B->index, now_s());
     }
-    const uint64_t cap = (uint64_t)nf + used / 4096 + 16;  // min >= 4096 (rcdc_check_params)
+    const uint64_t cap = (uint64_t)nf + ubytes / 4096 + 16;  // min >= 4096 (rcdc_check_params)
     std::vector<uint64_t> cuts(std::max<uint64_t>(cap, 1)), counts(std::max<uint32_t>(nf, 1));
     rcdc_status rs = rcdc_plan_results(P.plan, cuts.data(), cuts.size(), counts.data());
     if (rs == RCDC_ERR_CAPACITY) {
@@ -749,25 +1009,44 @@ bool stage_a(Ing *g, Batch *B) {
     }
     ING_ST(g, rs, "chunk results");
     mark(g, B->index, now_s());
-    // chunk lists
-    uint64_t nchunks = 0;
-    for (uint32_t i = 0; i < nf; i++) nchunks += counts[i];
-    B->cuts.assign(cuts.begin(), cuts.begin() + nchunks);
+    // chunk lists: a stream's last chunk of a batch (not its end) is its
+    // carry, not a chunk yet -- every earlier cut is final
     B->ncuts.resize(nf);
-    B->c_off.resize(nchunks);
-    B->c_len.resize(nchunks);
+    std::vector<rcdc_copy_ref> ccr;  // the new carries, device
+    std::vector<std::pair<Unit *, uint64_t>> carries;  // (unit, carry start in the unit)
     {
         uint64_t k = 0;
         for (uint32_t i = 0; i < nf; i++) {
-            B->ncuts[i] = (uint32_t)counts[i];
-            uint64_t prev = 0;
-            for (uint64_t j = 0; j < counts[i]; j++, k++) {
-                B->c_off[k] = offs[i] + prev;
-                B->c_len[k] = B->cuts[k] - prev;
-                prev = B->cuts[k];
+            Unit &u = B->units[i];
+            const uint64_t n = counts[i];
+            uint64_t keep = n;
+            if (u.st && (!u.final || u.aborted)) {
+                keep = n ? n - 1 : 0;
+                const uint64_t from = keep ? cuts[k + keep - 1] : 0;
+                if (!u.aborted) {
+                    carries.push_back({&u, from});
+                    if (u.len > from) {
+                        rcdc_copy_ref c{};
+                        c.in_off = u.off + from;
+                        c.out_off = (uint64_t)u.st->cslot * g->max_chunk;
+                        c.len = u.len - from;
+                        c.src = 0;
+                        ccr.push_back(c);
+                    }
+                }
             }
+            B->ncuts[i] = (uint32_t)keep;
+            uint64_t prev = 0;
+            for (uint64_t j = 0; j < keep; j++) {
+                B->cuts.push_back(cuts[k + j]);
+                B->c_off.push_back(u.off + prev);
+                B->c_len.push_back(cuts[k + j] - prev);
+                prev = cuts[k + j];
+            }
+            k += n;
         }
     }
+    const uint64_t nchunks = B->c_off.size();
     B->ids.assign(nchunks * 32, 0);
     // 3. ids: short chunks on the device (own stream per pipeline slot), long
     // ones on host threads from the input slot
@@ -790,6 +1069,53 @@ bool stage_a(Ing *g, Batch *B) {
     std::vector<uint32_t> long_idx;
     for (uint64_t k = 0; k < nchunks; k++)
         (B->c_len[k] > long_thr ? long_idx : B->short_idx).push_back((uint32_t)k);
+    // the long chunks' host bytes: in place, or gathered from a stream's
+    // host pieces (a chunk that starts in the carry) before the carries move
+    B->c_host.assign(nchunks, nullptr);
+    if (!long_idx.empty()) {
+        std::vector<uint32_t> unit_of(nchunks);
+        for (uint32_t i = 0, k = 0; i < nf; i++)
+            for (uint32_t j = 0; j < B->ncuts[i]; j++) unit_of[k++] = i;
+        for (uint32_t k : long_idx) {
+            const Unit &u = B->units[unit_of[k]];
+            const uint64_t rel = B->c_off[k] - u.off;
+            B->c_host[k] = unit_host(u, rel, B->c_len[k]);
+            if (!B->c_host[k]) {
+                B->gathers.emplace_back(B->c_len[k]);
+                unit_gather(u, rel, B->c_len[k], B->gathers.back().data());
+                B->c_host[k] = B->gathers.back().data();
+            }
+        }
+    }
+    // the streams' new carries (device: one copy; host: their bytes), and
+    // the carry slots of streams that ended
+    if (!ccr.empty()) {
+        const void *csrc[1] = {P.arena};
+        ING_ST(g, rcdc_copy_ranges(g->ctx, csrc, 1, ccr.data(), (uint32_t)ccr.size(), g->carry_pool,
+                                   g->s_comp),
+               "stream carry");
+    }
+    for (auto &c : carries) {
+        Unit &u = *c.first;
+        StreamSt &st = *u.st;
+        std::vector<uint8_t> h(u.len - c.second);
+        if (!h.empty()) unit_gather(u, c.second, h.size(), h.data());
+        st.hcarry = std::move(h);
+        st.base = u.base + c.second;
+        st.carry_len = u.len - c.second;
+    }
+    {
+        std::lock_guard<std::mutex> lk(g->mu);
+        for (Unit &u : B->units)
+            if (u.st && u.final && u.st->cslot >= 0) {
+                g->free_cslots.push_back(u.st->cslot);
+                u.st->cslot = -1;
+                u.st->hcarry.clear();
+                u.st->hcarry.shrink_to_fit();
+                g->closing_streams--;
+            }
+        g->cv_slot.notify_all();
+    }
     std::sort(B->short_idx.begin(), B->short_idx.end(),
               [&](uint32_t a, uint32_t b) { return B->c_len[a] > B->c_len[b]; });
     const uint64_t ns = B->short_idx.size();
@@ -797,13 +1123,13 @@ bool stage_a(Ing *g, Batch *B) {
         if (getenv("RCDC_ALLOC_LOG") && P.refs_cap)
             fprintf(stderr, "rcdc ingest: regrow refs %llu -> %llu\n", (unsigned long long)P.refs_cap,
                     (unsigned long long)ns);
-        if (P.h_refs) ING_HIP(g, hipHostFree(P.h_refs));
-        if (P.d_refs) ING_HIP(g, hipFree(P.d_refs));
-        if (P.d_dig) ING_HIP(g, hipFree(P.d_dig));
+        ING_HIP(g, ing_free(&P.h_refs));
+        ING_HIP(g, ing_free(&P.d_refs));
+        ING_HIP(g, ing_free(&P.d_dig));
         P.refs_cap = ns + ns / 4 + 64;
-        ING_HIP(g, hipHostMalloc((void **)&P.h_refs, P.refs_cap * 16, hipHostMallocDefault));
-        ING_HIP(g, hipMalloc((void **)&P.d_refs, P.refs_cap * 16));
-        ING_HIP(g, hipMalloc((void **)&P.d_dig, P.refs_cap * 32));
+        ING_HIP(g, ing_alloc(g, &P.h_refs, P.refs_cap * 16, true));
+        ING_HIP(g, ing_alloc(g, &P.d_refs, P.refs_cap * 16, false));
+        ING_HIP(g, ing_alloc(g, &P.d_dig, P.refs_cap * 32, false));
     }
     for (uint64_t j = 0; j < ns; j++) {
         P.h_refs[2 * j] = B->c_off[B->short_idx[j]];
@@ -835,7 +1161,7 @@ bool stage_a(Ing *g, Batch *B) {
             std::vector<uint64_t> ls;
             std::vector<uint8_t> dig(32 * grp.size());
             for (uint32_t k : grp) {
-                ptrs.push_back(in->host + bp->c_off[k]);
+                ptrs.push_back(bp->c_host[k]);
                 ls.push_back(bp->c_len[k]);
             }
             hash_group(ptrs.data(), ls.data(), (uint32_t)grp.size(), dig.data(), mb);
@@ -944,7 +1270,7 @@ bool stage_a(Ing *g, Batch *B) {
     {
         std::lock_guard<std::mutex> lk(g->mu);
         g->st.bytes_in += bytes;
-        g->st.files += nf;
+        g->st.files += nfiles;
         g->st.chunks += nchunks;
         g->st.batches++;
     }
@@ -952,12 +1278,17 @@ bool stage_a(Ing *g, Batch *B) {
 }
 
 // ---- stage B: dedup, per-file results, packs ------------------------------
+constexpr uint32_t kNoSlot = 0xFFFFFFFFu;  // stage B with no batch: close the open pack
+
 bool stage_b(Ing *g, Batch *B, bool finalize) {
-    PSlot &P = g->ps[B->pslot];
+    const bool has_slot = B->pslot != kNoSlot;
+    PSlot &P = g->ps[has_slot ? B->pslot : 0];
     const uint64_t n = B->c_len.size();
     mark(g, B->index, now_s());
-    ING_HIP(g, wait_event(P.ev_ids));
-    ING_HIP(g, hipStreamWaitEvent(g->s_back, P.ev_sealed, 0));
+    if (has_slot) {
+        ING_HIP(g, wait_event(P.ev_ids));
+        ING_HIP(g, hipStreamWaitEvent(g->s_back, P.ev_sealed, 0));
+    }
     mark(g, B->index, now_s());
     const uint64_t ns = B->short_idx.size();
     if (ns) {
@@ -977,7 +1308,7 @@ bool stage_b(Ing *g, Batch *B, bool finalize) {
     for (uint64_t k = 0; k < n; k++) {
         Id32 id;
         memcpy(id.b, B->ids.data() + 32 * k, 32);
-        if (!g->known.insert(id).second) continue;
+        if (!g->idx->insert(id)) continue;
         is_new[k] = 1;
         rcdc_pack_blob b{};
         b.in_off = B->seal_off[k];
@@ -988,21 +1319,48 @@ bool stage_b(Ing *g, Batch *B, bool finalize) {
         memcpy(b.id, id.b, 32);
         nb.push_back(b);
     }
-    // per-file results (the tree's content lists, file_archiver.rs:144-168)
+    // per-file results (the tree's content lists, file_archiver.rs:144-168):
+    // a whole file at once; a stream's chunks accumulate until its end
     {
         uint64_t k = 0;
-        for (size_t i = 0; i < B->files.size(); i++) {
+        for (size_t i = 0; i < B->units.size(); i++) {
+            const Unit &u = B->units[i];
+            const uint32_t ne = B->ncuts[i];
+            uint32_t nnew = 0;
+            for (uint32_t j = 0; j < ne; j++) nnew += is_new[k + j];
             rcdc_ingest_file_result fr{};
-            fr.tag = B->files[i].tag;
-            fr.len = B->files[i].len;
-            fr.nchunks = B->ncuts[i];
-            fr.cuts = B->cuts.data() + k;
-            fr.ids = B->ids.data() + 32 * k;
-            for (uint32_t j = 0; j < B->ncuts[i]; j++) fr.nnew += is_new[k + j];
-            k += B->ncuts[i];
-            if (g->file_cb) {
+            bool deliver_file = false;
+            if (!u.st) {
+                fr.tag = u.tag;
+                fr.len = u.len;
+                fr.nchunks = ne;
+                fr.nnew = nnew;
+                fr.cuts = B->cuts.data() + k;
+                fr.ids = B->ids.data() + 32 * k;
+                deliver_file = true;
+            } else {
+                StreamSt &st = *u.st;
+                for (uint32_t j = 0; j < ne; j++) st.cuts.push_back(u.base + B->cuts[k + j]);
+                st.ids.insert(st.ids.end(), B->ids.begin() + 32 * k, B->ids.begin() + 32 * (k + ne));
+                st.nnew += nnew;
+                if (u.final && !u.aborted) {
+                    fr.tag = st.tag;
+                    fr.len = u.base + u.len;  // the stream's length (its last cut)
+                    fr.nchunks = (uint32_t)st.cuts.size();
+                    fr.nnew = st.nnew;
+                    fr.cuts = st.cuts.data();
+                    fr.ids = st.ids.data();
+                    deliver_file = true;
+                }
+            }
+            k += ne;
+            if (deliver_file && g->file_cb) {
                 std::lock_guard<std::mutex> lk(g->cb_mu);
                 g->file_cb(g->user, &fr);
+            }
+            if (u.st && u.final) {
+                std::vector<uint64_t>().swap(u.st->cuts);
+                std::vector<uint8_t>().swap(u.st->ids);
             }
         }
     }
@@ -1011,6 +1369,11 @@ bool stage_b(Ing *g, Batch *B, bool finalize) {
     blobs.insert(blobs.end(), nb.begin(), nb.end());
     // should_save (packer.rs:659-671) pack by pack; take_data adds each closed
     // pack's size to the sizer (:749-758)
+    // ... and by age (MAX_AGE, packer.rs:63,668-670): the open pack carried in
+    // from earlier batches is saved once its first blob is pack_max_age old
+    const double tnow = now_s();
+    const bool carried = !g->carry_blobs.empty();
+    const bool aged = carried && tnow - g->pack_t0 >= g->pack_max_age;
     std::vector<std::pair<uint32_t, uint32_t>> grp;
     size_t b0 = 0;
     while (b0 < blobs.size()) {
@@ -1023,7 +1386,7 @@ bool stage_b(Ing *g, Batch *B, bool finalize) {
             e++;
         }
         const bool closed = sz >= limit || e - b0 >= kMaxPackCount;
-        if (!closed && !finalize) break;
+        if (!closed && !finalize && !(aged && b0 == 0)) break;
         grp.push_back({(uint32_t)b0, (uint32_t)(e - b0)});
         g->sizer.current += sz + hdr + 32 + 4;
         b0 = e;
@@ -1045,7 +1408,9 @@ bool stage_b(Ing *g, Batch *B, bool finalize) {
             total += sz;
         }
     }
-    const void *srcs[2] = {P.staging, g->carry[g->carry_cur] ? g->carry[g->carry_cur] : P.staging};
+    const void *cur_carry = g->carry[g->carry_cur];
+    const void *srcs[2] = {has_slot ? (const void *)P.staging : cur_carry,
+                           cur_carry ? cur_carry : (const void *)P.staging};
     std::vector<uint32_t> boffs(std::max<size_t>(open_from, 1));
     OutSlot *out = nullptr;
     // The packs go back in groups of whole packs of ~256 MiB, each with its
@@ -1059,13 +1424,19 @@ bool stage_b(Ing *g, Batch *B, bool finalize) {
     };
     std::vector<D2HGroup> d2h_groups;
     if (!grp.empty()) {
-        if (!ensure_dev(g, &g->d_packs, &g->d_packs_cap, total + 64)) return false;
-        // the last pack build's D2H must be done with d_packs (once the pump
-        // has enqueued it, ev_out marks its end)
+        // the last pack build's D2H must be done with d_packs: once the pump
+        // has enqueued its last piece, ev_out marks its end
         if (g->last_d2h)
             while (!g->last_d2h->load() && !g->err)
                 std::this_thread::sleep_for(std::chrono::microseconds(50));
         if (g->err) return false;
+        if (total + 64 > g->d_packs_cap) {
+            // a regrow frees d_packs: every D2H piece reading it must have
+            // run, not only been enqueued (hipFree waits for queued work, but
+            // the pump enqueues pieces one by one)
+            ING_HIP(g, wait_event(g->ev_out));
+            if (!ensure_dev(g, &g->d_packs, &g->d_packs_cap, total + 64)) return false;
+        }
         ING_HIP(g, hipStreamWaitEvent(g->s_back, g->ev_out, 0));
         ING_ST(g, rcdc_pack_build_raw_multi(g->ctx, g->cfg.key, srcs, 2, blobs.data(),
                                             (uint32_t)open_from, packs.data(),
@@ -1090,9 +1461,9 @@ bool stage_b(Ing *g, Batch *B, bool finalize) {
             if (getenv("RCDC_ALLOC_LOG") && out->cap)
                 fprintf(stderr, "rcdc ingest: regrow out slot %llu -> %llu\n",
                         (unsigned long long)out->cap, (unsigned long long)total);
-            if (out->host) ING_HIP(g, hipHostFree(out->host));
+            ING_HIP(g, ing_free(&out->host));
             out->cap = total + total / 4;
-            ING_HIP(g, hipHostMalloc((void **)&out->host, out->cap, hipHostMallocDefault));
+            ING_HIP(g, ing_alloc(g, &out->host, out->cap, true));
         }
         // the D2H goes to the feeder's pump, piece by piece, after the build
         // (the first group's job orders the copy stream after it; the rest
@@ -1141,6 +1512,9 @@ bool stage_b(Ing *g, Batch *B, bool finalize) {
                "carry");
         g->carry_cur = nx;
     }
+    // the open pack's age: from its first blob (a pack that starts in this
+    // batch is new; one carried on keeps its time)
+    if (!rest.empty() && (open_from > 0 || !carried)) g->pack_t0 = tnow;
     g->carry_blobs = std::move(rest);
     if (!grp.empty()) {
         std::vector<std::shared_ptr<PackJob>> jobs;
@@ -1179,7 +1553,7 @@ bool stage_b(Ing *g, Batch *B, bool finalize) {
         }
         g->wait_cv.notify_one();
     }
-    ING_HIP(g, hipEventRecord(P.ev_retired, g->s_back));
+    if (has_slot) ING_HIP(g, hipEventRecord(P.ev_retired, g->s_back));
     {
         std::lock_guard<std::mutex> lk(g->mu);
         g->st.new_blobs += nb.size();
@@ -1199,6 +1573,8 @@ void reap_inputs(Ing *g) {
             s->state = kFree;
             s->used = 0;
             s->files.clear();
+            s->has_stream = false;
+            s->t_first = 0;
             g->cv_slot.notify_all();
         }
 }
@@ -1219,10 +1595,9 @@ void worker_main(Ing *g) {
                 B = std::move(g->submitted.front());
                 g->submitted.pop_front();
             } else {
-                bool waiting_commits = false;  // a closed slot whose files are not all in
-                for (auto &x : g->in) waiting_commits |= x->state == kClosed;
-                done = g->finishing && g->ready.empty() && g->open == nullptr && !waiting_commits &&
-                       g->submitting == 0;
+                // closed slots whose files are not all in wait in closed_q
+                done = g->finishing && g->ready.empty() && g->open == nullptr &&
+                       g->closed_q.empty() && g->submitting == 0;
             }
         }
         if (B) {
@@ -1248,7 +1623,7 @@ void back_main(Ing *g) {
     (void)hipSetDevice(g->device);
     for (;;) {
         std::unique_ptr<Batch> B;
-        bool last = false, all_done = false, fin_carry = false;
+        bool last = false, all_done = false, fin_carry = false, aged = false;
         {
             std::unique_lock<std::mutex> lk(g->mu);
             for (;;) {
@@ -1258,9 +1633,17 @@ void back_main(Ing *g) {
                 }
                 if (!g->inflight.empty() && g->inflight.front()->long_jobs == 0) break;
                 if (g->inflight.empty() && g->front_done) break;
+                // MAX_AGE with no batch coming: the open pack is saved on its
+                // own (a trickle backup leaves recent packs behind)
+                if (g->inflight.empty() && !g->carry_blobs.empty() &&
+                    now_s() - g->pack_t0 >= g->pack_max_age) {
+                    aged = true;
+                    break;
+                }
                 g->cv_slot.wait_for(lk, std::chrono::microseconds(200));
             }
-            if (!g->inflight.empty()) {
+            if (aged) {
+            } else if (!g->inflight.empty()) {
                 B = std::move(g->inflight.front());
                 g->inflight.pop_front();
                 last = g->front_done && g->inflight.empty();
@@ -1268,6 +1651,13 @@ void back_main(Ing *g) {
                 all_done = true;
                 fin_carry = !g->carry_blobs.empty();
             }
+        }
+        if (aged) {
+            Batch empty;
+            empty.pslot = kNoSlot;
+            empty.index = g->nbatches;
+            if (!stage_b(g, &empty, true)) return;
+            continue;
         }
         if (B) {
             if (!stage_b(g, B.get(), last)) return;
@@ -1279,7 +1669,8 @@ void back_main(Ing *g) {
         if (all_done) {
             if (fin_carry) {  // Packer::finalize with nothing else left
                 Batch empty;
-                empty.pslot = 0;
+                empty.pslot = kNoSlot;
+                empty.index = g->nbatches;
                 if (!stage_b(g, &empty, true)) return;
             }
             std::unique_lock<std::mutex> lk(g->mu);
@@ -1290,21 +1681,225 @@ void back_main(Ing *g) {
     }
 }
 
+// Closed slots whose reservations are all in enter the pipeline (`ready`).
+// A slot holding stream pieces enters only at the head of the close order:
+// a stream's pieces are chunked in the order they were reserved, and its
+// carry passes from batch to batch.  Others may pass a slot still waiting
+// for a commit.  A slot left with nothing (every file cancelled) is free.
+void promote_locked(Ing *g) {
+    bool head = true;
+    for (auto it = g->closed_q.begin(); it != g->closed_q.end();) {
+        InSlot *s = *it;
+        if (s->open_res == 0 && (head || !s->has_stream)) {
+            it = g->closed_q.erase(it);
+            bool empty = true;
+            for (const FileEnt &f : s->files) empty &= f.cancelled;
+            if (empty) {
+                s->state = kFree;
+                s->used = 0;
+                s->files.clear();
+                s->has_stream = false;
+                s->t_first = 0;
+            } else {
+                g->ready.push_back(s);
+            }
+            g->cv_slot.notify_all();
+            continue;
+        }
+        head = false;
+        ++it;
+    }
+}
+
 void close_open_locked(Ing *g) {
     InSlot *s = g->open;
     if (!s) return;
     g->open = nullptr;
-    g->nclosed++;
+    s->close_seq = g->nclosed++;
     s->state = kClosed;
-    if (s->open_res == 0) {
-        if (s->files.empty()) {
-            s->state = kFree;
-            s->used = 0;
-        } else {
-            g->ready.push_back(s);
-        }
-    }
+    g->closed_q.push_back(s);
+    promote_locked(g);
     g->cv_slot.notify_all();
+}
+
+// Space for len bytes in the open slot (a new one when it does not fit).  A
+// stream's piece goes right after the stream's previous piece when that is
+// committed and the last thing in the slot (the two are then one range).
+rcdc_status reserve_locked(Ing *g, std::unique_lock<std::mutex> &lk, uint64_t len,
+                           const std::shared_ptr<StreamSt> &st, bool final, uint8_t **buf,
+                           uint64_t *ticket) {
+    for (;;) {
+        if (g->err) return set_error(g->err, g->err_msg.c_str());
+        if (g->finishing) return set_error(RCDC_ERR_INVALID_INPUT, "ingest already finishing");
+        InSlot *s = g->open;
+        // the first slot closes at a quarter: the device starts sooner
+        const uint64_t cap_now = g->nclosed == 0 ? std::max(g->batch_cap / 4, len)
+                                                 : (s ? s->cap : 0);
+        uint64_t place = s ? s->used : 0;
+        if (s && st && !s->files.empty()) {
+            const FileEnt &b = s->files.back();
+            if (b.st == st && b.done && !b.cancelled && s->used == round_up(b.off + b.res, 256))
+                place = b.off + b.len;
+        }
+        if (s && place + len > cap_now) {
+            close_open_locked(g);
+            s = nullptr;
+            place = 0;
+        }
+        if (!s) {
+            for (auto &x : g->in)
+                if (x->state == kFree) {
+                    s = x.get();
+                    break;
+                }
+            if (s) {
+                s->state = kOpen;
+                s->used = 0;
+                s->files.clear();
+                s->has_stream = false;
+                s->t_first = 0;
+                g->open = s;
+            }
+        }
+        if (s) {
+            FileEnt f;
+            f.off = place;
+            f.res = len;
+            f.st = st;
+            f.final = final;
+            s->files.push_back(f);
+            s->used = round_up(place + len, 256);
+            s->open_res++;
+            s->has_stream |= st != nullptr;
+            if (s->files.size() == 1) s->t_first = now_s();
+            size_t idx = 0;
+            for (; idx < g->in.size(); idx++)
+                if (g->in[idx].get() == s) break;
+            *ticket = ((uint64_t)idx << 32) | (uint64_t)(s->files.size() - 1);
+            *buf = s->host + place;
+            return RCDC_OK;
+        }
+        g->cv_slot.wait_for(lk, std::chrono::milliseconds(1));
+        lk.unlock();
+        reap_inputs(g);
+        lk.lock();
+    }
+}
+
+// Commit (or cancel) a reservation.
+rcdc_status commit_locked(Ing *g, uint64_t ticket, uint64_t tag, uint64_t len, bool cancel) {
+    const uint64_t si = ticket >> 32, fi = ticket & 0xFFFFFFFFull;
+    if (si >= g->in.size() || fi >= g->in[si]->files.size() || g->in[si]->files[fi].done ||
+        (g->in[si]->state != kOpen && g->in[si]->state != kClosed))
+        return set_error(RCDC_ERR_INVALID_INPUT, "bad ticket");
+    InSlot *s = g->in[si].get();
+    FileEnt &f = s->files[fi];
+    if (len > f.res) return set_error(RCDC_ERR_INVALID_INPUT, "commit longer than the reservation");
+    if (!f.st) f.tag = tag;
+    f.len = cancel ? 0 : len;
+    f.done = true;
+    f.cancelled = cancel;
+    if (f.st) {
+        f.st->fed += f.len;
+        f.st->open_pieces--;
+    }
+    s->open_res--;
+    if (s->state == kClosed && s->open_res == 0) promote_locked(g);
+    return RCDC_OK;
+}
+
+std::shared_ptr<StreamSt> find_stream(Ing *g, uint64_t h) {
+    auto it = g->streams.find(h);
+    return it == g->streams.end() ? nullptr : it->second;
+}
+
+rcdc_status stream_end(Ing *g, uint64_t handle, bool abort) {
+    if (!g) return set_error(RCDC_ERR_INVALID_INPUT, "null argument");
+    std::unique_lock<std::mutex> lk(g->mu);
+    auto st = find_stream(g, handle);
+    if (!st) return set_error(RCDC_ERR_INVALID_INPUT, "unknown stream");
+    if (st->open_pieces)
+        return set_error(RCDC_ERR_INVALID_INPUT, "stream has pieces not committed or cancelled");
+    // a zero-byte final piece carries the end through the pipeline
+    uint8_t *buf;
+    uint64_t t;
+    if (rcdc_status rs = reserve_locked(g, lk, 0, st, true, &buf, &t)) return rs;
+    st->closed = true;
+    st->aborted = abort;
+    g->streams.erase(handle);
+    g->closing_streams++;
+    return commit_locked(g, t, 0, 0, false);
+}
+
+// Engine buffer sizes for a config (create and rcdc_ingest_footprint).
+struct Sizes {
+    uint64_t batch_cap, max_chunk, min_chunk;
+    uint32_t depth, nin, nout, nthreads, max_streams;
+    uint64_t out_slot, asm_base, asm_cap, arena, staging, refs_cap, frames, carry, carry_pool;
+    uint64_t pinned() const { return nin * batch_cap + nout * out_slot + depth * refs_cap * 16; }
+    uint64_t device() const {
+        return depth * (arena + staging + refs_cap * 48) + 2 * frames + 2 * carry + carry_pool;
+    }
+};
+
+Sizes engine_sizes(const rcdc_ctx *ctx, const rcdc_ingest_config *cfg, uint64_t pack_size) {
+    Sizes z{};
+    z.batch_cap = round_up(cfg->batch_bytes ? cfg->batch_bytes : (2ull << 30), 256);
+    z.max_chunk = round_up(std::max<uint64_t>(ctx_max_size(ctx), 64), 256);
+    z.min_chunk = std::max<uint64_t>(ctx_min_size(ctx), 4096);
+    z.depth = cfg->depth ? cfg->depth : 4;
+    z.nin = std::max(cfg->in_slots ? cfg->in_slots : 4u, 2u);
+    z.nout = std::max(cfg->out_slots ? cfg->out_slots : 6u, 1u);
+    z.nthreads = cfg->hash_threads ? cfg->hash_threads : 10;
+    z.max_streams = cfg->max_streams ? cfg->max_streams : 16;
+    z.out_slot = z.batch_cap + z.batch_cap / 16 + (64ull << 20);
+    // a batch's stream units gathered: its pieces plus one carry per stream
+    z.asm_base = round_up(z.batch_cap + 1024, 256);
+    z.asm_cap = z.batch_cap + (uint64_t)z.max_streams * (z.max_chunk + 256) + 256;
+    z.arena = z.asm_base + z.asm_cap + 1024;
+    const uint64_t chunked = z.batch_cap + (uint64_t)z.max_streams * z.max_chunk;
+    z.staging = chunked + chunked / 64 + (64ull << 20);
+    z.frames = z.staging;
+    z.refs_cap = chunked / z.min_chunk * 2 + 1024;
+    z.carry = std::max<uint64_t>(pack_size * 2, 128ull << 20);
+    z.carry_pool = (uint64_t)z.max_streams * z.max_chunk;
+    return z;
+}
+
+// Every buffer, stream, event and plan of the engine (threads stopped or
+// never started); safe on a partly built engine.
+void free_all(Ing *g) {
+    (void)hipSetDevice(g->device);
+    for (auto &s : g->in) {
+        (void)ing_free(&s->host);
+        if (s->h2d) (void)hipEventDestroy(s->h2d);
+        s->h2d = nullptr;
+    }
+    for (auto &o : g->outs) (void)ing_free(&o->host);
+    for (auto &P : g->ps) {
+        if (P.plan) rcdc_plan_destroy(P.plan);
+        P.plan = nullptr;
+        (void)ing_free(&P.arena);
+        (void)ing_free(&P.staging);
+        (void)ing_free(&P.d_refs);
+        (void)ing_free(&P.d_dig);
+        (void)ing_free(&P.h_refs);
+        for (hipEvent_t *e : {&P.ev_ids, &P.ev_sealed, &P.ev_retired})
+            if (*e) (void)hipEventDestroy(*e), *e = nullptr;
+        if (P.s_ids) (void)hipStreamDestroy(P.s_ids);
+        P.s_ids = nullptr;
+    }
+    (void)ing_free(&g->frames);
+    (void)ing_free(&g->d_packs);
+    (void)ing_free(&g->carry[0]);
+    (void)ing_free(&g->carry[1]);
+    (void)ing_free(&g->carry_pool);
+    for (hipStream_t *q : {&g->s_in, &g->s_comp, &g->s_out, &g->s_back})
+        if (*q) (void)hipStreamDestroy(*q), *q = nullptr;
+    for (hipEvent_t *e : {&g->ev_comp, &g->ev_back, &g->ev_out})
+        if (*e) (void)hipEventDestroy(*e), *e = nullptr;
+    if (g->own_idx) delete g->idx;
+    g->idx = nullptr;
 }
 
 }  // namespace
@@ -1328,7 +1923,27 @@ void rcdc_ingest_config_default(rcdc_ingest_config *c) {
     c->in_slots = 4;
     c->out_slots = 6;
     c->hash_threads = 10;
+    c->max_streams = 16;
     c->long_chunk = 2ull << 20;
+    c->pack_max_age_ms = 300000;  // packer.rs:63 MAX_AGE = 5 min
+    c->slot_max_age_ms = 1000;
+}
+
+rcdc_status rcdc_ingest_footprint(const rcdc_ctx *ctx, const rcdc_ingest_config *cfg,
+                                  uint64_t *pinned, uint64_t *device) {
+    if (!ctx || !cfg) return set_error(RCDC_ERR_INVALID_INPUT, "null argument");
+    PackSizer ps{cfg->pack_size ? cfg->pack_size : (32ull << 20), cfg->pack_grow_factor,
+                 cfg->pack_size_limit ? cfg->pack_size_limit : 0xFFFFFFFFull, cfg->pack_current_size};
+    const Sizes z = engine_sizes(ctx, cfg, ps.pack_size());
+    if (pinned) *pinned = z.pinned();
+    if (device) *device = z.device();
+    return RCDC_OK;
+}
+
+void rcdc_ingest_mem_live(uint64_t *pinned, uint64_t *device) {
+    std::lock_guard<std::mutex> lk(g_alloc_mu);
+    if (pinned) *pinned = g_live_pinned;
+    if (device) *device = g_live_dev;
 }
 
 rcdc_status rcdc_ingest_create(rcdc_ctx *ctx, const rcdc_ingest_config *cfg,
@@ -1345,51 +1960,69 @@ rcdc_status rcdc_ingest_create(rcdc_ctx *ctx, const rcdc_ingest_config *cfg,
     g->user = user;
     g->device = ctx_device(ctx);
     g->prof = getenv("RCDC_INGEST_PROF") ? std::max(atoi(getenv("RCDC_INGEST_PROF")), 1) : 0;
+    if (const char *e = getenv("RCDC_INGEST_FAIL_ALLOC")) g->fail_alloc = (uint32_t)std::max(atoi(e), 0);
     g->level = cfg->zstd_level;
     g->compress = cfg->compress != 0;
     g->verify = cfg->extra_verify != 0;
-    g->batch_cap = round_up(cfg->batch_bytes ? cfg->batch_bytes : (2ull << 30), 256);
-    g->long_chunk = cfg->long_chunk ? cfg->long_chunk : (2ull << 20);
-    if (const char *e = getenv("RCDC_INGEST_KCOPY")) g->kcopy = (uint32_t)std::max(atoi(e), 0);
-    if (const char *e = getenv("RCDC_INGEST_COPY_PIECE"))
-        g->copy_piece = std::max<uint64_t>(strtoull(e, nullptr, 10), 1ull << 20);
-    g->depth = cfg->depth ? cfg->depth : 4;
-    g->nin = std::max(cfg->in_slots ? cfg->in_slots : 4u, 2u);
-    g->nout = std::max(cfg->out_slots ? cfg->out_slots : 4u, 1u);
-    g->nthreads = cfg->hash_threads ? cfg->hash_threads : 8;
     g->sizer.default_size = cfg->pack_size ? cfg->pack_size : (32ull << 20);
     g->sizer.grow = cfg->pack_grow_factor;
     g->sizer.limit = cfg->pack_size_limit ? cfg->pack_size_limit : 0xFFFFFFFFull;
     g->sizer.current = cfg->pack_current_size;
+    const Sizes z = engine_sizes(ctx, cfg, g->sizer.pack_size());
+    g->batch_cap = z.batch_cap;
+    g->long_chunk = cfg->long_chunk ? cfg->long_chunk : (2ull << 20);
+    if (const char *e = getenv("RCDC_INGEST_KCOPY")) g->kcopy = (uint32_t)std::max(atoi(e), 0);
+    if (const char *e = getenv("RCDC_INGEST_COPY_PIECE"))
+        g->copy_piece = std::max<uint64_t>(strtoull(e, nullptr, 10), 1ull << 20);
+    g->depth = z.depth;
+    g->nin = z.nin;
+    g->nout = z.nout;
+    g->nthreads = z.nthreads;
+    g->max_chunk = z.max_chunk;
+    g->asm_base = z.asm_base;
+    g->asm_cap = z.asm_cap;
+    g->pack_max_age = (cfg->pack_max_age_ms ? cfg->pack_max_age_ms : 300000) / 1e3;
+    g->slot_max_age = (cfg->slot_max_age_ms ? cfg->slot_max_age_ms : 1000) / 1e3;
+    g->idx = new rcdc_index();
+    g->own_idx = true;
+    for (uint32_t i = 0; i < z.max_streams; i++) g->free_cslots.push_back((int)(z.max_streams - 1 - i));
     Ing *gp = g.get();
     (void)hipSetDevice(g->device);
+    // any failure below: everything allocated so far is freed
     auto fail_hip = [&](hipError_t e, const char *what) {
+        free_all(gp);
         return set_error(RCDC_ERR_INTERNAL,
                          (std::string(what) + ": " + hipGetErrorString(e)).c_str());
+    };
+    auto fail_st = [&](rcdc_status st) {
+        const std::string m = rcdc_last_error();
+        free_all(gp);
+        return set_error(st, m.c_str());
     };
     hipError_t e;
     for (uint32_t i = 0; i < g->nin; i++) {
         auto s = std::make_unique<InSlot>();
         s->cap = g->batch_cap;
-        if ((e = hipHostMalloc((void **)&s->host, s->cap, hipHostMallocDefault)) != hipSuccess)
-            return fail_hip(e, "input slot");
-        if ((e = hipEventCreateWithFlags(&s->h2d, hipEventDisableTiming)) != hipSuccess)
-            return fail_hip(e, "event");
+        InSlot *sp = s.get();
         g->in.push_back(std::move(s));
+        if ((e = ing_alloc(gp, &sp->host, sp->cap, true)) != hipSuccess) return fail_hip(e, "input slot");
+        if ((e = hipEventCreateWithFlags(&sp->h2d, hipEventDisableTiming)) != hipSuccess)
+            return fail_hip(e, "event");
     }
     for (uint32_t i = 0; i < g->nout; i++) {
         auto o = std::make_unique<OutSlot>();
-        o->cap = g->batch_cap + g->batch_cap / 16 + (64ull << 20);
-        if ((e = hipHostMalloc((void **)&o->host, o->cap, hipHostMallocDefault)) != hipSuccess)
-            return fail_hip(e, "output slot");
+        o->cap = z.out_slot;
+        OutSlot *op = o.get();
         g->outs.push_back(std::move(o));
+        if ((e = ing_alloc(gp, &op->host, op->cap, true)) != hipSuccess) return fail_hip(e, "output slot");
     }
     // the open pack's carry buffers, sized for a default pack and its slack
     for (int c = 0; c < 2; c++) {
-        const uint64_t cc = std::max<uint64_t>(g->sizer.pack_size() * 2, 128ull << 20);
-        if ((e = hipMalloc((void **)&g->carry[c], cc)) != hipSuccess) return fail_hip(e, "carry");
-        g->carry_cap[c] = cc;
+        if ((e = ing_alloc(gp, &g->carry[c], z.carry, false)) != hipSuccess) return fail_hip(e, "carry");
+        g->carry_cap[c] = z.carry;
     }
+    if ((e = ing_alloc(gp, &g->carry_pool, z.carry_pool, false)) != hipSuccess)
+        return fail_hip(e, "stream carries");
     g->ps.resize(g->depth);
     for (auto &P : g->ps) {
         // the chunk-id kernel runs for up to ~60 ms (a 2 MiB chunk's
@@ -1405,15 +2038,13 @@ rcdc_status rcdc_ingest_create(rcdc_ctx *ctx, const rcdc_ingest_config *cfg,
             (e = hipEventCreateWithFlags(&P.ev_retired, hipEventDisableTiming)) != hipSuccess)
             return fail_hip(e, "stream");
         // device buffers sized for a full batch up front (a hipFree inside
-        // the pipeline would synchronise the device)
-        const uint64_t nmax = g->batch_cap / 4096 + 1024;
-        if ((e = hipMalloc((void **)&P.arena, g->batch_cap + 1024)) != hipSuccess)
-            return fail_hip(e, "arena");
-        P.arena_cap = g->batch_cap + 1024;
-        const uint64_t stg = g->batch_cap + g->batch_cap / 64 + (64ull << 20);
-        if ((e = hipMalloc((void **)&P.staging, stg)) != hipSuccess) return fail_hip(e, "staging");
-        P.staging_cap = stg;
-        (void)nmax;
+        // the pipeline would synchronise the device): the slot's bytes, then
+        // the assembly region for streams' gathered pieces and carries
+        if ((e = ing_alloc(gp, &P.arena, z.arena, false)) != hipSuccess) return fail_hip(e, "arena");
+        P.arena_cap = z.arena;
+        if ((e = ing_alloc(gp, &P.staging, z.staging, false)) != hipSuccess)
+            return fail_hip(e, "staging");
+        P.staging_cap = z.staging;
         // the plan built once for a full-batch layout (allocations and
         // synchronous uploads here, not inside the pipeline); each batch then
         // re-lays it out on its compute stream, reusing the buffers
@@ -1429,7 +2060,7 @@ rcdc_status rcdc_ingest_create(rcdc_ctx *ctx, const rcdc_ingest_config *cfg,
         }
         if (rcdc_status ps = rcdc_plan_create(ctx, off0.data(), len0.data(), kPlanStreams,
                                               g->batch_cap + 256, &P.plan))
-            return ps;
+            return fail_st(ps);
         // ... and run once in that layout and in the one-stream layout (the
         // walk path's buffers at full size; the arena's bytes do not matter):
         // a plan's first run in a new layout allocated inside the pipeline,
@@ -1437,10 +2068,10 @@ rcdc_status rcdc_ingest_create(rcdc_ctx *ctx, const rcdc_ingest_config *cfg,
         // kernel (r5u: 30-55 ms in each slot's first relayout)
         {
             std::vector<uint64_t> wc(g->batch_cap / 4096 + kPlanStreams + 16), wn(kPlanStreams);
-            if (rcdc_status ps = rcdc_plan_run(P.plan, P.arena, nullptr)) return ps;
+            if (rcdc_status ps = rcdc_plan_run(P.plan, P.arena, nullptr)) return fail_st(ps);
             if (rcdc_status ps = rcdc_plan_results(P.plan, wc.data(), wc.size(), wn.data());
                 ps && ps != RCDC_ERR_CAPACITY)
-                return ps;
+                return fail_st(ps);
             for (uint32_t ns : {1u, 2u, 4u, 16u}) {  // walked layouts of 1-16 streams
                 std::vector<uint64_t> o(ns), l(ns);
                 const uint64_t each = (g->batch_cap / ns) & ~255ull;
@@ -1450,27 +2081,24 @@ rcdc_status rcdc_ingest_create(rcdc_ctx *ctx, const rcdc_ingest_config *cfg,
                 }
                 if (rcdc_status ps = rcdc::plan_relayout(P.plan, o.data(), l.data(), ns,
                                                          g->batch_cap + 256, nullptr))
-                    return ps;
-                if (rcdc_status ps = rcdc_plan_run(P.plan, P.arena, nullptr)) return ps;
+                    return fail_st(ps);
+                if (rcdc_status ps = rcdc_plan_run(P.plan, P.arena, nullptr)) return fail_st(ps);
                 if (rcdc_status ps = rcdc_plan_results(P.plan, wc.data(), wc.size(), wn.data());
                     ps && ps != RCDC_ERR_CAPACITY)
-                    return ps;
+                    return fail_st(ps);
             }
         }
         // short-chunk refs for a batch of minimum-size chunks
-        P.refs_cap = g->batch_cap / std::max<uint64_t>(rcdc::ctx_min_size(ctx), 4096) * 2 + 1024;
-        if ((e = hipHostMalloc((void **)&P.h_refs, P.refs_cap * 16, hipHostMallocDefault)) != hipSuccess ||
-            (e = hipMalloc((void **)&P.d_refs, P.refs_cap * 16)) != hipSuccess ||
-            (e = hipMalloc((void **)&P.d_dig, P.refs_cap * 32)) != hipSuccess)
+        P.refs_cap = z.refs_cap;
+        if ((e = ing_alloc(gp, &P.h_refs, P.refs_cap * 16, true)) != hipSuccess ||
+            (e = ing_alloc(gp, &P.d_refs, P.refs_cap * 16, false)) != hipSuccess ||
+            (e = ing_alloc(gp, &P.d_dig, P.refs_cap * 32, false)) != hipSuccess)
             return fail_hip(e, "refs");
     }
-    {
-        const uint64_t f = g->batch_cap + g->batch_cap / 64 + (64ull << 20);
-        if ((e = hipMalloc((void **)&g->frames, f)) != hipSuccess) return fail_hip(e, "frames");
-        g->frames_cap = f;
-        if ((e = hipMalloc((void **)&g->d_packs, f)) != hipSuccess) return fail_hip(e, "packs");
-        g->d_packs_cap = f;
-    }
+    if ((e = ing_alloc(gp, &g->frames, z.frames, false)) != hipSuccess) return fail_hip(e, "frames");
+    g->frames_cap = z.frames;
+    if ((e = ing_alloc(gp, &g->d_packs, z.frames, false)) != hipSuccess) return fail_hip(e, "packs");
+    g->d_packs_cap = z.frames;
     if ((e = hipStreamCreateWithFlags(&g->s_in, hipStreamNonBlocking)) != hipSuccess ||
         (e = hipStreamCreateWithFlags(&g->s_comp, hipStreamNonBlocking)) != hipSuccess ||
         (e = hipStreamCreateWithFlags(&g->s_out, hipStreamNonBlocking)) != hipSuccess ||
@@ -1496,7 +2124,7 @@ rcdc_status rcdc_ingest_add_index(rcdc_ingest *g, const uint8_t *ids, uint64_t n
     for (uint64_t i = 0; i < n; i++) {
         Id32 id;
         memcpy(id.b, ids + 32 * i, 32);
-        g->known.insert(id);
+        g->idx->insert(id);
     }
     return RCDC_OK;
 }
@@ -1504,81 +2132,98 @@ rcdc_status rcdc_ingest_add_index(rcdc_ingest *g, const uint8_t *ids, uint64_t n
 rcdc_status rcdc_ingest_reserve(rcdc_ingest *g, uint64_t len, uint8_t **buf, uint64_t *ticket) {
     if (!g || !buf || !ticket) return set_error(RCDC_ERR_INVALID_INPUT, "null argument");
     if (len > g->batch_cap)
-        return set_error(RCDC_ERR_UNSUPPORTED, "file larger than the ingest batch (batch_bytes)");
+        return set_error(RCDC_ERR_UNSUPPORTED,
+                         "file larger than the ingest batch (batch_bytes): feed it as a stream "
+                         "(rcdc_ingest_stream_open)");
     std::unique_lock<std::mutex> lk(g->mu);
-    for (;;) {
-        if (g->err) return set_error(g->err, g->err_msg.c_str());
-        if (g->finishing) return set_error(RCDC_ERR_INVALID_INPUT, "ingest already finishing");
-        InSlot *s = g->open;
-        // the first slot closes at a quarter: the device starts sooner
-        const uint64_t cap_now = g->nclosed == 0 ? std::max(g->batch_cap / 4, len)
-                                                 : (s ? s->cap : 0);
-        if (s && s->used + len > cap_now) {
-            close_open_locked(g);
-            s = nullptr;
-        }
-        if (!s) {
-            for (auto &x : g->in)
-                if (x->state == kFree) {
-                    s = x.get();
-                    break;
-                }
-            if (s) {
-                s->state = kOpen;
-                s->used = 0;
-                s->files.clear();
-                g->open = s;
-            }
-        }
-        if (s) {
-            FileEnt f;
-            f.off = s->used;
-            f.res = len;
-            s->files.push_back(f);
-            s->used = round_up(s->used + len, 256);
-            s->open_res++;
-            size_t idx = 0;
-            for (; idx < g->in.size(); idx++)
-                if (g->in[idx].get() == s) break;
-            *ticket = ((uint64_t)idx << 32) | (uint64_t)(s->files.size() - 1);
-            *buf = s->host + f.off;
-            return RCDC_OK;
-        }
-        g->cv_slot.wait_for(lk, std::chrono::milliseconds(1));
-        lk.unlock();
-        reap_inputs(g);
-        lk.lock();
-    }
+    return reserve_locked(g, lk, len, nullptr, false, buf, ticket);
 }
 
 rcdc_status rcdc_ingest_commit(rcdc_ingest *g, uint64_t ticket, uint64_t tag, uint64_t len) {
     if (!g) return set_error(RCDC_ERR_INVALID_INPUT, "null argument");
     std::lock_guard<std::mutex> lk(g->mu);
-    const uint64_t si = ticket >> 32, fi = ticket & 0xFFFFFFFFull;
-    if (si >= g->in.size() || fi >= g->in[si]->files.size() || g->in[si]->files[fi].done)
-        return set_error(RCDC_ERR_INVALID_INPUT, "bad ticket");
-    InSlot *s = g->in[si].get();
-    FileEnt &f = s->files[fi];
-    if (len > f.res) return set_error(RCDC_ERR_INVALID_INPUT, "commit longer than the reservation");
-    f.tag = tag;
-    f.len = len;
-    f.done = true;
-    s->open_res--;
-    if (s->state == kClosed && s->open_res == 0) {
-        g->ready.push_back(s);
-        g->cv_slot.notify_all();
+    return commit_locked(g, ticket, tag, len, false);
+}
+
+rcdc_status rcdc_ingest_cancel(rcdc_ingest *g, uint64_t ticket) {
+    if (!g) return set_error(RCDC_ERR_INVALID_INPUT, "null argument");
+    std::lock_guard<std::mutex> lk(g->mu);
+    return commit_locked(g, ticket, 0, 0, true);
+}
+
+rcdc_status rcdc_ingest_stream_open(rcdc_ingest *g, uint64_t tag, uint64_t size_hint,
+                                    uint64_t *stream) {
+    if (!g || !stream) return set_error(RCDC_ERR_INVALID_INPUT, "null argument");
+    std::unique_lock<std::mutex> lk(g->mu);
+    for (;;) {
+        if (g->err) return set_error(g->err, g->err_msg.c_str());
+        if (g->finishing) return set_error(RCDC_ERR_INVALID_INPUT, "ingest already finishing");
+        if (!g->free_cslots.empty()) break;
+        if (!g->closing_streams)
+            return set_error(RCDC_ERR_UNSUPPORTED, "max_streams streams are open");
+        // streams that ended free their carry slots once their last batch
+        // has been chunked: send the open slot on its way
+        close_open_locked(g);
+        g->cv_slot.wait_for(lk, std::chrono::milliseconds(1));
     }
+    auto st = std::make_shared<StreamSt>();
+    st->handle = g->next_stream++;
+    st->tag = tag;
+    st->hint = size_hint;
+    st->cslot = g->free_cslots.back();
+    g->free_cslots.pop_back();
+    g->streams[st->handle] = st;
+    *stream = st->handle;
     return RCDC_OK;
+}
+
+rcdc_status rcdc_ingest_stream_reserve(rcdc_ingest *g, uint64_t stream, uint64_t len,
+                                       uint8_t **buf, uint64_t *ticket) {
+    if (!g || !buf || !ticket) return set_error(RCDC_ERR_INVALID_INPUT, "null argument");
+    if (len > g->batch_cap)
+        return set_error(RCDC_ERR_UNSUPPORTED, "piece larger than the ingest batch (batch_bytes)");
+    std::unique_lock<std::mutex> lk(g->mu);
+    auto st = find_stream(g, stream);
+    if (!st) return set_error(RCDC_ERR_INVALID_INPUT, "unknown stream");
+    st->open_pieces++;
+    const rcdc_status rs = reserve_locked(g, lk, len, st, false, buf, ticket);
+    if (rs) st->open_pieces--;
+    return rs;
+}
+
+rcdc_status rcdc_ingest_stream_close(rcdc_ingest *g, uint64_t stream) {
+    return stream_end(g, stream, false);
+}
+
+rcdc_status rcdc_ingest_stream_abort(rcdc_ingest *g, uint64_t stream) {
+    return stream_end(g, stream, true);
 }
 
 rcdc_status rcdc_ingest_add(rcdc_ingest *g, uint64_t tag, const void *data, uint64_t len) {
     if (!g || (len && !data)) return set_error(RCDC_ERR_INVALID_INPUT, "null argument");
     uint8_t *buf;
     uint64_t t;
-    rcdc_status s = rcdc_ingest_reserve(g, len, &buf, &t);
-    if (s) return s;
-    memcpy(buf, data, len);
-    return rcdc_ingest_commit(g, t, tag, len);
+    if (len <= g->batch_cap) {
+        rcdc_status s = rcdc_ingest_reserve(g, len, &buf, &t);
+        if (s) return s;
+        memcpy(buf, data, len);
+        return rcdc_ingest_commit(g, t, tag, len);
+    }
+    // larger than a batch: a stream of quarter-batch pieces
+    uint64_t h;
+    if (rcdc_status s = rcdc_ingest_stream_open(g, tag, len, &h)) return s;
+    const uint64_t piece = std::max<uint64_t>(g->batch_cap / 4 & ~255ull, 256);
+    for (uint64_t o = 0; o < len; o += piece) {
+        const uint64_t n = std::min(piece, len - o);
+        rcdc_status s = rcdc_ingest_stream_reserve(g, h, n, &buf, &t);
+        if (s) {
+            (void)rcdc_ingest_stream_abort(g, h);
+            return s;
+        }
+        memcpy(buf, (const uint8_t *)data + o, n);
+        if ((s = rcdc_ingest_commit(g, t, 0, n))) return s;
+    }
+    return rcdc_ingest_stream_close(g, h);
 }
 
 rcdc_status rcdc_ingest_flush(rcdc_ingest *g) {
@@ -1592,6 +2237,8 @@ rcdc_status rcdc_ingest_finish(rcdc_ingest *g, rcdc_ingest_stats *stats) {
     if (!g) return set_error(RCDC_ERR_INVALID_INPUT, "null argument");
     {
         std::unique_lock<std::mutex> lk(g->mu);
+        if (!g->streams.empty())
+            return set_error(RCDC_ERR_INVALID_INPUT, "streams still open (close or abort them first)");
         close_open_locked(g);
         g->finishing = true;
         g->cv_slot.notify_all();
@@ -1642,35 +2289,45 @@ void rcdc_ingest_destroy(rcdc_ingest *g) {
         if (t.joinable()) t.join();
     (void)hipSetDevice(g->device);
     (void)hipDeviceSynchronize();
-    for (auto &s : g->in) {
-        (void)hipHostFree(s->host);
-        (void)hipEventDestroy(s->h2d);
-    }
-    for (auto &o : g->outs) (void)hipHostFree(o->host);
-    for (auto &P : g->ps) {
-        if (P.plan) rcdc_plan_destroy(P.plan);
-        (void)hipFree(P.arena);
-        (void)hipFree(P.staging);
-        (void)hipFree(P.d_refs);
-        (void)hipFree(P.d_dig);
-        (void)hipHostFree(P.h_refs);
-        (void)hipStreamDestroy(P.s_ids);
-        (void)hipEventDestroy(P.ev_ids);
-        (void)hipEventDestroy(P.ev_sealed);
-        (void)hipEventDestroy(P.ev_retired);
-    }
-    (void)hipFree(g->frames);
-    (void)hipFree(g->d_packs);
-    (void)hipFree(g->carry[0]);
-    (void)hipFree(g->carry[1]);
-    (void)hipStreamDestroy(g->s_in);
-    (void)hipStreamDestroy(g->s_comp);
-    (void)hipStreamDestroy(g->s_out);
-    (void)hipStreamDestroy(g->s_back);
-    (void)hipEventDestroy(g->ev_comp);
-    (void)hipEventDestroy(g->ev_back);
-    (void)hipEventDestroy(g->ev_out);
+    free_all(g);
     delete g;
+}
+
+rcdc_status rcdc_index_create(rcdc_index **out) {
+    if (!out) return set_error(RCDC_ERR_INVALID_INPUT, "null argument");
+    *out = new rcdc_index();
+    return RCDC_OK;
+}
+
+void rcdc_index_destroy(rcdc_index *idx) { delete idx; }
+
+rcdc_status rcdc_index_add(rcdc_index *idx, const uint8_t *ids, uint64_t n) {
+    if (!idx || (n && !ids)) return set_error(RCDC_ERR_INVALID_INPUT, "null argument");
+    for (uint64_t i = 0; i < n; i++) {
+        Id32 id;
+        memcpy(id.b, ids + 32 * i, 32);
+        idx->insert(id);
+    }
+    return RCDC_OK;
+}
+
+uint64_t rcdc_index_size(const rcdc_index *idx) {
+    return idx ? const_cast<rcdc_index *>(idx)->size() : 0;
+}
+
+rcdc_status rcdc_ingest_set_index(rcdc_ingest *g, rcdc_index *idx) {
+    if (!g || !idx) return set_error(RCDC_ERR_INVALID_INPUT, "null argument");
+    std::lock_guard<std::mutex> lk(g->mu);
+    if (g->nbatches) return set_error(RCDC_ERR_INVALID_INPUT, "index set after the first batch");
+    if (g->idx == idx) return RCDC_OK;
+    for (auto &sh : g->idx->sh) {
+        std::lock_guard<std::mutex> l2(sh.mu);
+        for (const Id32 &id : sh.set) idx->insert(id);
+    }
+    if (g->own_idx) delete g->idx;
+    g->idx = idx;
+    g->own_idx = false;
+    return RCDC_OK;
 }
 
 rcdc_status rcdc_sha256_host_one(const void *data, uint64_t len, uint8_t *digest) {

@@ -429,15 +429,31 @@ hipError_t poll_event(hipEvent_t ev) {
     }
 }
 
+// One polling event per device and thread: an event can only be recorded on
+// a stream of the device it was created on, and a thread may serve contexts
+// on several GPUs.  The events are destroyed when the thread exits.
+struct PollEvents {
+    static constexpr int kMaxDev = 64;
+    hipEvent_t ev[kMaxDev] = {};
+    ~PollEvents() {
+        for (int d = 0; d < kMaxDev; d++)
+            if (ev[d] && hipSetDevice(d) == hipSuccess) (void)hipEventDestroy(ev[d]);
+    }
+};
+
 hipError_t poll_stream(hipStream_t st) {
     if (!poll_mode()) return hipStreamSynchronize(st);
-    thread_local hipEvent_t ev = nullptr;
-    if (!ev) {
-        const hipError_t e = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
-        if (e != hipSuccess) return e;
-    }
-    const hipError_t e = hipEventRecord(ev, st);
+    thread_local PollEvents pe;
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);  // the caller's DeviceGuard: the stream's device
     if (e != hipSuccess) return e;
+    if (dev < 0 || dev >= PollEvents::kMaxDev) return hipStreamSynchronize(st);
+    hipEvent_t &ev = pe.ev[dev];
+    if (!ev && (e = hipEventCreateWithFlags(&ev, hipEventDisableTiming)) != hipSuccess) {
+        ev = nullptr;
+        return e;
+    }
+    if ((e = hipEventRecord(ev, st)) != hipSuccess) return e;
     return poll_event(ev);
 }
 
@@ -1551,6 +1567,7 @@ rcdc_status plan_relayout(rcdc_plan *pl, const uint64_t *offs, const uint64_t *l
 }
 int ctx_device(const rcdc_ctx *ctx) { return ctx ? ctx->device : 0; }
 uint64_t ctx_min_size(const rcdc_ctx *ctx) { return ctx ? ctx->min : 0; }
+uint64_t ctx_max_size(const rcdc_ctx *ctx) { return ctx ? ctx->max : 0; }
 rcdc_status set_error(rcdc_status st, const char *msg) { return fail(st, "%s", msg); }
 }  // namespace rcdc
 

@@ -30,7 +30,8 @@ class IngestConfig(ctypes.Structure):
                 ("extra_verify", u32), ("hash_threads", u32), ("pack_size", u64),
                 ("pack_grow_factor", u64), ("pack_size_limit", u64),
                 ("pack_current_size", u64), ("batch_bytes", u64), ("depth", u32),
-                ("in_slots", u32), ("out_slots", u32), ("pad", u32), ("long_chunk", u64)]
+                ("in_slots", u32), ("out_slots", u32), ("max_streams", u32), ("long_chunk", u64),
+                ("pack_max_age_ms", u32), ("slot_max_age_ms", u32)]
 
 
 class IngestBlob(ctypes.Structure):
@@ -132,21 +133,93 @@ class NativeIngest:
 
     def add_file(self, tag: int, path: str) -> None:
         """Reserve the file's size, read it straight into the page-locked slot
-        (readinto: no intermediate copy), commit what was read."""
+        (readinto: no intermediate copy), commit what was read.  A read that
+        fails cancels the reservation (rcdc_ingest_cancel: the reference logs
+        and skips the file, archiver.rs:197-203) and re-raises."""
         n = os.path.getsize(path)
+        if n > self.cfg.batch_bytes:
+            with open(path, "rb", buffering=0) as f:
+                self.add_stream(tag, f, size_hint=n)
+            return
         buf, ticket = ctypes.c_void_p(), u64()
         self._check(_lib.lib().rcdc_ingest_reserve(self._h, n, ctypes.byref(buf),
                                                    ctypes.byref(ticket)))
         got = 0
-        if n:
-            mv = memoryview((ctypes.c_char * n).from_address(buf.value)).cast("B")
-            with open(path, "rb", buffering=0) as f:
-                while got < n:
-                    r = f.readinto(mv[got:])
-                    if not r:
-                        break
-                    got += r
+        try:
+            if n:
+                mv = memoryview((ctypes.c_char * n).from_address(buf.value)).cast("B")
+                with open(path, "rb", buffering=0) as f:
+                    while got < n:
+                        r = f.readinto(mv[got:])
+                        if not r:
+                            break
+                        got += r
+        except BaseException:
+            _lib.lib().rcdc_ingest_cancel(self._h, ticket.value)
+            raise
         self._check(_lib.lib().rcdc_ingest_commit(self._h, ticket.value, int(tag), got))
+
+    # ---- streams: any Read, of any or unknown length ---------------------------
+    def stream_open(self, tag: int, size_hint: int = 0) -> int:
+        h = u64()
+        self._check(_lib.lib().rcdc_ingest_stream_open(self._h, int(tag), int(size_hint),
+                                                       ctypes.byref(h)))
+        return h.value
+
+    def stream_reserve(self, stream: int, n: int):
+        """(memoryview of n page-locked bytes, ticket) for the stream's next piece."""
+        buf, ticket = ctypes.c_void_p(), u64()
+        self._check(_lib.lib().rcdc_ingest_stream_reserve(self._h, stream, int(n),
+                                                          ctypes.byref(buf), ctypes.byref(ticket)))
+        mv = memoryview((ctypes.c_char * max(n, 1)).from_address(buf.value)).cast("B")[:n]
+        return mv, ticket.value
+
+    def commit(self, ticket: int, n: int, tag: int = 0) -> None:
+        self._check(_lib.lib().rcdc_ingest_commit(self._h, ticket, int(tag), int(n)))
+
+    def cancel(self, ticket: int) -> None:
+        self._check(_lib.lib().rcdc_ingest_cancel(self._h, ticket))
+
+    def stream_close(self, stream: int) -> None:
+        self._check(_lib.lib().rcdc_ingest_stream_close(self._h, stream))
+
+    def stream_abort(self, stream: int) -> None:
+        self._check(_lib.lib().rcdc_ingest_stream_abort(self._h, stream))
+
+    def add_stream(self, tag: int, reader, piece: int = 16 << 20, size_hint: int = 0) -> int:
+        """Feed a readable binary object (readinto) until EOF as one file:
+        ChunkIter::from_config(cfg, reader, size_hint) (chunker.rs:22-47).  A
+        failing read aborts the stream (its completed chunks stay packed, as
+        Packer::add had them) and re-raises.  Returns the bytes read."""
+        h = self.stream_open(tag, size_hint)
+        total = 0
+        try:
+            while True:
+                mv, t = self.stream_reserve(h, piece)
+                got = 0
+                try:
+                    while got < piece:
+                        r = reader.readinto(mv[got:])
+                        if not r:
+                            break
+                        got += r
+                except BaseException:
+                    self.cancel(t)
+                    raise
+                self.commit(t, got)
+                total += got
+                if got < piece:
+                    break
+        except BaseException:
+            _lib.lib().rcdc_ingest_stream_abort(self._h, h)
+            raise
+        self.stream_close(h)
+        return total
+
+    def set_index(self, index: "NativeIndex") -> None:
+        """Dedup against a set shared with other engines (multi-device ingest)."""
+        self._check(_lib.lib().rcdc_ingest_set_index(self._h, index.handle))
+        self._index = index  # keep it alive while the engine uses it
 
     def flush(self) -> None:
         self._check(_lib.lib().rcdc_ingest_flush(self._h))
@@ -167,6 +240,113 @@ class NativeIngest:
             self.close()
         except Exception:  # interpreter shutdown
             pass
+
+
+class NativeIndex:
+    """rcdc_index: one dedup set shared by the engines of several devices, so
+    each blob is packed once per backup (the reference's single Packer,
+    archiver.rs:195, blob/packer.rs:304-315)."""
+
+    def __init__(self, ids=None):
+        h = ctypes.c_void_p()
+        st = _lib.lib().rcdc_index_create(ctypes.byref(h))
+        if st:
+            raise status_error(st, _lib.last_error())
+        self.handle = h
+        if ids is not None and len(ids):
+            a = np.ascontiguousarray(ids, np.uint8).reshape(-1, 32)
+            st = _lib.lib().rcdc_index_add(h, a.ctypes.data, len(a))
+            if st:
+                raise status_error(st, _lib.last_error())
+
+    def __len__(self) -> int:
+        return int(_lib.lib().rcdc_index_size(self.handle))
+
+    def close(self) -> None:
+        if getattr(self, "handle", None):
+            _lib.lib().rcdc_index_destroy(self.handle)
+            self.handle = None
+
+
+class MultiIngest:
+    """N engines (one per device context) behind one file router and one
+    dedup set.  Files go to the engine with the fewest bytes so far (greedy
+    LPT online; shard.assign_lpt is the same rule offline); every engine
+    dedups against the shared NativeIndex, so a chunk found by several
+    engines is packed by exactly one.  Results: the union of the engines'
+    files and packs."""
+
+    def __init__(self, ctxs, key: bytes, level: Optional[int] = 0, index_ids=None, **cfg):
+        self.index = NativeIndex(index_ids)
+        self.engines = []
+        try:
+            for c in ctxs:
+                e = NativeIngest(c, key, level=level, **cfg)
+                e.set_index(self.index)
+                self.engines.append(e)
+        except BaseException:
+            self.close()
+            raise
+        self.load = [0] * len(self.engines)
+        self._mu = threading.Lock()
+
+    def _pick(self, n: int) -> "NativeIngest":
+        with self._mu:
+            i = min(range(len(self.load)), key=lambda j: (self.load[j], j))
+            self.load[i] += n
+        return self.engines[i]
+
+    def add(self, tag: int, data) -> None:
+        a = np.frombuffer(bytes(data), np.uint8) if isinstance(
+            data, (bytes, bytearray, memoryview)) else np.asarray(data)
+        self._pick(int(a.size)).add(tag, a)
+
+    def add_file(self, tag: int, path: str) -> None:
+        self._pick(os.path.getsize(path)).add_file(tag, path)
+
+    def finish(self) -> dict:
+        tot: Dict[str, float] = {}
+        for e in self.engines:
+            for k, v in e.finish().items():
+                tot[k] = tot.get(k, 0) + v
+        return tot
+
+    @property
+    def files(self) -> Dict[int, tuple]:
+        out: Dict[int, tuple] = {}
+        for e in self.engines:
+            out.update(e.files)
+        return out
+
+    @property
+    def packs(self) -> List[dict]:
+        return [p for e in self.engines for p in e.packs]
+
+    def close(self) -> None:
+        for e in self.engines:
+            e.close()
+        self.engines = []
+        self.index.close()
+
+
+def mem_live():
+    """(page-locked, device) bytes held by the process's ingest engines."""
+    p, d = u64(), u64()
+    _lib.lib().rcdc_ingest_mem_live(ctypes.byref(p), ctypes.byref(d))
+    return p.value, d.value
+
+
+def footprint(ctx, **cfg):
+    """(page-locked, device) bytes rcdc_ingest_create allocates for cfg."""
+    c = default_config()
+    for k, v in cfg.items():
+        setattr(c, k, v)
+    p, d = u64(), u64()
+    st = _lib.lib().rcdc_ingest_footprint(ctx.handle, ctypes.byref(c), ctypes.byref(p),
+                                          ctypes.byref(d))
+    if st:
+        raise status_error(st, _lib.last_error())
+    return p.value, d.value
 
 
 def sha256_host_one(data) -> bytes:

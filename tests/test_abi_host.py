@@ -29,7 +29,35 @@ def test_header_symbols_exported(rcdc_lib):
 
 
 def test_abi_version(rcdc_lib):
-    assert rcdc_lib.rcdc_abi_version() == 4
+    assert rcdc_lib.rcdc_abi_version() == 5
+
+
+def test_ingest_config_layout(rcdc_lib):
+    """rcdc_ingest_config as ctypes sees it (native_ingest.IngestConfig) ==
+    the C struct: the defaults land in the right fields (ABI 5 added
+    max_streams, pack_max_age_ms, slot_max_age_ms)."""
+    from rustic_core_amd.native_ingest import IngestConfig, default_config
+    assert ctypes.sizeof(IngestConfig) == 152
+    c = default_config()
+    assert (c.zstd_level, c.compress, c.extra_verify, c.hash_threads) == (0, 1, 1, 10)
+    assert (c.pack_size, c.pack_grow_factor, c.pack_size_limit) == (32 << 20, 32, 0xFFFFFFFF)
+    assert (c.batch_bytes, c.depth, c.in_slots, c.out_slots) == (2 << 30, 4, 4, 6)
+    assert (c.max_streams, c.long_chunk) == (16, 2 << 20)
+    assert (c.pack_max_age_ms, c.slot_max_age_ms) == (300000, 1000)  # packer.rs:63 MAX_AGE
+
+
+def test_shared_index_host(rcdc_lib):
+    """rcdc_index: the dedup set engines share (no GPU needed)."""
+    import hashlib
+    from rustic_core_amd.native_ingest import NativeIndex, mem_live
+    ids = np.frombuffer(b"".join(hashlib.sha256(bytes([i])).digest() for i in range(100)),
+                        np.uint8)
+    idx = NativeIndex(ids)
+    assert len(idx) == 100
+    assert rcdc_lib.rcdc_index_add(idx.handle, ids.ctypes.data, 100) == 0
+    assert len(idx) == 100  # a set
+    idx.close()
+    assert mem_live() == (0, 0)
 
 
 @pytest.mark.parametrize("avg,mn,mx,status", [

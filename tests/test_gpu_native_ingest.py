@@ -212,16 +212,39 @@ def test_native_ingest_files_from_disk_threads(gpu_ctx, tmp_path):
 
 
 def test_native_ingest_rejects(gpu_ctx):
+    import ctypes
+
+    from oracle import oracle
+    from rustic_core_amd import _lib
     from rustic_core_amd.errors import RusticError
     from rustic_core_amd.native_ingest import NativeIngest
     ing = NativeIngest(gpu_ctx, KEY, batch_bytes=8 << 20, depth=2)
     try:
-        with pytest.raises(RusticError):  # larger than a slot
-            ing.add(0, np.zeros(9 << 20, np.uint8))
+        buf, t = ctypes.c_void_p(), ctypes.c_uint64()
+        # one reservation is at most a slot; a larger file goes in as a stream
+        assert _lib.lib().rcdc_ingest_reserve(ing._h, 9 << 20, ctypes.byref(buf),
+                                              ctypes.byref(t)) == 1  # Unsupported
+        big = np.random.default_rng(5).integers(0, 256, 9 << 20, dtype=np.uint8)
+        ing.add(0, big)  # rcdc_ingest_add: pieces of a stream
         ing.add(1, np.ones(1000, np.uint8))
+        h = ing.stream_open(2)
+        with pytest.raises(RusticError):  # a piece larger than a slot
+            ing.stream_reserve(h, 9 << 20)
+        mv, tk = ing.stream_reserve(h, 4096)
+        with pytest.raises(RusticError):  # a piece still reserved
+            ing.stream_close(h)
+        with pytest.raises(RusticError):  # open streams block finish
+            ing.finish()
+        mv[:] = b"z" * 4096
+        ing.commit(tk, 4096)
+        ing.stream_close(h)
+        with pytest.raises(RusticError):  # the handle is gone
+            ing.stream_reserve(h, 10)
         stats = ing.finish()
-        assert stats["files"] == 1 and stats["packs"] == 1
+        assert stats["files"] == 3
+        assert np.array_equal(ing.files[0][0], oracle.chunk_cuts(big))
+        assert list(ing.files[2][0]) == [4096]
         with pytest.raises(RusticError):  # after finish
-            ing.add(2, b"x")
+            ing.add(3, b"x")
     finally:
         ing.close()

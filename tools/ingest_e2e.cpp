@@ -21,9 +21,12 @@
 // computed and delivered).  Bound: the same input bytes H2D in batch-sized
 // copies from page-locked memory with the run's pack bytes D2H on a second
 // stream at the same time -- what PCIe allows this job in both directions.
-// Checks: every pack id recomputed (rcdc_sha256_host_one) over the pack
-// bytes the callback saw, blob counts, new blobs == distinct chunk ids, and
-// the pack byte total.
+// Checks (an extra, untimed run): every pack id recomputed with OpenSSL
+// (EVP SHA-256, not the library's own SHA code) over the pack bytes the
+// callback saw; every chunk id recomputed with OpenSSL from the file on disk
+// at the cuts the engine returned; new blobs == distinct chunk ids; the pack
+// byte total.  --cuts-out FILE writes every file's cuts (u64 file, u64 n,
+// n x u64) for bench.py to diff against the oracle.
 //
 // Output: one JSON line (stdout; also --json FILE).
 #include <hip/hip_runtime.h>
@@ -45,7 +48,14 @@
 #include <thread>
 #include <vector>
 
+#include <openssl/evp.h>
+
 #include "../include/rcdc.h"
+
+static void sha256_ossl(const uint8_t *p, uint64_t n, uint8_t out[32]) {
+    unsigned int len = 32;
+    EVP_Digest(p, (size_t)n, out, &len, EVP_sha256(), nullptr);
+}
 
 static uint64_t splitmix64(uint64_t x) {
     x += 0x9E3779B97F4A7C15ull;
@@ -105,6 +115,8 @@ struct Sink {
     uint64_t blobs = 0, files = 0, chunks = 0, nnew = 0;
     std::set<std::string> chunk_ids;
     bool check = false;
+    std::vector<std::vector<uint64_t>> cuts;  // check: per file (tag)
+    std::vector<std::vector<uint8_t>> ids;
 };
 
 static void on_pack(void *user, const rcdc_ingest_pack *p) {
@@ -117,7 +129,7 @@ static void on_pack(void *user, const rcdc_ingest_pack *p) {
     r.id_ok = true;
     if (s->check) {
         uint8_t d[32];
-        rcdc_sha256_host_one(p->data, p->size, d);
+        sha256_ossl(p->data, p->size, d);
         r.id_ok = memcmp(d, p->id, 32) == 0;
         // the trailing u32 is the sealed header's length (packfile.rs)
         uint32_t hl;
@@ -135,9 +147,57 @@ static void on_file(void *user, const rcdc_ingest_file_result *f) {
     s->files++;
     s->chunks += f->nchunks;
     s->nnew += f->nnew;
-    if (s->check)
+    if (s->check) {
         for (uint32_t i = 0; i < f->nchunks; i++)
             s->chunk_ids.insert(std::string((const char *)f->ids + 32 * i, 32));
+        if (f->tag >= s->cuts.size()) {
+            s->cuts.resize(f->tag + 1);
+            s->ids.resize(f->tag + 1);
+        }
+        s->cuts[f->tag].assign(f->cuts, f->cuts + f->nchunks);
+        s->ids[f->tag].assign(f->ids, f->ids + 32ull * f->nchunks);
+    }
+}
+
+// Every chunk id of the checked run recomputed with OpenSSL from the file on
+// disk at the engine's cuts (16 threads); the cuts must also end at the
+// file's length.
+static bool chunk_ids_check(const Sink &s, const std::vector<std::string> &paths, uint64_t fsize) {
+    std::atomic<int> next{0};
+    std::atomic<bool> ok{s.cuts.size() == paths.size()};
+    std::vector<std::thread> ws;
+    for (int w = 0; w < 16; w++)
+        ws.emplace_back([&] {
+            std::vector<uint8_t> buf(fsize);
+            for (int f; (f = next++) < (int)s.cuts.size();) {
+                const int fd = open(paths[f].c_str(), O_RDONLY);
+                uint64_t o = 0;
+                while (o < fsize) {
+                    const ssize_t r = pread(fd, buf.data() + o, fsize - o, (off_t)o);
+                    if (r <= 0) break;
+                    o += (uint64_t)r;
+                }
+                close(fd);
+                const auto &c = s.cuts[f];
+                if (o != fsize || c.empty() || c.back() != fsize) {
+                    ok = false;
+                    continue;
+                }
+                uint64_t prev = 0;
+                for (size_t i = 0; i < c.size(); i++) {
+                    uint8_t d[32];
+                    if (c[i] <= prev || c[i] > fsize) {
+                        ok = false;
+                        break;
+                    }
+                    sha256_ossl(buf.data() + prev, c[i] - prev, d);
+                    if (memcmp(d, s.ids[f].data() + 32 * i, 32)) ok = false;
+                    prev = c[i];
+                }
+            }
+        });
+    for (auto &w : ws) w.join();
+    return ok;
 }
 
 // H2D of `in_bytes` in batch-sized copies (4 device slots, one stream) while
@@ -229,6 +289,7 @@ int main(int argc, char **argv) {
     const int in_slots = atoi(arg(argc, argv, "--in-slots", "4"));
     const int reps = atoi(arg(argc, argv, "--reps", "2"));
     const char *json = arg(argc, argv, "--json", nullptr);
+    const char *cuts_out = arg(argc, argv, "--cuts-out", nullptr);
     const bool check = !flag(argc, argv, "--no-check");
     const bool keep = flag(argc, argv, "--keep");
     const int level = atoi(arg(argc, argv, "--level", "0"));
@@ -415,6 +476,16 @@ int main(int argc, char **argv) {
     const bool dedup_ok = !check || (sink.blobs == sink.nnew && sink.nnew == sink.chunk_ids.size() &&
                                      stc.new_blobs == stb.new_blobs && stc.chunks == stb.chunks);
     const bool bytes_ok = !check || pbytes == stc.pack_bytes;
+    const bool cids_ok = !check || chunk_ids_check(sink, paths, fsize);
+    if (check && cuts_out) {
+        FILE *f = fopen(cuts_out, "wb");
+        for (size_t i = 0; f && i < sink.cuts.size(); i++) {
+            const uint64_t hdr[2] = {(uint64_t)i, (uint64_t)sink.cuts[i].size()};
+            fwrite(hdr, 8, 2, f);
+            fwrite(sink.cuts[i].data(), 8, sink.cuts[i].size(), f);
+        }
+        if (f) fclose(f);
+    }
     // ---- bound ------------------------------------------------------------------
     double h2d_alone = 0;
     const double bound_s = pcie_bound(stb.bytes_in, stb.pack_bytes, batch, &h2d_alone);
@@ -434,7 +505,9 @@ int main(int argc, char **argv) {
              "page-locked memory, no engine\"}, "
              "\"frac_of_bound\": %.3f, "
              "\"checks\": {\"pack_ids_ok\": %s, \"pack_seq_ok\": %s, \"dedup_ok\": %s, "
-             "\"pack_bytes_ok\": %s, \"checked\": %s}, "
+             "\"pack_bytes_ok\": %s, \"chunk_ids_ok\": %s, \"checked\": %s, "
+             "\"checker\": \"OpenSSL EVP SHA-256 of every pack and of every chunk re-read from "
+             "disk at the engine's cuts\"}, "
              "\"config\": {\"readers\": %d, \"batch_bytes\": %llu, \"depth\": %d, "
              "\"hash_threads\": %d, \"in_slots\": %d, \"zstd_level\": %d, \"extra_verify\": true, "
              "\"reps\": %d, \"gpu_max_hw_queues\": \"%s\"}, "
@@ -449,7 +522,8 @@ int main(int argc, char **argv) {
              (unsigned long long)stb.chunks, (unsigned long long)stb.new_blobs,
              (unsigned long long)stb.batches, gib / bound_s, bound_s, h2d_alone, rd, bound_s / best,
              ids_ok ? "true" : "false", seq_ok ? "true" : "false", dedup_ok ? "true" : "false",
-             bytes_ok ? "true" : "false", check ? "true" : "false", readers,
+             bytes_ok ? "true" : "false", cids_ok ? "true" : "false", check ? "true" : "false",
+             readers,
              (unsigned long long)batch, depth, threads, in_slots, level, reps,
              getenv("GPU_MAX_HW_QUEUES"), nfiles,
              (unsigned long long)(fsize >> 20), dir.c_str());
@@ -464,5 +538,5 @@ int main(int argc, char **argv) {
     if (!keep)
         for (auto &p : paths) unlink(p.c_str());
     rcdc_ctx_destroy(ctx);
-    return (ids_ok && seq_ok && dedup_ok && bytes_ok) ? 0 : 3;
+    return (ids_ok && seq_ok && dedup_ok && bytes_ok && cids_ok) ? 0 : 3;
 }
