@@ -528,9 +528,10 @@ uint64_t rcdc_zstd_tables_size(void);
  *
  * Memory (rcdc_ingest_footprint gives the exact figures for a config):
  * page-locked in_slots x batch_bytes + out_slots x (batch_bytes + 1/16 +
- * 64 MiB) -- about 21 GiB at the defaults (4 + 6 slots of 2 GiB) -- and
- * device depth x (2 x batch_bytes + max_streams x max) plus ~2.1 batches of
- * compression / pack buffers (~21 GiB at the defaults on a 288 GB GPU).     */
+ * 64 MiB) -- 16.75 GiB at the defaults (4 + 4 slots of 2 GiB) -- and on
+ * the device depth x (2 x batch_bytes + max_streams x max + a sealed-blob
+ * staging area of ~batch_bytes) plus two batch-sized compression / pack
+ * buffers: ~30 GiB at the defaults, about a tenth of an MI355X's HBM.      */
 typedef struct rcdc_ingest rcdc_ingest;
 
 typedef struct {
@@ -546,7 +547,7 @@ typedef struct {
     uint64_t batch_bytes;       /* input slot / device batch bytes (default 2 GiB)     */
     uint32_t depth;             /* batches in flight on the device (default 4)         */
     uint32_t in_slots;          /* page-locked input slots (default 4)                 */
-    uint32_t out_slots;         /* page-locked pack buffers (default 6)                */
+    uint32_t out_slots;         /* page-locked pack buffers (default 4)                */
     uint32_t max_streams;       /* streams open at once (default 16; each holds a
                                    device carry of max bytes)                          */
     uint64_t long_chunk;        /* chunks above this get their id on the host (2 MiB) */

@@ -1849,7 +1849,7 @@ Sizes engine_sizes(const rcdc_ctx *ctx, const rcdc_ingest_config *cfg, uint64_t 
     z.min_chunk = std::max<uint64_t>(ctx_min_size(ctx), 4096);
     z.depth = cfg->depth ? cfg->depth : 4;
     z.nin = std::max(cfg->in_slots ? cfg->in_slots : 4u, 2u);
-    z.nout = std::max(cfg->out_slots ? cfg->out_slots : 6u, 1u);
+    z.nout = std::max(cfg->out_slots ? cfg->out_slots : 4u, 1u);
     z.nthreads = cfg->hash_threads ? cfg->hash_threads : 10;
     z.max_streams = cfg->max_streams ? cfg->max_streams : 16;
     z.out_slot = z.batch_cap + z.batch_cap / 16 + (64ull << 20);
@@ -1921,7 +1921,7 @@ void rcdc_ingest_config_default(rcdc_ingest_config *c) {
     c->batch_bytes = 2ull << 30;
     c->depth = 4;
     c->in_slots = 4;
-    c->out_slots = 6;
+    c->out_slots = 4;
     c->hash_threads = 10;
     c->max_streams = 16;
     c->long_chunk = 2ull << 20;

@@ -41,7 +41,7 @@ def test_ingest_config_layout(rcdc_lib):
     c = default_config()
     assert (c.zstd_level, c.compress, c.extra_verify, c.hash_threads) == (0, 1, 1, 10)
     assert (c.pack_size, c.pack_grow_factor, c.pack_size_limit) == (32 << 20, 32, 0xFFFFFFFF)
-    assert (c.batch_bytes, c.depth, c.in_slots, c.out_slots) == (2 << 30, 4, 4, 6)
+    assert (c.batch_bytes, c.depth, c.in_slots, c.out_slots) == (2 << 30, 4, 4, 4)
     assert (c.max_streams, c.long_chunk) == (16, 2 << 20)
     assert (c.pack_max_age_ms, c.slot_max_age_ms) == (300000, 1000)  # packer.rs:63 MAX_AGE
 

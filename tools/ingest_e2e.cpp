@@ -287,6 +287,7 @@ int main(int argc, char **argv) {
     const int depth = atoi(arg(argc, argv, "--depth", "4"));
     const int threads = atoi(arg(argc, argv, "--hash-threads", "14"));
     const int in_slots = atoi(arg(argc, argv, "--in-slots", "4"));
+    const int out_slots = atoi(arg(argc, argv, "--out-slots", "0"));  // 0: the default
     const int reps = atoi(arg(argc, argv, "--reps", "2"));
     const char *json = arg(argc, argv, "--json", nullptr);
     const char *cuts_out = arg(argc, argv, "--cuts-out", nullptr);
@@ -358,6 +359,7 @@ int main(int argc, char **argv) {
     cfg.depth = (uint32_t)depth;
     cfg.hash_threads = (uint32_t)threads;
     cfg.in_slots = (uint32_t)in_slots;
+    if (out_slots > 0) cfg.out_slots = (uint32_t)out_slots;
 
     auto run = [&](Sink &sink, int nf, rcdc_ingest_stats *st, double *el) {
         rcdc_ingest *ing = nullptr;
@@ -509,7 +511,8 @@ int main(int argc, char **argv) {
              "\"checker\": \"OpenSSL EVP SHA-256 of every pack and of every chunk re-read from "
              "disk at the engine's cuts\"}, "
              "\"config\": {\"readers\": %d, \"batch_bytes\": %llu, \"depth\": %d, "
-             "\"hash_threads\": %d, \"in_slots\": %d, \"zstd_level\": %d, \"extra_verify\": true, "
+             "\"hash_threads\": %d, \"in_slots\": %d, \"out_slots\": %u, \"zstd_level\": %d, "
+             "\"extra_verify\": true, "
              "\"reps\": %d, \"gpu_max_hw_queues\": \"%s\"}, "
              "\"data\": \"%d files x %llu MiB of splitmix64 words with a zero run at the start of "
              "every 4 MiB block (~half zeros), written to %s and read once before the run\", "
@@ -524,7 +527,7 @@ int main(int argc, char **argv) {
              ids_ok ? "true" : "false", seq_ok ? "true" : "false", dedup_ok ? "true" : "false",
              bytes_ok ? "true" : "false", cids_ok ? "true" : "false", check ? "true" : "false",
              readers,
-             (unsigned long long)batch, depth, threads, in_slots, level, reps,
+             (unsigned long long)batch, depth, threads, in_slots, cfg.out_slots, level, reps,
              getenv("GPU_MAX_HW_QUEUES"), nfiles,
              (unsigned long long)(fsize >> 20), dir.c_str());
     printf("%s\n", line);
