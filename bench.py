@@ -870,6 +870,7 @@ def main():
     # around the scan kernel of every --time-every-th step
     # (rcdc_plan_set_timing: sampling keeps most steps free of event gaps)
     plan.set_timing(True, every=args.time_every)
+    stitch_warm = sliced.stitch_s if sliced is not None else 0.0  # (warmup steps' stitches)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
@@ -890,6 +891,20 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     el_max = float(t.item())
 
+    stitch = None
+    if sliced is not None and world > 1:
+        # per step, the plan's end to the stitch result (SlicedStream.step):
+        # the crossing window, one all_gather, its .cpu(), the host walk;
+        # timed steps only (the counters restart here), max over ranks
+        n_st = max(args.steps, 1)
+        st_t = torch.tensor([(sliced.stitch_s - stitch_warm) / n_st * 1e3], dtype=torch.float64,
+                            device=coll_device(dev))
+        dist.all_reduce(st_t, op=dist.ReduceOp.MAX)
+        stitch = {"ms_per_step_max_rank": round(float(st_t.item()), 4), "steps": n_st,
+                  "backend": dist.get_backend(),
+                  "how": "host clock from the plan's end (device synchronised) to the stitch "
+                         "result: rcdc_plan_window, one all_gather_into_tensor of 3 + k words "
+                         "per rank, its .cpu(), the host walk over the windows"}
     if args.workload == "C5":
         total_bytes = desc["stream_bytes_total"] * args.steps
     else:
@@ -1064,6 +1079,8 @@ def main():
             "roofline": roofline,
             "untimed_steps_run": nw,
         }
+        if stitch is not None:
+            line["stitch"] = stitch
         line.update(out_extra)
         print(json.dumps(line), flush=True)
     plan.close()

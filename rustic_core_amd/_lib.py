@@ -13,6 +13,9 @@ import subprocess
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "librcdc.so")
+# A/B builds of the same sources (tools/ab_lib.sh) load from RCDC_LIB instead
+if os.environ.get("RCDC_LIB"):
+    LIB_PATH = os.path.abspath(os.environ["RCDC_LIB"])
 CSRC = os.path.join(_HERE, "csrc")
 
 # Every entry point of include/rcdc.h (checked by tests/test_abi.py).

@@ -175,6 +175,13 @@ struct WalkParams {
 };
 constexpr uint32_t kWalkZoneFast = 1;  // zones on the scan's slide (zone_wave_fast)
 constexpr uint32_t kWalkKReset = 2;    // counters reset in the walk kernel, queue by qbase
+// kWalkStatic: a wave's first piece (walk) or boundary (check) is its global
+// wave index, only later ones come from the queue counter: with one atomic
+// per wave at the start, thousands of waves queued on one L2 address (C5:
+// 3200 one-piece waves, the median piece 82 us, mostly that wait).  A walk
+// then adds exactly nunits to ctr[0] (one failed take per wave that had a
+// static piece, one take per dynamic piece).
+constexpr uint32_t kWalkStatic = 4;
 
 constexpr uint64_t kEndOpen = 1ull << 63;
 constexpr uint64_t kEndPos = (1ull << 42) - 1;  // position bits of an end word

@@ -794,6 +794,8 @@ rcdc_status plan_build(rcdc_ctx *ctx, rcdc_plan *pl, const uint64_t *offs, const
     wp.flags = kWalkZoneFast | kWalkKReset;
     if (const char *e = getenv("RCDC_WALK_ZONEFAST"); e && atoi(e) == 0) wp.flags &= ~kWalkZoneFast;
     if (const char *e = getenv("RCDC_WALK_KRESET"); e && atoi(e) == 0) wp.flags &= ~kWalkKReset;
+    wp.flags |= kWalkStatic;
+    if (const char *e = getenv("RCDC_WALK_STATIC"); e && atoi(e) == 0) wp.flags &= ~kWalkStatic;
     wp.cost_blocks = 4096;
     wp.cost_samples = 64;
     if (const char *e = getenv("RCDC_COST_SAMPLES")) {
@@ -990,7 +992,8 @@ rcdc_status plan_run(rcdc_plan *pl, const void *d_arena, hipStream_t stream) {
     HIP_TRY(launch_walk((const uint8_t *)d_arena, pl->d_sds, pl->d_wunits, wprm, ctx->d_tables,
                         wpiece, pstatus, ctr, wblocks, stream, ordered));
     if (!pl->wunits.empty() && (wprm.flags & kWalkKReset))  // takes of this run: one per
-        pl->wqbase[set] += (uint32_t)pl->wunits.size() + wblocks * 16u;  // piece, one failed per wave
+        pl->wqbase[set] += (uint32_t)pl->wunits.size() +     // piece, one failed per wave;
+                           ((wprm.flags & kWalkStatic) ? 0u : wblocks * 16u);  // static: nunits
     if (dbg) {
         HIP_TRY(hipStreamSynchronize(stream));
         uint32_t h[4] = {0, 0, 0, 0};

@@ -330,6 +330,12 @@ __device__ __forceinline__ Chain scan_segment_early(__amdgpu_buffer_rsrc_t rsrc,
 // reduced: the top byte of out << 8 sits at bits deg .. deg + 7 and MOD's
 // (i << deg) term cancels it.  idx_shift = deg - 32 mod 2^32 (wraps for
 // deg < 32; idx_shift + 32 = deg either way).  Ends with a workgroup barrier.
+//
+// In three LDS steps: the 512 global words are read once (one load per
+// thread, not a dependent pair per copy: the prologue is on the critical
+// path of short launches -- C5's walk and check, C2's scan), OM is formed in
+// copy 0, and copy 0 is replicated.
+#ifdef RCDC_AB_FILL_DIRECT  // A/B only (tools/ab_lib.sh): round 5's direct fill
 __device__ __forceinline__ void fill_tables(uint8_t *s_tab, const uint64_t *__restrict__ gtab,
                                             uint32_t idx_shift, uint32_t tid, uint32_t nthreads) {
     for (uint32_t i = tid; i < 256u * kTableRepl; i += nthreads) {
@@ -343,6 +349,39 @@ __device__ __forceinline__ void fill_tables(uint8_t *s_tab, const uint64_t *__re
     }
     __syncthreads();
 }
+#else
+__device__ __forceinline__ void fill_tables(uint8_t *s_tab, const uint64_t *__restrict__ gtab,
+                                            uint32_t idx_shift, uint32_t tid, uint32_t nthreads) {
+    static_assert(kTableRepl == 32, "copy layout: entry e, copy c at e * 256 + c * 8");
+    uint2 *om = reinterpret_cast<uint2 *>(s_tab);
+    uint2 *md = reinterpret_cast<uint2 *>(s_tab + kTableBytes);
+    // 1. raw OUT[e] into OM copy 1 (overwritten in step 3), MOD[e] into MOD copy 0
+    for (uint32_t i = tid; i < 512u; i += nthreads) {
+        const uint64_t v = gtab[i];
+        const uint2 w = make_uint2((uint32_t)v, (uint32_t)(v >> 32));
+        if (i < 256u) om[i * 32u + 1u] = w;
+        else md[(i - 256u) * 32u] = w;
+    }
+    __syncthreads();
+    // 2. OM[e] = OUT[e] ^ MOD[top(OUT[e])] (idx_shift + 32 = deg) into copy 0
+    for (uint32_t e = tid; e < 256u; e += nthreads) {
+        const uint2 ot = om[e * 32u + 1u];
+        const uint32_t idx = (uint32_t)(((((uint64_t)ot.y << 32) | ot.x) >> (idx_shift + 32u)) & 255u);
+        const uint2 mt = md[idx * 32u];
+        om[e * 32u] = make_uint2(ot.x ^ mt.x, ot.y ^ mt.y);
+    }
+    __syncthreads();
+    // 3. copies 1 .. 31 of both tables from copy 0
+    for (uint32_t i = tid; i < 256u * 32u; i += nthreads) {
+        const uint32_t e = i >> 5, c = i & 31u;
+        if (c) {
+            om[i] = om[e * 32u];
+            md[i] = md[e * 32u];
+        }
+    }
+    __syncthreads();
+}
+#endif
 
 __device__ __forceinline__ Consts make_consts(uint32_t lane, uint32_t mask, uint32_t idx_shift) {
     Consts k;

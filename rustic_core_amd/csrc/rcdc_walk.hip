@@ -658,10 +658,18 @@ __global__ __launch_bounds__(1024, 1) void rcdc_walk_kernel(
     W.early = prm.early;
     W.zonefast = __builtin_amdgcn_readfirstlane(prm.flags & kWalkZoneFast);
     uint64_t help_rounds = 0, help_bytes = 0;  // rounds this wave ran for others
-    for (;;) {
-        uint32_t q = 0;
-        if (lane == 0) q = atomicAdd(&ctr[0], 1u) - prm.qbase;
-        q = __builtin_amdgcn_readfirstlane(q);
+    // kWalkStatic: the first piece is the wave's global index, later ones
+    // come from the counter, offset by the launch's waves (all scalars: no
+    // state live across the walk)
+    auto take = [&]() -> uint32_t {
+        uint32_t t = 0;
+        if (lane == 0)
+            t = atomicAdd(&ctr[0], 1u) - prm.qbase + ((prm.flags & kWalkStatic) ? gridDim.x * 16u : 0u);
+        return __builtin_amdgcn_readfirstlane(t);
+    };
+    uint32_t q = (prm.flags & kWalkStatic) ? __builtin_amdgcn_readfirstlane(blockIdx.x * 16u + wave)
+                                           : take();
+    for (;; q = take()) {
         if (q >= prm.nunits) break;
         const uint32_t u = __builtin_amdgcn_readfirstlane(prm.order[q]);
         const uint64_t t0 = prm.trace ? (uint64_t)wall_clock64() : 0;
@@ -1101,10 +1109,16 @@ __global__ __launch_bounds__(CT, 1) void rcdc_walk_check_kernel(
     W.early = 0;
     W.zonefast = __builtin_amdgcn_readfirstlane(prm.flags & kWalkZoneFast);
     const uint64_t mn = prm.min_size, mx = prm.max_size;
-    for (;;) {
-        uint32_t u = 0;
-        if (lane == 0) u = atomicAdd(&ctr[2], 1u);
-        u = __builtin_amdgcn_readfirstlane(u);
+    auto take = [&]() -> uint32_t {  // (kWalkStatic as the walk kernel)
+        uint32_t t = 0;
+        if (lane == 0)
+            t = atomicAdd(&ctr[2], 1u) + ((prm.flags & kWalkStatic) ? gridDim.x * (CT / 64u) : 0u);
+        return __builtin_amdgcn_readfirstlane(t);
+    };
+    uint32_t u = (prm.flags & kWalkStatic)
+                     ? __builtin_amdgcn_readfirstlane(blockIdx.x * (CT / 64u) + wave)
+                     : take();
+    for (;; u = take()) {
         if (u >= prm.nunits) break;
         const WalkUnit U = units[u];
         if (U.piece == 0) continue;

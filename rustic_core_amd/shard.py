@@ -250,10 +250,25 @@ class SlicedStream:
         self.chunk_from = device_chunk_from(ctx, arena, self.a, self.b, self.e, total,
                                             stream=stream)
         self.last = None
+        self.stitch_s, self.nstitch = 0.0, 0  # world > 1: plan end -> stitch result
 
     def step(self):
         self.plan.run(self.arena.data_ptr(), self.stream)
+        if self.world == 1:
+            self.last = self.stitch()
+            return self.last
+        # the stitch waits for the plan anyway (its window, then the gather's
+        # host copy): wait here first, so the time from the plan's end to the
+        # stitch result (window + all_gather + .cpu() + host walk) is measured
+        import time
+
+        import torch
+        if self.arena.is_cuda:
+            torch.cuda.synchronize(self.arena.device)
+        t1 = time.perf_counter()
         self.last = self.stitch()
+        self.stitch_s += time.perf_counter() - t1
+        self.nstitch += 1
         return self.last
 
     def stitch(self):

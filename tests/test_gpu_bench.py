@@ -94,3 +94,5 @@ def test_bench_eight_ranks_c5(gpu_ctx):
                       n=8)
     assert line["parity"]["mismatches"] == 0
     assert line["config"]["stream_bytes_total"] == 512 << 20
+    # the per-step stitch (plan end -> window, all_gather, .cpu(), host walk)
+    assert line["stitch"]["ms_per_step_max_rank"] > 0 and line["stitch"]["backend"] == "gloo"
