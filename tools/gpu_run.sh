@@ -73,7 +73,8 @@ case $MODE in
     for W in ${WORKLOADS:-C4 C3 C2}; do
       D=$OUT/$W; mkdir -p $D
       B=$(bench_cmd $W)
-      timeout -k 10 400 python -u $B --steps 10 --warmup 3 > $D/line.json 2> $D/line.err || { tail $D/line.err; exit 1; }
+      w=$(echo $W | tr A-Z a-z)  # (tools/pmc_json.py reads $D/<w>.json)
+      timeout -k 10 400 python -u $B --steps 10 --warmup 3 > $D/$w.json 2> $D/$w.err || { tail $D/$w.err; exit 1; }
       for c in FETCH_SIZE WRITE_SIZE; do
         timeout -s KILL 240 rocprofv3 --pmc $c -d $D/pmc_$c -o run --output-format csv -- \
           python -u $B --steps 3 --warmup 1 --prewarm 0 --no-parity > $D/pmc_$c.log 2>&1 \

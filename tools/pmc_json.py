@@ -1,10 +1,10 @@
-"""profiles/pmc_<workload>.json from a tools/gpu_round3.sh run: per-launch
+"""profiles/pmc_<workload>.json from a `tools/gpu_run.sh pmc` run: per-launch
 FETCH_SIZE / WRITE_SIZE of the dominant kernel (separate rocprofv3 passes),
 FETCH converted with the calibration measured for per-lane 64-B bursts
 (profiles/r01_pmc_hbm.txt, tools/ubench/stream_pattern mode 3: FETCH_SIZE
 reports 0.518 of the bytes read), next to the bench line's lane-hashed bytes.
 
-  python tools/pmc_json.py gpurun_out/r3f2 C3 rcdc_walk_kernel "source text"
+  python tools/pmc_json.py gpurun_out/pmc/C3 C3 rcdc_walk_kernel "source text"
 """
 import csv
 import glob
