@@ -312,3 +312,32 @@ def test_two_engines_one_dedup_set(gpu_ctx):
                 assert hashlib.sha256(raw).digest() == bytes(bid)
     finally:
         m.close()
+
+
+def test_stream_slots_recycled(gpu_ctx):
+    """max_streams = 2: a third open stream is refused while two are open;
+    streams opened after closes wait for the closed ones' carry slots (their
+    last batch chunked) and go on -- eight streams through two slots, one
+    thread, every result checked."""
+    from oracle import oracle
+    from rustic_core_amd.errors import RusticError
+    files = [_mixed(9 * MiB + 1000 * k, 120 + k) for k in range(8)]
+    ing = _ingest(gpu_ctx, batch_bytes=16 * MiB, pack_size=4 * MiB, pack_grow_factor=0,
+                  depth=2, max_streams=2)
+    try:
+        a, b = ing.stream_open(100), ing.stream_open(101)
+        with pytest.raises(RusticError):  # max_streams open
+            ing.stream_open(102)
+        ing.stream_close(a)
+        ing.stream_close(b)
+        for i, f in enumerate(files):
+            assert ing.add_stream(i, io.BytesIO(f.tobytes()), piece=5 * MiB) == f.size
+        stats = ing.finish()
+        assert stats["files"] == len(files) + 2
+        assert ing.files[100][0].size == 0 and ing.files[101][0].size == 0  # empty streams
+        for i, f in enumerate(files):
+            assert np.array_equal(ing.files[i][0], oracle.chunk_cuts(f)), i
+        for p in ing.packs:
+            assert hashlib.sha256(p["data"]).digest() == p["id"]
+    finally:
+        ing.close()
