@@ -1471,9 +1471,22 @@ bool stage_b(Ing *g, Batch *B, bool finalize) {
         hipEvent_t after;
         ING_HIP(g, hipEventCreateWithFlags(&after, hipEventDisableTiming));
         ING_HIP(g, hipEventRecord(after, g->s_back));
-        static const uint64_t group_bytes =
+        static const uint64_t group_bytes_env =
             getenv("RCDC_INGEST_D2H_GROUP") ? strtoull(getenv("RCDC_INGEST_D2H_GROUP"), nullptr, 10)
                                             : 256ull << 20;
+        // The last two batches' packs go back one pack per group: each pack's
+        // id starts as soon as that pack has landed.  Their ids are the end of
+        // the run, and in groups of ~256 MiB the last group's packs were
+        // still being hashed ~43 ms after the last copy (r6i timeline, 16
+        // files: landed 385 ms, last id 429 ms).
+        static const bool tail_single =
+            !(getenv("RCDC_INGEST_TAIL_SINGLE") && atoi(getenv("RCDC_INGEST_TAIL_SINGLE")) == 0);
+        bool tail_b;
+        {
+            std::lock_guard<std::mutex> lk(g->mu);
+            tail_b = finalize || (g->finishing && g->front_done && g->inflight.size() <= 1);
+        }
+        const uint64_t group_bytes = tail_single && tail_b ? 1 : group_bytes_env;
         for (size_t a = 0; a < grp.size();) {
             size_t b = a + 1;
             while (b < grp.size() && packs[b].out_off - packs[a].out_off < group_bytes) b++;
