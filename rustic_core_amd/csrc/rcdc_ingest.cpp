@@ -2234,7 +2234,12 @@ rcdc_status rcdc_ingest_add(rcdc_ingest *g, uint64_t tag, const void *data, uint
             return s;
         }
         memcpy(buf, (const uint8_t *)data + o, n);
-        if ((s = rcdc_ingest_commit(g, t, 0, n))) return s;
+        if ((s = rcdc_ingest_commit(g, t, 0, n))) {
+            const std::string m = rcdc_last_error();
+            (void)rcdc_ingest_cancel(g, t);  // (a failed commit leaves the piece open)
+            (void)rcdc_ingest_stream_abort(g, h);
+            return set_error(s, m.c_str());
+        }
     }
     return rcdc_ingest_stream_close(g, h);
 }
