@@ -17,7 +17,6 @@ constructor raises.
 from __future__ import annotations
 
 import collections
-import concurrent.futures
 import ctypes
 import enum
 import io
@@ -39,7 +38,7 @@ DEFAULT_CHUNK_MIN_SIZE = 512 * KB
 DEFAULT_CHUNK_MAX_SIZE = 8 * MB
 # Bytes requested from the reader per read(): large reads, the cut points do
 # not depend on how the stream is split (the reference reads 4 KiB, rabin.rs:12).
-READ_SIZE = 16 * MB
+READ_SIZE = int(os.environ.get("RCDC_READ_MIB", "16")) * MB
 
 
 class Chunker(enum.Enum):
@@ -386,25 +385,105 @@ def _iter_done() -> None:
                     break
 
 
-def _read_ahead(reader, blk: _Block, pos: int) -> int:
-    """The reader thread's read into blk from pos; the future holds `blk`
-    (through these arguments) until the read has returned, so the block
-    cannot be freed or handed to another iterator under it."""
-    return _read_into(reader, blk.mv[pos:])
+# Large files run as a pipeline of three threads: the reader thread reads
+# block after block, the feeder thread feeds each read to the device stream
+# (rcdc_stream_feed: H2D, chunking, cuts back), and the caller's thread
+# copies the chunks out.  All three release the GIL in their native calls, so
+# a file's reads, device passes and chunk copies overlap (one-thread order
+# was read -> feed -> copies, ~28 ms per 256 MiB, tools/c1_profile.py).
+# PIPE_BLOCKS bounds the blocks one iterator holds (read, fed or not yet
+# copied out).
+PIPE_BLOCKS = int(os.environ.get("RCDC_PIPE_BLOCKS", "4"))
 
 
-_readers = None
-_readers_lock = threading.Lock()
+class _Pipe:
+    """The reader and feeder threads of one iterator.  Items on `out`, in
+    file order: (block, start, n, retire_block, cuts, eof), or an exception
+    to raise where the consumer reaches it."""
 
+    def __init__(self, reader, stream, first):
+        self.reader, self.stream = reader, stream
+        self.stop = threading.Event()
+        self.room = threading.Semaphore(PIPE_BLOCKS - 1)  # (`first`'s block is held)
+        self.feed_q = collections.deque()
+        self.feed_cv = threading.Condition()
+        self.out = collections.deque()
+        self.out_cv = threading.Condition()
+        self._put_feed(first)
+        self.blk, self.pos = (None, 0) if first[3] else (first[0], first[1] + first[2])
+        self.t_read = threading.Thread(target=self._read_loop, name="rcdc-read", daemon=True)
+        self.t_feed = threading.Thread(target=self._feed_loop, name="rcdc-feed", daemon=True)
+        self.t_feed.start()
+        self.t_read.start()
 
-def _reader_pool():
-    """Threads for the read-ahead of large files (one read in flight per
-    iterator)."""
-    global _readers
-    with _readers_lock:
-        if _readers is None:
-            _readers = concurrent.futures.ThreadPoolExecutor(16, thread_name_prefix="rcdc-read")
-        return _readers
+    def _put_feed(self, item):
+        with self.feed_cv:
+            self.feed_q.append(item)
+            self.feed_cv.notify()
+
+    def _put_out(self, item):
+        with self.out_cv:
+            self.out.append(item)
+            self.out_cv.notify()
+
+    def _read_loop(self):
+        try:
+            while not self.stop.is_set():
+                if self.blk is None:
+                    while not self.room.acquire(timeout=0.05):
+                        if self.stop.is_set():
+                            return
+                    self.blk, self.pos = _block(), 0
+                blk, p = self.blk, self.pos
+                n = _read_into(self.reader, blk.mv[p:])
+                self.pos = p + n
+                retire = not n or READ_SIZE - self.pos < MIN_READ
+                if retire:
+                    self.blk = None
+                self._put_feed((blk, p, n, retire))
+                if not n:
+                    return
+        except BaseException as e:  # RusticError (read), or anything else
+            self._put_feed(e)
+        finally:
+            self._put_feed(None)  # the feeder's end
+
+    def _feed_loop(self):
+        while True:
+            with self.feed_cv:
+                while not self.feed_q:
+                    self.feed_cv.wait()
+                item = self.feed_q.popleft()
+            if item is None:
+                return
+            if isinstance(item, BaseException):
+                self._put_out(item)
+                return
+            blk, p, n, retire = item
+            try:
+                cuts = self.stream.feed(blk.mv[p:p + n], not n) if not self.stop.is_set() else None
+            except BaseException as e:
+                self.stop.set()
+                self._put_out(e)
+                return
+            if cuts is None:
+                return
+            self._put_out((blk, p, n, retire, cuts, not n))
+            if not n:
+                return
+
+    def get(self):
+        with self.out_cv:
+            while not self.out:
+                self.out_cv.wait()
+            return self.out.popleft()
+
+    def close(self):
+        """Stop reading and feeding; returns once neither thread can touch a
+        block or the stream again."""
+        self.stop.set()
+        self.t_read.join()
+        self.t_feed.join()
 
 
 class RabinChunkIter:
@@ -414,6 +493,7 @@ class RabinChunkIter:
     ``Some(Err(..))`` items (after which iteration stops).  The reader fills
     pooled page-locked blocks in place; every read is fed to the device
     stream as it lands; a chunk is one copy out of the block(s) it lies in.
+    A file whose first read fills a whole block goes through a _Pipe.
     """
 
     def __init__(self, ctx: Context, reader, size_hint: int = 0):
@@ -422,15 +502,17 @@ class RabinChunkIter:
         self._reader = reader
         self.size_hint = size_hint  # capacity hint only; never affects cuts
         self._stream = _Stream(ctx)
-        self._blk = None                  # block taking the next read
+        self._blk = None                  # block taking the next read (no pipe)
         self._pos = 0
-        self._segs = collections.deque()  # [block, start, n, last use]: read, not yet yielded
+        # [block, start, n, retire, piped]: read, not yet yielded (piped: the
+        # block counts against the pipe's PIPE_BLOCKS)
+        self._segs = collections.deque()
         self._base = 0                    # absolute offset of the next chunk
         self._cuts = collections.deque()
         self._eof = False
         self._finished = False
         self._threaded = False
-        self._ahead = None                # the next read, running on a reader thread
+        self._pipe = None
         _iter_started()
 
     def __iter__(self) -> Iterator[bytes]:
@@ -438,31 +520,39 @@ class RabinChunkIter:
 
     def _fill(self) -> None:
         while not self._cuts and not self._eof:
+            if self._pipe is not None:
+                item = self._pipe.get()
+                if isinstance(item, BaseException):
+                    raise item
+                blk, p, n, retire, cuts, eof = item
+                self._eof = eof
+                self._segs.append([blk, p, n, retire, True])
+                self._cuts.extend(cuts.tolist())
+                continue
             if self._blk is None:
                 self._blk, self._pos = _block(), 0
             blk, p = self._blk, self._pos
-            if self._ahead is not None:  # the read started during the last feed
-                fut, self._ahead = self._ahead, None
-                n = fut.result()
-            else:
-                n = _read_into(self._reader, blk.mv[p:])
-            self._eof = not n
+            n = _read_into(self._reader, blk.mv[p:])
             self._pos = p + n
-            last = self._eof or READ_SIZE - self._pos < MIN_READ
-            if last:
+            retire = not n or READ_SIZE - self._pos < MIN_READ
+            if retire:
                 self._blk = None
-            # a large file (a read filled a whole block): the next read runs
-            # on a reader thread while this piece is fed and cut (both
-            # release the GIL); it fills bytes past everything fed
-            if n and (self._threaded or n == READ_SIZE) and os.environ.get("RCDC_READ_AHEAD", "1") != "0":
+            # a large file (a read filled a whole block): the rest runs as a
+            # pipeline (reader, feeder and this thread), this read included
+            if n == READ_SIZE and os.environ.get("RCDC_READ_AHEAD", "1") != "0":
                 self._threaded = True
-                if self._blk is None:
-                    self._blk, self._pos = _block(), 0
-                self._ahead = _reader_pool().submit(_read_ahead, self._reader, self._blk,
-                                                    self._pos)
+                self._pipe = _Pipe(self._reader, self._stream, (blk, p, n, retire))
+                self._blk = None
+                continue
+            self._eof = not n
             cuts = self._stream.feed(blk.mv[p:p + n], self._eof)
-            self._segs.append([blk, p, n, last])
+            self._segs.append([blk, p, n, retire, False])
             self._cuts.extend(cuts.tolist())
+
+    def _retire(self, seg) -> None:
+        _release(seg[0])
+        if seg[4] and self._pipe is not None:
+            self._pipe.room.release()
 
     def _take(self, k: int) -> bytes:
         """The next k bytes read, releasing spent blocks.  The chunk is a new
@@ -485,26 +575,24 @@ class RabinChunkIter:
             if not s[2]:
                 segs.popleft()
                 if s[3]:
-                    _release(s[0])
+                    self._retire(s)
         while segs and not segs[0][2]:  # the EOF read's empty segment
             s = segs.popleft()
             if s[3]:
-                _release(s[0])
+                self._retire(s)
         return chunk
 
     def _finish(self) -> None:
         """End of iteration (EOF, an error, or the caller dropping the
-        iterator): wait for a read still running on a reader thread before
-        the blocks can go back to the pool, then close the device stream."""
+        iterator): stop the pipe's threads (a read or feed they are in
+        finishes first) before the blocks can go back to the pool, then
+        close the device stream."""
         if self._finished:
             return
         self._finished = True
-        fut, self._ahead = self._ahead, None
-        if fut is not None:
-            try:
-                fut.result()
-            except Exception:  # the read's own error is moot now
-                pass
+        if self._pipe is not None:
+            self._pipe.close()
+            self._pipe = None
         self._blk = None
         self._segs.clear()
         self._stream.close()

@@ -124,7 +124,7 @@ def test_read_error_after_earlier_reads(fake):
 @pytest.mark.parametrize("how", ["close", "del"])
 def test_abandoned_iterator_waits_for_read_ahead(fake, monkeypatch, how):
     """A caller that stops early (close, or drops the iterator) while a read
-    runs on a reader thread: the iterator waits for that read before its
+    runs on the pipe's reader thread: the iterator waits for that read before its
     blocks can be freed or reused (the thread would otherwise
     write into a block another iterator owns)."""
     import threading
@@ -142,8 +142,10 @@ def test_abandoned_iterator_waits_for_read_ahead(fake, monkeypatch, how):
 
         def readinto(self, mv):
             self.calls += 1
-            if self.calls >= 2:  # the read-ahead
-                started.set()
+            if self.calls >= 2:  # the pipe's reads (the first one's block is
+                # fed before the consumer sees a cut: the next read runs)
+                if self.calls >= 3:
+                    started.set()
                 time.sleep(0.3)
             mv[:len(mv)] = bytes(len(mv))
             log.append("read")
@@ -151,8 +153,8 @@ def test_abandoned_iterator_waits_for_read_ahead(fake, monkeypatch, how):
 
     it = C.RabinChunkIter(_Ctx(), _Slow())
     assert len(next(it)) == K
-    assert started.wait(5) and it._ahead is not None
-    blk = it._blk
+    assert started.wait(5) and it._pipe is not None
+    blk = it._pipe.blk
     if how == "close":
         it.close()
     else:
@@ -161,3 +163,32 @@ def test_abandoned_iterator_waits_for_read_ahead(fake, monkeypatch, how):
     log.append("closed")
     assert log[-2:] == ["read", "closed"]
     assert blk.ptr or blk._keep is not None  # still a live block
+
+
+def test_pipe_holds_at_most_pipe_blocks(fake):
+    """A consumer that stops taking chunks: the pipe's reader stops once
+    PIPE_BLOCKS blocks are read and not yet copied out, and resumes as the
+    consumer retires blocks."""
+    import time
+    reads = []
+
+    class _Count(io.RawIOBase):
+        def __init__(self, n):
+            self._b = io.BytesIO(bytes(n))
+
+        def readable(self):
+            return True
+
+        def readinto(self, mv):
+            reads.append(len(mv))
+            b = self._b.read(len(mv))
+            mv[:len(b)] = b
+            return len(b)
+
+    n = 200 << 20
+    it = C.RabinChunkIter(_Ctx(), _Count(n))
+    next(it)
+    time.sleep(0.3)
+    assert it._pipe is not None and len(reads) <= C.PIPE_BLOCKS
+    total = K + sum(len(c) for c in it)
+    assert total == n and len(reads) == n // C.READ_SIZE + 2  # (+ the last partial, EOF)

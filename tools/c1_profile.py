@@ -1,67 +1,84 @@
-"""Where C1's drop-in time goes (bench.py run_c1's file through
-ChunkIter.from_config): wall time split into the file reads (_read_into),
-the device feeds (_Stream.feed: H2D, chunking, cuts D2H) and the rest
-(chunk copies, Python).  Prints one JSON line.
+"""Where a C1 pass goes (one 256 MiB file through ChunkIter.from_config):
+wall time per pass, and the time inside the reader thread's reads, the
+device stream feeds and the chunk copies (wrapped in place; the sums
+overlap: large files run as a pipe of reader, feeder and consumer threads).
 
-  python tools/c1_profile.py [--mib 256] [--passes 5]
+  python tools/c1_profile.py [MiB] [passes]
 """
-import argparse
-import json
 import os
 import sys
 import tempfile
+import threading
 import time
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-import bench  # noqa: E402  (the C1 input generator)
-from rustic_core_amd import ChunkIter, ConfigFile, chunker  # noqa: E402
+import numpy as np
 
-ap = argparse.ArgumentParser()
-ap.add_argument("--mib", type=int, default=256)
-ap.add_argument("--passes", type=int, default=5)
-a = ap.parse_args()
-n = a.mib << 20
-data = bench.stdrng_numpy(0x256, n)
-fd, path = tempfile.mkstemp(prefix="rcdc_c1p_", dir=os.environ.get("TMPDIR", "/tmp"))
-with os.fdopen(fd, "wb") as f:
-    f.write(data.tobytes())
-acc = {"read_s": 0.0, "feed_s": 0.0}
-orig_read, orig_feed = chunker._read_into, chunker._Stream.feed
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+from rustic_core_amd import ChunkIter, ConfigFile  # noqa: E402
+from rustic_core_amd import chunker  # noqa: E402
+
+acc = {"read": 0.0, "read_n": 0, "feed": 0.0, "feed_n": 0, "take": 0.0, "take_n": 0}
+lock = threading.Lock()
 
 
-def t_read(*x, **k):
-    t = time.perf_counter()
-    try:
-        return orig_read(*x, **k)
-    finally:
-        acc["read_s"] += time.perf_counter() - t
+def wrap(obj, name, key):
+    f = getattr(obj, name)
+
+    def g(*a, **k):
+        t = time.perf_counter()
+        try:
+            return f(*a, **k)
+        finally:
+            with lock:
+                acc[key] += time.perf_counter() - t
+                acc[key + "_n"] += 1
+    setattr(obj, name, g)
 
 
-def t_feed(self, *x, **k):
-    t = time.perf_counter()
-    try:
-        return orig_feed(self, *x, **k)
-    finally:
-        acc["feed_s"] += time.perf_counter() - t
+def main():
+    mib = int(sys.argv[1]) if len(sys.argv) > 1 else 256
+    passes = int(sys.argv[2]) if len(sys.argv) > 2 else 10
+    n = mib << 20
+    data = np.random.default_rng(7).integers(0, 256, n, dtype=np.uint8)
+    fd, path = tempfile.mkstemp(prefix="rcdc_c1p_", dir=os.environ.get("TMPDIR", "/tmp"))
+    with os.fdopen(fd, "wb") as f:
+        f.write(data.tobytes())
+    cfg = ConfigFile.new(2, 0x003DA3358B4DC173)
 
-
-chunker._read_into, chunker._Stream.feed = t_read, t_feed
-cfg = ConfigFile.new(2, bench.POLY)
-try:
-    def one_pass():
+    def one():
+        k = 0
         with open(path, "rb") as f:
-            return sum(1 for _ in ChunkIter.from_config(cfg, f, n))
-    one_pass()
-    acc["read_s"] = acc["feed_s"] = 0.0
-    t0 = time.perf_counter()
-    for _ in range(a.passes):
-        one_pass()
-    wall = time.perf_counter() - t0
-finally:
+            for c in ChunkIter.from_config(cfg, f, n):
+                k += len(c)
+        assert k == n
+
+    one()
+    one()
+    # the plain sequential read of the file alone (page cache, 16 MiB reads)
+    buf = bytearray(16 << 20)
+    t = time.perf_counter()
+    for _ in range(passes):
+        with open(path, "rb", buffering=0) as f:
+            while f.readinto(buf):
+                pass
+    t_read = (time.perf_counter() - t) / passes
+    wrap(chunker, "_read_into", "read")
+    wrap(chunker._Stream, "feed", "feed")
+    wrap(chunker.RabinChunkIter, "_take", "take")
+    t = time.perf_counter()
+    for _ in range(passes):
+        one()
+    el = (time.perf_counter() - t) / passes
     os.unlink(path)
-out = {"mib": a.mib, "passes": a.passes, "gibs": round(n * a.passes / wall / 2**30, 3),
-       "wall_ms_per_pass": round(wall / a.passes * 1e3, 2),
-       "read_ms_per_pass": round(acc["read_s"] / a.passes * 1e3, 2),
-       "feed_ms_per_pass": round(acc["feed_s"] / a.passes * 1e3, 2)}
-out["rest_ms_per_pass"] = round(out["wall_ms_per_pass"] - out["read_ms_per_pass"] - out["feed_ms_per_pass"], 2)
-print(json.dumps(out))
+    out = {"mib": mib, "ms_per_pass": round(el * 1e3, 2), "gibs": round(n / el / 2**30, 2),
+           "plain_read_ms": round(t_read * 1e3, 2)}
+    for k in ("read", "feed", "take"):
+        out[k + "_ms_per_pass"] = round(acc[k] / passes * 1e3, 2)
+        out[k + "_calls_per_pass"] = acc[k + "_n"] // passes
+    print(out)
+
+
+if __name__ == "__main__":
+    main()
