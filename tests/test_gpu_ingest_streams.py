@@ -341,3 +341,36 @@ def test_stream_slots_recycled(gpu_ctx):
             assert hashlib.sha256(p["data"]).digest() == p["id"]
     finally:
         ing.close()
+
+
+@pytest.mark.parametrize("params", [
+    (0x003DA3358B4DC173, 64 << 10, 256 << 10, 1 << 20),     # small chunks: many carries
+    ((1 << 40) | 0x1B, 128 << 10, 512 << 10, 4 << 20),       # another degree (40)
+])
+def test_streams_other_parameters(params):
+    """Streams and carries with a repository's other chunker parameters
+    (ConfigFile chunk_size / min / max and poly, configfile.rs): the carry
+    is the open chunk (< max bytes) whatever max is.  Cuts vs the oracle with
+    the same parameters, ids vs hashlib, packs opened, dedup replayed."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from rustic_core_amd.chunker import Context
+    poly, mn, avg, mx = params
+    ctx = Context.get(poly, mn, avg, mx, device=0)
+    files = [_mixed(23 * MiB + 17, 71), _mixed(9 * MiB, 72),
+             np.random.default_rng(73).integers(0, 256, 5 * MiB + 3, dtype=np.uint8)]
+    files.append(files[0][:7 * MiB].copy())
+    ing = _ingest(ctx, batch_bytes=4 * MiB, pack_size=2 * MiB, pack_grow_factor=0,
+                  long_chunk=512 << 10, depth=3, max_streams=4)
+    try:
+        for i, f in enumerate(files):
+            if i % 2 == 0:
+                assert ing.add_stream(i, ChoppyReader(f, 80 + i), piece=1 * MiB + 5) == f.size
+            else:
+                ing.add(i, f)
+        stats = ing.finish()
+        assert stats["batches"] >= 10
+        _check_all(files, ing, stats, 0, params=params)
+    finally:
+        ing.close()

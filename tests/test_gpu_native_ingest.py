@@ -101,10 +101,11 @@ def _run(gpu_ctx, files, level=0, via_path=None, threads=1, index_ids=(), **cfg)
         raise
 
 
-def _check_all(files, ing, stats, level, index_ids=()):
+def _check_all(files, ing, stats, level, index_ids=(), params=None):
+    """params: (poly, min, avg, max) of the engine's context (default: rustic's)."""
     from oracle import oracle, zstd_ref
     assert stats["files"] == len(files) == len(ing.files)
-    want_cuts = [oracle.chunk_cuts(f) for f in files]
+    want_cuts = [oracle.chunk_cuts(f, *params) if params else oracle.chunk_cuts(f) for f in files]
     for i, f in enumerate(files):
         cuts, ids, nnew, ln = ing.files[i]
         assert ln == f.size
