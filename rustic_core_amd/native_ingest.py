@@ -146,14 +146,22 @@ class NativeIngest:
                                                    ctypes.byref(ticket)))
         got = 0
         try:
-            if n:
-                mv = memoryview((ctypes.c_char * n).from_address(buf.value)).cast("B")
-                with open(path, "rb", buffering=0) as f:
+            with open(path, "rb", buffering=0) as f:
+                if n:
+                    mv = memoryview((ctypes.c_char * n).from_address(buf.value)).cast("B")
                     while got < n:
                         r = f.readinto(mv[got:])
                         if not r:
                             break
                         got += r
+                # a file that grew since its size was taken: the reference
+                # reads to EOF (rabin.rs:110-191), so this one goes as a stream
+                grew = got == n and f.read(1)
+                if grew:
+                    _lib.lib().rcdc_ingest_cancel(self._h, ticket.value)
+                    f.seek(0)
+                    self.add_stream(tag, f, size_hint=n)
+                    return
         except BaseException:
             _lib.lib().rcdc_ingest_cancel(self._h, ticket.value)
             raise
@@ -186,11 +194,15 @@ class NativeIngest:
     def stream_abort(self, stream: int) -> None:
         self._check(_lib.lib().rcdc_ingest_stream_abort(self._h, stream))
 
-    def add_stream(self, tag: int, reader, piece: int = 16 << 20, size_hint: int = 0) -> int:
+    def add_stream(self, tag: int, reader, piece: Optional[int] = None, size_hint: int = 0) -> int:
         """Feed a readable binary object (readinto) until EOF as one file:
         ChunkIter::from_config(cfg, reader, size_hint) (chunker.rs:22-47).  A
         failing read aborts the stream (its completed chunks stay packed, as
-        Packer::add had them) and re-raises.  Returns the bytes read."""
+        Packer::add had them) and re-raises.  Returns the bytes read.
+        piece: bytes per reservation (default 16 MiB, at most a quarter batch,
+        as rcdc_ingest_add cuts a large file)."""
+        if piece is None:
+            piece = max(min(16 << 20, self.cfg.batch_bytes // 4) & ~255, 256)
         h = self.stream_open(tag, size_hint)
         total = 0
         try:
@@ -203,10 +215,10 @@ class NativeIngest:
                         if not r:
                             break
                         got += r
+                    self.commit(t, got)
                 except BaseException:
-                    self.cancel(t)
+                    _lib.lib().rcdc_ingest_cancel(self._h, t)  # (a no-op once committed)
                     raise
-                self.commit(t, got)
                 total += got
                 if got < piece:
                     break

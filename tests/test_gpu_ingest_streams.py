@@ -374,3 +374,26 @@ def test_streams_other_parameters(params):
         _check_all(files, ing, stats, 0, params=params)
     finally:
         ing.close()
+
+
+def test_add_file_that_grew(gpu_ctx, tmp_path, monkeypatch):
+    """A file that grew between its size and its read: the reference reads
+    to EOF (rabin.rs:110-191), so add_file drops its reservation and feeds
+    the whole file as a stream; cuts, ids and packs as for the full bytes."""
+    import os
+    files = [_mixed(6 * MiB + 999, 91), _mixed(3 * MiB, 92)]
+    paths = []
+    for i, f in enumerate(files):
+        p = tmp_path / f"f{i}"
+        p.write_bytes(f.tobytes())
+        paths.append(str(p))
+    real = os.path.getsize
+    monkeypatch.setattr(os.path, "getsize", lambda p: max(real(p) - 4097, 0))
+    ing = _ingest(gpu_ctx, batch_bytes=8 * MiB, pack_size=4 * MiB, pack_grow_factor=0)
+    try:
+        for i, p in enumerate(paths):
+            ing.add_file(i, p)
+        stats = ing.finish()
+        _check_all(files, ing, stats, 0)
+    finally:
+        ing.close()
