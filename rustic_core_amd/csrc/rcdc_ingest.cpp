@@ -198,7 +198,7 @@ struct Batch {
     std::vector<uint32_t> ncuts;    // per unit: chunks final in this batch
     std::vector<uint64_t> c_off, c_len;  // per chunk: arena offset, length
     std::vector<const uint8_t *> c_host;  // long chunks: their bytes in host memory
-    std::vector<std::vector<uint8_t>> gathers;  // long chunks split over host pieces
+    std::vector<std::vector<uint8_t>> gathers;  // long chunks split over host pieces; old carries
     std::vector<uint8_t> ids;            // 32 B per chunk
     std::vector<uint32_t> short_idx;     // chunks whose ids the device computes
     std::vector<uint64_t> seal_off, seal_len, ulen;
@@ -1095,11 +1095,16 @@ bool stage_a(Ing *g, Batch *B) {
                                    g->s_comp),
                "stream carry");
     }
+    // A long chunk's host bytes may lie inside the old carry (c_host points
+    // into it: a chunk of exactly max bytes that ended a batch's unit is
+    // the next batch's carry, whole): the old carries stay with the batch
+    // until its host id jobs are done (stage B runs after them)
     for (auto &c : carries) {
         Unit &u = *c.first;
         StreamSt &st = *u.st;
         std::vector<uint8_t> h(u.len - c.second);
         if (!h.empty()) unit_gather(u, c.second, h.size(), h.data());
+        B->gathers.push_back(std::move(st.hcarry));
         st.hcarry = std::move(h);
         st.base = u.base + c.second;
         st.carry_len = u.len - c.second;
@@ -1110,8 +1115,8 @@ bool stage_a(Ing *g, Batch *B) {
             if (u.st && u.final && u.st->cslot >= 0) {
                 g->free_cslots.push_back(u.st->cslot);
                 u.st->cslot = -1;
-                u.st->hcarry.clear();
-                u.st->hcarry.shrink_to_fit();
+                B->gathers.push_back(std::move(u.st->hcarry));
+                u.st->hcarry = std::vector<uint8_t>();
                 g->closing_streams--;
             }
         g->cv_slot.notify_all();

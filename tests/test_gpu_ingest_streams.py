@@ -397,3 +397,31 @@ def test_add_file_that_grew(gpu_ctx, tmp_path, monkeypatch):
         _check_all(files, ing, stats, 0)
     finally:
         ing.close()
+
+
+def test_long_chunk_inside_the_old_carry():
+    """tools/soak_ingest.py seed 24: text whose chunks are all max bytes, a
+    stream whose unit ends exactly at a chunk's max, so the next batch's
+    first chunk is the whole carry; it is longer than long_chunk, so its id
+    is hashed on the host from the carry's bytes.  Round 6 freed those bytes
+    when the carry was replaced, before the host job read them (wrong ids)."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from rustic_core_amd.chunker import Context
+    params = ((1 << 40) | 0x1B, 64 << 10, 256 << 10, 1 << 20)
+    ctx = Context.get(*params, device=0)
+    text = np.frombuffer(b"id,name,value\n17,alpha,3.25\n", np.uint8)
+    files = [np.resize(text, 1207054).copy(), np.resize(text, 4903720).copy(),
+             np.resize(text, 9 * MiB + 77).copy(), np.resize(text, 3 * MiB).copy()]
+    for rep in range(3):
+        ing = _ingest(ctx, batch_bytes=2 * MiB + 256, depth=1, in_slots=3, out_slots=2,
+                      max_streams=1, long_chunk=256 << 10, pack_size=4 * MiB, pack_grow_factor=0,
+                      hash_threads=7)
+        try:
+            for i, f in enumerate(files):
+                ing.add(i, f)
+            stats = ing.finish()
+            _check_all(files, ing, stats, 0, params=params)
+        finally:
+            ing.close()
