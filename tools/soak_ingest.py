@@ -7,7 +7,11 @@ add_stream with short reads and random piece sizes, or from a file on disk),
 the engine shape (batch_bytes 1-64 MiB, depth, slots, streams, long-chunk
 threshold, pack size and grow factor) and the zstd level (stored blobs,
 0 = default, 1, 3, 7), and checks every cut, chunk id, pack id, pack header,
-blob and dedup decision.  Exits 1 on a mismatch with the case's seed.
+blob and dedup decision.  Some streams fail mid-way (their read raises: the
+stream is aborted, its completed chunks stay packed, no file result), some
+reservations are cancelled, and some cases run two engines over one shared
+dedup set (MultiIngest: every new id packed exactly once across both).
+Exits 1 on a mismatch with the case's seed.
 
   python tools/soak_ingest.py [seconds] [seed]
 """
@@ -23,8 +27,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 sys.path.insert(0, os.path.join(ROOT, "tools"))
-from tests.test_gpu_native_ingest import KEY, _check_all  # noqa: E402
-from tests.test_gpu_ingest_streams import ChoppyReader  # noqa: E402
+from tests.test_gpu_native_ingest import KEY  # noqa: E402
+from tests.test_gpu_ingest_streams import ChoppyReader, FailingReader  # noqa: E402
 from soak import POLYS  # noqa: E402
 
 KiB, MiB = 1 << 10, 1 << 20
@@ -52,9 +56,74 @@ def gen(rng, kind, n, earlier):
     return rng.integers(0, 256, n, dtype=np.uint8)
 
 
+def _chunks(data, cuts):
+    prev = 0
+    for c in cuts:
+        yield data[prev:int(c)]
+        prev = int(c)
+
+
+def check(events, engines, stats, level, params, ordered):
+    """events: (tag, bytes, kind, fed) in add order; kind full / aborted /
+    cancelled.  The checks of tests/test_gpu_native_ingest._check_all,
+    with aborted streams' completed chunks in the replay (all the cuts of
+    the fed prefix but the last) and, with two engines (ordered False),
+    the packed ids compared as a set, each exactly once."""
+    import hashlib
+    from oracle import oracle, zstd_ref
+    full = [(t, d) for t, d, k, _ in events if k == "full"]
+    files = {}
+    for e in engines:
+        files.update(e.files)
+    assert stats["files"] == len(full) == len(files), ("files", stats["files"], len(full), len(files))
+    seen, new, by_id = set(), [], {}
+    for t, d, k, fed in events:
+        if k == "cancelled":
+            continue
+        if k == "full":
+            cuts = oracle.chunk_cuts(d, *params)
+            got_cuts, ids, nnew, ln = files[t]
+            assert ln == d.size, ("len", t)
+            assert np.array_equal(got_cuts, cuts), ("cuts", t)
+            for j, c in enumerate(_chunks(d, cuts)):
+                assert bytes(ids[j]) == hashlib.sha256(c.tobytes()).digest(), ("id", t, j)
+        else:  # aborted: the fed prefix's final cuts
+            cuts = oracle.chunk_cuts(d[:fed], *params)[:-1]
+        for c in _chunks(d, cuts):
+            h = hashlib.sha256(c.tobytes()).digest()
+            by_id.setdefault(h, c)
+            if h not in seen:
+                seen.add(h)
+                new.append(h)
+    assert stats["new_blobs"] == len(new), ("new_blobs", stats["new_blobs"], len(new))
+    packed = []
+    for e in engines:
+        assert [p["seq"] for p in e.packs] == list(range(len(e.packs))), "pack seq"
+        for p in e.packs:
+            data = p["data"]
+            assert len(data) == p["size"] and hashlib.sha256(data).digest() == p["id"], "pack id"
+            parsed = oracle.parse_pack(KEY, data)
+            assert len(parsed) == len(p["blobs"]), "pack header"
+            end = 0
+            for (tpe, off, ln, ulen, bid), (id_, boff, blen, bulen, btype) in zip(parsed, p["blobs"]):
+                assert off == boff and ln == blen and bytes(bid) == id_ and ulen == bulen, "blob entry"
+                plain = oracle.open_(KEY, data[off:off + ln])
+                raw = zstd_ref.decompress(plain) if level is not None else plain
+                assert hashlib.sha256(raw).digest() == id_, "blob bytes"
+                end = off + ln
+                packed.append(id_)
+            assert end + p["header_len"] + 4 == p["size"], "pack size"
+    if ordered:
+        assert packed == new, "Packer::add order"
+    else:
+        assert len(packed) == len(set(packed)) and set(packed) == set(new), "packed once"
+
+
 def one_case(seed, tmp):
+    import ctypes
+    from rustic_core_amd import _lib
     from rustic_core_amd.chunker import Context
-    from rustic_core_amd.native_ingest import NativeIngest
+    from rustic_core_amd.native_ingest import MultiIngest, NativeIngest
     rng = np.random.default_rng(seed)
     poly = POLYS[int(rng.integers(0, len(POLYS)))]
     mn, avg, mx = PARAMS[int(rng.integers(0, len(PARAMS)))]
@@ -73,38 +142,71 @@ def one_case(seed, tmp):
                pack_size=int(rng.choice([1, 4, 32])) * MiB,
                pack_grow_factor=int(rng.choice([0, 32])), hash_threads=int(rng.integers(1, 11)))
     level = [None, 0, 1, 3, 7][int(rng.integers(0, 5))]
-    ing = NativeIngest(ctx, KEY, level=level, **cfg)
-    how = []
-    try:
-        for i, f in enumerate(files):
-            h = int(rng.integers(0, 3))
-            how.append(h)
-            if h == 0:
-                ing.add(i, f)
-            elif h == 1:
-                piece = int(rng.integers(64 * KiB, max(batch // 4, 64 * KiB + 1)))
-                assert ing.add_stream(i, ChoppyReader(f, seed * 100 + i), piece=piece,
-                                      size_hint=int(rng.integers(0, 2 * f.size + 1))) == f.size
-            else:
-                p = os.path.join(tmp, f"s{seed}_{i}")
-                with open(p, "wb") as fh:
-                    fh.write(f.tobytes())
-                ing.add_file(i, p)
-                os.unlink(p)
-        stats = ing.finish()
-        _check_all(files, ing, stats, level, params=(poly, mn, avg, mx))
-    finally:
-        ing.close()
+    multi = rng.random() < 0.2
+    events = []
+    if multi:
+        m = MultiIngest([ctx, ctx], KEY, level=level, **cfg)
+        engines = m.engines
+        try:
+            for i, f in enumerate(files):
+                m.add(i, f)
+                events.append((i, f, "full", f.size))
+            stats = m.finish()
+            check(events, engines, stats, level, (poly, mn, avg, mx), ordered=False)
+        finally:
+            m.close()
+    else:
+        ing = NativeIngest(ctx, KEY, level=level, **cfg)
+        engines = [ing]
+        try:
+            for i, f in enumerate(files):
+                h = int(rng.integers(0, 5))
+                if h == 0 or h == 4:
+                    ing.add(i, f)
+                    events.append((i, f, "full", f.size))
+                elif h == 1:
+                    piece = int(rng.integers(64 * KiB, max(batch // 4, 64 * KiB + 1)))
+                    if rng.random() < 0.25 and f.size > 1:  # the read fails mid-way
+                        fail_at = int(rng.integers(1, f.size))
+                        try:
+                            ing.add_stream(i, FailingReader(f, seed * 100 + i, fail_at), piece=piece)
+                            raise AssertionError("the failing read did not raise")
+                        except OSError:
+                            pass
+                        events.append((i, f, "aborted", fail_at // piece * piece))
+                    else:
+                        assert ing.add_stream(i, ChoppyReader(f, seed * 100 + i), piece=piece,
+                                              size_hint=int(rng.integers(0, 2 * f.size + 1))) == f.size
+                        events.append((i, f, "full", f.size))
+                elif h == 2:
+                    p = os.path.join(tmp, f"s{seed}_{i}")
+                    with open(p, "wb") as fh:
+                        fh.write(f.tobytes())
+                    ing.add_file(i, p)
+                    os.unlink(p)
+                    events.append((i, f, "full", f.size))
+                else:  # a reservation whose read fails: cancelled
+                    buf, t = ctypes.c_void_p(), ctypes.c_uint64()
+                    n = min(f.size, batch)
+                    assert _lib.lib().rcdc_ingest_reserve(ing._h, n, ctypes.byref(buf),
+                                                          ctypes.byref(t)) == 0
+                    ing.cancel(t.value)
+                    events.append((i, f, "cancelled", 0))
+            stats = ing.finish()
+            check(events, engines, stats, level, (poly, mn, avg, mx), ordered=True)
+        finally:
+            ing.close()
     return {"seed": seed, "files": len(files), "bytes": int(sum(f.size for f in files)),
             "batches": int(stats["batches"]), "packs": int(stats["packs"]), "level": level,
-            "how": how, "cfg": cfg, "params": [hex(poly), mn, avg, mx]}
+            "multi": multi, "kinds": [e[2] for e in events], "cfg": cfg,
+            "params": [hex(poly), mn, avg, mx]}
 
 
 def main():
     secs = float(sys.argv[1]) if len(sys.argv) > 1 else 300
     seed0 = int(sys.argv[2]) if len(sys.argv) > 2 else 1
     t0 = last = time.time()
-    n = nbytes = packs = 0
+    n = nbytes = packs = aborted = cancelled = multi = 0
     seed = seed0
     with tempfile.TemporaryDirectory(dir=os.environ.get("TMPDIR", "/tmp")) as tmp:
         while time.time() - t0 < secs:
@@ -116,12 +218,16 @@ def main():
             n += 1
             nbytes += r["bytes"]
             packs += r["packs"]
+            aborted += r["kinds"].count("aborted")
+            cancelled += r["kinds"].count("cancelled")
+            multi += r["multi"]
             seed += 1
             if time.time() - last > 60:
                 last = time.time()
                 print(json.dumps({"cases": n, "packs": packs, "gib": round(nbytes / 2**30, 2)}),
                       flush=True)
-    print(json.dumps({"soak_ingest": "ok", "cases": n, "packs": packs,
+    print(json.dumps({"soak_ingest": "ok", "cases": n, "packs": packs, "aborted_streams": aborted,
+                      "cancelled": cancelled, "two_engine_cases": multi,
                       "gib": round(nbytes / 2**30, 2), "seeds": [seed0, seed - 1],
                       "seconds": round(time.time() - t0, 1)}), flush=True)
 
