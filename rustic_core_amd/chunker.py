@@ -392,8 +392,22 @@ def _iter_done() -> None:
 # a file's reads, device passes and chunk copies overlap (one-thread order
 # was read -> feed -> copies, ~28 ms per 256 MiB, tools/c1_profile.py).
 # PIPE_BLOCKS bounds the blocks one iterator holds (read, fed or not yet
-# copied out).
+# copied out), raised to what the device stream needs to see a cut: it runs
+# a pass only once rcdc_stream_batch_bytes are buffered after its last cut,
+# and the consumer frees no block until then (with 2 blocks of reads short
+# of 16 MiB the pipe waited for itself: tools/soak_stream.py).
 PIPE_BLOCKS = int(os.environ.get("RCDC_PIPE_BLOCKS", "4"))
+
+
+def _pipe_blocks(ctx) -> int:
+    """Blocks a pipe may hold: the block with the consumer's position
+    (as little as 1 unconsumed byte), enough blocks of >= READ_SIZE -
+    MIN_READ bytes to reach the stream's pass size, and the one being read."""
+    h = getattr(ctx, "handle", None)
+    batch = int(_lib.lib().rcdc_stream_batch_bytes(h)) if h is not None else \
+        max(16 * MB, 2 * ctx.max_size + 256)
+    need = 2 + -(-batch // (READ_SIZE - MIN_READ))
+    return max(PIPE_BLOCKS, need)
 
 
 class _Pipe:
@@ -401,10 +415,10 @@ class _Pipe:
     file order: (block, start, n, retire_block, cuts, eof), or an exception
     to raise where the consumer reaches it."""
 
-    def __init__(self, reader, stream, first):
+    def __init__(self, reader, stream, first, blocks):
         self.reader, self.stream = reader, stream
         self.stop = threading.Event()
-        self.room = threading.Semaphore(PIPE_BLOCKS - 1)  # (`first`'s block is held)
+        self.room = threading.Semaphore(blocks - 1)  # (`first`'s block is held)
         self.feed_q = collections.deque()
         self.feed_cv = threading.Condition()
         self.out = collections.deque()
@@ -541,7 +555,8 @@ class RabinChunkIter:
             # pipeline (reader, feeder and this thread), this read included
             if n == READ_SIZE and os.environ.get("RCDC_READ_AHEAD", "1") != "0":
                 self._threaded = True
-                self._pipe = _Pipe(self._reader, self._stream, (blk, p, n, retire))
+                self._pipe = _Pipe(self._reader, self._stream, (blk, p, n, retire),
+                                   _pipe_blocks(self._ctx))
                 self._blk = None
                 continue
             self._eof = not n

@@ -192,3 +192,62 @@ def test_pipe_holds_at_most_pipe_blocks(fake):
     assert it._pipe is not None and len(reads) <= C.PIPE_BLOCKS
     total = K + sum(len(c) for c in it)
     assert total == n and len(reads) == n // C.READ_SIZE + 2  # (+ the last partial, EOF)
+
+
+def test_pipe_never_waits_for_itself(monkeypatch):
+    """The device stream hands out cuts only once it holds its pass size
+    (16 MiB + 256) after its last cut, and a block goes back only when all
+    of its bytes are copied out.  A last cut one byte before a block's end
+    and reads short of 16 MiB then need a third block: with PIPE_BLOCKS = 2
+    the round-6 pipe waited for itself (tools/soak_stream.py).  The bound is
+    raised to what the stream needs (_pipe_blocks)."""
+    import threading
+    B = (16 << 20) + 256
+    n = 64 << 20
+    M = 1 << 20
+    # cuts <= max (8 MiB) apart; the first pass (fed 31 MiB + 1) ends right
+    # after the cut at 31 MiB, so its block keeps one unconsumed byte
+    cuts_all = [8 * M, 16 * M, 24 * M, 31 * M, 38 * M, 46 * M, 54 * M, 62 * M, n]
+
+    class _Batched:
+        def __init__(self, ctx):
+            self.fed, self.base, self.closed = 0, 0, False
+
+        def feed(self, data, fin):
+            self.fed += len(data)
+            if not fin and self.fed - self.base < B:
+                return np.zeros(0, np.uint64)
+            out = [c for c in cuts_all if self.base < c < self.fed or (fin and c == self.fed)]
+            if out:
+                self.base = out[-1]
+            return np.array(out, np.uint64)
+
+        def close(self):
+            self.closed = True
+
+    class _Reads(io.RawIOBase):
+        def __init__(self):
+            self._b, self._first = io.BytesIO(bytes(n)), True
+
+        def readable(self):
+            return True
+
+        def readinto(self, mv):
+            k = len(mv) if self._first else min(len(mv), (15 << 20) + 1)
+            self._first = False
+            b = self._b.read(k)
+            mv[:len(b)] = b
+            return len(b)
+
+    monkeypatch.setattr(C, "_Stream", _Batched)
+    monkeypatch.setattr(C, "check_rabin_params", lambda *a: None)
+    monkeypatch.setattr(C, "PIPE_BLOCKS", 2)
+    got = []
+
+    def run():
+        got.extend(len(c) for c in C.RabinChunkIter(_Ctx(), _Reads()))
+    t = threading.Thread(target=run, daemon=True)
+    t.start()
+    t.join(20)
+    assert not t.is_alive(), "the pipe waited for itself"
+    assert got == np.diff([0] + cuts_all).tolist()
