@@ -2653,7 +2653,8 @@ rcdc_status zstd_compress(rcdc_ctx *ctx, int level, const void *d_in, const rcdc
                           hipMemcpyHostToDevice));
     }
     const uint32_t grid = zstd_block_grid((uint32_t)std::max(ctx->num_cus, 1), level);
-    if ((rs = ensure_dev(&ctx->d_zstd_seq, &ctx->cap_zstd_seq, (uint64_t)grid * kZstdMaxSeq)))
+    // (+ 8 words: the last wave's 16-byte literal loads may pass its region by 20 bytes)
+    if ((rs = ensure_dev(&ctx->d_zstd_seq, &ctx->cap_zstd_seq, (uint64_t)grid * kZstdMaxSeq + 8)))
         return rs;
     const uint64_t nbl = blks.size(), nbo = blobs.size();
     if ((rs = ensure_dev(&ctx->d_zstd_blobs, &ctx->cap_zstd_blobs, nbo))) return rs;
@@ -2671,14 +2672,101 @@ rcdc_status zstd_compress(rcdc_ctx *ctx, int level, const void *d_in, const rcdc
                            hipMemcpyHostToDevice, st));
     HIP_TRY(hipMemcpyAsync(ctx->d_zstd_blks, blks.data(), nbl * sizeof(ZstdBlk),
                            hipMemcpyHostToDevice, st));
+    if (const char *e = getenv("RCDC_ZSTD_DBG"); e && (atoi(e) & 32)) {  // the buffers, to place a fault
+        auto rng = [](const char *nm, const void *p, uint64_t bytes) {
+            fprintf(stderr, "rcdc zstd buf %-6s [%p, %p) %llu B\n", nm, p, (const void *)((const char *)p + bytes),
+                    (unsigned long long)bytes);
+        };
+        rng("seq", ctx->d_zstd_seq, ctx->cap_zstd_seq * 8);
+        rng("slots", ctx->d_zstd_slots, ctx->cap_zstd_slots);
+        rng("far", ctx->d_zstd_far, ctx->cap_zstd_far * 4);
+        rng("res", ctx->d_zstd_res, ctx->cap_zstd_res * 8);
+        rng("bpos", ctx->d_zstd_bpos, ctx->cap_zstd_bpos * 8);
+        rng("blobs", ctx->d_zstd_blobs, ctx->cap_zstd_blobs * sizeof(ZstdBlob));
+        rng("blks", ctx->d_zstd_blks, ctx->cap_zstd_blks * sizeof(ZstdBlk));
+        rng("tabs", ctx->d_zstd_tabs, ctx->cap_zstd_tabs * sizeof(ZstdTables));
+        rng("queue", ctx->d_zstd_queue, ctx->cap_zstd_queue * 4);
+        rng("in", d_in, 0);
+        rng("out", d_out, 0);
+        fprintf(stderr, "rcdc zstd grid %u nblk %llu maxw %llu level %d\n", grid, (unsigned long long)nbl,
+                (unsigned long long)maxw, level);
+    }
+    // RCDC_ZSTD_GUARD=1 (debugging): every scratch buffer of this call is a
+    // fresh allocation with 16 MiB of 0xCD before and after it, checked after
+    // the call; a kernel that strays past one is reported, not faulted
+    struct GBuf {
+        uint8_t *base = nullptr;
+        uint64_t bytes = 0;
+        const char *name = "";
+    };
+    std::vector<GBuf> gbufs;
+    static const bool zguard = getenv("RCDC_ZSTD_GUARD") != nullptr;
+    constexpr uint64_t kG = 16ull << 20;
+    auto galloc = [&](const char *nm, uint64_t bytes) -> uint8_t * {
+        GBuf b;
+        b.name = nm;
+        b.bytes = bytes;
+        if (hipMalloc((void **)&b.base, bytes + 2 * kG) != hipSuccess) return nullptr;
+        (void)hipMemset(b.base, 0xCD, bytes + 2 * kG);
+        gbufs.push_back(b);
+        return b.base + kG;
+    };
+    ZstdBlob *u_blobs = ctx->d_zstd_blobs;
+    ZstdBlk *u_blks = ctx->d_zstd_blks;
+    ZstdTables *u_tabs = ctx->d_zstd_tabs;
+    uint8_t *u_slots = ctx->d_zstd_slots;
+    uint64_t *u_seq = ctx->d_zstd_seq, *u_bpos = ctx->d_zstd_bpos, *u_lens = ctx->d_zstd_lens;
+    uint2 *u_res = ctx->d_zstd_res;
+    uint32_t *u_queue = ctx->d_zstd_queue, *u_far = farw ? ctx->d_zstd_far : nullptr;
+    if (zguard) {
+        HIP_TRY(hipStreamSynchronize(st));
+        u_blobs = (ZstdBlob *)galloc("blobs", nbo * sizeof(ZstdBlob));
+        u_blks = (ZstdBlk *)galloc("blks", nbl * sizeof(ZstdBlk));
+        u_tabs = (ZstdTables *)galloc("tabs", sizeof(ZstdTables));
+        u_slots = galloc("slots", maxw * kZstdSlot);
+        u_seq = (uint64_t *)galloc("seq", ((uint64_t)grid * kZstdMaxSeq + 8) * 8);
+        u_bpos = (uint64_t *)galloc("bpos", nbl * 8);
+        u_lens = (uint64_t *)galloc("lens", nbo * 8);
+        u_res = (uint2 *)galloc("res", nbl * 8);
+        u_queue = (uint32_t *)galloc("queue", wins.size() * 128 * 4);
+        if (farw) u_far = (uint32_t *)galloc("far", farw * 4);
+        for (const GBuf &gb : gbufs)
+            if (!gb.base) return fail(RCDC_ERR_INTERNAL, "zstd guard allocation");
+        HIP_TRY(hipMemcpy(u_blobs, blobs.data(), nbo * sizeof(ZstdBlob), hipMemcpyHostToDevice));
+        HIP_TRY(hipMemcpy(u_blks, blks.data(), nbl * sizeof(ZstdBlk), hipMemcpyHostToDevice));
+        HIP_TRY(hipMemcpy(u_tabs, &zstd_tables(), sizeof(ZstdTables), hipMemcpyHostToDevice));
+        HIP_TRY(hipMemset(u_queue, 0, wins.size() * 128 * 4));
+        for (const GBuf &gb : gbufs)
+            fprintf(stderr, "rcdc zstd guarded %-6s [%p, %p)\n", gb.name, (void *)(gb.base + kG),
+                    (void *)(gb.base + kG + gb.bytes));
+    }
     for (size_t k = 0; k < wins.size(); k++) {
         const Win &w = wins[k];
-        HIP_TRY(launch_zstd((const uint8_t *)d_in, (uint8_t *)d_out, ctx->d_zstd_blobs + w.blob0,
-                            (uint32_t)w.nblob, ctx->d_zstd_blks + w.blk0, (uint32_t)w.nblk,
-                            ctx->d_zstd_tabs, ctx->d_zstd_slots, ctx->d_zstd_seq, grid,
-                            ctx->d_zstd_res + w.blk0, ctx->d_zstd_bpos + w.blk0,
-                            ctx->d_zstd_lens + w.blob0, ctx->d_zstd_queue + 128 * k,
-                            farw ? ctx->d_zstd_far : nullptr, level, st));
+        HIP_TRY(launch_zstd((const uint8_t *)d_in, (uint8_t *)d_out, u_blobs + w.blob0,
+                            (uint32_t)w.nblob, u_blks + w.blk0, (uint32_t)w.nblk,
+                            u_tabs, u_slots, u_seq, grid, u_res + w.blk0, u_bpos + w.blk0,
+                            u_lens + w.blob0, u_queue + 128 * k, u_far, level, st));
+    }
+    if (zguard) {
+        HIP_TRY(hipStreamSynchronize(st));
+        std::vector<uint8_t> gh(kG);
+        for (const GBuf &gb : gbufs)
+            for (int side = 0; side < 2; side++) {
+                const uint8_t *gp = side ? gb.base + kG + gb.bytes : gb.base;
+                HIP_TRY(hipMemcpy(gh.data(), gp, kG, hipMemcpyDeviceToHost));
+                int64_t lo = -1, hi = -1;
+                for (uint64_t i = 0; i < kG; i++)
+                    if (gh[i] != 0xCD) {
+                        if (lo < 0) lo = (int64_t)i;
+                        hi = (int64_t)i;
+                    }
+                if (lo >= 0)
+                    fprintf(stderr, "rcdc zstd GUARD HIT %s %s: guard bytes %lld..%lld written\n", gb.name,
+                            side ? "after" : "before", (long long)lo, (long long)hi);
+            }
+        HIP_TRY(hipMemcpy(out_lens, u_lens, nbo * 8, hipMemcpyDeviceToHost));
+        for (const GBuf &gb : gbufs) (void)hipFree(gb.base);
+        return null_leave(ctx, hip_stream, st);
     }
     HIP_TRY(hipMemcpyAsync(out_lens, ctx->d_zstd_lens, nbo * 8, hipMemcpyDeviceToHost, st));
     // the host descriptors die with this call

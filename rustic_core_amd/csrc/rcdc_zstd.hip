@@ -770,7 +770,16 @@ __device__ void huf_stream(const uint8_t *lbuf, uint32_t a, uint32_t b, const ui
         uint4 v = make_uint4(0, 0, 0, 0);
         if (tl < len) {
             cnt = len - tl < 16 ? len - tl : 16u;
-            v = ld16(lbuf + b - tl - 16);  // literal b-1-tl is byte 15
+            // literal b-1-tl is byte 15.  The first stream's last group
+            // starts before lbuf, which is the scratch buffer's first byte
+            // for wave 0 when its block has no sequences: only bytes at or
+            // after lbuf are read (a 16-byte load there faulted, r6 zstd soak)
+            const uint8_t *p = lbuf + b - tl - 16;
+            if (b - tl >= 16)
+                v = ld16(p);
+            else
+                v = make_uint4(ld4_lo(p, lbuf), ld4_lo(p + 4, lbuf), ld4_lo(p + 8, lbuf),
+                               ld4_lo(p + 12, lbuf));
             for (uint32_t k = 0; k < cnt; k++) bits += code[byte_of(v, 15 - k)] >> 16;
         }
         uint32_t incl = bits;
@@ -2039,6 +2048,15 @@ hipError_t launch_zstd(const uint8_t *in, uint8_t *out, const ZstdBlob *blobs, u
                            dense);
     }
     static const uint32_t dbg = getenv("RCDC_ZSTD_DBG") ? (uint32_t)atoi(getenv("RCDC_ZSTD_DBG")) : 0u;
+    // RCDC_ZSTD_DBG bit 4 (16): wait after each kernel and name the one that failed
+    auto step = [&](const char *what) -> hipError_t {
+        if (!(dbg & 16u)) return hipSuccess;
+        const hipError_t e = hipStreamSynchronize(stream);
+        if (e != hipSuccess) fprintf(stderr, "rcdc zstd: %s failed: %s\n", what, hipGetErrorString(e));
+        return e;
+    };
+    if (far && nblk)
+        if (const hipError_t e = step("far build + far map")) return e;
     const uint32_t g = nblk < grid ? nblk : grid;
     if (g) {
         auto *k = !z.narrow      ? rcdc_zstd_block_kernel<11, false>
@@ -2046,9 +2064,11 @@ hipError_t launch_zstd(const uint8_t *in, uint8_t *out, const ZstdBlob *blobs, u
                                  : rcdc_zstd_block_kernel<13, true>;
         hipLaunchKernelGGL(k, dim3(g), dim3(64), 0, stream, in, blobs, blks, nblk, tabs, slots,
                            seqbuf, res, dbg, z.key, queue, far);
+        if (const hipError_t e = step("block kernel")) return e;
     }
     hipLaunchKernelGGL(rcdc_zstd_frame_kernel, dim3((nblobs + 255) / 256), dim3(256), 0, stream,
                        blobs, nblobs, res, bpos, out, out_lens);
+    if (const hipError_t e = step("frame kernel")) return e;
     // A/B knobs: RCDC_ZSTD_COPY=1 loads dword-aligned dwordx4 + one dword per
     // 16 B instead of 16-aligned loads with a lane shuffle (default, random
     // blocks +13 %); RCDC_ZSTD_NT=0 (with COPY=1) plain loads and stores
@@ -2060,6 +2080,7 @@ hipError_t launch_zstd(const uint8_t *in, uint8_t *out, const ZstdBlob *blobs, u
     if (nblk)
         hipLaunchKernelGGL(copy, dim3(nblk), dim3(kZstdCopyThreads), 0, stream, in, blobs, blks,
                            res, bpos, slots, out);
+    if (const hipError_t e = step("copy kernel")) return e;
     return hipGetLastError();
 }
 

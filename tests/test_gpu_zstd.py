@@ -343,3 +343,33 @@ def test_rle_edges(gpu_ctx):
             pads.append((i * 2 + which) % 16)
     frames = _compress(gpu_ctx, datas, in_pad=pads)
     _check(frames, datas)
+
+
+def test_literal_only_block_on_wave_zero():
+    """Round 6's soak fault (tools/soak_zstd.py seed 2, level 22): wave 0's
+    block had no sequences, so its literals started at the sequence
+    scratch's first byte, and the first Huffman stream's last 16-byte load
+    began up to 15 bytes before it -- an illegal access when the page below
+    the allocation was unmapped, as in a fresh process (3 of 3 runs).  The
+    case is replayed as its process's first compression call, then a
+    literal-only block (a flat 120-symbol alphabet: direct Huffman weights,
+    ~6.9 bits a byte, next to no 5-byte repeats) on wave 0 at every level family."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, os.path.join(root, "tools", "soak_zstd.py"), "60", "2", "1"],
+                       cwd=root, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0 and '"soak_zstd": "ok"' in r.stdout, (r.stdout[-2000:], r.stderr[-2000:])
+    from oracle import oracle
+    from rustic_core_amd.chunker import Context
+    ctx = Context.get(oracle.DEFAULT_POLY, oracle.DEFAULT_MIN, oracle.DEFAULT_AVG,
+                      oracle.DEFAULT_MAX, device=0)
+    rng = np.random.default_rng(7)
+    for n in (100, 1000, 4099, 65536 + 7, 131072):
+        d = bytes(rng.integers(0, 120, n).astype(np.uint8))
+        for level in (1, 3, 22):
+            frames = _compress(ctx, [d], level=level)
+            _check(frames, [d])
+            if n >= 4096:
+                assert len(frames[0]) < 0.95 * n  # Huffman literals, not raw
