@@ -777,6 +777,8 @@ __device__ void check_compressed(Dec &D, DecLds &L, const uint8_t *p, uint32_t b
     if (nseq) {
         if (q >= end) { D.bad = kCkCorrupt; return; }
         const uint32_t modes = *q++;
+        // reserved bits 1-0 must be zero (RFC 8878 3.1.1.3.2.1; libzstd 1.5,
+        // the reference's, rejects them, 1.4.8 decodes)
         if (modes & 3u) { D.bad = kCkCorrupt; return; }
         // tables in the order LL, OF, ML
         for (int k = 0; k < 3; k++) {
