@@ -434,7 +434,10 @@ typedef struct {
     uint64_t out_off;
 } rcdc_zstd_ref;
 
-/* Worst-case frame size of a len-byte blob (header + stored blocks). */
+/* Worst-case frame size of a len-byte blob (header + stored blocks):
+ * len + 3 per 128 KiB block + 9, + 10 above 2^27 bytes (those frames carry a
+ * window descriptor: rustic's decode_all refuses windows above 2^27 + 1, and
+ * a single-segment frame's window is its content size). */
 uint64_t rcdc_zstd_bound(uint64_t len);
 
 /* Compress n blobs (refs is a HOST array).  level: zstd's range

@@ -15,8 +15,9 @@ decoding is pinned.
 
 Decoders used as checkers (two independent builds):
   - the system libzstd (libzstd.so.1, 1.4.8) through ctypes: ZSTD_decompress,
-    ZSTD_getFrameContentSize, and ZSTD_compress for the CPU baseline (the
-    library rustic itself links, at another version);
+    ZSTD_decompressStream (decode_all's streaming decoder, with its window
+    limit), ZSTD_getFrameContentSize, and ZSTD_compress for the CPU baseline
+    (the library rustic itself links, at another version);
   - pyarrow's bundled zstd codec (cross-check).
 """
 from __future__ import annotations
@@ -49,6 +50,12 @@ def lib() -> ctypes.CDLL:
         L.ZSTD_getFrameContentSize.argtypes = [vp, sz]
         L.ZSTD_findFrameCompressedSize.restype = sz
         L.ZSTD_findFrameCompressedSize.argtypes = [vp, sz]
+        L.ZSTD_createDStream.restype = vp
+        L.ZSTD_freeDStream.argtypes = [vp]
+        L.ZSTD_initDStream.restype = sz
+        L.ZSTD_initDStream.argtypes = [vp]
+        L.ZSTD_decompressStream.restype = sz
+        L.ZSTD_decompressStream.argtypes = [vp, vp, vp]
         _lib = L
     return _lib
 
@@ -93,6 +100,36 @@ def decompress(frame: bytes, size: Optional[int] = None) -> bytes:
     buf = ctypes.create_string_buffer(max(size, 1))
     n = _check(lib().ZSTD_decompress(buf, size, frame, len(frame)))
     return buf.raw[:n]
+
+
+class _ZBuf(ctypes.Structure):
+    _fields_ = [("ptr", ctypes.c_void_p), ("size", ctypes.c_size_t), ("pos", ctypes.c_size_t)]
+
+
+def decompress_stream(frame: bytes) -> bytes:
+    """decode_all as rustic runs it: the zstd crate's streaming Decoder
+    (ZSTD_decompressStream with libzstd's defaults, so frames asking for a
+    window above 2^27 + 1 bytes are refused -- single-segment frames ask for
+    their content size).  One frame; raises ZstdError."""
+    L = lib()
+    ds = L.ZSTD_createDStream()
+    try:
+        _check(L.ZSTD_initDStream(ds))
+        src = ctypes.create_string_buffer(frame, len(frame))
+        ib = _ZBuf(ctypes.cast(src, ctypes.c_void_p), len(frame), 0)
+        step = 1 << 20
+        dst = ctypes.create_string_buffer(step)
+        out = []
+        while True:
+            ob = _ZBuf(ctypes.cast(dst, ctypes.c_void_p), step, 0)
+            r = _check(L.ZSTD_decompressStream(ds, ctypes.byref(ob), ctypes.byref(ib)))
+            out.append(dst.raw[:ob.pos])
+            if r == 0:
+                return b"".join(out)
+            if ob.pos == 0 and ib.pos == len(frame):
+                raise ZstdError("truncated frame")
+    finally:
+        L.ZSTD_freeDStream(ds)
 
 
 def decompress_pyarrow(frame: bytes, size: int) -> bytes:

@@ -48,7 +48,7 @@ def zstd_bounds(lens) -> np.ndarray:
     """rcdc_zstd_bound of every length (numpy; the same formula)."""
     lens = np.asarray(lens, np.int64)
     nblk = np.maximum((lens + (128 << 10) - 1) // (128 << 10), 1)
-    return lens + 3 * nblk + 9
+    return lens + 3 * nblk + np.where(lens > (1 << 27), 10, 9)  # + the window byte
 
 
 def frame_layout(lens, align: int = 16):

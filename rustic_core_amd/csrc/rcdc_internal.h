@@ -267,6 +267,10 @@ struct AeadUnit {  // 16 B
 // sequences coded with the predefined FSE tables).  Matches stay inside their
 // block.
 constexpr uint32_t kZstdBlock = 128u * 1024u;     // ZSTD_BLOCKSIZE_MAX
+// Frames of blobs above kZstdSingleMax bytes are not single-segment: they
+// declare a 2^kZstdWindowLog window (rcdc_zstd_frame_kernel)
+constexpr uint32_t kZstdSingleMax = 1u << 27;
+constexpr uint32_t kZstdWindowLog = 20;
 constexpr uint32_t kZstdSlot = kZstdBlock + 64u;  // scratch per block: compressed content
 constexpr uint32_t kZstdMaxSeq = kZstdBlock / 4u + 1u;  // matches are >= 4 bytes
 constexpr uint32_t kZstdTypeRaw = 0, kZstdTypeRle = 1, kZstdTypeComp = 2;

@@ -2911,7 +2911,9 @@ rcdc_status rcdc_copy_ranges(rcdc_ctx *ctx, const void *const *d_ins, uint32_t n
     return null_leave(ctx, hip_stream, st);
 }
 
-uint64_t rcdc_zstd_bound(uint64_t len) { return len + 3 * zstd_blocks(len) + 9; }
+uint64_t rcdc_zstd_bound(uint64_t len) {
+    return len + 3 * zstd_blocks(len) + (len > kZstdSingleMax ? 10 : 9);  // + the window byte
+}
 
 rcdc_status rcdc_zstd_compress(rcdc_ctx *ctx, int level, const void *d_in,
                                const rcdc_zstd_ref *refs, uint32_t n, void *d_out,

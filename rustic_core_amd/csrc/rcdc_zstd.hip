@@ -1791,8 +1791,12 @@ __global__ __launch_bounds__(64, (NARROW ? HL - 1 : HL) == 11 ? 4 : 2) void rcdc
     }
 }
 
-// A thread per blob: the frame header (magic, single-segment descriptor,
-// content size) and each block's output position; out_lens[i] = frame bytes.
+// A thread per blob: the frame header (magic, descriptor, content size) and
+// each block's output position; out_lens[i] = frame bytes.  Blobs up to
+// kZstdSingleMax bytes get single-segment frames (the window is the content
+// size); larger ones declare a 1 MiB window, above every offset the parse
+// emits (< 3 blocks: far candidates reach two blocks back), since rustic's
+// decode_all refuses windows above 2^27 + 1 bytes (libzstd's default limit).
 __global__ void rcdc_zstd_frame_kernel(const ZstdBlob *__restrict__ blobs, uint32_t nblobs,
                                        const uint2 *__restrict__ res, uint64_t *__restrict__ bpos,
                                        uint8_t *__restrict__ out, uint64_t *__restrict__ out_lens) {
@@ -1811,10 +1815,15 @@ __global__ void rcdc_zstd_frame_kernel(const ZstdBlob *__restrict__ blobs, uint3
         h[5] = (uint8_t)v;
         h[6] = (uint8_t)(v >> 8);
         hl = 7;
-    } else {
+    } else if (B.len <= kZstdSingleMax) {
         h[4] = 0xA0;  // 4 bytes
         for (int j = 0; j < 4; j++) h[5 + j] = (uint8_t)(B.len >> (8 * j));
         hl = 9;
+    } else {
+        h[4] = 0x80;  // FCS_flag 2 (4 bytes), not single-segment
+        h[5] = (uint8_t)((kZstdWindowLog - 10) << 3);  // Window_Descriptor: 2^20, mantissa 0
+        for (int j = 0; j < 4; j++) h[6 + j] = (uint8_t)(B.len >> (8 * j));
+        hl = 10;
     }
     uint8_t *o = out + B.out_off;
     for (uint32_t j = 0; j < hl; j++) o[j] = h[j];

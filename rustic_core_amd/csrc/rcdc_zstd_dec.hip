@@ -992,6 +992,17 @@ __device__ void check_compressed(Dec &D, DecLds &L, const uint8_t *p, uint32_t b
     }
 }
 
+// The window a frame asks its decoder for (RFC 8878 3.1.1.1.2; a
+// single-segment frame's is its content size) fits the limit of rustic's
+// decode_all: the zstd crate's streaming decoder keeps libzstd's default,
+// windows up to 2^27 + 1 bytes (ZSTD_WINDOWLOG_LIMIT_DEFAULT; larger ones
+// fail with "Frame requires too much memory for decoding").
+__device__ __forceinline__ bool window_ok(uint32_t single, uint32_t wd, uint64_t fcs) {
+    if (single) return fcs <= (1ull << 27) + 1ull;
+    const uint64_t base = 1ull << (10u + (wd >> 3));
+    return base + (base >> 3) * (wd & 7u) <= (1ull << 27) + 1ull;
+}
+
 // One frame; returns its status.
 __device__ uint32_t check_frame(const uint8_t *f, uint64_t flen, const uint8_t *data, uint64_t dlen,
                                 DecLds &L, uint8_t *scratch, uint32_t lane, bool prof) {
@@ -1017,6 +1028,7 @@ __device__ uint32_t check_frame(const uint8_t *f, uint64_t flen, const uint8_t *
     for (uint32_t i = 0; i < fcs_len; i++) fcs |= (uint64_t)q[i] << (8 * i);
     if (fcs_len == 2) fcs += 256;
     q += fcs_len;
+    if (!window_ok(single, single ? 0u : f[5], fcs)) return kCkCorrupt;
     if (fcs_len && fcs != dlen) return kCkMismatch;
     Dec D;
     D.data = data;
@@ -1144,6 +1156,7 @@ __global__ __launch_bounds__(256) void rcdc_zstd_blocks_kernel(
         for (uint32_t j = 0; j < fcs_len; j++) fcs |= (uint64_t)q[j] << (8 * j);
         if (fcs_len == 2) fcs += 256;
         q += fcs_len;
+        if (!window_ok(single, single ? 0u : f[5], fcs)) { st = kCkCorrupt; break; }
         if (fcs_len && fcs != dlen) { st = kCkMismatch; break; }
         uint64_t k = 0;
         for (;;) {

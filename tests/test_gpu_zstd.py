@@ -373,3 +373,52 @@ def test_literal_only_block_on_wave_zero():
             _check(frames, [d])
             if n >= 4096:
                 assert len(frames[0]) < 0.95 * n  # Huffman literals, not raw
+
+
+def test_blobs_above_128_mib_decode_with_decode_all(gpu_ctx):
+    """rustic's decode_all refuses frames asking for a window above 2^27 + 1
+    bytes, and a single-segment frame asks for its content size: blobs above
+    128 MiB get a 1 MiB window descriptor instead (all offsets are below 3
+    blocks), blobs up to 128 MiB stay single-segment.  Both decode through
+    the streaming decoder and pass the device check; the check refuses a
+    single-segment 129 MiB frame as decode_all does (status 2)."""
+    import sys
+    sys.path.insert(0, __file__.rsplit("/", 1)[0])
+    from zstd_model import frame
+    from rustic_core_amd.compress import CHECK_OK, check_frames
+    import torch
+    rng = np.random.default_rng(129)
+    pat = rng.integers(0, 256, 1000, dtype=np.uint8)
+    datas = []
+    for n in (128 << 20, (129 << 20) + 77):
+        a = np.resize(pat, n)
+        noise = rng.integers(0, n, n // 500)
+        a[noise] = rng.integers(0, 256, noise.size, dtype=np.uint8)
+        datas.append(a.tobytes())
+    frames = _compress(gpu_ctx, datas, level=3)
+    assert frames[0][4] == 0xA0 and frames[1][4] == 0x80 and frames[1][5] == (20 - 10) << 3
+    for fr, d in zip(frames, datas):
+        assert zr.decompress_stream(fr) == d
+        assert len(fr) < len(d) // 4
+    B = 128 << 10
+    rle = [frame([(1, b"\x00", B)] * ((m << 20) // B), m << 20) for m in (128, 129)]
+    allf = frames + rle
+    blobs = datas + [bytes(128 << 20), bytes(129 << 20)]
+    fo, o = [], 0
+    for f in allf:
+        fo.append(o)
+        o += len(f) + 16
+    farr = np.zeros(o + 64, np.uint8)
+    for a, f in zip(fo, allf):
+        farr[a:a + len(f)] = np.frombuffer(f, np.uint8)
+    do, o = [], 0
+    for d in blobs:
+        do.append(o)
+        o += len(d) + 16
+    darr = np.zeros(o + 64, np.uint8)
+    for a, d in zip(do, blobs):
+        darr[a:a + len(d)] = np.frombuffer(d, np.uint8)
+    d_f, d_d = torch.from_numpy(farr).to("cuda:0"), torch.from_numpy(darr).to("cuda:0")
+    st = check_frames(gpu_ctx, d_f.data_ptr(), fo, [len(f) for f in allf], d_d.data_ptr(), do,
+                      [len(d) for d in blobs])
+    assert st.tolist() == [CHECK_OK, CHECK_OK, CHECK_OK, 2]

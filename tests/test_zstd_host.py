@@ -270,3 +270,37 @@ def test_model_repeat_offsets(T):
         assert zr.decompress(fr) == d
         if len(blk) <= len(d):
             assert zr.decompress_pyarrow(fr, len(d)) == d
+
+
+def test_window_limit_of_decode_all():
+    """rustic's decode_all (the zstd crate's streaming decoder) refuses
+    frames asking for a window above 2^27 + 1 bytes; single-segment frames ask
+    for their content size, so blobs above 128 MiB get a window descriptor
+    (rcdc_zstd_frame_kernel) and one more header byte in the bound."""
+    import sys
+    sys.path.insert(0, __file__.rsplit("/", 1)[0])
+    from zstd_model import frame
+    B = 128 << 10
+    for mib, ok in ((128, True), (129, False)):
+        n = mib << 20
+        fr = frame([(1, b"\x00", B)] * (n // B), n)
+        assert len(zr.decompress(fr)) == n  # the one-shot decoder has no limit
+        if ok:
+            assert zr.decompress_stream(fr) == bytes(n)
+        else:
+            with pytest.raises(zr.ZstdError):
+                zr.decompress_stream(fr)
+    # the same 129 MiB with a 1 MiB window descriptor: accepted
+    n = 129 << 20
+    fr = frame([(1, b"\x00", B)] * (n // B), n)
+    fr = fr[:4] + bytes([0x80, (20 - 10) << 3]) + n.to_bytes(4, "little") + fr[9:]
+    assert zr.decompress_stream(fr) == bytes(n)
+
+
+def test_bound_large_blobs(rcdc_lib):
+    from rustic_core_amd.compress import zstd_bounds
+    for n in (0, 1, 1 << 27, (1 << 27) + 1, (1 << 32) - 1):
+        nb = max((n + (128 << 10) - 1) // (128 << 10), 1)
+        want = n + 3 * nb + (10 if n > (1 << 27) else 9)
+        assert rcdc_lib.rcdc_zstd_bound(n) == want
+        assert int(zstd_bounds([n])[0]) == want

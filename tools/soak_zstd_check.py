@@ -8,7 +8,8 @@ frames: bit flips, byte and span overwrites, zeroed spans, truncation, bytes
 appended, edits aimed at block headers and at the first bytes of a block's
 literals / sequences sections, random garbage behind a good header, and
 another frame's body behind this frame's header.  The device must accept
-(status 0) exactly the frames libzstd decodes to the blob; a wrong blob
+(status 0) exactly the frames libzstd's streaming decoder (rustic's
+decode_all, window limit included) decodes to the blob; a wrong blob
 length or byte must give status 1 or 2.  Exits 1 on a disagreement with the
 case's seed.
 
@@ -136,7 +137,8 @@ def reserved_modes_bits(fr):
 
 def libzstd_ok(frame, data):
     try:
-        ok = zr.frame_size(frame) == len(frame) and zr.decompress(frame, len(data) + 64) == data
+        # decode_all's decoder: streaming, with libzstd's default window limit
+        ok = zr.frame_size(frame) == len(frame) and zr.decompress_stream(frame) == data
     except zr.ZstdError:
         return False
     return ok and not reserved_modes_bits(frame)
