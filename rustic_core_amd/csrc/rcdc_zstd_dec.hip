@@ -565,17 +565,24 @@ __device__ int read_huf_weights(const uint8_t *p, int64_t avail, DecLds &L, uint
         wsync();
     }
     // the last weight is implied: the weights fill a power of two
-    uint32_t total = 0;
+    uint32_t total = 0, ones = 0;
     for (uint32_t i = 0; i < n; i++) {
         const uint32_t wi = L.w[i];
         if (wi > 11) return -1;
         total += wi ? (1u << (wi - 1)) : 0u;
+        ones += wi == 1u;
     }
     if (total == 0) return -1;
     const uint32_t tl = highbit32(total) + 1;
     if (tl > 11) return -1;
     const uint32_t rest = (1u << tl) - total;
     if (rest & (rest - 1)) return -1;
+    // HUF_readStats' tree check: an even number, at least 2, of weight-1
+    // symbols (codes of the full table log), the implied last one included.
+    // Without it a table whose codes are all shorter than its log decodes,
+    // but libzstd calls it corrupt (r6 checker soak, seed 5627)
+    ones += rest == 1u;
+    if (ones < 2 || (ones & 1u)) return -1;
     wsync();
     if (lane == 0) L.w[n] = (uint8_t)(highbit32(rest) + 1);
     *nw = n + 1;

@@ -226,3 +226,25 @@ def test_process_blobs_extra_verify(gpu_ctx):
             verify_sealed(gpu_ctx, key, bad.data_ptr(), s_offs, s_lens, d_in.data_ptr(), offs, lens,
                           level is not None)
         assert e.value.kind == ErrorKind.Verification
+
+
+def test_huffman_tree_without_full_length_codes_rejected(gpu_ctx):
+    """tools/soak_zstd_check.py seed 5627: a libzstd level-2 frame whose
+    FSE-coded Huffman weights had one bit changed (byte 16, 0x10 -> 0x12; the
+    files are that case's frame, the untouched frame and the blob,
+    tests/golden/zck_s5627.*).  The weights still decode to a table that
+    decodes the blob, but it has no weight-1 symbol, and libzstd's
+    HUF_readStats calls such a table corrupt (at least two weight-1
+    symbols, an even number).  The device agrees: status 2; the untouched
+    frame passes."""
+    import os
+    g = os.path.join(os.path.dirname(__file__), "golden", "zck_s5627.")
+    bad, good, data = (open(g + x, "rb").read() for x in ("frame", "good", "data"))
+    assert bad[16] == 0x12 and good[16] == 0x10 and bad[:16] == good[:16]
+    for fr, ok in ((bad, False), (good, True)):
+        try:
+            dec = zr.decompress_stream(fr) == data
+        except zr.ZstdError:
+            dec = False
+        assert dec == ok
+    assert _check(gpu_ctx, [bad, good], [data, data]).tolist() == [2, 0]

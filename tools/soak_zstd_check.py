@@ -228,6 +228,12 @@ def one_case(seed, torch, ctx):
                  "frame_len": len(f), "data_len": len(d)}
             if len(f) <= 4096:  # small enough to replay on the host
                 e["frame"], e["good"] = f.hex(), frames[i].hex()
+            dump = os.environ.get("SOAK_DUMP")  # a directory: the frame, its source and the blob
+            if dump:
+                os.makedirs(dump, exist_ok=True)
+                for tag, b in (("frame", f), ("good", frames[i]), ("data", d)):
+                    with open(os.path.join(dump, f"s{seed}_{i}.{tag}"), "wb") as fh:
+                        fh.write(b)
             errs.append(e)
     return {"seed": seed, "frames": nb, "bytes": int(sum(len(d) for d in datas)),
             "corrupt": kinds.count("corrupt"), "errors": errs}
