@@ -28,6 +28,11 @@ sys.path.insert(0, ROOT)
 
 sys.path.insert(0, os.path.join(ROOT, "tools"))
 from tests.test_gpu_native_ingest import KEY  # noqa: E402
+
+# zstd levels drawn (None: stored blobs); SOAK_LEVELS="22,-5,4" replaces the
+# list (the default keeps earlier seeds replayable)
+LEVELS = [None, 0, 1, 3, 7] if not os.environ.get("SOAK_LEVELS") else \
+    [None if x == "none" else int(x) for x in os.environ["SOAK_LEVELS"].split(",")]
 from tests.test_gpu_ingest_streams import ChoppyReader, FailingReader  # noqa: E402
 from soak import POLYS  # noqa: E402
 
@@ -108,7 +113,7 @@ def check(events, engines, stats, level, params, ordered):
             for (tpe, off, ln, ulen, bid), (id_, boff, blen, bulen, btype) in zip(parsed, p["blobs"]):
                 assert off == boff and ln == blen and bytes(bid) == id_ and ulen == bulen, "blob entry"
                 plain = oracle.open_(KEY, data[off:off + ln])
-                raw = zstd_ref.decompress(plain) if level is not None else plain
+                raw = zstd_ref.decompress_stream(plain) if level is not None else plain  # decode_all
                 assert hashlib.sha256(raw).digest() == id_, "blob bytes"
                 end = off + ln
                 packed.append(id_)
@@ -141,7 +146,8 @@ def one_case(seed, tmp):
                long_chunk=int(rng.choice([256 * KiB, 1 * MiB, 2 * MiB, 64 * MiB])),
                pack_size=int(rng.choice([1, 4, 32])) * MiB,
                pack_grow_factor=int(rng.choice([0, 32])), hash_threads=int(rng.integers(1, 11)))
-    level = [None, 0, 1, 3, 7][int(rng.integers(0, 5))]
+    levels = LEVELS
+    level = levels[int(rng.integers(0, len(levels)))]
     multi = rng.random() < 0.2
     events = []
     if multi:
