@@ -106,18 +106,21 @@ class _ZBuf(ctypes.Structure):
     _fields_ = [("ptr", ctypes.c_void_p), ("size", ctypes.c_size_t), ("pos", ctypes.c_size_t)]
 
 
-def decompress_stream(frame: bytes) -> bytes:
+def decompress_stream(frame: bytes, step: int = 8192) -> bytes:
     """decode_all as rustic runs it: the zstd crate's streaming Decoder
     (ZSTD_decompressStream with libzstd's defaults, so frames asking for a
     window above 2^27 + 1 bytes are refused -- single-segment frames ask for
-    their content size).  One frame; raises ZstdError."""
+    their content size), read through `step`-byte output buffers (io::copy's
+    8 KiB).  A frame whose content fits the first buffer takes libzstd's
+    one-pass shortcut instead, which checks no window and refuses empty
+    compressed blocks; larger ones go through the stage machine.  One frame;
+    raises ZstdError."""
     L = lib()
     ds = L.ZSTD_createDStream()
     try:
         _check(L.ZSTD_initDStream(ds))
         src = ctypes.create_string_buffer(frame, len(frame))
         ib = _ZBuf(ctypes.cast(src, ctypes.c_void_p), len(frame), 0)
-        step = 1 << 20
         dst = ctypes.create_string_buffer(step)
         out = []
         while True:

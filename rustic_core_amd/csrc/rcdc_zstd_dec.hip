@@ -1010,6 +1010,18 @@ __device__ __forceinline__ bool window_ok(uint32_t single, uint32_t wd, uint64_t
     return base + (base >> 3) * (wd & 7u) <= (1ull << 27) + 1ull;
 }
 
+// decode_all (decrypt.rs:71-95) reads the decoder through io::copy into a
+// Vec, whose first read offers 8 KiB of output (DEFAULT_BUF_SIZE).  A frame
+// whose content size is known and fits takes libzstd's one-pass shortcut
+// (ZSTD_decompressStream -> ZSTD_decompress_usingDDict): no window limit,
+// and an empty compressed block is corrupt.  Other frames go through the
+// stage machine: the window limit applies and empty blocks of any type are
+// skipped.  The checker follows the path decode_all would take.
+constexpr uint64_t kDecodeAllFirstOut = 8192;
+__device__ __forceinline__ bool one_pass(uint32_t fcs_len, uint64_t fcs) {
+    return fcs_len && fcs <= kDecodeAllFirstOut;
+}
+
 // One frame; returns its status.
 __device__ uint32_t check_frame(const uint8_t *f, uint64_t flen, const uint8_t *data, uint64_t dlen,
                                 DecLds &L, uint8_t *scratch, uint32_t lane, bool prof) {
@@ -1035,7 +1047,8 @@ __device__ uint32_t check_frame(const uint8_t *f, uint64_t flen, const uint8_t *
     for (uint32_t i = 0; i < fcs_len; i++) fcs |= (uint64_t)q[i] << (8 * i);
     if (fcs_len == 2) fcs += 256;
     q += fcs_len;
-    if (!window_ok(single, single ? 0u : f[5], fcs)) return kCkCorrupt;
+    const bool shortcut = one_pass(fcs_len, fcs);
+    if (!shortcut && !window_ok(single, single ? 0u : f[5], fcs)) return kCkCorrupt;
     if (fcs_len && fcs != dlen) return kCkMismatch;
     Dec D;
     D.data = data;
@@ -1069,6 +1082,10 @@ __device__ uint32_t check_frame(const uint8_t *f, uint64_t flen, const uint8_t *
             if (!wave_cmp(data + D.out, nullptr, q[0], 1, bsize, lane)) return kCkMismatch;
             D.out += bsize;
             q += 1;
+        } else if (bsize == 0 && !shortcut) {
+            // an empty compressed block: the stage machine skips blocks of 0
+            // bytes whatever their type (ZSTD_decompressContinue); the one-pass
+            // path calls it corrupt, below (r6 checker soak, seeds 8485, 8527)
         } else {
             if (bsize > kBlockMax || bsize == 0 || q + bsize > end) return kCkCorrupt;
             check_compressed(D, L, q, bsize, scratch, lane);
@@ -1163,7 +1180,10 @@ __global__ __launch_bounds__(256) void rcdc_zstd_blocks_kernel(
         for (uint32_t j = 0; j < fcs_len; j++) fcs |= (uint64_t)q[j] << (8 * j);
         if (fcs_len == 2) fcs += 256;
         q += fcs_len;
-        if (!window_ok(single, single ? 0u : f[5], fcs)) { st = kCkCorrupt; break; }
+        if (!one_pass(fcs_len, fcs) && !window_ok(single, single ? 0u : f[5], fcs)) {
+            st = kCkCorrupt;
+            break;
+        }
         if (fcs_len && fcs != dlen) { st = kCkMismatch; break; }
         uint64_t k = 0;
         for (;;) {

@@ -248,3 +248,30 @@ def test_huffman_tree_without_full_length_codes_rejected(gpu_ctx):
             dec = False
         assert dec == ok
     assert _check(gpu_ctx, [bad, good], [data, data]).tolist() == [2, 0]
+
+
+def test_empty_compressed_block_as_decode_all(gpu_ctx):
+    """tools/soak_zstd_check.py seeds 8485 and 8527: empty compressed blocks.
+    decode_all's streaming decoder skips them, unless the frame declares a
+    content size that fits its first 8 KiB output buffer: then it decodes in
+    one pass, which calls them corrupt.  The device takes the same path."""
+    import sys
+    sys.path.insert(0, __file__.rsplit("/", 1)[0])
+    from zstd_model import frame
+    fr = bytes.fromhex("28b52ffd0002050000")
+    assert zr.decompress_stream(fr) == b""
+    d = bytes(range(256)) * 100
+    f2 = frame([(2, b"", 0), (0, d, len(d))], len(d))  # an empty compressed block, then raw
+    assert zr.decompress_stream(f2) == d
+    bad = frame([(2, b"", 0), (0, d, len(d))], len(d) + 1)  # content size off by one
+    assert _check(gpu_ctx, [fr, f2, bad], [b"", d, d + b"x"]).tolist() == [0, 0, 1]
+    # seed 8527: the same block in a frame declaring content size 0 takes
+    # decode_all's one-pass path (its first 8 KiB output buffer holds the
+    # content), which calls the block corrupt
+    one = bytes.fromhex("28b52ffd2000050000")
+    with pytest.raises(zr.ZstdError):
+        zr.decompress_stream(one)
+    small = frame([(2, b"", 0), (0, d[:5000], 5000)], 5000)
+    with pytest.raises(zr.ZstdError):
+        zr.decompress_stream(small)
+    assert _check(gpu_ctx, [one, small], [b"", d[:5000]]).tolist() == [2, 2]

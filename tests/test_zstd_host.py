@@ -304,3 +304,29 @@ def test_bound_large_blobs(rcdc_lib):
         want = n + 3 * nb + (10 if n > (1 << 27) else 9)
         assert rcdc_lib.rcdc_zstd_bound(n) == want
         assert int(zstd_bounds([n])[0]) == want
+
+
+def test_checker_soak_verdict_helpers():
+    """tools/soak_zstd_check.py's host side: block_spots walks libzstd frames
+    (single-segment or with a window descriptor), reserved_modes_bits flags
+    the seed-604 frame (RFC 8878 3.1.1.3.2.1) and not its source, and the
+    verdict follows decode_all's streaming decoder."""
+    import os
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(__file__)), "tools"))
+    import soak_zstd_check as S
+    bad = bytes.fromhex("28b52ffd60f61945000008000101f24aef84")
+    good = bytes.fromhex("28b52ffd60f61945000008000100f24aef84")
+    assert S.reserved_modes_bits(bad) and not S.reserved_modes_bits(good)
+    d = zr.decompress(good)
+    assert zr.decompress(bad) == d  # libzstd 1.4.8 decodes it; 1.5 and the device do not
+    assert S.libzstd_ok(good, d) and not S.libzstd_ok(bad, d)
+    rng = np.random.default_rng(3)
+    for n, level in ((100, 3), (300000, 1), (700000, 19)):
+        data = rng.integers(0, 8, n, dtype=np.uint8).tobytes()
+        fr = zr.compress(data, level)
+        heads, bodies = S.block_spots(fr)
+        assert heads and heads[-1] + 3 <= len(fr)
+        assert S.libzstd_ok(fr, data) and not S.libzstd_ok(fr, data + b"x")
+        for _ in range(20):
+            S.corrupt(rng, fr, fr)  # any corruption is a byte string
