@@ -478,6 +478,10 @@ typedef struct {
  * 1 it decodes to other bytes or another length (ErrorKind::Verification,
  * decrypt.rs:516-526), 2 malformed or not readable here (a dictionary, a
  * skippable frame, bytes after the frame).  A frame checksum is skipped.
+ * Malformed means what decode_all's decoder refuses on the path it would
+ * take: one pass when the declared content size fits its first 8 KiB
+ * read, otherwise the streaming stage machine (a window above 2^27 + 1
+ * bytes is refused there, and empty blocks of any type are skipped).
  * flags bit 0 (RCDC_CHECK_STORED): the "frames" are stored bytes (blobs of an
  * uncompressed repository), compared as they are.  Synchronous.  Calls on one context take turns; the context keeps a
  * 128 KiB literal scratch per resident wave (256 MiB on 256 CUs).          */
